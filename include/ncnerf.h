@@ -1,0 +1,131 @@
+/*
+ * ncnerf.h — C ABI of libncnerf.so, the MI355X (gfx950) hot path of the normal-clustering NeRF
+ * training step.  Every entry point:
+ *   - takes plain device pointers, element counts and a hipStream_t passed as `void*`
+ *     (the caller's current stream; never the legacy default stream);
+ *   - never allocates, frees or synchronises: buffers are sized by the caller (the one size that
+ *     is data dependent — the marched sample count — is produced on device by the count/scan pass
+ *     and read back by the caller, exactly where the reference slices by counter[0]);
+ *   - returns 0 (hipSuccess) or a hipError_t code; ncn_last_error() returns a message.
+ * No torch types cross this boundary.  The Python drop-in (normal-clustering-nerf_amd/ncnerf_amd/
+ * vren.py, custom_functions.py, ngp_mt.py, losses.py) binds these with ctypes; INTEGRATION.md shows
+ * the binding a maintainer adds on the reference side.
+ *
+ * Layout conventions: float3 arrays are AoS (N,3) contiguous as in the reference; rays_a is (R,3)
+ * int64 (ray_idx, start, n_samples) in RAY ORDER (the reference's atomic order is
+ * nondeterministic, raymarching.cu:237-238).
+ */
+#ifndef NCNERF_H
+#define NCNERF_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* ncn_last_error(void);
+int ncn_version(void);
+
+/* ---- occupancy utilities: replaces vren.morton3D / morton3D_invert / packbits
+ *      (binding.cpp:42-72, raymarching.cu:62-161) ---- */
+int ncn_morton3D(const int32_t* coords, int64_t n, int32_t* out, void* stream);
+int ncn_morton3D_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream);
+int ncn_packbits(const float* density_grid, int64_t n_bytes, float threshold, uint8_t* bitfield, void* stream);
+
+/* ---- ray / AABB: replaces vren.ray_aabb_intersect (binding.cpp:12-24, intersection.cu:59-100).
+ *      hits_t (R,max_hits,2) and hits_voxel_idx (R,max_hits) are fully written (-1 when empty). ---- */
+int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays,
+                           const float* centers, const float* half_sizes, int64_t n_voxels, int max_hits,
+                           int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx, void* stream);
+
+/* ---- training marcher: replaces vren.raymarching_train (raymarching.cu:283-332).
+ * Pass 1 (walk): one walk per ray; samples go to a per-ray slab [R][max_samples] (xyz: 3 floats,
+ *   t, dt) and counts[r] = n_samples.  slab_* sized R*max_samples (no zero fill needed).
+ * Pass 2 (scan): rays_a[r] = (r, exclusive_scan(counts)[r], counts[r]); counter = {S, R}.
+ * Pass 3 (pack): compacts the slab into xyzs (S,3), dirs (S,3), deltas (S), ts (S).
+ * hits_t is (R,2) (the caller's hits_t[:,0] view made contiguous). ---- */
+int ncn_march_train_walk(const float* rays_o, const float* rays_d, const float* hits_t, const float* noise,
+                         int64_t n_rays, const uint8_t* bitfield, int cascades, float scale,
+                         float exp_step_factor, int grid_size, int max_samples,
+                         int32_t* counts, float* slab_xyz, float* slab_t, float* slab_dt, void* stream);
+int ncn_march_train_scan(const int32_t* counts, int64_t n_rays, int64_t* rays_a, int32_t* counter, void* stream);
+int ncn_march_train_pack(const float* rays_d, const int64_t* rays_a, int64_t n_rays, int max_samples,
+                         const float* slab_xyz, const float* slab_t, const float* slab_dt,
+                         float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
+
+/* ---- test-time marcher: replaces vren.raymarching_test (raymarching.cu:407-454).
+ * Outputs (A,N_samples[,3]) are fully written (zeros past n_eff).  Mutates hits_t[r][0]. ---- */
+int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive, int64_t n_alive,
+                   const uint8_t* bitfield, int cascades, float scale, float exp_step_factor, int grid_size,
+                   int max_samples, int n_samples, float* xyzs, float* dirs, float* deltas, float* ts,
+                   int32_t* n_eff, void* stream);
+
+/* ---- compositing: replaces vren.composite_train_multi_fw / _bw / composite_test_multi_fw
+ *      (volumerendering.cu:140-176, 367-418, 553-586).  All outputs fully written (no pre-zeroing).
+ *      In _bw any of dL_dopacity / dL_ddepth / dL_drend / dL_dws may be NULL (== zeros). ---- */
+int ncn_composite_train_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
+                           const int64_t* rays_a, int64_t n_rays, int64_t n_samples, int n_rend, float T_threshold,
+                           int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws,
+                           void* stream);
+int ncn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drend,
+                           const float* dL_dws, const float* sigmas, const float* raws, const float* ws,
+                           const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
+                           int64_t n_samples, int n_rend, const float* opacity, const float* depth,
+                           const float* rend, float T_threshold, float* dL_dsigmas, float* dL_draws, void* stream);
+int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
+                          int64_t* alive, int64_t n_alive, int n_samples, int n_rend, float T_threshold,
+                          const int32_t* n_eff, float* opacity, float* depth, float* rend, void* stream);
+
+/* ---- NGPMT field: replaces tcnn Encoding(Grid/Hash) + sigma_net + rgb_net + TruncExp
+ *      (ngp_mt.py:70-113, 157-229; custom_functions.py:162-173).
+ * Hash grid geometry (16 levels, 2 features) is described by `levels` = 16 x {scale f32 bits,
+ *   resolution, params, offset} as uint32 (see ncnerf_amd/ngp_mt.py:grid_levels).
+ * weights_packed: fp16 MFMA fragments produced by ncn_field_pack_weights from the fp32 masters
+ *   W1 (64,32) W2 (16,64) W3 (64,19) W4 (64,64) W5 (3,64) concatenated (size NCN_FIELD_NW floats).
+ * enc_cache: fp16 encoding cache for the backward, NCN_ENC_BYTES_PER_SAMPLE bytes per sample
+ *   (rounded up to 16 samples); may be NULL for inference.
+ * mode 0: full (sigmas + rgbs), mode 1: density only (sigmas; dirs/rgbs ignored). ---- */
+#define NCN_FIELD_NW (64 * 32 + 16 * 64 + 64 * 19 + 64 * 64 + 3 * 64)
+#define NCN_FIELD_PACKED_HALVES 19456
+#define NCN_ENC_BYTES_PER_SAMPLE 64
+int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void* stream);
+int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* table, const uint32_t* levels,
+                  float xyz_min, float xyz_extent, const uint16_t* weights_packed, int mode,
+                  float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
+/* Backward: accumulates (+=) into grad_table (n_entries,2) with f32 atomics and writes per-block
+ * weight-gradient slabs (n_blocks x NCN_FIELD_NW) into `slab`; ncn_field_reduce_wgrad sums them
+ * in a fixed order into grad_w (+=).  n_blocks is returned by ncn_field_bwd_blocks(n). */
+int ncn_field_bwd_blocks(int64_t n);
+int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_t* levels, float xyz_min,
+                  float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
+                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, void* stream);
+int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream);
+
+/* ---- normal clustering loss path: replaces _extract_normals_from_ray_batch
+ *      (hypersim_src/utils.py:504-541) and the faiss + torch cluster block of NeRFMTLoss
+ *      (losses.py:47-166, 420-478). ---- */
+int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
+                    const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals, void* stream);
+int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
+                    const int64_t* x2, const int64_t* x3, int64_t n_tri, const float* dL_dnormals,
+                    float* dL_ddepth, void* stream);
+/* One workgroup: validity filter, spherical k-means (K<=32, niter), cluster selection, the three
+ * cluster losses and their gradient w.r.t. the normals, scaled by w_ort / w_dot / w_l1.
+ * out_losses[0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter; [3] = valid n;
+ * out_labels (n_tri) int32 in {0,+-1,+-2,+-3} (-9 = invalid normal); out_centroids (K,3);
+ * dL_dnormals (3,n_tri,3) fully written: the gradient of w_ort*ort, w_dot*centr_dot and w_l1*centr_L1
+ * separately, so any upstream weighting of the three terms is a 3-term combination. */
+int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
+                     float w_ort, float w_dot, float w_l1, float* out_losses, int32_t* out_labels,
+                     float* out_centroids, float* dL_dnormals, void* stream);
+
+/* ---- optimizer (train_nerf.py:262-291, 954-955): global-norm clip + Adam over a flat buffer. ---- */
+int ncn_sumsq(const float* x, int64_t n, float* out_partial /* >= 1024 floats */, void* stream);
+int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+             const float* sumsq_partial, float max_norm, float lr, float beta1, float beta2, float eps,
+             float weight_decay, int step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

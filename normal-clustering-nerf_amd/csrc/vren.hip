@@ -1,0 +1,819 @@
+// Ray-AABB intersection, occupancy-grid ray marching, front-to-back compositing and the occupancy
+// utilities for gfx950.  Replaces the reference `vren` kernels (models/csrc/intersection.cu,
+// raymarching.cu, volumerendering.cu); every kernel cites the lines whose semantics it keeps.
+//
+// Floating-point contract: contraction is OFF for this whole file; the FMAs that the reference's
+// nvcc build contracts (default --fmad=true) are written as explicit fmaf(), identically in the
+// CPU oracle (oracle/vren_ref.c).  Division is IEEE (hipcc default correctly-rounded f32 div).
+// This makes sample positions, voxel indices and sample counts bit-identical to the oracle.
+#pragma clang fp contract(off)
+
+#include "common.h"
+#include "../../include/ncnerf.h"
+
+#define SQRT3 1.73205080757f
+
+namespace ncn {
+
+__device__ __forceinline__ float clampf_(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }
+__device__ __forceinline__ float signf_(float x) { return copysignf(1.0f, x); }
+
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+// raymarching.cu:44-50
+__device__ __forceinline__ uint32_t morton3D(uint32_t x, uint32_t y, uint32_t z) {
+    return expand_bits(x) | (expand_bits(y) << 1) | (expand_bits(z) << 2);
+}
+// raymarching.cu:52-60
+__device__ __forceinline__ uint32_t morton3D_invert(uint32_t x) {
+    x = x & 0x49249249u;
+    x = (x | (x >> 2)) & 0xc30c30c3u;
+    x = (x | (x >> 4)) & 0x0f00f00fu;
+    x = (x | (x >> 8)) & 0xff0000ffu;
+    x = (x | (x >> 16)) & 0x0000ffffu;
+    return x;
+}
+
+// raymarching.cu:19-32
+__device__ __forceinline__ int mip_from_pos(float x, float y, float z, int cascades) {
+    const float mx = fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z)));
+    int e;
+    frexpf(mx, &e);
+    return min(cascades - 1, max(0, e + 1));
+}
+__device__ __forceinline__ int mip_from_dt(float dt, int grid_size, int cascades) {
+    int e;
+    frexpf(dt * (float)grid_size, &e);
+    return min(cascades - 1, max(0, e));
+}
+
+// Marcher constants.  calc_dt (raymarching.cu:11-13) = clamp(t*esf, SQRT3/max_samples, SQRT3*2*scale/G)
+struct MarchConst {
+    float esf, dt_min, dt_max, scale, gsi;
+    int cascades, G, max_samples;
+    uint32_t G3;
+};
+__device__ __forceinline__ MarchConst make_march_const(int cascades, float scale, float esf, int G, int max_samples,
+                                                       float dt_scale) {
+    MarchConst m;
+    m.esf = esf;
+    m.dt_min = SQRT3 / (float)max_samples;
+    m.dt_max = SQRT3 * 2 * dt_scale / (float)G;
+    m.scale = scale;
+    m.gsi = 1.0f / (float)G;
+    m.cascades = cascades;
+    m.G = G;
+    m.max_samples = max_samples;
+    m.G3 = (uint32_t)G * G * G;
+    return m;
+}
+__device__ __forceinline__ float calc_dt(const MarchConst& m, float t) { return clampf_(t * m.esf, m.dt_min, m.dt_max); }
+
+// One occupancy probe at t (raymarching.cu:205-220).  Returns the voxel (nx,ny,nz), mip bound and
+// the bitfield index; `cache_bi/cache_b` memoise the last bitfield byte (same byte => same bits).
+template <bool ONE_CASCADE>
+__device__ __forceinline__ bool probe(const MarchConst& m, const uint8_t* __restrict__ bitfield, float x, float y,
+                                      float z, float dt, int& nx, int& ny, int& nz, float& mip_bound,
+                                      uint32_t& cache_bi, uint32_t& cache_b) {
+    int mip;
+    if (ONE_CASCADE) {
+        mip = 0;  // min(cascades-1, ...) == 0 for both mip_from_pos and mip_from_dt
+    } else {
+        mip = max(mip_from_pos(x, y, z, m.cascades), mip_from_dt(dt, m.G, m.cascades));
+    }
+    mip_bound = fminf(scalbnf(1.0f, mip - 1), m.scale);
+    const float mip_bound_inv = 1.0f / mip_bound;
+    nx = (int)clampf_(0.5f * fmaf(x, mip_bound_inv, 1.0f) * (float)m.G, 0.0f, m.G - 1.0f);
+    ny = (int)clampf_(0.5f * fmaf(y, mip_bound_inv, 1.0f) * (float)m.G, 0.0f, m.G - 1.0f);
+    nz = (int)clampf_(0.5f * fmaf(z, mip_bound_inv, 1.0f) * (float)m.G, 0.0f, m.G - 1.0f);
+    const uint32_t idx = (uint32_t)mip * m.G3 + morton3D((uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
+    const uint32_t bi = idx >> 3;
+    if (bi != cache_bi) {
+        cache_b = bitfield[bi];
+        cache_bi = bi;
+    }
+    return (cache_b >> (idx & 7)) & 1u;
+}
+
+// Empty-voxel skip (raymarching.cu:224-233).
+__device__ __forceinline__ float skip_voxel(const MarchConst& m, float t, float x, float y, float z, float dx,
+                                            float dy, float dz, float dxi, float dyi, float dzi, int nx, int ny,
+                                            int nz, float mip_bound) {
+    const float tx = fmaf(fmaf(0.5f, signf_(dx), (float)nx + 0.5f) * m.gsi * 2 - 1, mip_bound, -x) * dxi;
+    const float ty = fmaf(fmaf(0.5f, signf_(dy), (float)ny + 0.5f) * m.gsi * 2 - 1, mip_bound, -y) * dyi;
+    const float tz = fmaf(fmaf(0.5f, signf_(dz), (float)nz + 0.5f) * m.gsi * 2 - 1, mip_bound, -z) * dzi;
+    const float t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    do {
+        t += calc_dt(m, t);
+    } while (t < t_target);
+    return t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// raymarching_train pass 1: one lane per ray walks it once (raymarching.cu:184-234) and writes the
+// samples into its slab row.  64-lane workgroups spread the (latency-bound) walks over the CUs.
+template <bool ONE_CASCADE>
+__global__ __launch_bounds__(64) void march_train_walk_kernel(
+    const float* __restrict__ rays_o, const float* __restrict__ rays_d, const float* __restrict__ hits_t,
+    const float* __restrict__ noise, int64_t R, const uint8_t* __restrict__ bitfield, int cascades, float scale,
+    float esf, int G, int max_samples, int32_t* __restrict__ counts, float* __restrict__ slab_xyz,
+    float* __restrict__ slab_t, float* __restrict__ slab_dt) {
+    const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= R) return;
+    const MarchConst m = make_march_const(cascades, scale, esf, G, max_samples, scale);
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t1 = hits_t[2 * r];
+    const float t2 = hits_t[2 * r + 1];
+    if (t1 >= 0) {  // :195-198
+        const float dt = calc_dt(m, t1);
+        t1 = fmaf(dt, noise[r], t1);
+    }
+    float* sx = slab_xyz + r * (int64_t)max_samples * 3;
+    float* st = slab_t + r * (int64_t)max_samples;
+    float* sd = slab_dt + r * (int64_t)max_samples;
+    uint32_t cache_bi = 0xFFFFFFFFu, cache_b = 0;
+    float t = t1;
+    int n = 0;
+    while (0 <= t && t < t2 && n < max_samples) {  // :204
+        const float x = fmaf(t, dx, ox), y = fmaf(t, dy, oy), z = fmaf(t, dz, oz);
+        const float dt = calc_dt(m, t);
+        int nx, ny, nz;
+        float mip_bound;
+        if (probe<ONE_CASCADE>(m, bitfield, x, y, z, dt, nx, ny, nz, mip_bound, cache_bi, cache_b)) {
+            sx[3 * n] = x;
+            sx[3 * n + 1] = y;
+            sx[3 * n + 2] = z;
+            st[n] = t;
+            sd[n] = dt;
+            t += dt;
+            n++;
+        } else {
+            t = skip_voxel(m, t, x, y, z, dx, dy, dz, dxi, dyi, dzi, nx, ny, nz, mip_bound);
+        }
+    }
+    counts[r] = n;
+}
+
+// raymarching_train pass 2: exclusive scan of the counts in ray order (one workgroup; replaces the
+// atomicAdd start offsets of raymarching.cu:237-241) -> rays_a, counter = {S, R}.
+__global__ __launch_bounds__(1024) void march_train_scan_kernel(const int32_t* __restrict__ counts, int64_t R,
+                                                                int64_t* __restrict__ rays_a,
+                                                                int32_t* __restrict__ counter) {
+    __shared__ int wave_tot[16];
+    __shared__ int carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < R; base += 4096) {
+        const int64_t i0 = base + (int64_t)tid * 4;
+        int c[4];
+        int local = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            c[j] = (i0 + j < R) ? counts[i0 + j] : 0;
+            local += c[j];
+        }
+        int incl = local;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        if (lane == 63) wave_tot[wid] = incl;
+        __syncthreads();
+        int wave_off = 0, block_tot = 0;
+        for (int w = 0; w < 16; w++) {
+            if (w < wid) wave_off += wave_tot[w];
+            block_tot += wave_tot[w];
+        }
+        const int carry = carry_s;
+        int run = carry + wave_off + incl - local;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t i = i0 + j;
+            if (i < R) {
+                rays_a[3 * i] = i;
+                rays_a[3 * i + 1] = run;
+                rays_a[3 * i + 2] = c[j];
+            }
+            run += c[j];
+        }
+        __syncthreads();
+        if (tid == 0) carry_s = carry + block_tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        counter[0] = carry_s;
+        counter[1] = (int32_t)R;
+    }
+}
+
+// raymarching_train pass 3: one wave per ray copies its slab row to the packed outputs
+// (coalesced 4-byte lanes) and broadcasts the ray direction into dirs (raymarching.cu:263-268).
+__global__ __launch_bounds__(256) void march_train_pack_kernel(
+    const float* __restrict__ rays_d, const int64_t* __restrict__ rays_a, int64_t R, int max_samples,
+    const float* __restrict__ slab_xyz, const float* __restrict__ slab_t, const float* __restrict__ slab_dt,
+    float* __restrict__ xyzs, float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= R) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int cnt = (int)rays_a[3 * n + 2];
+    const float d3[3] = {rays_d[3 * ray], rays_d[3 * ray + 1], rays_d[3 * ray + 2]};
+    const float* sx = slab_xyz + ray * (int64_t)max_samples * 3;
+    const float* st = slab_t + ray * (int64_t)max_samples;
+    const float* sd = slab_dt + ray * (int64_t)max_samples;
+    for (int k = lane; k < 3 * cnt; k += 64) {
+        xyzs[3 * start + k] = sx[k];
+        dirs[3 * start + k] = d3[k % 3];
+    }
+    for (int k = lane; k < cnt; k += 64) {
+        ts[start + k] = st[k];
+        deltas[start + k] = sd[k];
+    }
+}
+
+// raymarching_test (raymarching.cu:335-404): one lane per alive ray; writes all N_samples slots
+// (zeros past n_eff, as the torch::zeros outputs of :422-427).  Quirk q3: calc_dt receives
+// `cascades` as its scale (:370, :399).
+template <bool ONE_CASCADE>
+__global__ __launch_bounds__(64) void march_test_kernel(const float* __restrict__ rays_o,
+                                                        const float* __restrict__ rays_d, float* __restrict__ hits_t,
+                                                        const int64_t* __restrict__ alive, int64_t A,
+                                                        const uint8_t* __restrict__ bitfield, int cascades,
+                                                        float scale, float esf, int G, int max_samples, int NS,
+                                                        float* __restrict__ xyzs, float* __restrict__ dirs,
+                                                        float* __restrict__ deltas, float* __restrict__ ts,
+                                                        int32_t* __restrict__ n_eff) {
+    const int64_t n = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (n >= A) return;
+    const MarchConst m = make_march_const(cascades, scale, esf, G, max_samples, (float)cascades);
+    const int64_t r = alive[n];
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t = hits_t[2 * r];
+    const float t2 = hits_t[2 * r + 1];
+    float* X = xyzs + n * (int64_t)NS * 3;
+    float* D = dirs + n * (int64_t)NS * 3;
+    float* DT = deltas + n * (int64_t)NS;
+    float* TS = ts + n * (int64_t)NS;
+    uint32_t cache_bi = 0xFFFFFFFFu, cache_b = 0;
+    int s = 0;
+    while (t < t2 && s < NS) {
+        const float x = fmaf(t, dx, ox), y = fmaf(t, dy, oy), z = fmaf(t, dz, oz);
+        const float dt = calc_dt(m, t);
+        int nx, ny, nz;
+        float mip_bound;
+        if (probe<ONE_CASCADE>(m, bitfield, x, y, z, dt, nx, ny, nz, mip_bound, cache_bi, cache_b)) {
+            X[3 * s] = x; X[3 * s + 1] = y; X[3 * s + 2] = z;
+            D[3 * s] = dx; D[3 * s + 1] = dy; D[3 * s + 2] = dz;
+            TS[s] = t;
+            DT[s] = dt;
+            t += dt;
+            hits_t[2 * r] = t;
+            s++;
+        } else {
+            t = skip_voxel(m, t, x, y, z, dx, dy, dz, dxi, dyi, dzi, nx, ny, nz, mip_bound);
+        }
+    }
+    for (int k = s; k < NS; k++) {
+        X[3 * k] = 0.f; X[3 * k + 1] = 0.f; X[3 * k + 2] = 0.f;
+        D[3 * k] = 0.f; D[3 * k + 1] = 0.f; D[3 * k + 2] = 0.f;
+        TS[k] = 0.f;
+        DT[k] = 0.f;
+    }
+    n_eff[n] = s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ray_aabb_intersect (intersection.cu:5-56 + :95-97 sort): one lane per ray, voxels in order,
+// slots sorted stably by t1 (empty slots carry t1 = -1 and therefore sort first, as torch::sort does).
+template <int MAXH>
+__global__ __launch_bounds__(256) void ray_aabb_kernel(const float* __restrict__ rays_o,
+                                                       const float* __restrict__ rays_d, int64_t R,
+                                                       const float* __restrict__ centers,
+                                                       const float* __restrict__ half_sizes, int64_t V, int max_hits,
+                                                       int32_t* __restrict__ hit_cnt, float* __restrict__ hits_t,
+                                                       int64_t* __restrict__ hits_idx) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= R) return;
+    float o[3] = {rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2]};
+    float inv[3] = {1.0f / rays_d[3 * r], 1.0f / rays_d[3 * r + 1], 1.0f / rays_d[3 * r + 2]};
+    float h1[MAXH], h2[MAXH];
+    int64_t hv[MAXH];
+#pragma unroll
+    for (int k = 0; k < MAXH; k++) { h1[k] = -1.0f; h2[k] = -1.0f; hv[k] = -1; }
+    int cnt = 0;
+    for (int64_t v = 0; v < V; v++) {
+        float a1[3], a2[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const float c = centers[3 * v + k], hs = half_sizes[3 * v + k];
+            const float tmin = (c - hs - o[k]) * inv[k];
+            const float tmax = (c + hs - o[k]) * inv[k];
+            a1[k] = fminf(tmin, tmax);
+            a2[k] = fmaxf(tmin, tmax);
+        }
+        float t1 = fmaxf(fmaxf(a1[0], a1[1]), a1[2]);
+        float t2 = fminf(fminf(a2[0], a2[1]), a2[2]);
+        if (t1 > t2) { t1 = -1.0f; t2 = -1.0f; }
+        if (t2 > 0) {
+            if (cnt < max_hits) {
+#pragma unroll
+                for (int k = 0; k < MAXH; k++)
+                    if (k == cnt) { h1[k] = fmaxf(t1, 0.0f); h2[k] = t2; hv[k] = v; }
+            }
+            cnt++;
+        }
+    }
+    // stable insertion sort of the max_hits slots by t1
+    for (int i = 1; i < max_hits; i++) {
+        for (int j = i; j > 0; j--) {
+            if (h1[j - 1] > h1[j]) {
+                float a = h1[j]; h1[j] = h1[j - 1]; h1[j - 1] = a;
+                float b = h2[j]; h2[j] = h2[j - 1]; h2[j - 1] = b;
+                int64_t c = hv[j]; hv[j] = hv[j - 1]; hv[j - 1] = c;
+            } else {
+                break;
+            }
+        }
+    }
+    hit_cnt[r] = cnt;
+    for (int k = 0; k < max_hits; k++) {
+        hits_t[(r * max_hits + k) * 2] = h1[k];
+        hits_t[(r * max_hits + k) * 2 + 1] = h2[k];
+        hits_idx[r * max_hits + k] = hv[k];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Compositing.  One wave per ray segment (rays are independent, the segment is contiguous in the
+// ray-ordered sample arrays).  Each lane owns 4 consecutive samples, so a 256-sample chunk costs
+// one set of loads per lane; the transmittance is a wave-level inclusive product scan of the
+// lane products, carried across chunks.  The early stop (T <= T_threshold, volumerendering.cu:133)
+// is found with a ballot; the stopping sample is composited and counted out (quirk q6).
+constexpr int SPL = 4;  // samples per lane
+constexpr int CHUNK = 64 * SPL;
+
+template <int C>
+struct RendAcc {
+    float v[C];
+};
+
+// volumerendering.cu:97-137
+template <int C>
+__global__ __launch_bounds__(256) void composite_fw_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
+    int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
+    float* __restrict__ rend, float* __restrict__ ws) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= R) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+    float Tc = 1.0f, acc_o = 0.f, acc_d = 0.f;
+    float acc_r[C];
+#pragma unroll
+    for (int i = 0; i < C; i++) acc_r[i] = 0.f;
+    int total = N;
+    bool done = false;
+    for (int base = 0; base < N; base += CHUNK) {
+        const int k0 = base + lane * SPL;
+        if (done) {
+#pragma unroll
+            for (int j = 0; j < SPL; j++)
+                if (k0 + j < N) ws[start + k0 + j] = 0.f;
+            continue;
+        }
+        float a[SPL], om[SPL], tt[SPL], rr[SPL][C];
+        bool valid[SPL];
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            const int64_t s = start + k0 + j;
+            valid[j] = (k0 + j) < N;
+            const float sg = valid[j] ? sigmas[s] : 0.f;
+            const float dl = valid[j] ? deltas[s] : 0.f;
+            tt[j] = valid[j] ? ts[s] : 0.f;
+#pragma unroll
+            for (int i = 0; i < C; i++) rr[j][i] = valid[j] ? raws[s * C + i] : 0.f;
+            a[j] = 1.0f - __expf(-sg * dl);
+            om[j] = 1.0f - a[j];
+        }
+        float lp = om[0];
+#pragma unroll
+        for (int j = 1; j < SPL; j++) lp *= om[j];
+        const float incl = wave_incl_prod(lp, lane);
+        float excl = __shfl_up(incl, 1, 64);
+        if (lane == 0) excl = 1.0f;
+        float T = Tc * excl;
+        float Tb[SPL];
+        int my_stop = SPL;
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            Tb[j] = T;
+            T *= om[j];
+            if (valid[j] && T <= T_thr && my_stop == SPL) my_stop = j;
+        }
+        const uint64_t mask = __ballot(my_stop < SPL);
+        int stop_lane = 64, stop_j = SPL;
+        if (mask) {
+            stop_lane = __builtin_ctzll(mask);
+            stop_j = __shfl(my_stop, stop_lane, 64);
+        }
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            const bool inc = valid[j] && (lane < stop_lane || (lane == stop_lane && j <= stop_j));
+            const float w = inc ? a[j] * Tb[j] : 0.f;
+            if (valid[j]) ws[start + k0 + j] = w;
+#pragma unroll
+            for (int i = 0; i < C; i++) acc_r[i] = fmaf(w, rr[j][i], acc_r[i]);
+            acc_d = fmaf(w, tt[j], acc_d);
+            acc_o += w;
+        }
+        if (mask) {
+            done = true;
+            total = base + stop_lane * SPL + stop_j;
+        }
+        Tc = __shfl(T, 63, 64);
+    }
+    acc_o = wave_sum(acc_o);
+    acc_d = wave_sum(acc_d);
+#pragma unroll
+    for (int i = 0; i < C; i++) acc_r[i] = wave_sum(acc_r[i]);
+    if (lane == 0) {
+        opacity[ray] = acc_o;
+        depth[ray] = acc_d;
+#pragma unroll
+        for (int i = 0; i < C; i++) rend[ray * C + i] = acc_r[i];
+        total_samples[ray] = total;
+    }
+}
+
+// volumerendering.cu:297-364.  T is the post-update transmittance (quirk q10); d/r are inclusive
+// prefix sums of w*t and w*raw; (sum - pre[s]) is the suffix of dL_dws*ws over the WHOLE marched
+// segment (:331-335).  Evaluation order of dL_dsigmas follows :349-359.
+template <int C>
+__global__ __launch_bounds__(256) void composite_bw_kernel(
+    const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
+    const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
+    const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
+    const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
+    float* __restrict__ dL_draws) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= R) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+    const float dO = dL_dopacity ? dL_dopacity[ray] : 0.f;
+    const float dD = dL_ddepth ? dL_ddepth[ray] : 0.f;
+    const float O = opacity[ray], D = depth[ray];
+    float dR[C], RE[C];
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        dR[i] = dL_drend ? dL_drend[ray * C + i] : 0.f;
+        RE[i] = rend[ray * C + i];
+    }
+    // total of dL_dws*ws over the segment
+    float tot = 0.f;
+    if (dL_dws) {
+        for (int k = lane; k < N; k += 64) tot = fmaf(dL_dws[start + k], ws[start + k], tot);
+        tot = wave_sum(tot);
+    }
+    float Tc = 1.0f, cd = 0.f, cpw = 0.f;
+    float cr[C];
+#pragma unroll
+    for (int i = 0; i < C; i++) cr[i] = 0.f;
+    bool done = false;
+    for (int base = 0; base < N; base += CHUNK) {
+        const int k0 = base + lane * SPL;
+        if (done) {
+#pragma unroll
+            for (int j = 0; j < SPL; j++)
+                if (k0 + j < N) {
+                    const int64_t s = start + k0 + j;
+                    dL_dsigmas[s] = 0.f;
+#pragma unroll
+                    for (int i = 0; i < C; i++) dL_draws[s * C + i] = 0.f;
+                }
+            continue;
+        }
+        float a[SPL], om[SPL], tt[SPL], dl[SPL], rr[SPL][C], pw[SPL];
+        bool valid[SPL];
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            const int64_t s = start + k0 + j;
+            valid[j] = (k0 + j) < N;
+            const float sg = valid[j] ? sigmas[s] : 0.f;
+            dl[j] = valid[j] ? deltas[s] : 0.f;
+            tt[j] = valid[j] ? ts[s] : 0.f;
+#pragma unroll
+            for (int i = 0; i < C; i++) rr[j][i] = valid[j] ? raws[s * C + i] : 0.f;
+            pw[j] = (dL_dws && valid[j]) ? dL_dws[s] * ws[s] : 0.f;
+            a[j] = 1.0f - __expf(-sg * dl[j]);
+            om[j] = 1.0f - a[j];
+        }
+        float lp = om[0];
+#pragma unroll
+        for (int j = 1; j < SPL; j++) lp *= om[j];
+        const float inclP = wave_incl_prod(lp, lane);
+        float exclP = __shfl_up(inclP, 1, 64);
+        if (lane == 0) exclP = 1.0f;
+        float T = Tc * exclP;
+        float w[SPL], Ta[SPL];
+        int my_stop = SPL;
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            w[j] = a[j] * T;
+            T *= om[j];
+            Ta[j] = T;
+            if (valid[j] && T <= T_thr && my_stop == SPL) my_stop = j;
+        }
+        const uint64_t mask = __ballot(my_stop < SPL);
+        int stop_lane = 64, stop_j = SPL;
+        if (mask) {
+            stop_lane = __builtin_ctzll(mask);
+            stop_j = __shfl(my_stop, stop_lane, 64);
+        }
+        bool inc[SPL];
+        float ld = 0.f, lpw = 0.f, lr[C];
+#pragma unroll
+        for (int i = 0; i < C; i++) lr[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            inc[j] = valid[j] && (lane < stop_lane || (lane == stop_lane && j <= stop_j));
+            if (!inc[j]) w[j] = 0.f;
+            ld = fmaf(w[j], tt[j], ld);
+#pragma unroll
+            for (int i = 0; i < C; i++) lr[i] = fmaf(w[j], rr[j][i], lr[i]);
+            lpw += pw[j];
+        }
+        // exclusive lane prefixes
+        const float id = wave_incl_sum(ld, lane), ipw = wave_incl_sum(lpw, lane);
+        float ed = __shfl_up(id, 1, 64), epw = __shfl_up(ipw, 1, 64);
+        if (lane == 0) { ed = 0.f; epw = 0.f; }
+        float run_d = cd + ed, run_pw = cpw + epw;
+        float run_r[C], ir[C];
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            ir[i] = wave_incl_sum(lr[i], lane);
+            float er = __shfl_up(ir[i], 1, 64);
+            if (lane == 0) er = 0.f;
+            run_r[i] = cr[i] + er;
+        }
+#pragma unroll
+        for (int j = 0; j < SPL; j++) {
+            run_d = fmaf(w[j], tt[j], run_d);
+            run_pw += pw[j];
+#pragma unroll
+            for (int i = 0; i < C; i++) run_r[i] = fmaf(w[j], rr[j][i], run_r[i]);
+            if (!valid[j]) continue;
+            const int64_t s = start + k0 + j;
+            if (!inc[j]) {
+                dL_dsigmas[s] = 0.f;
+#pragma unroll
+                for (int i = 0; i < C; i++) dL_draws[s * C + i] = 0.f;
+                continue;
+            }
+            const float dws = dL_dws ? dL_dws[s] : 0.f;
+            float g = dO * (1 - O) + dD * (tt[j] * Ta[j] - (D - run_d)) + Ta[j] * dws - (tot - run_pw);
+#pragma unroll
+            for (int i = 0; i < C; i++) {
+                dL_draws[s * C + i] = dR[i] * w[j];
+                g += dR[i] * (rr[j][i] * Ta[j] - (RE[i] - run_r[i]));
+            }
+            dL_dsigmas[s] = g * dl[j];
+        }
+        cd = __shfl(cd + id, 63, 64);
+        cpw = __shfl(cpw + ipw, 63, 64);
+#pragma unroll
+        for (int i = 0; i < C; i++) cr[i] = __shfl(cr[i] + ir[i], 63, 64);
+        if (mask) done = true;
+        Tc = __shfl(T, 63, 64);
+    }
+}
+
+// composite_test_multi_fw (volumerendering.cu:504-550): lane per alive ray, serial (test path).
+__global__ __launch_bounds__(256) void composite_test_kernel(const float* __restrict__ sigmas,
+                                                             const float* __restrict__ raws,
+                                                             const float* __restrict__ deltas,
+                                                             const float* __restrict__ ts, int64_t* __restrict__ alive,
+                                                             int64_t A, int NS, int C, float T_thr,
+                                                             const int32_t* __restrict__ n_eff,
+                                                             float* __restrict__ opacity, float* __restrict__ depth,
+                                                             float* __restrict__ rend) {
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= A) return;
+    if (n_eff[n] == 0) {
+        alive[n] = -1;
+        return;
+    }
+    const int64_t r = alive[n];
+    float T = 1.0f - opacity[r];
+    for (int s = 0; s < n_eff[n]; s++) {
+        const int64_t k = n * (int64_t)NS + s;
+        const float a = 1.0f - __expf(-sigmas[k] * deltas[k]);
+        const float w = a * T;
+        for (int i = 0; i < C; i++) rend[r * C + i] = fmaf(w, raws[k * C + i], rend[r * C + i]);
+        depth[r] = fmaf(w, ts[k], depth[r]);
+        opacity[r] += w;
+        T *= 1.0f - a;
+        if (T <= T_thr) {
+            alive[n] = -1;
+            break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// raymarching.cu:62-70, 90-101, 122-141
+__global__ void morton3D_kernel(const int32_t* __restrict__ c, int64_t n, int32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] = (int32_t)morton3D((uint32_t)c[3 * i], (uint32_t)c[3 * i + 1], (uint32_t)c[3 * i + 2]);
+}
+__global__ void morton3D_invert_kernel(const int32_t* __restrict__ idx, int64_t n, int32_t* __restrict__ c) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int32_t ind = idx[i];
+    c[3 * i + 0] = (int32_t)morton3D_invert((uint32_t)(ind >> 0));
+    c[3 * i + 1] = (int32_t)morton3D_invert((uint32_t)(ind >> 1));
+    c[3 * i + 2] = (int32_t)morton3D_invert((uint32_t)(ind >> 2));
+}
+__global__ void packbits_kernel(const float4* __restrict__ grid, int64_t n_bytes, float thr,
+                                uint8_t* __restrict__ bitfield) {
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= n_bytes) return;
+    const float4 lo = grid[2 * n], hi = grid[2 * n + 1];
+    const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) bits |= (v[i] > thr) ? (1u << i) : 0u;
+    bitfield[n] = (uint8_t)bits;
+}
+
+}  // namespace ncn
+
+using namespace ncn;
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+extern "C" {
+
+int ncn_morton3D(const int32_t* coords, int64_t n, int32_t* out, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(morton3D_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, coords, n, out);
+    NCN_LAUNCH_CHECK("ncn_morton3D");
+    return 0;
+}
+
+int ncn_morton3D_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(morton3D_invert_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, indices, n,
+                       coords);
+    NCN_LAUNCH_CHECK("ncn_morton3D_invert");
+    return 0;
+}
+
+int ncn_packbits(const float* density_grid, int64_t n_bytes, float threshold, uint8_t* bitfield, void* stream) {
+    if (n_bytes <= 0) return 0;
+    NCN_REQUIRE(((uintptr_t)density_grid & 15) == 0, hipErrorInvalidValue, "ncn_packbits: grid must be 16B aligned");
+    hipLaunchKernelGGL(packbits_kernel, dim3(cdiv(n_bytes, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)density_grid, n_bytes, threshold, bitfield);
+    NCN_LAUNCH_CHECK("ncn_packbits");
+    return 0;
+}
+
+int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays, const float* centers,
+                           const float* half_sizes, int64_t n_voxels, int max_hits, int32_t* hit_cnt, float* hits_t,
+                           int64_t* hits_voxel_idx, void* stream) {
+    if (n_rays <= 0) return 0;
+    NCN_REQUIRE(max_hits >= 1 && max_hits <= 16, hipErrorInvalidValue,
+                "ncn_ray_aabb_intersect: max_hits must be in [1,16] (got %d)", max_hits);
+    dim3 g(cdiv(n_rays, 256)), b(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (max_hits == 1)
+        hipLaunchKernelGGL(ray_aabb_kernel<1>, g, b, 0, s, rays_o, rays_d, n_rays, centers, half_sizes, n_voxels,
+                           max_hits, hit_cnt, hits_t, hits_voxel_idx);
+    else if (max_hits <= 4)
+        hipLaunchKernelGGL(ray_aabb_kernel<4>, g, b, 0, s, rays_o, rays_d, n_rays, centers, half_sizes, n_voxels,
+                           max_hits, hit_cnt, hits_t, hits_voxel_idx);
+    else
+        hipLaunchKernelGGL(ray_aabb_kernel<16>, g, b, 0, s, rays_o, rays_d, n_rays, centers, half_sizes, n_voxels,
+                           max_hits, hit_cnt, hits_t, hits_voxel_idx);
+    NCN_LAUNCH_CHECK("ncn_ray_aabb_intersect");
+    return 0;
+}
+
+int ncn_march_train_walk(const float* rays_o, const float* rays_d, const float* hits_t, const float* noise,
+                         int64_t n_rays, const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
+                         int grid_size, int max_samples, int32_t* counts, float* slab_xyz, float* slab_t,
+                         float* slab_dt, void* stream) {
+    if (n_rays <= 0) return 0;
+    NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && grid_size <= 1024 && max_samples >= 1, hipErrorInvalidValue,
+                "ncn_march_train_walk: bad cascades/grid_size/max_samples");
+    dim3 g(cdiv(n_rays, 64)), b(64);
+    if (cascades == 1)
+        hipLaunchKernelGGL(march_train_walk_kernel<true>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, noise,
+                           n_rays, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, counts,
+                           slab_xyz, slab_t, slab_dt);
+    else
+        hipLaunchKernelGGL(march_train_walk_kernel<false>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t,
+                           noise, n_rays, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, counts,
+                           slab_xyz, slab_t, slab_dt);
+    NCN_LAUNCH_CHECK("ncn_march_train_walk");
+    return 0;
+}
+
+int ncn_march_train_scan(const int32_t* counts, int64_t n_rays, int64_t* rays_a, int32_t* counter, void* stream) {
+    hipLaunchKernelGGL(march_train_scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, n_rays, rays_a,
+                       counter);
+    NCN_LAUNCH_CHECK("ncn_march_train_scan");
+    return 0;
+}
+
+int ncn_march_train_pack(const float* rays_d, const int64_t* rays_a, int64_t n_rays, int max_samples,
+                         const float* slab_xyz, const float* slab_t, const float* slab_dt, float* xyzs, float* dirs,
+                         float* deltas, float* ts, void* stream) {
+    if (n_rays <= 0) return 0;
+    hipLaunchKernelGGL(march_train_pack_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, rays_d,
+                       rays_a, n_rays, max_samples, slab_xyz, slab_t, slab_dt, xyzs, dirs, deltas, ts);
+    NCN_LAUNCH_CHECK("ncn_march_train_pack");
+    return 0;
+}
+
+int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive, int64_t n_alive,
+                   const uint8_t* bitfield, int cascades, float scale, float exp_step_factor, int grid_size,
+                   int max_samples, int n_samples, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* n_eff,
+                   void* stream) {
+    if (n_alive <= 0) return 0;
+    NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && n_samples >= 1, hipErrorInvalidValue, "ncn_march_test: bad args");
+    dim3 g(cdiv(n_alive, 64)), b(64);
+    if (cascades == 1)
+        hipLaunchKernelGGL(march_test_kernel<true>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, alive,
+                           n_alive, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, n_samples,
+                           xyzs, dirs, deltas, ts, n_eff);
+    else
+        hipLaunchKernelGGL(march_test_kernel<false>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, alive,
+                           n_alive, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, n_samples,
+                           xyzs, dirs, deltas, ts, n_eff);
+    NCN_LAUNCH_CHECK("ncn_march_test");
+    return 0;
+}
+
+#define NCN_DISPATCH_C(C_RT, KERNEL, ...)                                                       \
+    switch (C_RT) {                                                                            \
+        case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                             \
+        case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                             \
+        case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                             \
+        case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break;                             \
+        default: ncn::set_error("unsupported n_rend=%d (supported: 1,3,4,6)", C_RT);           \
+                 return (int)hipErrorInvalidValue;                                             \
+    }
+
+int ncn_composite_train_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
+                           const int64_t* rays_a, int64_t n_rays, int64_t n_samples, int n_rend, float T_threshold,
+                           int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws,
+                           void* stream) {
+    if (n_rays <= 0) return 0;
+    (void)n_samples;
+    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, sigmas, raws,
+                   deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rend, ws);
+    NCN_LAUNCH_CHECK("ncn_composite_train_fw");
+    return 0;
+}
+
+int ncn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drend,
+                           const float* dL_dws, const float* sigmas, const float* raws, const float* ws,
+                           const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
+                           int64_t n_samples, int n_rend, const float* opacity, const float* depth, const float* rend,
+                           float T_threshold, float* dL_dsigmas, float* dL_draws, void* stream) {
+    if (n_rays <= 0) return 0;
+    (void)n_samples;
+    NCN_DISPATCH_C(n_rend, composite_bw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
+                   dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
+                   T_threshold, dL_dsigmas, dL_draws);
+    NCN_LAUNCH_CHECK("ncn_composite_train_bw");
+    return 0;
+}
+
+int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
+                          int64_t* alive, int64_t n_alive, int n_samples, int n_rend, float T_threshold,
+                          const int32_t* n_eff, float* opacity, float* depth, float* rend, void* stream) {
+    if (n_alive <= 0) return 0;
+    hipLaunchKernelGGL(composite_test_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, sigmas,
+                       raws, deltas, ts, alive, n_alive, n_samples, n_rend, T_threshold, n_eff, opacity, depth, rend);
+    NCN_LAUNCH_CHECK("ncn_composite_test_fw");
+    return 0;
+}
+
+}  // extern "C"

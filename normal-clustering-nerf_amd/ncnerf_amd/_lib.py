@@ -1,0 +1,105 @@
+"""ctypes binding of libncnerf.so (the C ABI declared in include/ncnerf.h).
+
+This is the only place Python talks to the HIP kernels.  There is NO CPU fallback: if the library
+is missing, or a kernel is called with a CPU tensor, the call raises.  Tensors are passed as raw
+device pointers and sizes, on torch's *current* HIP stream (never the legacy default stream).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libncnerf.so")
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+U32 = ctypes.c_uint32
+F32 = ctypes.c_float
+
+# name -> argtypes (stream last); every function returns int (hipError_t)
+SIGNATURES = {
+    "ncn_morton3D": [P, I64, P, P],
+    "ncn_morton3D_invert": [P, I64, P, P],
+    "ncn_packbits": [P, I64, F32, P, P],
+    "ncn_ray_aabb_intersect": [P, P, I64, P, P, I64, I32, P, P, P, P],
+    "ncn_march_train_walk": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, P, P, P, P, P],
+    "ncn_march_train_scan": [P, I64, P, P, P],
+    "ncn_march_train_pack": [P, P, I64, I32, P, P, P, P, P, P, P, P],
+    "ncn_march_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
+    "ncn_composite_train_fw": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, P],
+    "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
+    "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
+    "ncn_field_pack_weights": [P, P, P],
+    "ncn_field_fwd": [P, P, I64, P, P, F32, F32, P, I32, P, P, P, P],
+    "ncn_field_bwd_blocks": [I64],
+    "ncn_field_bwd": [P, P, I64, P, F32, F32, P, P, P, P, P, P, P],
+    "ncn_field_reduce_wgrad": [P, I32, P, P],
+    "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
+    "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P],
+    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, P, P, P],
+    "ncn_sumsq": [P, I64, P, P],
+    "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P],
+}
+
+_lib = None
+
+
+class NcnError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libncnerf.so (after torch's HIP runtime, so both share one libamdhip64)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NcnError(f"libncnerf.so not found at {LIB_PATH}: run __graft_entry__.build() "
+                           f"(make -C normal-clustering-nerf_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        L.ncn_last_error.argtypes = []
+        L.ncn_last_error.restype = ctypes.c_char_p
+        L.ncn_version.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES) + ["ncn_last_error", "ncn_version"]
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().ncn_last_error().decode(errors="replace")
+        raise NcnError(f"{name} failed (hipError {rc}): {msg}")
+    return rc
+
+
+def stream():
+    return P(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    """Raw device pointer of a CUDA tensor (None -> NULL)."""
+    if t is None:
+        return P(None)
+    return P(t.data_ptr())
+
+
+def check_input(t, name):
+    """The reference's CHECK_INPUT (models/csrc/include/utils.h:4-6)."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+def check_dtype(t, dtype, name):
+    if t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {dtype} (got {t.dtype})")

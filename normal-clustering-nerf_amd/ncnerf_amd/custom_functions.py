@@ -1,0 +1,100 @@
+"""autograd.Functions of the reference models/custom_functions.py:8-173, backed by the HIP `vren`.
+
+Same class names, `apply` signatures, outputs and `custom_fwd(cast_inputs=float32)` behaviour.
+"""
+import torch
+from torch.amp import custom_bwd, custom_fwd
+
+from . import vren
+
+
+class RayAABBIntersector(torch.autograd.Function):
+    """custom_functions.py:8-29 -> (hits_cnt (R), hits_t (R,max_hits,2), hits_voxel_idx (R,max_hits))"""
+
+    @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, rays_o, rays_d, center, half_size, max_hits):
+        return tuple(vren.ray_aabb_intersect(rays_o, rays_d, center, half_size, max_hits))
+
+
+class RayMarcher(torch.autograd.Function):
+    """custom_functions.py:55-112.
+
+    forward -> (rays_a, xyzs, dirs, deltas, ts, total_samples).  `noise` is drawn on device as in
+    the reference (custom_functions.py:83); tests may pass an explicit `noise` tensor (quirk q8).
+    backward: dL/drays_o = sum over a ray's samples of dL/dxyzs, dL/drays_d = sum of dL/dxyzs*t +
+    dL/ddirs (the reference's segment_csr, :107-110), accumulated by ray_idx."""
+
+    @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, grid_size,
+                max_samples, noise=None):
+        if noise is None:
+            noise = torch.rand_like(rays_o[:, 0])
+        rays_a, xyzs, dirs, deltas, ts, counter = vren.raymarching_train(
+            rays_o, rays_d, hits_t.contiguous(), density_bitfield, cascades, scale, exp_step_factor, noise.contiguous(),
+            grid_size, max_samples)
+        total_samples = counter[0]
+        ctx.save_for_backward(rays_a, ts)
+        ctx.n_rays = rays_o.shape[0]
+        return rays_a, xyzs, dirs, deltas, ts, total_samples
+
+    @staticmethod
+    @custom_bwd(device_type="cuda")
+    def backward(ctx, dL_drays_a, dL_dxyzs, dL_ddirs, dL_ddeltas, dL_dts, dL_dtotal_samples):
+        rays_a, ts = ctx.saved_tensors
+        seg = torch.repeat_interleave(rays_a[:, 0], rays_a[:, 2])
+        dev, R = ts.device, ctx.n_rays
+        dL_drays_o = torch.zeros(R, 3, device=dev)
+        dL_drays_d = torch.zeros(R, 3, device=dev)
+        if dL_dxyzs is not None:
+            dL_drays_o.index_add_(0, seg, dL_dxyzs)
+            dL_drays_d.index_add_(0, seg, dL_dxyzs * ts[:, None])
+        if dL_ddirs is not None:
+            dL_drays_d.index_add_(0, seg, dL_ddirs)
+        return dL_drays_o, dL_drays_d, None, None, None, None, None, None, None, None
+
+
+class VolumeRenderer(torch.autograd.Function):
+    """custom_functions.py:115-159 -> (total_samples (scalar), opacity, depth, rend, ws).
+
+    Unused output gradients arrive as None (set_materialize_grads(False)) and are passed to the
+    kernel as NULL instead of zero tensors — numerically identical to the reference, which
+    receives materialised zeros."""
+
+    @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold):
+        sigmas = sigmas.contiguous(); raws = raws.contiguous()
+        total_samples, opacity, depth, rend, ws = vren.composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a,
+                                                                                  T_threshold)
+        ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
+        ctx.T_threshold = T_threshold
+        ctx.set_materialize_grads(False)
+        return total_samples.sum(), opacity, depth, rend, ws
+
+    @staticmethod
+    @custom_bwd(device_type="cuda")
+    def backward(ctx, dL_dtotal_samples, dL_dopacity, dL_ddepth, dL_drend, dL_dws):
+        sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws = ctx.saved_tensors
+        c = lambda t: None if t is None else t.contiguous().float()
+        dL_dsigmas, dL_draws = vren.composite_train_multi_bw(c(dL_dopacity), c(dL_ddepth), c(dL_drend), c(dL_dws),
+                                                             sigmas, raws, ws, deltas, ts, rays_a, opacity, depth,
+                                                             rend, ctx.T_threshold)
+        return dL_dsigmas, dL_draws, None, None, None, None
+
+
+class TruncExp(torch.autograd.Function):
+    """custom_functions.py:162-173 (the field kernel fuses this; kept for API parity)."""
+
+    @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.exp(x)
+
+    @staticmethod
+    @custom_bwd(device_type="cuda")
+    def backward(ctx, dL_dout):
+        x = ctx.saved_tensors[0]
+        return dL_dout * torch.exp(x.clamp(-15, 15))

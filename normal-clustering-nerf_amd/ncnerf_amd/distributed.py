@@ -1,0 +1,43 @@
+"""Data parallelism of the reference (PL DDPPlugin, train_nerf.py:944-952) on torch.distributed.
+
+One process per GPU; backend "nccl" is RCCL on ROCm (xGMI).  Every rank draws its own ray batch
+(weak scaling, 8192 rays per rank as in the reference, base.py:94-171); the only data-path exchange
+is ONE all-reduce of the flat gradient buffer (hash table + MLPs, ~45.7 MB fp32) per step, averaged
+over ranks.  The occupancy grid is kept identical on every rank by broadcasting rank 0's density
+grid + bitfield after each refresh (the reference relies on DDP buffer broadcast).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """Initialise the default process group from RANK/WORLD_SIZE/MASTER_* (torchrun) if present."""
+    if "WORLD_SIZE" not in os.environ or int(os.environ["WORLD_SIZE"]) <= 1:
+        return 0, 1
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend)
+    return dist.get_rank(), dist.get_world_size()
+
+
+def allreduce_grads(flat_grad):
+    """Average the flat gradient over ranks (single bucket: the buffer is contiguous)."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
+        flat_grad.div_(dist.get_world_size())
+
+
+def broadcast_occupancy(model, src=0):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        if hasattr(model, "density_grid"):
+            dist.broadcast(model.density_grid, src)
+        dist.broadcast(model.density_bitfield, src)
+
+
+def shard_patches(n_patches_global, rank, world):
+    """Patch-granular shard [lo, hi) of a global batch (never splits an 8x8 patch)."""
+    per = n_patches_global // world
+    return rank * per, (rank + 1) * per

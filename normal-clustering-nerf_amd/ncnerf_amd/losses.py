@@ -1,0 +1,219 @@
+"""NeRFMTLoss of the reference losses.py:169-587 for the training hot path.
+
+Kept: the photometric MSE (losses.py:349-355), opacity entropy (:358-362), depth L2 (:372-385),
+normals-from-depth vs GT normals L1/dot (:388-411), RegNeRF depth smoothness (:414-418) and the
+normal-clustering block (:420-509) with its weight schedule (:217) and validity filter (:246-262).
+The clustering block runs on the GPU end to end: `_extract_normals_from_ray_batch`
+(hypersim_src/utils.py:504-541) is `ncn_normals_fwd/bwd`, and faiss k-means + the cluster selection
++ the three cluster losses + their gradient are ONE workgroup kernel (`ncn_cluster_loss`), so the
+step no longer copies normals to the host (losses.py:434) or syncs on `.item()`s.
+
+The k-means is a deterministic spherical Lloyd k-means (stratified seeded init, faiss-style
+empty-cluster split); faiss itself is not available and unpinned, see DESIGN.md.
+
+Not provided (weight 0 in every reference config, hyperparameters.py:33-49): distortion, semantic,
+Manhattan-NeRF and the canonical-direction terms (raise if enabled).
+"""
+import einops
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+from ._lib import F32, I32, I64, U32, call, check_input, ptr, stream
+
+
+class _Normals(torch.autograd.Function):
+    """hypersim_src/utils.py:504-541: n = normalize(cross(P2-P1, P3-P1)), P = rays_o + rays_d*depth."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, depth, x1, x2, x3):
+        T = x1.shape[0]
+        normals = torch.empty(T, 3, dtype=torch.float32, device=depth.device)
+        call("ncn_normals_fwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals),
+             stream())
+        ctx.save_for_backward(rays_o, rays_d, depth, x1, x2, x3)
+        return normals
+
+    @staticmethod
+    def backward(ctx, dn):
+        rays_o, rays_d, depth, x1, x2, x3 = ctx.saved_tensors
+        ddepth = torch.zeros_like(depth)
+        if dn is not None:
+            call("ncn_normals_bwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(x1.shape[0]),
+                 ptr(dn.contiguous()), ptr(ddepth), stream())
+        return None, None, ddepth, None, None, None
+
+
+def extract_normals_from_ray_batch(rays_o, rays_d, depth, x123_idx):
+    """Drop-in for datasets/hypersim_src/utils.py:_extract_normals_from_ray_batch (fp32)."""
+    f = lambda t: t.float().contiguous()
+    idx = lambda t: t.long().contiguous()
+    for t, n in ((rays_o, "rays_o"), (rays_d, "rays_d"), (depth, "depth")):
+        if not t.is_cuda:
+            raise RuntimeError(f"{n} must be a CUDA tensor")
+    return _Normals.apply(f(rays_o), f(rays_d), f(depth), idx(x123_idx["x1"]), idx(x123_idx["x2"]),
+                          idx(x123_idx["x3"]))
+
+
+class _ClusterLoss(torch.autograd.Function):
+    """losses.py:420-478 on the GPU.  Returns the three weighted terms (ort, centr_dot, centr_L1)
+    and, as non-differentiable extras, the labels and the k-means centroids."""
+
+    @staticmethod
+    def forward(ctx, normals, K, niter, seed, t_sim, w):
+        T = normals.shape[0]
+        dev = normals.device
+        out = torch.empty(4, dtype=torch.float32, device=dev)
+        labels = torch.empty(T, dtype=torch.int32, device=dev)
+        cents = torch.zeros(K, 3, dtype=torch.float32, device=dev)
+        dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]), F32(w[1]),
+             F32(w[2]), ptr(out), ptr(labels), ptr(cents), ptr(dn), stream())
+        ctx.save_for_backward(dn)
+        ctx.mark_non_differentiable(labels, cents, out)
+        wt = torch.tensor(w, dtype=torch.float32, device=dev)
+        return out[:3] * wt, labels, cents, out
+
+    @staticmethod
+    def backward(ctx, g, _g_labels, _g_cents, _g_out):
+        (dn,) = ctx.saved_tensors
+        if g is None:
+            return None, None, None, None, None, None
+        return torch.einsum("q,qtc->tc", g.float(), dn), None, None, None, None, None
+
+
+def cluster_losses(norm_depth, K=20, niter=20, seed=1234, t_similar=0.99, w=(1.0, 1.0, 1.0)):
+    """Weighted (ort, centr_dot, centr_L1) terms, labels (+-1..3, 0, -9 invalid), centroids, raw stats."""
+    check_input(norm_depth, "norm_depth")
+    return _ClusterLoss.apply(norm_depth, K, niter, seed, t_similar, tuple(float(x) for x in w))
+
+
+class NeRFMTLoss(nn.Module):
+    """losses.py:169-587 (hot-path subset, see module docstring)."""
+
+    def __init__(self, hparams_dict):
+        super().__init__()
+        h = hparams_dict
+        self.opacity_w = h.get("loss_opacity_w", 0)
+        self.distortion_w = h.get("loss_distortion_w", 0)
+        self.depth_w = h.get("loss_depth_w", 0)
+        self.sem_w = h.get("loss_sem_w", 0)
+        self.manhattan_nerf_w = h.get("loss_manhattan_nerf_w", 0)
+        self.norm_DEpth_L1_w = h.get("loss_norm_depth_L1_w", 0)
+        self.norm_DEpth_dot_w = h.get("loss_norm_depth_dot_w", 0)
+        self.norm_CAN_tres = h.get("loss_norm_can_tres", 0)
+        self.norm_D_C_ort_dot_w = h.get("loss_norm_D_C_ort_dot_w", 0)
+        self.norm_D_C_centr_dot_w = h.get("loss_norm_D_C_centr_dot_w", 0)
+        self.norm_D_C_centr_L1_w = h.get("loss_norm_D_C_centr_L1_w", 0)
+        self.norm_D_C_can_dot_w = h.get("loss_norm_D_C_can_dot_w", 0)
+        self.norm_D_C_can_L1_w = h.get("loss_norm_D_C_can_L1_w", 0)
+        self.reg_depth_w = h.get("loss_reg_depth_w", 0)
+        self.ray_sampling_strategy = h.get("ray_sampling_strategy", None)
+        self.random_tr_poses = h.get("random_tr_poses", False)
+        self.pred_norm_depth = h.get("pred_norm_depth", False)
+        self.kmeans_seed = h.get("kmeans_seed", 1234)
+        for name in ("distortion_w", "sem_w", "manhattan_nerf_w", "norm_D_C_can_dot_w", "norm_D_C_can_L1_w"):
+            if getattr(self, name) > 0:
+                raise NotImplementedError(f"loss term {name} is not part of the ported hot path (0 in all configs)")
+        if self.norm_DEpth_L1_w > 0 or self.norm_DEpth_dot_w > 0:
+            self.norm_GT = "normals_depth" if h.get("loss_norm_GT_depth", False) else "normals"
+        start = h.get("loss_norm_can_start", 0)
+        self.can_sched_start = start
+        self.can_sched_end = h.get("loss_norm_can_end", -1)
+        grow = h.get("loss_norm_can_grow", 1)
+        self.w_sched = lambda w, step: max(0, min(w, (step - start) * (w / grow)))  # losses.py:217
+        self.L1_norm = lambda x, y: ((torch.abs(x - y)).sum(-1)).mean()
+        self.dot_prod = lambda x, y: (1.0 - torch.nn.CosineSimilarity(dim=-1)(x, y)).mean()
+        if self.pred_norm_depth:
+            assert self.ray_sampling_strategy in ["all_images_triang", "all_images_triang_val", "same_image_triang",
+                                                  "all_images_triang_patch", "same_image_triang_patch"]
+        self.last_cluster = None  # (labels, centroids, raw stats) of the last step, for logging/tests
+
+    @staticmethod
+    def _validity(loss, dev):
+        """losses.py:246-262 without host syncs: non-finite -> 0."""
+        if loss.nelement() != 1:
+            return torch.tensor(0.0, device=dev)
+        return torch.where(torch.isfinite(loss), loss, torch.zeros_like(loss))
+
+    def forward(self, pred_raw, target_raw, **kwargs):
+        pred_w_gt, target_gt, pred_unsup = {}, {}, {}
+        gt_l = target_raw["rgb"].shape[0]
+        for k in ("rgb", "depth", "normals", "normals_depth"):
+            if k in target_raw:
+                target_gt[k] = target_raw[k]
+        pred_w_gt["rgb"] = pred_raw["rgb"][:gt_l]
+        pred_w_gt["depth"] = pred_raw["depth"][:gt_l]
+        pred_w_gt["rays_o"] = pred_raw["rays_o"][:gt_l]
+        pred_w_gt["rays_d"] = pred_raw["rays_d"][:gt_l]
+        unsup_start = gt_l if self.random_tr_poses else 0
+        pred_unsup["opacity"] = pred_raw["opacity"]
+        pred_unsup["depth"] = pred_raw["depth"][unsup_start:]
+        pred_unsup["rays_o"] = pred_raw["rays_o"][unsup_start:]
+        pred_unsup["rays_d"] = pred_raw["rays_d"][unsup_start:]
+        dev = pred_raw["rgb"].device
+
+        def get_triang_idx(seq_len):
+            pix = einops.rearrange(torch.arange(0, seq_len, device=dev), "(n s) -> n s", s=3)
+            return {"x1": pix[:, 0], "x2": pix[:, 1], "x3": pix[:, 2]}
+
+        def get_patch_triang_idx(seq_len, patch_s, off):
+            pix = einops.rearrange(torch.arange(0, seq_len, device=dev), "(n s) -> n s", s=patch_s)
+            return {k: einops.rearrange(pix[:, torch.as_tensor(off[k], device=dev)], "n s -> (n s)")
+                    for k in ("x1", "x2", "x3")}
+
+        n_unsup, n_w_gt = pred_unsup["depth"].shape[0], pred_w_gt["rgb"].shape[0]
+        if self.ray_sampling_strategy in ["all_images_triang", "same_image_triang"]:
+            pred_w_gt["x123_idx"] = get_triang_idx(n_w_gt)
+            pred_unsup["x123_idx"] = get_triang_idx(n_unsup)
+        elif self.ray_sampling_strategy in ["all_images_triang_patch", "same_image_triang_patch"]:
+            off = {"x1": target_raw["x1_offsets_local"], "x2": target_raw["x2_offsets_local"],
+                   "x3": target_raw["x3_offsets_local"]}
+            pred_w_gt["x123_idx"] = get_patch_triang_idx(n_w_gt, target_raw["patch_area"], off)
+            pred_unsup["x123_idx"] = get_patch_triang_idx(n_unsup, target_raw["patch_area"], off)
+        if self.pred_norm_depth:
+            pred_w_gt["norm_depth"] = extract_normals_from_ray_batch(pred_w_gt["rays_o"], pred_w_gt["rays_d"],
+                                                                     pred_w_gt["depth"], pred_w_gt["x123_idx"])
+            if unsup_start == 0:
+                pred_unsup["norm_depth"] = pred_w_gt["norm_depth"]
+            else:
+                pred_unsup["norm_depth"] = extract_normals_from_ray_batch(pred_unsup["rays_o"], pred_unsup["rays_d"],
+                                                                          pred_unsup["depth"], pred_unsup["x123_idx"])
+        loss_d = {}
+        rgb_loss = ((pred_w_gt["rgb"] - target_gt["rgb"]) ** 2).mean()
+        loss_d["rgb"] = self._validity(rgb_loss, dev)
+        if self.opacity_w > 0:
+            o = pred_unsup["opacity"] + 1e-10
+            loss_d["opacity"] = self._validity(self.opacity_w * (-o * torch.log(o)).mean(), dev)
+        if self.depth_w > 0:
+            d_pred, d_tgt = pred_w_gt["depth"], target_gt["depth"]
+            valid = d_tgt > 0
+            loss_d["depth"] = self._validity(self.depth_w * ((d_pred[valid] - d_tgt[valid]) ** 2).mean(), dev)
+        if self.norm_DEpth_L1_w > 0 or self.norm_DEpth_dot_w > 0:
+            nd = pred_w_gt["norm_depth"]
+            tgt = target_gt[self.norm_GT][pred_w_gt["x123_idx"]["x1"]]
+            valid = tgt.abs().sum(-1) > 0
+            if self.norm_DEpth_L1_w > 0:
+                loss_d["norm_D_L1"] = self._validity(self.norm_DEpth_L1_w * self.L1_norm(nd[valid], tgt[valid]), dev)
+            if self.norm_DEpth_dot_w > 0:
+                loss_d["norm_D_dot"] = self._validity(self.norm_DEpth_dot_w * self.dot_prod(nd[valid], tgt[valid]),
+                                                      dev)
+        if self.reg_depth_w > 0 and kwargs["global_step"] > self.can_sched_start:
+            d_pred, x = pred_unsup["depth"], pred_unsup["x123_idx"]
+            reg = ((d_pred[x["x1"]] - d_pred[x["x2"]]) ** 2 + (d_pred[x["x1"]] - d_pred[x["x3"]]) ** 2).mean()
+            loss_d["reg_depth"] = self._validity(reg, dev)
+        if self.norm_D_C_ort_dot_w > 0 or self.norm_D_C_centr_dot_w > 0 or self.norm_D_C_centr_L1_w > 0:
+            step = kwargs["global_step"]
+            if step <= self.can_sched_end or self.can_sched_end == -1:
+                w = (self.w_sched(self.norm_D_C_ort_dot_w, step), self.w_sched(self.norm_D_C_centr_dot_w, step),
+                     self.w_sched(self.norm_D_C_centr_L1_w, step))
+                terms, labels, cents, raw = cluster_losses(pred_unsup["norm_depth"], K=20, niter=20,
+                                                           seed=self.kmeans_seed,
+                                                           t_similar=1.0 - self.norm_CAN_tres, w=w)
+                loss_d["norm_D_C_ort_dot"] = terms[0]
+                loss_d["norm_D_C_centr_dot"] = terms[1]
+                loss_d["norm_D_C_centr_L1"] = terms[2]
+                self.last_cluster = (labels, cents, raw)
+        loss_d["total"] = sum(lo for lo in loss_d.values())
+        return loss_d

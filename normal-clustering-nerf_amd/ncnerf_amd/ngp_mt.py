@@ -1,0 +1,311 @@
+"""NGPMT field of the reference models/ngp_mt.py:10-368 on the fused gfx950 kernels.
+
+Surface kept: `NGPMT(scale, grid_size, rgb_act='Sigmoid', pred_sem=False, pred_norm=False, **kw)`,
+attributes read by render() (center, half_size, density_bitfield, cascades, scale, grid_size,
+pred_norm, pred_sem), `forward(x, d) -> {'sigmas', 'rgbs'}`, `density(x, return_feat)`, and the
+occupancy-grid maintenance (get_all_cells, sample_uniform_and_occupied_cells,
+update_density_grid, mark_invisible_cells).  Parameter names keep tcnn's `<module>.params`
+(xyz_encoder.params / sigma_net.params / rgb_net.params) so the reference's optimizer grouping
+('xyz_encoder' in name -> no weight decay, train_nerf.py:262-274) applies unchanged.
+
+Memory layout (MI355X): all parameters live in ONE flat fp32 buffer
+  [hash table (n_entries x 2) | W1 (64,32) | W2 (16,64) | W3 (64,19) | W4 (64,64) | W5 (3,64)]
+and their gradients in a second flat buffer of the same layout, so the gradient all-reduce is a
+single RCCL call and the optimizer a single pass.  The backward accumulates straight into
+`param.grad` (views of the flat gradient buffer): hash-table gradients by f32 atomics, weight
+gradients through a fixed-order slab reduction.
+
+Not provided (off in every reference config, hyperparameters.py:26-30): pred_sem / pred_norm heads,
+rgb_act='None' exposure tonemappers.
+"""
+import math
+
+import numpy as np
+import torch
+from einops import rearrange
+from torch import nn
+
+from . import _lib, vren
+from ._lib import I32, I64, F32, call, ptr, stream
+
+L_LEVELS, F_PER_LEVEL, LOG2_T, N_MIN = 16, 2, 19, 16  # ngp_mt.py:40
+N_W = 64 * 32 + 16 * 64 + 64 * 19 + 64 * 64 + 3 * 64  # NCN_FIELD_NW
+N_PACKED_HALVES = 19456  # NCN_FIELD_PACKED_HALVES
+ENC_BYTES = 64  # NCN_ENC_BYTES_PER_SAMPLE
+W_SIGMA = 64 * 32 + 16 * 64
+W_RGB = N_W - W_SIGMA
+
+
+def grid_levels(scale, n_levels=L_LEVELS, log2_T=LOG2_T, n_min=N_MIN):
+    """Per-level tcnn geometry: b = exp(ln(2048*scale/N_min)/(L-1)) (ngp_mt.py:41);
+    grid_scale = exp2(l*log2(b))*N_min - 1 (fp32), resolution = ceil(scale)+1,
+    params = min(next_multiple(res^3, 8), 2^log2_T).  Returns (levels, n_entries)."""
+    b = math.exp(math.log(2048 * scale / n_min) / (n_levels - 1))
+    log2_pls = np.float32(np.log2(np.float32(b)))
+    levels, offset = [], 0
+    for l in range(n_levels):
+        s = np.float32(np.float32(np.exp2(np.float32(l) * log2_pls)) * np.float32(n_min) - np.float32(1.0))
+        res = int(math.ceil(float(s))) + 1
+        params = min(((res ** 3 + 7) // 8) * 8, 1 << log2_T)
+        levels.append(dict(scale=float(s), res=res, params=params, offset=offset))
+        offset += params
+    return levels, offset
+
+
+def level_words(levels):
+    """16 x {scale f32 bits, res, params, offset} as a host uint32 array (the C ABI `levels`)."""
+    w = np.zeros(64, np.uint32)
+    for l, lv in enumerate(levels):
+        w[4 * l] = np.frombuffer(np.float32(lv["scale"]).tobytes(), np.uint32)[0]
+        w[4 * l + 1], w[4 * l + 2], w[4 * l + 3] = lv["res"], lv["params"], lv["offset"]
+    return w
+
+
+class _ParamHolder(nn.Module):
+    """Stands in for a tcnn module: exposes `.params` (a view of the model's flat buffer)."""
+
+    def __init__(self, flat_view):
+        super().__init__()
+        self.params = nn.Parameter(flat_view)
+
+
+class _FieldFunction(torch.autograd.Function):
+    """Fused hash-grid + sigma_net + TruncExp + rgb_net (ncn_field_fwd / ncn_field_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, d, table, w_sigma, w_rgb, model, mode):
+        n = x.shape[0]
+        dev = x.device
+        need_grad = any(ctx.needs_input_grad[2:5])  # grad mode is off inside Function.forward
+        sigmas = torch.empty(n, dtype=torch.float32, device=dev)
+        rgbs = torch.empty(n, 3, dtype=torch.float32, device=dev) if mode == 0 else sigmas.new_empty(0, 3)
+        enc = None
+        if need_grad:
+            enc = torch.empty(((n + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev)
+        packed = model._pack_weights()
+        call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(table), model._levels_ptr,
+             F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(mode), ptr(sigmas),
+             ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
+        if need_grad:
+            ctx.save_for_backward(x, d, enc, packed)
+            ctx.model = model
+        if mode != 0:
+            ctx.mark_non_differentiable(rgbs)
+        ctx.set_materialize_grads(False)
+        return sigmas, rgbs
+
+    @staticmethod
+    def backward(ctx, dL_dsigmas, dL_drgbs):
+        x, d, enc, packed = ctx.saved_tensors
+        model = ctx.model
+        n = x.shape[0]
+        g_table, g_w = model._grad_views()
+        nb = _lib.lib().ncn_field_bwd_blocks(I64(n))
+        slab = torch.empty(nb * N_W, dtype=torch.float32, device=x.device)
+        c = lambda t: None if t is None else t.contiguous().float()
+        dsig, drgb = c(dL_dsigmas), c(dL_drgbs)
+        call("ncn_field_bwd", ptr(x), ptr(d), I64(n), model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent),
+             ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), stream())
+        call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
+        return None, None, None, None, None, None, None
+
+
+class NGPMT(nn.Module):
+    def __init__(self, scale, grid_size, rgb_act="Sigmoid", pred_sem=False, pred_norm=False, seed=1337, **kwargs):
+        super().__init__()
+        if rgb_act != "Sigmoid":
+            raise NotImplementedError("rgb_act='None' (exposure tonemappers) is off in every reference config")
+        if pred_sem or pred_norm:
+            raise NotImplementedError("pred_sem / pred_norm heads are off in every reference config")
+        self.pred_sem, self.pred_norm, self.rgb_act = pred_sem, pred_norm, rgb_act
+        self.scale = scale
+        self.register_buffer("center", torch.zeros(1, 3))
+        self.register_buffer("xyz_min", -torch.ones(1, 3) * scale)
+        self.register_buffer("xyz_max", torch.ones(1, 3) * scale)
+        self.register_buffer("half_size", (self.xyz_max - self.xyz_min) / 2)
+        self.cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)  # ngp_mt.py:34
+        self.grid_size = grid_size
+        self.register_buffer("density_bitfield", torch.zeros(self.cascades * grid_size ** 3 // 8, dtype=torch.uint8))
+        self.levels, self.n_entries = grid_levels(scale)
+        self._level_words = level_words(self.levels)
+        self._levels_ptr = self._level_words.ctypes.data_as(_lib.P)
+        self._xyz_min = float(np.float32(-scale))
+        self._xyz_extent = float(np.float32(scale) - np.float32(-scale))
+        n_table = self.n_entries * F_PER_LEVEL
+        self._n_table = n_table
+        flat = torch.zeros(n_table + N_W)
+        g = torch.Generator().manual_seed(seed)
+        flat[:n_table] = (torch.rand(n_table, generator=g) * 2 - 1) * 1e-4  # tcnn grid init U(-1e-4, 1e-4)
+        off = n_table
+        for o, i in ((64, 32), (16, 64), (64, 19), (64, 64), (3, 64)):  # Xavier-uniform MLP weights
+            a = math.sqrt(6.0 / (o + i))
+            flat[off:off + o * i] = (torch.rand(o * i, generator=g) * 2 - 1) * a
+            off += o * i
+        self._flat = flat
+        self.xyz_encoder = _ParamHolder(flat[:n_table])
+        self.sigma_net = _ParamHolder(flat[n_table:n_table + W_SIGMA])
+        self.rgb_net = _ParamHolder(flat[n_table + W_SIGMA:])
+        self._flat_grad = None
+        self._packed = None
+
+    # -- flat buffers --------------------------------------------------------------------------
+    def _apply(self, fn, recurse=True):
+        # keep the three parameters as views of one flat buffer across .to()/.cuda()
+        super()._apply(fn, recurse)
+        flat = fn(self._flat)
+        n_table = self._n_table
+        flat[:n_table].copy_(self.xyz_encoder.params.data)
+        flat[n_table:n_table + W_SIGMA].copy_(self.sigma_net.params.data)
+        flat[n_table + W_SIGMA:].copy_(self.rgb_net.params.data)
+        self._flat = flat
+        self.xyz_encoder.params.data = flat[:n_table]
+        self.sigma_net.params.data = flat[n_table:n_table + W_SIGMA]
+        self.rgb_net.params.data = flat[n_table + W_SIGMA:]
+        self._flat_grad = None
+        self._packed = None
+        return self
+
+    def flat_params(self):
+        return self._flat
+
+    def flat_grad(self):
+        """The flat gradient buffer; every parameter's .grad is a view of it."""
+        self._grad_views()
+        return self._flat_grad
+
+    def _grad_views(self):
+        ps = (self.xyz_encoder.params, self.sigma_net.params, self.rgb_net.params)
+        if self._flat_grad is None or self._flat_grad.device != self._flat.device:
+            self._flat_grad = torch.zeros_like(self._flat)
+        fg, n_table = self._flat_grad, self._n_table
+        views = (fg[:n_table], fg[n_table:n_table + W_SIGMA], fg[n_table + W_SIGMA:])
+        for p, v in zip(ps, views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                else:
+                    v.zero_()
+                p.grad = v
+        return fg[:n_table], fg[n_table:]
+
+    def _pack_weights(self):
+        if self._packed is None or self._packed.device != self._flat.device:
+            self._packed = torch.empty(N_PACKED_HALVES, dtype=torch.float16, device=self._flat.device)
+        call("ncn_field_pack_weights", ptr(self._flat[self._n_table:]), ptr(self._packed), stream())
+        return self._packed
+
+    # -- field -----------------------------------------------------------------------------------
+    def density(self, x, return_feat=False):
+        """ngp_mt.py:157-171 (density-only kernel mode)."""
+        if return_feat:
+            raise NotImplementedError("return_feat (the 16-d sigma_net feature) is only needed by the "
+                                      "pred_sem/pred_norm heads, which are not provided")
+        _lib.check_input(x, "x")
+        sigmas, _ = _FieldFunction.apply(x.float().contiguous(), None, self.xyz_encoder.params,
+                                         self.sigma_net.params, self.rgb_net.params, self, 1)
+        return sigmas
+
+    def forward(self, x, d, **kwargs):
+        """ngp_mt.py:196-229 -> {'sigmas': (N,), 'rgbs': (N,3)} (fp32)."""
+        x = x.float().contiguous()
+        d = d.float().contiguous()
+        _lib.check_input(x, "x")
+        _lib.check_input(d, "d")
+        sigmas, rgbs = _FieldFunction.apply(x, d, self.xyz_encoder.params, self.sigma_net.params,
+                                            self.rgb_net.params, self, 0)
+        return {"sigmas": sigmas, "rgbs": rgbs}
+
+    # -- occupancy grid maintenance (ngp_mt.py:231-368) --------------------------------------------
+    @torch.no_grad()
+    def get_all_cells(self):
+        indices = vren.morton3D(self.grid_coords).long()
+        return [(indices, self.grid_coords)] * self.cascades
+
+    @torch.no_grad()
+    def sample_uniform_and_occupied_cells(self, M, density_threshold):
+        cells = []
+        for c in range(self.cascades):
+            coords1 = torch.randint(self.grid_size, (M, 3), dtype=torch.int32, device=self.density_grid.device)
+            indices1 = vren.morton3D(coords1).long()
+            indices2 = torch.nonzero(self.density_grid[c] > density_threshold)[:, 0]
+            if len(indices2) > 0:
+                rand_idx = torch.randint(len(indices2), (M,), device=self.density_grid.device)
+                indices2 = indices2[rand_idx]
+            coords2 = vren.morton3D_invert(indices2.int().contiguous())
+            cells += [(torch.cat([indices1, indices2]), torch.cat([coords1, coords2]))]
+        return cells
+
+    @torch.no_grad()
+    def mark_invisible_cells(self, K, dev, poses, img_wh, near_distance, chunk=64 ** 3):
+        """ngp_mt.py:274-337 (pinhole K (3,3) tensor branch and the Hypersim NDC tuple branch)."""
+        N_cams = poses.shape[0]
+        self.count_grid = torch.zeros_like(self.density_grid)
+        w2c_R = rearrange(poses[:, :3, :3], "n a b -> n b a")
+        w2c_T = -w2c_R @ poses[:, :3, 3:]
+        cells = self.get_all_cells()
+        if isinstance(K, torch.Tensor):
+            K = K.to(dev)
+        elif isinstance(K, tuple):
+            M_ndc_from_cam, M_uv_from_ndc = K[0].to(dev), K[1].to(dev)
+            k_scale = K[3]
+        else:
+            raise AssertionError
+        for c in range(self.cascades):
+            indices, coords = cells[c]
+            for i in range(0, len(indices), chunk):
+                xyzs = coords[i:i + chunk] / (self.grid_size - 1) * 2 - 1
+                s = min(2 ** (c - 1), self.scale)
+                half_grid_size = s / self.grid_size
+                xyzs_w = (xyzs * (s - half_grid_size)).T
+                xyzs_c = w2c_R @ xyzs_w + w2c_T
+                if isinstance(K, torch.Tensor):
+                    uvd = K @ xyzs_c
+                    uv = uvd[:, :2] / uvd[:, 2:]
+                else:
+                    xyzs_c *= 2 * k_scale
+                    xyzs_c = torch.cat((xyzs_c, torch.ones_like(xyzs_c)[:, :1, :]), 1)
+                    xyz_clip = M_ndc_from_cam @ xyzs_c
+                    xyz_ndc = xyz_clip / xyz_clip[:, 3:]
+                    uvd = M_uv_from_ndc @ xyz_ndc
+                    uv = uvd[:, :2]
+                in_image = (uvd[:, 2] >= 0) & (uv[:, 0] >= 0) & (uv[:, 0] < img_wh[0]) & (uv[:, 1] >= 0) & \
+                           (uv[:, 1] < img_wh[1])
+                covered_by_cam = (uvd[:, 2] >= near_distance) & in_image
+                self.count_grid[c, indices[i:i + chunk]] = count = covered_by_cam.sum(0) / N_cams
+                too_near_to_cam = (uvd[:, 2] < near_distance) & in_image
+                valid_mask = (count > 0) & (~too_near_to_cam.any(0))
+                self.density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
+
+    @torch.no_grad()
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):
+        """ngp_mt.py:340-368.  Quirk q12: with no cell > 0 the mean is NaN and packbits, comparing
+        against NaN, clears the bitfield — reproduced."""
+        density_grid_tmp = torch.zeros_like(self.density_grid)
+        if warmup:
+            cells = self.get_all_cells()
+        else:
+            cells = self.sample_uniform_and_occupied_cells(self.grid_size ** 3 // 4, density_threshold)
+        for c in range(self.cascades):
+            indices, coords = cells[c]
+            s = min(2 ** (c - 1), self.scale)
+            half_grid_size = s / self.grid_size
+            xyzs_w = (coords / (self.grid_size - 1) * 2 - 1) * (s - half_grid_size)
+            xyzs_w += (torch.rand_like(xyzs_w) * 2 - 1) * half_grid_size
+            density_grid_tmp[c, indices] = self.density(xyzs_w.contiguous())
+        if erode:
+            decay = torch.clamp(decay ** (1 / self.count_grid), 0.1, 0.95)
+        self.density_grid = torch.where(self.density_grid < 0, self.density_grid,
+                                        torch.maximum(self.density_grid * decay, density_grid_tmp))
+        mean_density = self.density_grid[self.density_grid > 0].mean().item()
+        vren.packbits(self.density_grid.contiguous(), min(mean_density, density_threshold), self.density_bitfield)
+
+
+def register_grid_buffers(model):
+    """What train_nerf.py:153-157 does: density_grid (C, G^3) and grid_coords (G^3, 3) buffers."""
+    G = model.grid_size
+    model.register_buffer("density_grid", torch.zeros(model.cascades, G ** 3, device=model.center.device))
+    r = torch.arange(G, dtype=torch.int32, device=model.center.device)
+    zz, yy, xx = torch.meshgrid(r, r, r, indexing="ij")  # kornia create_meshgrid3d: index (d,h,w) -> (w,h,d)
+    coords = torch.stack([xx, yy, zz], -1).reshape(-1, 3)
+    model.register_buffer("grid_coords", coords.contiguous())
+    return model

@@ -1,0 +1,47 @@
+"""Optimizer step of the reference training loop on the flat parameter buffer.
+
+Reference: apex FusedAdam (AdamW mode, eps 1e-15) with two groups — hash-grid features (weight
+decay 0) and MLP weights (weight decay 1e-6) — (train_nerf.py:262-285), gradient clipping by global
+L2 norm 0.05 (train_nerf.py:955), CosineAnnealingLR over epochs (:286-288).  One sum-of-squares
+kernel + one Adam kernel per group; the clip factor never leaves the device.
+"""
+import math
+
+import torch
+
+from ._lib import F32, I32, I64, call, ptr, stream
+
+
+class FlatAdam:
+    def __init__(self, model, lr=1e-2, betas=(0.9, 0.999), eps=1e-15, weight_decay=(0.0, 1e-6), max_norm=0.05,
+                 num_epochs=None):
+        self.model = model
+        self.base_lr = self.lr = lr
+        self.betas, self.eps, self.wd, self.max_norm = betas, eps, weight_decay, max_norm
+        flat = model.flat_params()
+        self.m = torch.zeros_like(flat)
+        self.v = torch.zeros_like(flat)
+        self.part = torch.empty(1024, dtype=torch.float32, device=flat.device)
+        self.step_count = 0
+        self.num_epochs = num_epochs
+        self.n_table = model._n_table
+
+    def zero_grad(self):
+        self.model.flat_grad().zero_()
+
+    def set_epoch(self, epoch):
+        """CosineAnnealingLR(T_max=num_epochs, eta_min=0) stepped per epoch (train_nerf.py:286-288)."""
+        if self.num_epochs:
+            self.lr = 0.5 * self.base_lr * (1 + math.cos(math.pi * epoch / self.num_epochs))
+
+    def step(self):
+        self.step_count += 1
+        p = self.model.flat_params()
+        g = self.model.flat_grad()
+        s = stream()
+        call("ncn_sumsq", ptr(g), I64(g.numel()), ptr(self.part), s)
+        b1, b2 = self.betas
+        for lo, hi, wd in ((0, self.n_table, self.wd[0]), (self.n_table, p.numel(), self.wd[1])):
+            call("ncn_adam", ptr(p[lo:hi]), ptr(g[lo:hi]), ptr(self.m[lo:hi]), ptr(self.v[lo:hi]), I64(hi - lo),
+                 ptr(self.part), F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(wd),
+                 I32(self.step_count), s)

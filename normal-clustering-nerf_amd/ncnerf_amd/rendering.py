@@ -1,0 +1,156 @@
+"""render() of the reference models/rendering.py:9-242 on the HIP kernels.
+
+Same signature `render(model, rays_o, rays_d, **kwargs)`, same kwargs (near_distance, test_time,
+exp_step_factor, max_samples, T_threshold, anneal_*, random_bg, to_cpu/to_numpy, ...) and the same
+output dict, including the reference quirks that downstream losses depend on:
+  * results['rays_o'] = rays_d  (rendering.py:226-227, quirk q1)
+  * white background when exp_step_factor == 0 (rendering.py:232-240, quirk q2)
+Removed: the dead `(rays_a[:,2]==0).any()` host sync (rendering.py:195-196).
+Extension (test hook, not in the reference): kwargs['march_noise'] injects the marcher noise.
+"""
+import torch
+from einops import rearrange
+
+from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer
+from . import vren
+
+
+@torch.autocast("cuda")
+def render(model, rays_o, rays_d, **kwargs):
+    """rendering.py:9-42"""
+    near_distance = kwargs["near_distance"]
+    rays_o = rays_o.contiguous()
+    rays_d = rays_d.contiguous()
+    _, hits_t, _ = RayAABBIntersector.apply(rays_o, rays_d, model.center, model.half_size, 1)
+    hits_t[(hits_t[:, 0, 0] >= 0) & (hits_t[:, 0, 0] < near_distance), 0, 0] = near_distance
+    render_func = render_rays_test if kwargs.get("test_time", False) else render_rays_train
+    results = render_func(model, rays_o, rays_d, hits_t, **kwargs)
+    for k, v in results.items():
+        if kwargs.get("to_cpu", False):
+            v = v.cpu()
+            if kwargs.get("to_numpy", False):
+                v = v.numpy()
+        results[k] = v
+    return results
+
+
+@torch.no_grad()
+def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
+    """rendering.py:45-149: host-driven incremental march/composite of the alive rays."""
+    exp_step_factor = kwargs.get("exp_step_factor", 0.0)
+    max_samples = kwargs["max_samples"]
+    results = {}
+    N_rays = len(rays_o)
+    device = rays_o.device
+    opacity = torch.zeros(N_rays, device=device)
+    depth = torch.zeros(N_rays, device=device)
+    rend_l = 3 + (3 if model.pred_norm else 0) + (kwargs["n_sem_cls"] if model.pred_sem else 0)
+    rend = torch.zeros(N_rays, rend_l, device=device)
+    samples = total_samples = 0
+    alive_indices = torch.arange(N_rays, device=device)
+    min_samples = 1 if exp_step_factor == 0 else 4
+    hits_t0 = hits_t[:, 0].contiguous()
+    while samples < max_samples:
+        N_alive = len(alive_indices)
+        if N_alive == 0:
+            break
+        N_samples = max(min(N_rays // N_alive, 64), min_samples)
+        samples += N_samples
+        xyzs, dirs, deltas, ts, N_eff_samples = vren.raymarching_test(
+            rays_o, rays_d, hits_t0, alive_indices, model.density_bitfield, model.cascades, model.scale,
+            exp_step_factor, model.grid_size, max_samples, N_samples)
+        total_samples += N_eff_samples.sum()
+        xyzs = rearrange(xyzs, "n1 n2 c -> (n1 n2) c")
+        dirs = rearrange(dirs, "n1 n2 c -> (n1 n2) c")
+        valid_mask = ~torch.all(dirs == 0, dim=1)
+        if valid_mask.sum() == 0:
+            break
+        output = model(xyzs[valid_mask], dirs[valid_mask], **kwargs)
+        sigmas = torch.zeros(len(xyzs), device=device)
+        sigmas[valid_mask] = output["sigmas"].float()
+        sigmas = rearrange(sigmas, "(n1 n2) -> n1 n2", n2=N_samples)
+        rgbs = torch.zeros(len(xyzs), 3, device=device)
+        rgbs[valid_mask] = output["rgbs"].float()
+        raws = rearrange(rgbs, "(n1 n2) c -> n1 n2 c", n2=N_samples)
+        for key in (("norms",) if model.pred_norm else ()) + (("sems",) if model.pred_sem else ()):
+            extra = torch.zeros(len(xyzs), output[key].shape[1], device=device)
+            extra[valid_mask] = output[key].float()
+            raws = torch.cat((raws, rearrange(extra, "(n1 n2) c -> n1 n2 c", n2=N_samples)), dim=-1)
+        vren.composite_test_multi_fw(sigmas.contiguous(), raws.contiguous(), deltas, ts, hits_t0, alive_indices,
+                                     kwargs.get("T_threshold", 1e-4), N_eff_samples, opacity, depth, rend)
+        alive_indices = alive_indices[alive_indices >= 0]
+    hits_t[:, 0] = hits_t0
+    results["opacity"] = opacity
+    results["depth"] = depth
+    i = 3
+    results["rgb"] = rend[..., :i]
+    if model.pred_norm:
+        results["norm_nn"] = rend[..., i:i + 3]
+        if kwargs.get("pred_norm_nn_norm", False):
+            results["norm_nn"] = torch.nn.functional.normalize(results["norm_nn"], p=2.0, dim=-1)
+        i += 3
+    if model.pred_sem:
+        results["sem"] = rend[..., i:i + kwargs["n_sem_cls"]]
+    results["total_samples"] = total_samples
+    rgb_bg = torch.ones(3, device=device) if exp_step_factor == 0 else torch.zeros(3, device=device)
+    results["rgb"] += rgb_bg * rearrange(1 - opacity, "n -> n 1")
+    return results
+
+
+def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
+    """rendering.py:152-242"""
+    exp_step_factor = kwargs.get("exp_step_factor", 0.0)
+    max_samples = kwargs["max_samples"]
+    results = {}
+    anneal_step = kwargs.get("anneal_steps", 0)
+    global_step = kwargs.get("global_step", anneal_step)
+    if anneal_step > global_step:  # rendering.py:168-188
+        strategy = kwargs.get("anneal_strategy", "none")
+        if strategy == "avoid_near":
+            ps = 0.5
+            ray_mid = (hits_t[:, 0, 0] + hits_t[:, 0, 1]) / 2.0
+            n_i = min(max(global_step / anneal_step, ps), 1.0)
+            hits_t[:, 0, 0] = ray_mid + n_i * (hits_t[:, 0, 0] - ray_mid)
+        elif strategy == "depth":
+            depth = kwargs["depth"]
+            n_i = min(max(global_step / anneal_step, 0.05), 100.0)
+            hits_t[:, 0, 0] = torch.max(depth + n_i * (hits_t[:, 0, 0] - depth), hits_t[:, 0, 0])
+            hits_t[:, 0, 1] = torch.min(depth + n_i * (hits_t[:, 0, 1] - depth), hits_t[:, 0, 1])
+        else:
+            assert strategy == "none"
+    rays_a, xyzs, dirs, results["deltas"], results["ts"], results["rm_samples"] = RayMarcher.apply(
+        rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
+        model.grid_size, max_samples, kwargs.get("march_noise"))
+    for k, v in list(kwargs.items()):  # rendering.py:198-200
+        if isinstance(v, torch.Tensor) and k not in ("march_noise",):
+            kwargs[k] = torch.repeat_interleave(v[rays_a[:, 0]], rays_a[:, 2], 0)
+    output = model(xyzs, dirs, **kwargs)
+    sigmas = output["sigmas"]
+    raws = output["rgbs"]
+    if model.pred_norm:
+        raws = torch.cat((raws, output["norms"]), dim=-1)
+    if model.pred_sem:
+        raws = torch.cat((raws, output["sems"]), dim=-1)
+    (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = VolumeRenderer.apply(
+        sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4))
+    i = 3
+    results["rgb"] = rend[..., :i]
+    if model.pred_norm:
+        results["norm_nn"] = rend[..., i:i + 3]
+        if kwargs.get("pred_norm_nn_norm", False):
+            results["norm_nn"] = torch.nn.functional.normalize(results["norm_nn"], p=2.0, dim=-1)
+        i += 3
+    if model.pred_sem:
+        results["sem"] = rend[..., i:i + kwargs["n_sem_cls"]]
+    results["rays_d"] = rays_d
+    results["rays_o"] = rays_d  # rendering.py:227 (quirk q1)
+    results["rays_a"] = rays_a
+    results["depth_std"] = torch.ones_like(results["depth"], requires_grad=False)
+    if exp_step_factor == 0:
+        rgb_bg = torch.ones(3, device=rays_o.device)
+    elif kwargs.get("random_bg", False):
+        rgb_bg = torch.rand(3, device=rays_o.device)
+    else:
+        rgb_bg = torch.zeros(3, device=rays_o.device)
+    results["rgb"] = results["rgb"] + rgb_bg * rearrange(1 - results["opacity"], "n -> n 1")
+    return results

@@ -1,0 +1,170 @@
+"""ORACLE — test infrastructure only.  Never imported by the product path.
+
+Pure-PyTorch (CPU, fp32) restatement of the NGPMT field (reference models/ngp_mt.py:10-229):
+  * multires hash-grid encoding, tiny-cuda-nn "Grid/Hash" semantics (ngp_mt.py:70-82;
+    L=16, F=2, log2_T=19, N_min=16, b = exp(ln(2048*scale/N_min)/(L-1)), ngp_mt.py:40-41);
+  * sigma_net 32 -> 64 (ReLU) -> 16, no bias (ngp_mt.py:83-92) and sigma = TruncExp(h[:,0])
+    (ngp_mt.py:168-169, custom_functions.py:162-173);
+  * rgb_net cat([d/|d|, h]) 19 -> 64 -> 64 -> 3, ReLU hidden, Sigmoid output, no bias
+    (ngp_mt.py:103-113, 206-209).
+
+tiny-cuda-nn is NOT vendored in the reference (README.md:17, `pip install git+...tiny-cuda-nn` at
+no pinned commit) and is not importable here, so this restates tcnn's published algorithm:
+  grid_scale(l)  = exp2(l * log2(b)) * N_min - 1           (fp32)
+  resolution(l)  = ceil(grid_scale(l)) + 1
+  params(l)      = min(next_multiple(resolution^3, 8), 2^19)
+  pos            = fma(grid_scale, x, 0.5); pos_grid = floor(pos); frac = pos - floor(pos)
+  index          = dense x + y*res + z*res^2 while the stride stays <= params(l), else the
+                   coherent prime hash  x*1 ^ y*2654435761 ^ z*805459861  (uint32), then % params(l)
+  feature        = sum over the 8 corners of trilinear weight * table[index]
+PARITY UNPINNED for this file: no reference test or fixture pins tcnn's numerics.  The documented
+deviations from tcnn (fp32 table + fp32 interpolation instead of fp16) are listed in DESIGN.md.
+`emulate_f16=True` rounds the MLP operands to fp16 at the same points the HIP kernel does
+(fp16 MFMA inputs, fp32 accumulation), so the HIP path can be checked tightly.
+"""
+import math
+
+import numpy as np
+import torch
+
+L_LEVELS = 16
+F_PER_LEVEL = 2
+LOG2_T = 19
+N_MIN = 16
+PRIMES = (1, 2654435761, 805459861)
+
+
+def grid_levels(scale=0.5, n_levels=L_LEVELS, log2_T=LOG2_T, n_min=N_MIN):
+    """Per-level (grid_scale f32, resolution, params, offset, dense?) — ngp_mt.py:40-41 + tcnn."""
+    b = math.exp(math.log(2048 * scale / n_min) / (n_levels - 1))
+    log2_pls = np.float32(np.log2(np.float32(b)))
+    levels = []
+    offset = 0
+    for l in range(n_levels):
+        s = np.float32(np.exp2(np.float32(l) * log2_pls)) * np.float32(n_min) - np.float32(1.0)
+        s = np.float32(s)
+        res = int(math.ceil(float(s))) + 1
+        dense = res ** 3
+        params = ((dense + 7) // 8) * 8
+        params = min(params, 1 << log2_T)
+        levels.append(dict(scale=float(s), res=res, params=params, offset=offset,
+                           hashed=res ** 3 > params))
+        offset += params
+    return levels, offset
+
+
+def _grid_index(pg, res, params):
+    """tcnn grid_index for one level; pg int64 (...,3) holding uint32 values."""
+    stride = 1
+    index = torch.zeros(pg.shape[:-1], dtype=torch.int64)
+    for dim in range(3):
+        if stride > params:
+            break
+        index = (index + pg[..., dim] * stride) & 0xFFFFFFFF
+        stride *= res
+    if params < stride:
+        h = torch.zeros_like(index)
+        for dim in range(3):
+            h = h ^ ((pg[..., dim] * PRIMES[dim]) & 0xFFFFFFFF)
+        index = h
+    return index % params
+
+
+def hash_encode(x01, table, levels):
+    """x01: (N,3) f32 in [0,1]; table: (n_entries, 2) f32 -> (N, 32) f32 (level-major, 2 feats)."""
+    feats = []
+    xd = x01.double()
+    for lv in levels:
+        pos = (xd * lv["scale"] + 0.5).float()  # fma(scale, x, 0.5) in fp32 (exact product in f64)
+        fl = torch.floor(pos)
+        frac = pos - fl
+        pg = (fl.to(torch.int64)) & 0xFFFFFFFF  # (uint32)(int)floor
+        acc = torch.zeros(x01.shape[0], F_PER_LEVEL, dtype=torch.float32)
+        for c in range(8):
+            w = torch.ones(x01.shape[0], dtype=torch.float32)
+            pc = pg.clone()
+            for dim in range(3):
+                if c & (1 << dim):
+                    w = w * frac[:, dim]
+                    pc[:, dim] = (pc[:, dim] + 1) & 0xFFFFFFFF
+                else:
+                    w = w * (1 - frac[:, dim])
+            idx = _grid_index(pc, lv["res"], lv["params"]) + lv["offset"]
+            acc = acc + w[:, None] * table[idx]
+        feats.append(acc)
+    return torch.cat(feats, dim=1)
+
+
+def _f16(t, on):
+    return t.half().float() if on else t
+
+
+class FieldParams:
+    """fp32 master parameters: table (n_entries,2), W1 (64,32), W2 (16,64), W3 (64,19), W4 (64,64), W5 (3,64)."""
+
+    def __init__(self, table, W1, W2, W3, W4, W5):
+        self.table, self.W1, self.W2, self.W3, self.W4, self.W5 = table, W1, W2, W3, W4, W5
+
+    def tensors(self):
+        return [self.table, self.W1, self.W2, self.W3, self.W4, self.W5]
+
+
+def field_forward(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False):
+    """NGPMT.forward (ngp_mt.py:196-229) with density() (ngp_mt.py:157-171).
+    Returns sigmas (N), rgbs (N,3), h (N,16)."""
+    x01 = (xyzs - (-scale)) / (2 * scale)  # (x - xyz_min)/(xyz_max - xyz_min), ngp_mt.py:166
+    enc = hash_encode(x01, P.table, levels)
+    e = _f16(enc, emulate_f16)
+    h1 = torch.relu(e @ _f16(P.W1, emulate_f16).t())
+    h = _f16(h1, emulate_f16) @ _f16(P.W2, emulate_f16).t()
+    sig = torch.exp(h[:, 0])  # TruncExp forward
+    d = dirs / torch.norm(dirs, dim=1, keepdim=True)
+    xin = torch.cat([d, h], dim=1)
+    g1 = torch.relu(_f16(xin, emulate_f16) @ _f16(P.W3, emulate_f16).t())
+    g2 = torch.relu(_f16(g1, emulate_f16) @ _f16(P.W4, emulate_f16).t())
+    rgb = torch.sigmoid(_f16(g2, emulate_f16) @ _f16(P.W5, emulate_f16).t())
+    return sig, rgb, h
+
+
+class _TruncExp(torch.autograd.Function):
+    """custom_functions.py:162-173"""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.exp(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * torch.exp(x.clamp(-15, 15))
+
+
+def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False):
+    """Same as field_forward with TruncExp's clamped backward, differentiable w.r.t. P.  With
+    emulate_f16 the forward operands are rounded to fp16 where the HIP kernel rounds them (the
+    rounding is straight-through in the backward), so ReLU masks match the kernel's."""
+    q = lambda t: _f16(t, emulate_f16)
+    x01 = (xyzs - (-scale)) / (2 * scale)
+    enc = hash_encode(x01, P.table, levels)
+    h = q(torch.relu(q(enc) @ q(P.W1).t())) @ q(P.W2).t()
+    sig = _TruncExp.apply(h[:, 0])
+    d = dirs / torch.norm(dirs, dim=1, keepdim=True)
+    g = torch.relu(q(torch.cat([d, h], 1)) @ q(P.W3).t())
+    g = torch.relu(q(g) @ q(P.W4).t())
+    rgb = torch.sigmoid(q(g) @ q(P.W5).t())
+    return sig, rgb, h
+
+
+def init_params(seed=0, scale=0.5, table_init=1e-4):
+    """tcnn-style init: grid U(-1e-4, 1e-4); MLP weights Xavier-uniform."""
+    levels, n_entries = grid_levels(scale)
+    g = torch.Generator().manual_seed(seed)
+
+    def xavier(o, i):
+        a = math.sqrt(6.0 / (i + o))
+        return (torch.rand(o, i, generator=g) * 2 - 1) * a
+
+    table = (torch.rand(n_entries, 2, generator=g) * 2 - 1) * table_init
+    P = FieldParams(table, xavier(64, 32), xavier(16, 64), xavier(64, 19), xavier(64, 64), xavier(3, 64))
+    return P, levels

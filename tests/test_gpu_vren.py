@@ -1,0 +1,221 @@
+"""Parity of the HIP `vren` kernels (through the C ABI) with the CPU oracle (oracle/vren_ref.c).
+
+Bit-exact: ray/AABB hits, the marcher (rays_a, xyzs, dirs, deltas, ts, counter), morton, packbits.
+fp32 tolerance (stated per test): compositing forward/backward (the HIP transmittance is a wave
+product scan, the oracle a serial product; __expf vs expf).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import vren_ref
+from ncnerf_amd import vren
+from ncnerf_amd.synthetic import SyntheticScene
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def scene():
+    return SyntheticScene()
+
+
+def _edge_rays(rng, n):
+    """Random rays plus the reference edge cases: misses, starts inside, axis-parallel (1/d = inf)."""
+    o = rng.uniform(-0.9, 0.9, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[: n // 8, 1:] = 0.0  # parallel to x
+    d[n // 8: n // 4, 0] = 0.0  # in the yz plane
+    o[n // 4: n // 3] = rng.uniform(-0.2, 0.2, (n // 3 - n // 4, 3))  # inside the box
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o, d
+
+
+def test_ray_aabb_bitexact(dev):
+    rng = np.random.default_rng(0)
+    o, d = _edge_rays(rng, 4096)
+    for V, M in ((1, 1), (5, 3), (9, 9)):
+        c = rng.uniform(-0.5, 0.5, (V, 3)).astype(np.float32)
+        h = rng.uniform(0.05, 0.5, (V, 3)).astype(np.float32)
+        if V == 1:
+            c[:] = 0; h[:] = 0.5
+        out = vren.ray_aabb_intersect(*(torch.from_numpy(a).to(dev) for a in (o, d, c, h)), M)
+        ref = vren_ref.ray_aabb_intersect(o, d, c, h, M)
+        for a, r in zip(out, ref):
+            assert np.array_equal(a.cpu().numpy(), r, equal_nan=True)
+
+
+def test_morton_packbits_bitexact(dev):
+    rng = np.random.default_rng(1)
+    coords = rng.integers(0, 1024, (100000, 3)).astype(np.int32)
+    m = vren.morton3D(torch.from_numpy(coords).to(dev))
+    assert np.array_equal(m.cpu().numpy(), vren_ref.morton3D(coords))
+    inv = vren.morton3D_invert(m)
+    assert np.array_equal(inv.cpu().numpy(), vren_ref.morton3D_invert(m.cpu().numpy()))
+    assert np.array_equal(inv.cpu().numpy(), coords)
+    grid = rng.normal(size=(1, 128 ** 3)).astype(np.float32)
+    bf = torch.zeros(128 ** 3 // 8, dtype=torch.uint8, device=dev)
+    vren.packbits(torch.from_numpy(grid).to(dev), 0.3, bf)
+    assert np.array_equal(bf.cpu().numpy(), vren_ref.packbits(grid, 0.3))
+    vren.packbits(torch.from_numpy(grid).to(dev), float("nan"), bf)  # quirk q12: NaN threshold clears
+    assert int(bf.sum()) == 0
+
+
+def _march_inputs(scene, n, seed, dev, edge=False):
+    rng = np.random.default_rng(seed)
+    if edge:
+        o, d = _edge_rays(rng, n)
+    else:
+        b = scene.batch(((n + 63) // 64) * 64, seed)
+        o, d = b["rays_o"][:n].copy(), b["rays_d"][:n].copy()
+    _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
+    ht = ht[:, 0].copy()
+    near = (ht[:, 0] >= 0) & (ht[:, 0] < 0.01)  # rendering.py:28 near clamp
+    ht[near, 0] = 0.01
+    noise = rng.random(n, dtype=np.float32)
+    return o, d, ht, noise
+
+
+@pytest.mark.parametrize("n,edge,ms", [(8192, False, 1024), (2048, True, 1024), (777, False, 64), (1, False, 1024)])
+def test_raymarching_train_bitexact(dev, scene, n, edge, ms):
+    o, d, ht, noise = _march_inputs(scene, n, 7 + n, dev, edge)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    bf = T(scene.bitfield)
+    out = vren.raymarching_train(T(o), T(d), T(ht), bf, 1, 0.5, 0.0, T(noise), 128, ms)
+    ref = vren_ref.raymarching_train(o, d, ht, scene.bitfield, 1, 0.5, 0.0, noise, 128, ms)
+    names = ("rays_a", "xyzs", "dirs", "deltas", "ts", "counter")
+    for a, r, name in zip(out, ref, names):
+        a = a.cpu().numpy()
+        assert a.shape == r.shape, name
+        assert np.array_equal(a, r), f"{name}: {np.argwhere(a != r)[:5]}"
+    if not edge and n >= 2048:
+        S = int(ref[5][0])
+        assert 20 < S / n < 1024, f"unexpected samples/ray {S / n}"
+
+
+def test_raymarching_train_exp_step_and_cascades(dev, scene):
+    """exp_step_factor > 0 and cascades > 1 (scale 1.0 -> C=2) take the general mip path."""
+    rng = np.random.default_rng(3)
+    n = 1024
+    o, d = _edge_rays(rng, n)
+    o *= 2
+    _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 1.0, np.float32), 1)
+    ht = ht[:, 0].copy()
+    noise = rng.random(n, dtype=np.float32)
+    bf = np.concatenate([scene.bitfield, np.roll(scene.bitfield, 1000)])  # C=2 cascades
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = vren.raymarching_train(T(o), T(d), T(ht), T(bf), 2, 1.0, 1 / 256, T(noise), 128, 1024)
+    ref = vren_ref.raymarching_train(o, d, ht, bf, 2, 1.0, 1 / 256, noise, 128, 1024)
+    for a, r in zip(out, ref):
+        assert np.array_equal(a.cpu().numpy(), r)
+
+
+def test_raymarching_test_bitexact(dev, scene):
+    o, d, ht, _ = _march_inputs(scene, 3000, 11, dev)
+    alive = np.arange(0, 3000, 2, dtype=np.int64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    ht_dev = T(ht)
+    ht_ref = ht.copy()
+    for N in (1, 4, 64):
+        out = vren.raymarching_test(T(o), T(d), ht_dev, T(alive), T(scene.bitfield), 1, 0.5, 0.0, 128, 1024, N)
+        ref = vren_ref.raymarching_test(o, d, ht_ref, alive, scene.bitfield, 1, 0.5, 0.0, 128, 1024, N)
+        for a, r in zip(out, ref):
+            assert np.array_equal(a.cpu().numpy(), r)
+        assert np.array_equal(ht_dev.cpu().numpy(), ht_ref)  # hits_t mutation (raymarching.cu:390)
+
+
+def _composite_inputs(scene, n_rays, seed, sigma_scale=20.0, C=3):
+    o, d, ht, noise = _march_inputs(scene, n_rays, seed, None)
+    rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, scene.bitfield, 1, 0.5, 0.0,
+                                                                         noise, 128, 1024)
+    rng = np.random.default_rng(seed + 1)
+    S = int(counter[0])
+    sig = np.abs(rng.normal(0, sigma_scale, S)).astype(np.float32)
+    raws = rng.random((S, C), dtype=np.float32)
+    return rays_a, deltas, ts, sig, raws
+
+
+@pytest.mark.parametrize("sigma_scale", [20.0, 400.0, 0.0])
+def test_composite_fw_parity(dev, scene, sigma_scale):
+    """Tolerance: |Δ| <= 2e-5 + 2e-4*|ref| on opacity/depth/rend/ws; total_samples may differ by one
+    sample only where the stop is borderline (T within 1e-3 relative of T_threshold)."""
+    rays_a, deltas, ts, sig, raws = _composite_inputs(scene, 4096, 5, sigma_scale)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = vren.composite_train_multi_fw(T(sig), T(raws), T(deltas), T(ts), T(rays_a), 1e-4)
+    ref = vren_ref.composite_train_multi_fw(sig, raws, deltas, ts, rays_a, 1e-4)
+    tot, ref_tot = out[0].cpu().numpy(), ref[0]
+    assert np.mean(tot == ref_tot) > 0.999 and np.max(np.abs(tot - ref_tot)) <= 1
+    for a, r, name in zip(out[1:], ref[1:], ("opacity", "depth", "rend", "ws")):
+        np.testing.assert_allclose(a.cpu().numpy(), r, rtol=2e-4, atol=2e-5, err_msg=name)
+
+
+def test_composite_fw_edge(dev):
+    """Empty segments (N=0), a single sample, an immediately opaque first sample."""
+    rays_a = np.array([[0, 0, 0], [1, 0, 1], [2, 1, 3], [3, 4, 0], [4, 4, 300]], np.int64)
+    S = 304
+    rng = np.random.default_rng(0)
+    sig = rng.random(S, dtype=np.float32) * 10
+    sig[1] = 1e6  # opaque first sample of ray 2
+    raws = rng.random((S, 3), dtype=np.float32)
+    deltas = np.full(S, 1.7e-3, np.float32)
+    ts = np.cumsum(deltas).astype(np.float32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = vren.composite_train_multi_fw(T(sig), T(raws), T(deltas), T(ts), T(rays_a), 1e-4)
+    ref = vren_ref.composite_train_multi_fw(sig, raws, deltas, ts, rays_a, 1e-4)
+    assert np.array_equal(out[0].cpu().numpy(), ref[0])
+    for a, r in zip(out[1:], ref[1:]):
+        np.testing.assert_allclose(a.cpu().numpy(), r, rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("with_dws", [False, True])
+def test_composite_bw_parity(dev, scene, with_dws):
+    """Tolerance: |Δ| <= 1e-4*max|ref| + 1e-3*|ref| (cancellation in (R - r) terms)."""
+    rays_a, deltas, ts, sig, raws = _composite_inputs(scene, 2048, 9, 20.0)
+    ref_fw = vren_ref.composite_train_multi_fw(sig, raws, deltas, ts, rays_a, 1e-4)
+    _, O, D, RE, ws = ref_fw
+    rng = np.random.default_rng(2)
+    R, S = rays_a.shape[0], sig.shape[0]
+    dO = rng.normal(size=R).astype(np.float32)
+    dD = rng.normal(size=R).astype(np.float32)
+    dR = rng.normal(size=(R, 3)).astype(np.float32)
+    dW = rng.normal(size=S).astype(np.float32) if with_dws else None
+    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = vren.composite_train_multi_bw(T(dO), T(dD), T(dR), T(dW), T(sig), T(raws), T(ws), T(deltas), T(ts),
+                                        T(rays_a), T(O), T(D), T(RE), 1e-4)
+    ref = vren_ref.composite_train_multi_bw(dO, dD, dR, dW, sig, raws, ws, deltas, ts, rays_a, O, D, RE, 1e-4)
+    for a, r, name in zip(out, ref, ("dL_dsigmas", "dL_draws")):
+        a = a.cpu().numpy()
+        np.testing.assert_allclose(a, r, rtol=1e-3, atol=1e-4 * np.abs(r).max(), err_msg=name)
+
+
+def test_composite_test_parity(dev, scene):
+    rng = np.random.default_rng(4)
+    A, N, R = 2000, 8, 3000
+    alive = np.sort(rng.choice(R, A, replace=False)).astype(np.int64)
+    sig = np.abs(rng.normal(0, 50, (A, N))).astype(np.float32)
+    raws = rng.random((A, N, 3), dtype=np.float32)
+    deltas = np.full((A, N), 1.7e-3, np.float32)
+    ts = rng.random((A, N), dtype=np.float32)
+    n_eff = rng.integers(0, N + 1, A).astype(np.int32)
+    op = rng.random(R, dtype=np.float32) * 0.5
+    de = rng.random(R, dtype=np.float32)
+    re = rng.random((R, 3), dtype=np.float32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    al_d, op_d, de_d, re_d = T(alive), T(op), T(de), T(re)
+    vren.composite_test_multi_fw(T(sig), T(raws), T(deltas), T(ts), T(np.zeros((R, 2), np.float32)), al_d, 1e-4,
+                                 T(n_eff), op_d, de_d, re_d)
+    al_r, op_r, de_r, re_r = alive.copy(), op.copy(), de.copy(), re.copy()
+    vren_ref.composite_test_multi_fw(sig, raws, deltas, ts, None, al_r, 1e-4, n_eff, op_r, de_r, re_r)
+    assert np.array_equal(al_d.cpu().numpy(), al_r)
+    for a, r in ((op_d, op_r), (de_d, de_r), (re_d, re_r)):
+        np.testing.assert_allclose(a.cpu().numpy(), r, rtol=1e-5, atol=1e-6)
+
+
+def test_check_input_errors(dev):
+    """CHECK_INPUT semantics (utils.h:4-6): CPU or non-contiguous tensors raise RuntimeError."""
+    x = torch.zeros(4, 3)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        vren.morton3D(x.int())
+    y = torch.zeros(3, 4, dtype=torch.int32, device=dev).t()
+    with pytest.raises(RuntimeError, match="must be contiguous"):
+        vren.morton3D(y)
