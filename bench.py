@@ -1,0 +1,163 @@
+"""Training-throughput benchmark of the HIP hot path (BASELINE.json metric: training rays/s +
+samples/s at 1/2/4/8 GPUs).
+
+Workload (BASELINE.json configs[1] + [2]): one full training step per iteration on a synthetic
+Hypersim-shaped batch of 8192 rays per GPU (128 random 8x8 patches, ai_001_001 scene box,
+procedural room occupancy): ray/AABB -> occupancy-grid march -> fused hash-grid +
+MLP field -> composite -> rgb/opacity/normal-clustering losses -> backward -> [RCCL all-reduce of
+the flat gradient] -> clip + Adam, and the occupancy-grid refresh every 16 steps.  Inputs are
+generated on the device before the timed region.  N>1: one process per GPU (torchrun), weak
+scaling (8192 rays per rank), value = all ranks' rays / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+TIMED = ("ncn_composite_train_fw", "ncn_composite_train_bw", "ncn_march_train_walk", "ncn_field_fwd",
+         "ncn_field_bwd", "ncn_cluster_loss")
+
+
+def cpu_baseline(n_rays=2048, budget_s=15.0, max_steps=10):
+    """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on host cores)."""
+    from oracle.train_ref import CPUTrainer
+    from ncnerf_amd.synthetic import SyntheticScene
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    scene = SyntheticScene()
+    tr = CPUTrainer(scene.bitfield)
+    tr.step(scene.batch(n_rays, seed=999))  # warm-up
+    t0 = time.perf_counter()
+    steps = 0
+    while steps < max_steps and (time.perf_counter() - t0) < budget_s:
+        tr.step(scene.batch(n_rays, seed=steps))
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n_rays * steps / dt, 1), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} full training steps of {n_rays} rays (config #1) on the oracle CPU path "
+                      f"(oracle/train_ref.py: C marcher/compositor + torch fp32 field/losses), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rays", type=int, default=8192, help="rays per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-grid-update", action="store_true")
+    args = ap.parse_args()
+
+    from ncnerf_amd import _lib, distributed
+    from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
+    from ncnerf_amd.synthetic import SyntheticScene
+    from ncnerf_amd.trainer import Trainer
+
+    rank, world = distributed.init_from_env()
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    torch.manual_seed(1234 + rank)
+
+    scene = SyntheticScene()
+    model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+    with torch.no_grad():
+        model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
+        model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+    trainer = Trainer(model, update_grid=not args.no_grid_update)
+    n_batches = 8
+    batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
+    step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
+    for k in range(args.warmup):
+        trainer.step(batches[k % n_batches], global_step=step0 + k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _lib.TIMING = {n: [] for n in TIMED}
+    rm = torch.zeros((), dtype=torch.float64, device=dev)
+    vr = torch.zeros((), dtype=torch.float64, device=dev)
+    cf_bytes = torch.zeros((), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        results, _ = trainer.step(batches[k % n_batches], global_step=step0 + args.warmup + k)
+        S = results["rm_samples"].double()
+        Svr = results["vr_samples"].double()
+        rm += S
+        vr += Svr
+        cf_bytes += 24.0 * Svr + 4.0 * S + 52.0 * args.rays  # composite_fw algorithmic bytes
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    timing = _lib.TIMING
+    _lib.TIMING = None
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    tot = torch.stack([rm, vr]).reshape(2)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    el = float(elapsed.item())
+    kern = {}
+    for name, evs in timing.items():
+        if evs:
+            ms = [a.elapsed_time(b) for a, b in evs]
+            kern[name] = {"avg_us": round(1e3 * float(np.mean(ms)), 2), "launches": len(ms)}
+    cf_avg_s = kern["ncn_composite_train_fw"]["avg_us"] * 1e-6
+    cf_bytes_per_launch = float(cf_bytes.item()) / args.steps
+    achieved = cf_bytes_per_launch / cf_avg_s / 1e9
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    rays_total = args.rays * world * args.steps
+    value = rays_total / el
+    out = {
+        "metric": "training rays/sec (+ samples/sec)",
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * el / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (march/composite/losses); fp16-operand MFMA with fp32 accumulate in the field MLP",
+        "data": "synthetic Hypersim-shaped batches (ai_001_001 box, 8x8 patches, procedural room occupancy); "
+                "random-init NGPMT",
+        "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
+                   "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
+                   "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update},
+        "samples_per_s": round(float(tot[0].item()) / el, 1),
+        "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
+        "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),
+        "roofline": {"kernel": "composite_train_fw", "bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "algorithmic_bytes_per_launch": round(cf_bytes_per_launch),
+                     "avg_launch_us": kern["ncn_composite_train_fw"]["avg_us"]},
+        "kernels": kern,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

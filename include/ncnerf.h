@@ -94,7 +94,7 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* 
                   float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
 /* Backward: accumulates (+=) into grad_table (n_entries,2) with f32 atomics and writes per-block
  * weight-gradient slabs (n_blocks x NCN_FIELD_NW) into `slab`; ncn_field_reduce_wgrad sums them
- * in a fixed order into grad_w (+=).  n_blocks is returned by ncn_field_bwd_blocks(n). */
+ * into grad_w (+=).  n_blocks is returned by ncn_field_bwd_blocks(n). */
 int ncn_field_bwd_blocks(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_t* levels, float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,

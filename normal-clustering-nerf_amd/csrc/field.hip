@@ -141,20 +141,82 @@ __device__ __forceinline__ float2 encode_level(const float2* __restrict__ tab, c
     return acc;
 }
 
+// Backward scatter of one level for the 16 samples of a lane group (lanes 16g..16g+15 hold 16
+// consecutive samples, i.e. mostly consecutive points of one ray).
+//  1. Runs: lanes whose samples fall in the same base cell form runs; a segmented suffix sum over
+//     each run (4 doubling steps with DPP row shifts inside the 16-lane row) leaves the run total in
+//     its head lane.  At the coarse levels a group usually shares one cell: up to 16x fewer atomics
+//     on the few thousand hot entries.
+//  2. Coalescing: the two corners that differ only in x (tcnn's hash multiplies x by 1, so their
+//     entries are adjacent for dense levels and share a 64-B line 7/8 of the time for hashed ones)
+//     x 2 features = 16 contiguous bytes.  A quad of lanes takes one source lane's 4 values
+//     (quad_perm broadcast), so each f32-atomic instruction touches ~16 lines instead of 64:
+//     scattered single-lane atomics run ~17x below the coalesced atomic rate on MI355X.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_ROW_SL(int k) { return 0x100 + k; }  // dst[r] = src[r+k] inside a 16-lane row
+constexpr int DPP_ROW_SR(int k) { return 0x110 + k; }  // dst[r] = src[r-k]
+constexpr int DPP_QUAD_BCAST(int t) { return t * 0x55; }  // quad_perm [t,t,t,t]
+
+template <int K>
+__device__ __forceinline__ void run_sum(float& v, const int (&link)[4]) {
+    const float t = dppf<DPP_ROW_SL(1 << K)>(v);
+    if (link[K]) v += t;
+}
+
+template <int T>
+__device__ __forceinline__ void quad_atomics(float* __restrict__ grad, int j, bool head, const float (&V)[4],
+                                             uint32_t i0, uint32_t i1) {
+    const int bh = dppi<DPP_QUAD_BCAST(T)>((int)head);
+    const float b0 = dppf<DPP_QUAD_BCAST(T)>(V[0]), b1 = dppf<DPP_QUAD_BCAST(T)>(V[1]);
+    const float b2 = dppf<DPP_QUAD_BCAST(T)>(V[2]), b3 = dppf<DPP_QUAD_BCAST(T)>(V[3]);
+    const uint32_t e0 = (uint32_t)dppi<DPP_QUAD_BCAST(T)>((int)i0), e1 = (uint32_t)dppi<DPP_QUAD_BCAST(T)>((int)i1);
+    const float val = j == 0 ? b0 : (j == 1 ? b1 : (j == 2 ? b2 : b3));
+    const uint32_t e = j < 2 ? e0 : e1;
+    if (bh) atomicAdd(grad + 2 * (size_t)e + (j & 1), val);
+}
+
 __device__ __forceinline__ void scatter_level(float* __restrict__ grad, const LevelTable& L, int l, float x, float y,
-                                              float z, float g0, float g1) {
+                                              float z, float g0, float g1, bool valid, int r, int lane) {
     const LevelPos p = level_pos(L.scale[l], x, y, z);
     const uint32_t params = L.params[l], res = L.res[l], off = L.offset[l];
+    // run structure from the base cell (a sample outside [0,n) gets a key no valid sample has)
+    const int key = valid ? (int)(p.px + res * (p.py + res * p.pz)) : (int)(0xFFFFFFF0u - (uint32_t)r);
+    const int key_next = dppi<DPP_ROW_SL(1)>(key);
+    const int key_prev = dppi<DPP_ROW_SR(1)>(key);
+    int link[4];
+    link[0] = (r < 15) && (key_next == key);
+    link[1] = link[0] && dppi<DPP_ROW_SL(1)>(link[0]);
+    link[2] = link[1] && dppi<DPP_ROW_SL(2)>(link[1]);
+    link[3] = link[2] && dppi<DPP_ROW_SL(4)>(link[2]);
+    const bool head = valid && (r == 0 || key_prev != key);
+    const int j = lane & 3;
 #pragma unroll
-    for (int c = 0; c < 8; c++) {
-        const uint32_t cx = p.px + (c & 1), cy = p.py + ((c >> 1) & 1), cz = p.pz + ((c >> 2) & 1);
-        float wt = 1.0f;
-        wt *= (c & 1) ? p.fx : 1.0f - p.fx;
-        wt *= (c & 2) ? p.fy : 1.0f - p.fy;
-        wt *= (c & 4) ? p.fz : 1.0f - p.fz;
-        const uint32_t idx = off + grid_index(params, res, cx, cy, cz);
-        atomicAdd(grad + 2 * (size_t)idx, wt * g0);
-        atomicAdd(grad + 2 * (size_t)idx + 1, wt * g1);
+    for (int cp = 0; cp < 4; cp++) {  // corner pair: (x, x+1) at (y + (cp&1), z + (cp>>1))
+        const uint32_t cy = p.py + (cp & 1), cz = p.pz + (cp >> 1);
+        const float wy = (cp & 1) ? p.fy : 1.0f - p.fy;
+        const float wz = (cp & 2) ? p.fz : 1.0f - p.fz;
+        const float w0 = ((1.0f - p.fx) * wy) * wz, w1 = (p.fx * wy) * wz;
+        float V[4] = {valid ? w0 * g0 : 0.f, valid ? w0 * g1 : 0.f, valid ? w1 * g0 : 0.f, valid ? w1 * g1 : 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            run_sum<0>(V[q], link);
+            run_sum<1>(V[q], link);
+            run_sum<2>(V[q], link);
+            run_sum<3>(V[q], link);
+        }
+        const uint32_t i0 = off + grid_index(params, res, p.px, cy, cz);
+        const uint32_t i1 = off + grid_index(params, res, p.px + 1, cy, cz);
+        quad_atomics<0>(grad, j, head, V, i0, i1);
+        quad_atomics<1>(grad, j, head, V, i0, i1);
+        quad_atomics<2>(grad, j, head, V, i0, i1);
+        quad_atomics<3>(grad, j, head, V, i0, i1);
     }
 }
 
@@ -433,14 +495,17 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             for (int ks = 0; ks < 4; ks++) v = mfma16(frag(F, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
             dE[t] = v;
         }
-        if (valid) {
-            const float x = (xyzs[3 * s] - xyz_min) / xyz_extent;
-            const float y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
-            const float z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
-            scatter_level(grad_table, L, 2 * g, x, y, z, dE[0][0], dE[0][1]);
-            scatter_level(grad_table, L, 2 * g + 1, x, y, z, dE[0][2], dE[0][3]);
-            scatter_level(grad_table, L, 8 + 2 * g, x, y, z, dE[1][0], dE[1][1]);
-            scatter_level(grad_table, L, 9 + 2 * g, x, y, z, dE[1][2], dE[1][3]);
+        {
+            float x = 0.f, y = 0.f, z = 0.f;
+            if (valid) {
+                x = (xyzs[3 * s] - xyz_min) / xyz_extent;
+                y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
+                z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
+            }
+            scatter_level(grad_table, L, 2 * g, x, y, z, dE[0][0], dE[0][1], valid, r, lane);
+            scatter_level(grad_table, L, 2 * g + 1, x, y, z, dE[0][2], dE[0][3], valid, r, lane);
+            scatter_level(grad_table, L, 8 + 2 * g, x, y, z, dE[1][0], dE[1][1], valid, r, lane);
+            scatter_level(grad_table, L, 9 + 2 * g, x, y, z, dE[1][2], dE[1][3], valid, r, lane);
         }
         // ---- weight gradients: dW[out][in] += sum_s dY[out][s] X[in][s] ----
         // A operand = dY^T rows (out, lane r) over K = samples; B operand = X over K = samples.
@@ -528,12 +593,16 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     for (int i = threadIdx.x; i < NCN_FIELD_NW; i += BWD_THREADS) out[i] = red[i];
 }
 
+// Sum of the per-workgroup dW slabs: blockIdx.y takes a chunk of slabs (coalesced 1 KB rows),
+// chunk partials are added with f32 atomics (gw accumulates, like every .grad).
+constexpr int WRED_CHUNK = 16;
 __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb, float* __restrict__ gw) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= NCN_FIELD_NW) return;
+    const int b0 = blockIdx.y * WRED_CHUNK, b1 = min(nb, b0 + WRED_CHUNK);
     float s = 0.f;
-    for (int b = 0; b < nb; b++) s += slab[(int64_t)b * NCN_FIELD_NW + i];
-    gw[i] += s;
+    for (int b = b0; b < b1; b++) s += slab[(int64_t)b * NCN_FIELD_NW + i];
+    atomicAdd(gw + i, s);
 }
 
 static LevelTable make_table(const uint32_t* levels) {
@@ -601,8 +670,8 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_
 
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream) {
     if (n_blocks <= 0) return 0;
-    hipLaunchKernelGGL(reduce_wgrad_kernel, dim3(cdiv(NCN_FIELD_NW, 256)), dim3(256), 0, (hipStream_t)stream, slab,
-                       n_blocks, grad_w);
+    hipLaunchKernelGGL(reduce_wgrad_kernel, dim3(cdiv(NCN_FIELD_NW, 256), cdiv(n_blocks, WRED_CHUNK)), dim3(256), 0,
+                       (hipStream_t)stream, slab, n_blocks, grad_w);
     NCN_LAUNCH_CHECK("ncn_field_reduce_wgrad");
     return 0;
 }

@@ -45,6 +45,11 @@ SIGNATURES = {
 
 _lib = None
 
+# Optional per-kernel timing: when TIMING is a dict, `call` brackets each launch of the entry points
+# that are keys of TIMING with HIP events on the current stream (the stream the kernel runs on) and
+# appends (start, end) to TIMING[name].
+TIMING = None
+
 
 class NcnError(RuntimeError):
     pass
@@ -74,7 +79,15 @@ def exported_symbols():
 
 
 def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+    if TIMING is not None and name in TIMING:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib(), name)(*args)
+        e1.record()
+        TIMING[name].append((e0, e1))
+    else:
+        rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().ncn_last_error().decode(errors="replace")
         raise NcnError(f"{name} failed (hipError {rc}): {msg}")

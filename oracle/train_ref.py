@@ -1,0 +1,79 @@
+"""ORACLE — test infrastructure only: the pure-PyTorch/C CPU training step used as bench.py's
+`cpu_baseline` leg (kind "port") and as the CPU side of the end-to-end tests.
+
+Same step as ncnerf_amd/trainer.py, built only from the oracle restatements:
+  ray/AABB + near clamp (rendering.py:24-28) -> train marcher (oracle C) -> field (oracle torch,
+  fp32) -> composite fw/bw (oracle C inside an autograd.Function, custom_functions.py:115-159) ->
+  white background (rendering.py:232-240) -> rgb MSE + opacity + normals-from-depth + clustering
+  losses (losses_ref) -> backward -> global-norm clip 0.05 + AdamW(eps 1e-15) (train_nerf.py:262-285).
+"""
+import numpy as np
+import torch
+
+from . import field_ref, losses_ref, vren_ref
+
+
+class _Composite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, sigmas, raws, deltas, ts, rays_a, thr):
+        tot, op, de, rend, ws = vren_ref.composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, thr)
+        T = lambda a: torch.from_numpy(a)
+        ctx.save_for_backward(sigmas.detach(), raws.detach(), deltas, ts, rays_a, T(op), T(de), T(rend), T(ws))
+        ctx.thr = thr
+        return torch.tensor(float(tot.sum())), T(op), T(de), T(rend), T(ws)
+
+    @staticmethod
+    def backward(ctx, _g_tot, dO, dD, dR, dW):
+        sig, raws, deltas, ts, rays_a, op, de, rend, ws = ctx.saved_tensors
+        z = lambda g, like: torch.zeros_like(like) if g is None else g
+        ds, dr = vren_ref.composite_train_multi_bw(z(dO, op), z(dD, de), z(dR, rend), None if dW is None else dW, sig,
+                                                   raws, ws, deltas, ts, rays_a, op, de, rend, ctx.thr)
+        return torch.from_numpy(ds), torch.from_numpy(dr), None, None, None, None
+
+
+class CPUTrainer:
+    """Hypersim config: scale 0.5, G 128, max_samples 1024, near 0.01, loss weights as the trainer."""
+
+    def __init__(self, bitfield, seed=0, lr=1e-2, w_cluster=2e-3, opacity_w=1e-3):
+        P, self.levels = field_ref.init_params(seed=seed)
+        self.params = [t.requires_grad_(True) for t in P.tensors()]
+        self.P = field_ref.FieldParams(*self.params)
+        self.bitfield = np.ascontiguousarray(bitfield, np.uint8)
+        self.opt = torch.optim.AdamW([{"params": self.params[:1], "weight_decay": 0.0},
+                                      {"params": self.params[1:], "weight_decay": 1e-6}], lr=lr, eps=1e-15)
+        self.w_cluster, self.opacity_w = w_cluster, opacity_w
+
+    def step(self, batch, global_step=3000):
+        o, d = batch["rays_o"], batch["rays_d"]
+        R = o.shape[0]
+        _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
+        ht = ht[:, 0].copy()
+        near = (ht[:, 0] >= 0) & (ht[:, 0] < 0.01)
+        ht[near, 0] = 0.01
+        noise = torch.rand(R).numpy()
+        rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, self.bitfield, 1, 0.5, 0.0,
+                                                                             noise, 128, 1024)
+        self.opt.zero_grad()
+        sig, rgb, _ = field_ref.field_forward_autograd(torch.from_numpy(xyzs), torch.from_numpy(dirs), self.P,
+                                                       self.levels)
+        _, opacity, depth, rend, _ = _Composite.apply(sig, rgb, torch.from_numpy(deltas), torch.from_numpy(ts),
+                                                      torch.from_numpy(rays_a), 1e-4)
+        out_rgb = rend + 1.0 * (1 - opacity)[:, None]
+        loss = ((out_rgb - torch.from_numpy(batch["rgb"])) ** 2).mean()
+        oo = opacity + 1e-10
+        loss = loss + self.opacity_w * (-oo * torch.log(oo)).mean()
+        x1, x2, x3 = losses_ref.patch_triangle_index(R)
+        dt = torch.from_numpy(d)
+        n = losses_ref.normals_from_depth(dt, dt, depth, x1, x2, x3)  # rays_o := rays_d (quirk q1)
+        valid = losses_ref.valid_normals_mask(n.detach())
+        nv = n[valid]
+        if nv.shape[0] >= 20:
+            C, a = losses_ref.spherical_kmeans(nv.detach().numpy(), K=20, niter=20, seed=1234)
+            lab, _ = losses_ref.cluster_select(C, a, 0.99)
+            ort, cdot, cl1 = losses_ref.cluster_losses(nv, torch.from_numpy(lab))
+            w = losses_ref.w_sched(self.w_cluster, global_step)
+            loss = loss + w * (losses_ref.validity(ort) + losses_ref.validity(cdot) + losses_ref.validity(cl1))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.params, 0.05)
+        self.opt.step()
+        return float(loss.detach()), int(counter[0])
