@@ -81,6 +81,8 @@ def main():
     n_batches = 8
     batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
     step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
+    if trainer.update_grid:  # first-call costs of the refresh path stay out of the timed region
+        model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
     for k in range(args.warmup):
         trainer.step(batches[k % n_batches], global_step=step0 + k)
     torch.cuda.synchronize()

@@ -109,15 +109,18 @@ int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth
 int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
                     const int64_t* x2, const int64_t* x3, int64_t n_tri, const float* dL_dnormals,
                     float* dL_ddepth, void* stream);
-/* One workgroup: validity filter, spherical k-means (K<=32, niter), cluster selection, the three
- * cluster losses and their gradient w.r.t. the normals, scaled by w_ort / w_dot / w_l1.
+/* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations, one launch each over
+ * 32 workgroups), cluster selection, the three cluster losses and their gradient w.r.t. the
+ * normals, scaled by w_ort / w_dot / w_l1.  n_tri <= 16384.
  * out_losses[0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter; [3] = valid n;
- * out_labels (n_tri) int32 in {0,+-1,+-2,+-3} (-9 = invalid normal); out_centroids (K,3);
- * dL_dnormals (3,n_tri,3) fully written: the gradient of w_ort*ort, w_dot*centr_dot and w_l1*centr_L1
- * separately, so any upstream weighting of the three terms is a 3-term combination. */
+ * [4..6] = the weighted terms; out_labels (n_tri) int32 in {0,+-1,+-2,+-3} (-9 = invalid normal);
+ * out_centroids (K,3); dL_dnormals (3,n_tri,3) fully written: the gradient of w_ort*ort, w_dot*centr_dot and w_l1*centr_L1
+ * separately, so any upstream weighting of the three terms is a 3-term combination.
+ * workspace: ncn_cluster_workspace_words(K) 32-bit words of device scratch. */
+int64_t ncn_cluster_workspace_words(int K);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
                      float w_ort, float w_dot, float w_l1, float* out_losses, int32_t* out_labels,
-                     float* out_centroids, float* dL_dnormals, void* stream);
+                     float* out_centroids, float* dL_dnormals, float* workspace, void* stream);
 
 /* ---- optimizer (train_nerf.py:262-291, 954-955): global-norm clip + Adam over a flat buffer. ---- */
 int ncn_sumsq(const float* x, int64_t n, float* out_partial /* >= 1024 floats */, void* stream);

@@ -75,9 +75,20 @@ __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __r
 }
 
 // ---- clustering ----
-constexpr int CL_THREADS = 512;
+// Pipeline (one stream, no host round trip):
+//   prep  (1 WG)  : validity filter + ordered compaction (losses.py:427-430), seeded init
+//   iter  (NB WGs, niter launches): C_i = update(partials_{i-1}, C_{i-1}) (i>0), assign every valid
+//                   point to argmax <x, C_i>, per-workgroup partial sums (x, y, z, count) per cluster
+//   final (1 WG)  : C = update(partials_last), final search, cluster selection (losses.py:75-166),
+//                   flips, the three cluster losses and their analytic gradient (losses.py:441-478)
+// Every workgroup recomputes the centroid update from the same partials in the same fixed order,
+// so all of them hold bit-identical centroids.
+constexpr int CL_THREADS = 512;      // prep + final kernels
 constexpr int CL_WAVES = CL_THREADS / 64;
 constexpr int CL_MAX_TRI = 16384;
+constexpr int KM_THREADS = 256;      // iteration kernel
+constexpr int KM_WAVES = KM_THREADS / 64;
+constexpr int KM_BLOCKS = 32;
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     x = (x ^ (x >> 16)) * 0x7FEB352Du;
@@ -103,9 +114,9 @@ __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, fl
     return best;
 }
 
-// Block reduction of NV per-thread values into out[NV] (fixed order: lanes, then waves 0..15).
-template <int NV>
-__device__ __forceinline__ void block_reduce(float (&v)[NV], float* red /* [CL_WAVES][NV] */, float* out) {
+// Block reduction of NV per-thread values into out[NV] (fixed order: lanes, then waves).
+template <int NV, int WAVES>
+__device__ __forceinline__ void block_reduce(float (&v)[NV], float* red /* [WAVES][NV] */, float* out) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < NV; q++) {
@@ -113,32 +124,80 @@ __device__ __forceinline__ void block_reduce(float (&v)[NV], float* red /* [CL_W
         if (lane == 0) red[wid * NV + q] = s;
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < NV; q += CL_THREADS) {
+    for (int q = threadIdx.x; q < NV; q += WAVES * 64) {
         float s = 0.f;
-        for (int w = 0; w < CL_WAVES; w++) s += red[w * NV + q];
+        for (int w = 0; w < WAVES; w++) s += red[w * NV + q];
         out[q] = s;
     }
     __syncthreads();
 }
 
-template <int K>
-__global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
-    const float* __restrict__ normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort, float w_dot,
-    float w_l1, float* __restrict__ out_losses, int32_t* __restrict__ out_labels, float* __restrict__ out_centroids,
-    float* __restrict__ dn) {
-    __shared__ int map[CL_MAX_TRI];
-    __shared__ unsigned char asg[CL_MAX_TRI];
-    __shared__ float red[CL_WAVES * K * 4];
-    __shared__ float stats[K * 4];
-    __shared__ float C[K][3];
-    __shared__ int scan_w[CL_WAVES];
-    __shared__ int label_map[K];
-    __shared__ float cc[3][3], cm[3][3], cmn[3], ccnt[3], G[3][3][3];  // G[term][cluster][xyz]
-    __shared__ int ok_s;
-    __shared__ float sim[K][K], nc[K][3], cntk[K];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+// Workspace layout (32-bit words)
+struct KmWs {
+    int* map;        // [CL_MAX_TRI] compacted valid -> original index
+    int* nv;         // [1]
+    float* cent;     // [2][K][3]
+    float* part;     // [2][KM_BLOCKS][K][4]
+};
+__host__ __device__ inline KmWs km_ws(float* base, int K) {
+    KmWs w;
+    w.map = (int*)base;
+    w.nv = (int*)base + CL_MAX_TRI;
+    w.cent = base + CL_MAX_TRI + 4;
+    w.part = w.cent + 2 * K * 3;
+    return w;
+}
+__host__ __device__ inline int64_t km_ws_words(int K) { return CL_MAX_TRI + 4 + 2 * K * 3 + 2 * KM_BLOCKS * K * 4; }
 
-    // 1. ordered compaction of valid normals (losses.py:427-430)
+// Centroid update from the per-workgroup partials (called by ALL threads of a workgroup):
+// threads sum the partials of one (cluster, component) each in fixed workgroup order, then thread 0
+// forms the means, splits empty clusters from the largest (faiss: +-1/1024 on alternating
+// coordinates) and L2-normalises (spherical).
+template <int K>
+__device__ void km_update(const float* __restrict__ part, const float* __restrict__ Cprev, float (*C)[3],
+                          float* sums /* LDS [K*8] */) {
+    for (int q = threadIdx.x; q < K * 4; q += blockDim.x) {
+        float a = 0.f;
+        for (int b = 0; b < KM_BLOCKS; b++) a += part[b * K * 4 + q];
+        sums[q] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float (*nc)[3] = (float (*)[3])(sums + K * 4);  // LDS scratch [K][3] + [K] after the sums
+        float* cnt = sums + K * 7;
+        for (int k = 0; k < K; k++) {
+            cnt[k] = sums[4 * k + 3];
+            for (int q = 0; q < 3; q++) nc[k][q] = cnt[k] > 0.f ? sums[4 * k + q] / cnt[k] : Cprev[3 * k + q];
+        }
+        const float EPS = 1.0f / 1024.0f;
+        for (int k = 0; k < K; k++) {
+            if (cnt[k] == 0.f) {
+                int j = 0;
+                for (int q = 1; q < K; q++)
+                    if (cnt[q] > cnt[j]) j = q;
+                for (int q = 0; q < 3; q++) {
+                    if (q % 2 == 0) { nc[k][q] = nc[j][q] * (1 + EPS); nc[j][q] = nc[j][q] * (1 - EPS); }
+                    else { nc[k][q] = nc[j][q] * (1 - EPS); nc[j][q] = nc[j][q] * (1 + EPS); }
+                }
+                const float half = floorf(cnt[j] * 0.5f);
+                cnt[k] = half;
+                cnt[j] -= half;
+            }
+        }
+        for (int k = 0; k < K; k++) {
+            const float nr = fmaxf(sqrtf(nc[k][0] * nc[k][0] + nc[k][1] * nc[k][1] + nc[k][2] * nc[k][2]), 1e-30f);
+            for (int q = 0; q < 3; q++) C[k][q] = nc[k][q] / nr;
+        }
+    }
+    __syncthreads();
+}
+
+template <int K>
+__global__ __launch_bounds__(CL_THREADS) void cluster_prep_kernel(const float* __restrict__ normals, int n_tri,
+                                                                  uint32_t seed, float* __restrict__ wsb) {
+    const KmWs ws = km_ws(wsb, K);
+    __shared__ int scan_w[CL_WAVES];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int ch = (n_tri + CL_THREADS - 1) / CL_THREADS;
     const int b0 = tid * ch, b1 = min(n_tri, b0 + ch);
     int cnt = 0;
@@ -157,101 +216,119 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
         tot += scan_w[w];
     }
     int pos = woff + incl - cnt;
-    for (int i = b0; i < b1; i++) {
-        const bool v = valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]);
-        out_labels[i] = v ? 0 : -9;
-#pragma unroll
-        for (int q = 0; q < 9; q++) dn[(int64_t)(q / 3) * n_tri * 3 + 3 * i + (q % 3)] = 0.f;
-        if (v) map[pos++] = i;
-    }
-    const int nv = tot;
-    if (tid == 0) {
-        out_losses[0] = 0.f; out_losses[1] = 0.f; out_losses[2] = 0.f; out_losses[3] = (float)nv;
-    }
+    for (int i = b0; i < b1; i++)
+        if (valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2])) ws.map[pos++] = i;
+    if (tid == 0) ws.nv[0] = tot;
     __syncthreads();
-    if (nv < K) return;  // too few normals to cluster (faiss would refuse); no cluster loss
-
-    // 2. init: one seeded pick per stratum (oracle/losses_ref.py:kmeans_init_indices)
-    if (tid < K) {
-        const int lo = (int)(((int64_t)tid * nv) / K), hi = (int)(((int64_t)(tid + 1) * nv) / K);
+    // init: one seeded pick per stratum (oracle/losses_ref.py:kmeans_init_indices)
+    if (tid < K && tot >= K) {
+        const int lo = (int)(((int64_t)tid * tot) / K), hi = (int)(((int64_t)(tid + 1) * tot) / K);
         const int span = max(hi - lo, 1);
         const uint32_t h = mix32(seed * 0x9E3779B1u + (uint32_t)tid * 0x85EBCA77u + 1u);
-        const int i = map[lo + (int)(h % (uint32_t)span)];
-        C[tid][0] = normals[3 * i]; C[tid][1] = normals[3 * i + 1]; C[tid][2] = normals[3 * i + 2];
+        const int i = ws.map[lo + (int)(h % (uint32_t)span)];
+        for (int q = 0; q < 3; q++) ws.cent[3 * tid + q] = normals[3 * i + q];  // buffer 0 = "C_{-1}"
     }
-    __syncthreads();
+}
 
-    // 3. Lloyd iterations (assign by max inner product, mean, split empties, L2-normalise)
-    for (int it = 0; it < niter; it++) {
-        float S[K * 4];
-#pragma unroll
-        for (int q = 0; q < K * 4; q++) S[q] = 0.f;
-        for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = map[m];
-            const float x = normals[3 * i], y = normals[3 * i + 1], z = normals[3 * i + 2];
-            const int a = nearest<K>(C, x, y, z);
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const bool h = (a == k);
-                S[4 * k] += h ? x : 0.f;
-                S[4 * k + 1] += h ? y : 0.f;
-                S[4 * k + 2] += h ? z : 0.f;
-                S[4 * k + 3] += h ? 1.f : 0.f;
-            }
-        }
-        block_reduce<K * 4>(S, red, stats);
-        if (tid == 0) {
-            for (int k = 0; k < K; k++) {
-                cntk[k] = stats[4 * k + 3];
-                for (int q = 0; q < 3; q++) nc[k][q] = cntk[k] > 0.f ? stats[4 * k + q] / cntk[k] : C[k][q];
-            }
-            const float EPS = 1.0f / 1024.0f;
-            for (int k = 0; k < K; k++) {
-                if (cntk[k] == 0.f) {
-                    int j = 0;
-                    for (int q = 1; q < K; q++)
-                        if (cntk[q] > cntk[j]) j = q;
-                    for (int q = 0; q < 3; q++) {
-                        if (q % 2 == 0) { nc[k][q] = nc[j][q] * (1 + EPS); nc[j][q] = nc[j][q] * (1 - EPS); }
-                        else { nc[k][q] = nc[j][q] * (1 - EPS); nc[j][q] = nc[j][q] * (1 + EPS); }
-                    }
-                    const float half = floorf(cntk[j] * 0.5f);
-                    cntk[k] = half;
-                    cntk[j] -= half;
-                }
-            }
-            for (int k = 0; k < K; k++) {
-                const float nr = fmaxf(sqrtf(nc[k][0] * nc[k][0] + nc[k][1] * nc[k][1] + nc[k][2] * nc[k][2]), 1e-30f);
-                for (int q = 0; q < 3; q++) C[k][q] = nc[k][q] / nr;
-            }
-        }
+template <int K>
+__global__ __launch_bounds__(KM_THREADS) void kmeans_iter_kernel(const float* __restrict__ normals, int it,
+                                                                 float* __restrict__ wsb) {
+    const KmWs ws = km_ws(wsb, K);
+    __shared__ float C[K][3];
+    __shared__ float red[KM_WAVES * K * 4];
+    __shared__ float outp[K * 8];
+    const int nv = ws.nv[0];
+    if (nv < K) return;
+    const int tid = threadIdx.x;
+    // centroid buffer (i & 1) holds C_i; C_0 is the prep kernel's init (buffer 0)
+    if (it == 0) {
+        if (tid < K * 3) (&C[0][0])[tid] = ws.cent[tid];
         __syncthreads();
+    } else {
+        km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * K * 4, ws.cent + ((it - 1) & 1) * K * 3, C, outp);
+        if (blockIdx.x == 0 && tid < K * 3) ws.cent[(it & 1) * K * 3 + tid] = (&C[0][0])[tid];
     }
+    const int chunk = (nv + KM_BLOCKS - 1) / KM_BLOCKS;
+    const int m0 = blockIdx.x * chunk, m1 = min(nv, m0 + chunk);
+    float S[K * 4];
+#pragma unroll
+    for (int q = 0; q < K * 4; q++) S[q] = 0.f;
+    for (int m = m0 + tid; m < m1; m += KM_THREADS) {
+        const int i = ws.map[m];
+        const float x = normals[3 * i], y = normals[3 * i + 1], z = normals[3 * i + 2];
+        const int a = nearest<K>(C, x, y, z);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const bool h = (a == k);
+            S[4 * k] += h ? x : 0.f;
+            S[4 * k + 1] += h ? y : 0.f;
+            S[4 * k + 2] += h ? z : 0.f;
+            S[4 * k + 3] += h ? 1.f : 0.f;
+        }
+    }
+    block_reduce<K * 4, KM_WAVES>(S, red, outp);
+    float* mypart = ws.part + (it & 1) * KM_BLOCKS * K * 4 + blockIdx.x * K * 4;
+    for (int q = tid; q < K * 4; q += KM_THREADS) mypart[q] = outp[q];
+}
+
+template <int K>
+__global__ __launch_bounds__(CL_THREADS) void cluster_final_kernel(
+    const float* __restrict__ normals, int n_tri, int niter, float t_sim, float w_ort, float w_dot, float w_l1,
+    const float* __restrict__ wsb, float* __restrict__ out_losses, int32_t* __restrict__ out_labels,
+    float* __restrict__ out_centroids, float* __restrict__ dn) {
+    const KmWs ws = km_ws((float*)wsb, K);
+    __shared__ unsigned char asg[CL_MAX_TRI];
+    __shared__ float red[CL_WAVES * K];
+    __shared__ float stats[K * 8];
+    __shared__ float C[K][3];
+    __shared__ int label_map[K];
+    __shared__ float cc[3][3], cm[3][3], cmn[3], ccnt[3], G[3][3][3];  // G[term][cluster][xyz]
+    __shared__ int ok_s;
+    __shared__ float sim[K][K];
+    const int tid = threadIdx.x;
+    const int nv = ws.nv[0];
+    // outputs for every triangle: invalid -> -9, zero gradient everywhere
+    for (int i = tid; i < n_tri; i += CL_THREADS) {
+        out_labels[i] = valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]) ? 0 : -9;
+#pragma unroll
+        for (int q = 0; q < 9; q++) dn[(int64_t)(q / 3) * n_tri * 3 + 3 * i + (q % 3)] = 0.f;
+    }
+    if (tid == 0) {
+        out_losses[0] = 0.f; out_losses[1] = 0.f; out_losses[2] = 0.f; out_losses[3] = (float)nv;
+        out_losses[4] = 0.f; out_losses[5] = 0.f; out_losses[6] = 0.f;
+    }
+    if (nv < K) return;  // too few normals to cluster (faiss would refuse); no cluster loss
+    if (niter == 0) {
+        if (tid < K * 3) (&C[0][0])[tid] = ws.cent[tid];
+        __syncthreads();
+    } else {
+        km_update<K>(ws.part + ((niter - 1) & 1) * KM_BLOCKS * K * 4, ws.cent + ((niter - 1) & 1) * K * 3, C, stats);
+    }
+    if (tid < K * 3) out_centroids[tid] = (&C[0][0])[tid];
     // final search (losses.py:436) + cluster sizes
     {
         float S[K];
 #pragma unroll
         for (int k = 0; k < K; k++) S[k] = 0.f;
         for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = map[m];
+            const int i = ws.map[m];
             const int a = nearest<K>(C, normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]);
             asg[m] = (unsigned char)a;
 #pragma unroll
             for (int k = 0; k < K; k++) S[k] += (a == k) ? 1.f : 0.f;
         }
-        block_reduce<K>(S, red, stats);
+        block_reduce<K, CL_WAVES>(S, red, stats);
     }
-    // 4. cluster selection (losses.py:75-166) -> per original cluster label
+    // cluster selection (losses.py:75-166) -> label of every original cluster
     if (tid == 0) {
         for (int i = 0; i < K; i++)
             for (int j = 0; j < K; j++) sim[i][j] = C[i][0] * C[j][0] + C[i][1] * C[j][1] + C[i][2] * C[j][2];
         int c1 = 0;
         for (int k = 1; k < K; k++)
             if (stats[k] > stats[c1]) c1 = k;
-        // criteria[i][j] = |s(i,c1)| + |s(c1,j)| + |s(i,j)| ; mins over i (first), argmin over j (first)
         float best = 0.f;
         int c2 = -1, c3 = -1;
-        for (int j = 0; j < K; j++) {
+        for (int j = 0; j < K; j++) {  // criteria[i][j] = |s(i,c1)| + |s(c1,j)| + |s(i,j)|
             float mn = 0.f;
             int mi = -1;
             for (int i = 0; i < K; i++) {
@@ -274,17 +351,15 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
                 for (int k = 0; k < K; k++)
                     if (sim[co][k] > t_sim) lab[k] = -(q + 1);
         }
-        for (int k = 0; k < K; k++)
-            for (int q = 0; q < 3; q++) out_centroids[3 * k + q] = C[k][q];
     }
     __syncthreads();
-    // 5. flipped members, per-cluster means (losses.py:441-468)
+    // flipped members, per-cluster means (losses.py:441-468)
     {
         float S[12];
 #pragma unroll
         for (int q = 0; q < 12; q++) S[q] = 0.f;
         for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = map[m];
+            const int i = ws.map[m];
             const int lb = label_map[asg[m]];
             out_labels[i] = lb;
             const float sg = lb < 0 ? -1.f : 1.f;
@@ -298,7 +373,7 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
                 S[4 * c + 3] += h ? 1.f : 0.f;
             }
         }
-        block_reduce<12>(S, red, stats);
+        block_reduce<12, CL_WAVES>(S, red, stats);
     }
     if (tid == 0) {
         int ok = 1;
@@ -314,13 +389,13 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
     }
     __syncthreads();
     if (!ok_s) return;
-    // 6. per-cluster sums of x.c, |x-c|_1 and sign(x-c)
+    // per-cluster sums of x.c, |x-c|_1 and sign(x-c)
     {
         float S[15];
 #pragma unroll
         for (int q = 0; q < 15; q++) S[q] = 0.f;
         for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = map[m];
+            const int i = ws.map[m];
             const int lb = label_map[asg[m]];
             if (lb == 0) continue;
             const float sg = lb < 0 ? -1.f : 1.f;
@@ -341,7 +416,7 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
                 S[5 * c + 1] += l1;
             }
         }
-        block_reduce<15>(S, red, stats);
+        block_reduce<15, CL_WAVES>(S, red, stats);
     }
     if (tid == 0) {
         const float d12 = cc[0][0] * cc[1][0] + cc[0][1] * cc[1][1] + cc[0][2] * cc[1][2];
@@ -356,7 +431,8 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
         cdot /= 3.0f;
         cl1 /= 3.0f;
         out_losses[0] = ort; out_losses[1] = cdot; out_losses[2] = cl1;
-        // upstream gradient w.r.t. each centroid c_k
+        out_losses[4] = w_ort * ort; out_losses[5] = w_dot * cdot; out_losses[6] = w_l1 * cl1;
+        // upstream gradient w.r.t. each centroid c_k, per term
         const float s12 = d12 > 0.f ? 1.f : (d12 < 0.f ? -1.f : 0.f);
         const float s13 = d13 > 0.f ? 1.f : (d13 < 0.f ? -1.f : 0.f);
         const float s23 = d23 > 0.f ? 1.f : (d23 < 0.f ? -1.f : 0.f);
@@ -378,9 +454,9 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
             }
     }
     __syncthreads();
-    // 7. per-normal gradient (direct terms + through the centroid), times the flip sign
+    // per-normal gradient (direct terms + through the centroid), times the flip sign
     for (int m = tid; m < nv; m += CL_THREADS) {
-        const int i = map[m];
+        const int i = ws.map[m];
         const int lb = label_map[asg[m]];
         if (lb == 0) continue;
         const float sg = lb < 0 ? -1.f : 1.f;
@@ -397,11 +473,24 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_loss_kernel(
     }
 }
 
+template <int K>
+static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort,
+                           float w_dot, float w_l1, float* out_losses, int32_t* out_labels, float* out_centroids,
+                           float* dn, float* ws, hipStream_t s) {
+    hipLaunchKernelGGL(cluster_prep_kernel<K>, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, seed, ws);
+    for (int it = 0; it < niter; it++)
+        hipLaunchKernelGGL(kmeans_iter_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, it, ws);
+    hipLaunchKernelGGL(cluster_final_kernel<K>, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, niter, t_sim, w_ort,
+                       w_dot, w_l1, ws, out_losses, out_labels, out_centroids, dn);
+}
+
 }  // namespace ncn
 
 using namespace ncn;
 
 extern "C" {
+
+int64_t ncn_cluster_workspace_words(int K) { return km_ws_words(K); }
 
 int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1, const int64_t* x2,
                     const int64_t* x3, int64_t n_tri, float* normals, void* stream) {
@@ -423,17 +512,17 @@ int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth
 
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
                      float w_ort, float w_dot, float w_l1, float* out_losses, int32_t* out_labels,
-                     float* out_centroids, float* dL_dnormals, void* stream) {
+                     float* out_centroids, float* dL_dnormals, float* workspace, void* stream) {
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
-                "ncn_cluster_loss: n_tri=%lld exceeds the single-workgroup limit %d", (long long)n_tri, CL_MAX_TRI);
+                "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
     NCN_REQUIRE(niter >= 0, hipErrorInvalidValue, "ncn_cluster_loss: niter < 0");
     hipStream_t s = (hipStream_t)stream;
     if (K == 20)
-        hipLaunchKernelGGL(cluster_loss_kernel<20>, dim3(1), dim3(CL_THREADS), 0, s, normals, (int)n_tri, niter, seed,
-                           t_similar, w_ort, w_dot, w_l1, out_losses, out_labels, out_centroids, dL_dnormals);
+        launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, out_losses, out_labels,
+                           out_centroids, dL_dnormals, workspace, s);
     else if (K == 10)
-        hipLaunchKernelGGL(cluster_loss_kernel<10>, dim3(1), dim3(CL_THREADS), 0, s, normals, (int)n_tri, niter, seed,
-                           t_similar, w_ort, w_dot, w_l1, out_losses, out_labels, out_centroids, dL_dnormals);
+        launch_cluster<10>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, out_losses, out_labels,
+                           out_centroids, dL_dnormals, workspace, s);
     else
         NCN_REQUIRE(false, hipErrorInvalidValue, "ncn_cluster_loss: K must be 10 or 20 (got %d)", K);
     NCN_LAUNCH_CHECK("ncn_cluster_loss");

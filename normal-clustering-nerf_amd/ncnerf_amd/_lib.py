@@ -38,7 +38,8 @@ SIGNATURES = {
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P],
-    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, P, P, P],
+    "ncn_cluster_workspace_words": [I32],
+    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P],
 }
@@ -67,6 +68,7 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int
+        L.ncn_cluster_workspace_words.restype = ctypes.c_int64
         L.ncn_last_error.argtypes = []
         L.ncn_last_error.restype = ctypes.c_char_p
         L.ncn_version.restype = ctypes.c_int

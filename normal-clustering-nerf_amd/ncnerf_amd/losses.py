@@ -64,16 +64,17 @@ class _ClusterLoss(torch.autograd.Function):
     def forward(ctx, normals, K, niter, seed, t_sim, w):
         T = normals.shape[0]
         dev = normals.device
-        out = torch.empty(4, dtype=torch.float32, device=dev)
+        out = torch.empty(7, dtype=torch.float32, device=dev)
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.zeros(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]), F32(w[1]),
-             F32(w[2]), ptr(out), ptr(labels), ptr(cents), ptr(dn), stream())
+             F32(w[2]), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(dn)
+        terms = out[4:7].clone()
         ctx.mark_non_differentiable(labels, cents, out)
-        wt = torch.tensor(w, dtype=torch.float32, device=dev)
-        return out[:3] * wt, labels, cents, out
+        return terms, labels, cents, out
 
     @staticmethod
     def backward(ctx, g, _g_labels, _g_cents, _g_out):
