@@ -31,6 +31,23 @@ class _Composite(torch.autograd.Function):
         return torch.from_numpy(ds), torch.from_numpy(dr), None, None, None, None
 
 
+def render_train_ref(P, levels, rays_o, rays_d, bitfield, noise, near=0.01, max_samples=1024, T_thr=1e-4):
+    """rendering.py:9-42 + 152-242 (train path, exp_step_factor 0) on the oracle: returns the
+    differentiable rgb (with white background), depth, opacity and the marcher/compositor outputs."""
+    o, d = np.ascontiguousarray(rays_o, np.float32), np.ascontiguousarray(rays_d, np.float32)
+    _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
+    ht = ht[:, 0].copy()
+    nearm = (ht[:, 0] >= 0) & (ht[:, 0] < near)
+    ht[nearm, 0] = near
+    rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, bitfield, 1, 0.5, 0.0, noise, 128,
+                                                                         max_samples)
+    sig, rgb, _ = field_ref.field_forward_autograd(torch.from_numpy(xyzs), torch.from_numpy(dirs), P, levels)
+    vr, opacity, depth, rend, ws = _Composite.apply(sig, rgb, torch.from_numpy(deltas), torch.from_numpy(ts),
+                                                    torch.from_numpy(rays_a), T_thr)
+    return dict(rgb=rend + 1.0 * (1 - opacity)[:, None], depth=depth, opacity=opacity, ws=ws, rays_a=rays_a,
+                deltas=deltas, ts=ts, rm_samples=int(counter[0]), vr_samples=int(vr))
+
+
 class CPUTrainer:
     """Hypersim config: scale 0.5, G 128, max_samples 1024, near 0.01, loss weights as the trainer."""
 

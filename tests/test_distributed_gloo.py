@@ -1,0 +1,54 @@
+"""Multi-rank logic on CPU with gloo (world_size 2): gradient averaging of the flat buffer,
+patch sharding, occupancy broadcast."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Model:
+    def __init__(self, rank):
+        self.density_grid = torch.full((1, 64), float(rank))
+        self.density_bitfield = torch.full((8,), rank, dtype=torch.uint8)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from ncnerf_amd import distributed
+    r, w = distributed.init_from_env(backend="gloo")
+    assert (r, w) == (rank, world)
+    g = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    distributed.allreduce_grads(g)
+    m = _Model(rank)
+    distributed.broadcast_occupancy(m)
+    lo, hi = distributed.shard_patches(1024, rank, world)
+    q.put((rank, g.tolist(), float(m.density_grid.sum()), int(m.density_bitfield.sum()), lo, hi))
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [1.5 * i for i in range(10)]  # mean of i*1 and i*2
+    for rank, g, grid_sum, bf_sum, lo, hi in res:
+        assert g == want
+        assert grid_sum == 0.0 and bf_sum == 0  # rank 0's occupancy everywhere
+        assert (lo, hi) == (rank * 512, (rank + 1) * 512)

@@ -1,0 +1,114 @@
+"""The product HIP path against the golden vectors produced by the reference's own Python glue
+(tests/golden/make_golden.py), and an end-to-end training trajectory against the CPU oracle.
+
+Tolerances: marcher outputs exact; rgb/depth/opacity 3e-3 abs (fp16 MFMA operands in the field);
+MLP weight gradients rel-L2 5e-2; losses 2e-3 rel; cluster labels >= 99.5 % identical
+(GPU normals round differently from torch-CPU's double-accumulated norm)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import field_ref
+from oracle.train_ref import CPUTrainer
+from ncnerf_amd.losses import NeRFMTLoss
+from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
+from ncnerf_amd.rendering import render
+from ncnerf_amd.synthetic import SyntheticScene
+from ncnerf_amd.trainer import HYPERSIM_HPARAMS, Trainer
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(G, name), allow_pickle=False))
+
+
+def _model_from_oracle(P, dev):
+    m = NGPMT(scale=0.5, grid_size=128).to(dev)
+    flat, off = m.flat_params(), 0
+    with torch.no_grad():
+        for W in P.tensors():
+            flat[off:off + W.numel()].copy_(W.reshape(-1))
+            off += W.numel()
+    return m
+
+
+def test_render_train_vs_reference_glue(dev):
+    f = _load("render_train.npz")
+    scene = SyntheticScene()
+    P, _ = field_ref.init_params(seed=int(f["param_seed"]), table_init=float(f["table_init"]))
+    m = _model_from_oracle(P, dev)
+    m.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    res = render(m, T(f["rays_o"]), T(f["rays_d"]), near_distance=0.01, max_samples=1024, test_time=False,
+                 march_noise=T(f["noise"]))
+    assert int(res["rm_samples"]) == int(f["rm_samples"])
+    assert np.array_equal(res["rays_a"].cpu().numpy(), f["rays_a"])
+    assert np.array_equal(res["deltas"].cpu().numpy(), f["deltas"])
+    assert np.array_equal(res["ts"].cpu().numpy(), f["ts"])
+    assert torch.equal(res["rays_o"], res["rays_d"])  # quirk q1
+    for k in ("rgb", "depth", "opacity", "ws"):
+        np.testing.assert_allclose(res[k].detach().cpu().numpy(), f[k], atol=3e-3, err_msg=k)
+    loss = (res["rgb"] * T(f["loss_wr"])).sum() + (res["depth"] * T(f["loss_wd"])).sum() \
+        + (res["opacity"] * T(f["loss_wo"])).sum()
+    loss.backward()
+    for p, key in ((m.sigma_net.params, "grad_sigma_net"), (m.rgb_net.params, "grad_rgb_net")):
+        got, ref = p.grad.cpu().numpy(), f[key]
+        assert np.linalg.norm(got - ref) <= 5e-2 * np.linalg.norm(ref), key
+    gt = m.xyz_encoder.params.grad.view(-1, 2).cpu().numpy()
+    assert abs(np.linalg.norm(gt) - float(f["grad_table_norm"])) <= 5e-2 * float(f["grad_table_norm"])
+
+
+@pytest.mark.parametrize("name", ["loss_cluster.npz", "loss_cluster_ramp.npz"])
+def test_loss_vs_reference(dev, name):
+    f = _load(name)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    depth = T(f["depth"]).requires_grad_(True)
+    rgb = T(f["rgb_pred"]).requires_grad_(True)
+    op = T(f["opacity"]).requires_grad_(True)
+    rays_d = T(f["rays_d"])
+    pred = dict(rgb=rgb, depth=depth, opacity=op, rays_o=rays_d, rays_d=rays_d)
+    o1 = np.arange(64).reshape(8, 8)
+    target = dict(rgb=T(f["rgb_target"]), patch_area=64, x1_offsets_local=o1[1:, 1:].reshape(-1),
+                  x2_offsets_local=o1[:-1, 1:].reshape(-1), x3_offsets_local=o1[1:, :-1].reshape(-1))
+    loss = NeRFMTLoss(HYPERSIM_HPARAMS)
+    ld = loss(pred, target, global_step=int(f["step"]))
+    for k in ("rgb", "opacity", "norm_D_C_ort_dot", "norm_D_C_centr_dot", "norm_D_C_centr_L1", "total"):
+        np.testing.assert_allclose(float(ld[k]), float(f["loss_" + k]), rtol=2e-3, atol=1e-8, err_msg=k)
+    labels, cents, raw = loss.last_cluster
+    lab = labels.cpu().numpy()
+    lab = lab[lab != -9]
+    assert lab.shape == f["clust_ass_new"].shape
+    assert np.mean(lab == f["clust_ass_new"]) >= 0.995
+    ld["total"].backward()
+    for got, key in ((depth.grad, "grad_depth"), (rgb.grad, "grad_rgb"), (op.grad, "grad_opacity")):
+        ref = f[key]
+        assert np.linalg.norm(got.cpu().numpy() - ref) <= 2e-2 * np.linalg.norm(ref), key
+
+
+def test_training_trajectory_vs_cpu_oracle(dev):
+    """Same init, same batches, same marcher noise: 6 Adam steps of the full HIP training step
+    track the CPU oracle step (losses within 1 %)."""
+    scene = SyntheticScene()
+    torch.manual_seed(0)
+    cpu = CPUTrainer(scene.bitfield, seed=4)
+    P = field_ref.FieldParams(*[t.detach() for t in cpu.params])
+    m = register_grid_buffers(_model_from_oracle(P, dev))
+    m.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+    tr = Trainer(m, update_grid=False)
+    for k in range(6):
+        b = scene.batch(1024, seed=100 + k)
+        g = torch.Generator().manual_seed(k)
+        noise = torch.rand(1024, generator=g)
+        torch.manual_seed(1000 + k)  # the CPU trainer draws its noise with torch.rand
+        cpu_noise = torch.rand(1024)
+        torch.manual_seed(1000 + k)
+        l_cpu, _ = cpu.step(b, global_step=3000)
+        bt = {kk: (torch.from_numpy(v).to(dev) if isinstance(v, np.ndarray) else v) for kk, v in b.items()}
+        bt["march_noise"] = cpu_noise.to(dev)
+        _, ld = tr.step(bt, global_step=3000)
+        l_gpu = float(ld["total"])
+        assert abs(l_gpu - l_cpu) <= 1e-2 * abs(l_cpu), (k, l_gpu, l_cpu)

@@ -1,0 +1,73 @@
+"""Host-side logic of the product package that runs without a GPU."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import field_ref, losses_ref, vren_ref
+from ncnerf_amd import ngp_mt, synthetic
+from ncnerf_amd.losses import NeRFMTLoss
+from ncnerf_amd.trainer import HYPERSIM_HPARAMS
+
+
+def test_grid_levels_match_oracle_and_tcnn_sizes():
+    lv, n = ngp_mt.grid_levels(0.5)
+    lo, no = field_ref.grid_levels(0.5)
+    assert n == no
+    # fp32 grid_scale: level 5 is exp2(5*log2f(b))*16-1 = 63.0000x -> ceil+1 = 65 (tcnn rule)
+    assert [l["res"] for l in lv][:6] == [16, 22, 28, 37, 49, 65]
+    assert lv[-1]["res"] == 1025 and lv[-1]["params"] == 1 << 19
+    assert sum(l["params"] for l in lv) == n
+    w = ngp_mt.level_words(lv)
+    assert w.dtype == np.uint32 and w.shape == (64,)
+    assert np.frombuffer(w[0:1].tobytes(), np.float32)[0] == np.float32(lv[0]["scale"])
+
+
+def test_ngpmt_surface_on_cpu():
+    m = ngp_mt.NGPMT(scale=0.5, grid_size=128)
+    assert m.cascades == 1 and m.density_bitfield.numel() == 128 ** 3 // 8
+    names = dict(m.named_parameters())
+    assert set(names) == {"xyz_encoder.params", "sigma_net.params", "rgb_net.params"}
+    # the three parameters are views of ONE flat buffer (single all-reduce / single Adam pass)
+    flat = m.flat_params()
+    assert names["xyz_encoder.params"].data_ptr() == flat.data_ptr()
+    assert names["rgb_net.params"].numel() == ngp_mt.W_RGB
+    with pytest.raises(NotImplementedError):
+        ngp_mt.NGPMT(scale=0.5, grid_size=128, pred_sem=True)
+
+
+def test_synthetic_bitfield_matches_occupancy_through_morton():
+    sc = synthetic.SyntheticScene()
+    x, y, z = np.nonzero(sc.occ)
+    idx = vren_ref.morton3D(np.stack([x, y, z], 1).astype(np.int32)).astype(np.int64)
+    bits = (sc.bitfield[idx // 8] >> (idx % 8)) & 1
+    assert bits.all()
+    assert int(np.unpackbits(sc.bitfield).sum()) == sc.occ.sum()
+    np.testing.assert_array_equal(sc.bitfield, vren_ref.packbits(sc.density_grid, 0.5))
+
+
+def test_synthetic_batch_patch_layout():
+    sc = synthetic.SyntheticScene()
+    b = sc.batch(256, seed=1)
+    assert b["rays_o"].shape == (256, 3) and np.allclose(np.linalg.norm(b["rays_d"], axis=1), 1, atol=1e-6)
+    for p in range(4):  # every 8x8 patch shares one camera centre
+        assert np.all(b["rays_o"][64 * p:64 * (p + 1)] == b["rays_o"][64 * p])
+    x1, x2, x3 = losses_ref.patch_triangle_index(256)
+    assert len(x1) == 4 * 49 and x1[0] == 9 and x2[0] == 1 and x3[0] == 8  # base.py:53-58 layout
+
+
+def test_weight_schedule_matches_reference_formula():
+    loss = NeRFMTLoss(HYPERSIM_HPARAMS)
+    for step, want in ((0, 0.0), (500, 0.0), (1750, 1e-3), (3000, 2e-3), (10 ** 6, 2e-3)):
+        assert abs(loss.w_sched(2e-3, step) - want) < 1e-12
+        assert abs(losses_ref.w_sched(2e-3, step) - want) < 1e-12
+
+
+def test_loss_rejects_terms_outside_the_hot_path():
+    with pytest.raises(NotImplementedError):
+        NeRFMTLoss(dict(HYPERSIM_HPARAMS, loss_distortion_w=1e-3))
+
+
+def test_vren_rejects_cpu_tensors():
+    from ncnerf_amd import vren
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        vren.composite_train_multi_fw(*(torch.zeros(4) for _ in range(4)), torch.zeros(1, 3, dtype=torch.long), 1e-4)

@@ -1,0 +1,92 @@
+"""Pin the CPU oracle to the reference: compare it with golden vectors produced by the reference's own
+Python glue (tests/golden/make_golden.py; vren/tcnn/faiss stubbed by the oracle kernels).
+CPU only.  Tolerances: render outputs 1e-5 abs (same kernels, op-order differences in the torch
+glue only), marcher outputs exact; losses 1e-6 rel; gradients 1e-4 rel-L2."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import field_ref, losses_ref, vren_ref
+from oracle.train_ref import render_train_ref
+from ncnerf_amd.synthetic import SyntheticScene
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(G, name), allow_pickle=False))
+
+
+def test_render_train_glue():
+    f = _load("render_train.npz")
+    scene = SyntheticScene()
+    P, levels = field_ref.init_params(seed=int(f["param_seed"]), table_init=float(f["table_init"]))
+    P = field_ref.FieldParams(*[t.requires_grad_(True) for t in P.tensors()])
+    res = render_train_ref(P, levels, f["rays_o"], f["rays_d"], scene.bitfield, f["noise"])
+    assert res["rm_samples"] == int(f["rm_samples"]) and res["vr_samples"] == int(f["vr_samples"])
+    # the reference's rays_a order is the (sequential) stub's order = ray order here
+    assert np.array_equal(res["rays_a"], f["rays_a"])
+    assert np.array_equal(res["deltas"], f["deltas"]) and np.array_equal(res["ts"], f["ts"])
+    for k in ("rgb", "depth", "opacity", "ws"):
+        np.testing.assert_allclose(res[k].detach().numpy(), f[k], atol=1e-5, err_msg=k)
+    assert np.array_equal(f["rays_o_out"], f["rays_d"])  # quirk q1 is in the fixture
+    loss = (res["rgb"] * torch.from_numpy(f["loss_wr"])).sum() + (res["depth"] * torch.from_numpy(f["loss_wd"])).sum() \
+        + (res["opacity"] * torch.from_numpy(f["loss_wo"])).sum()
+    loss.backward()
+    gs = torch.cat([P.W1.grad.reshape(-1), P.W2.grad.reshape(-1)]).numpy()
+    gr = torch.cat([P.W3.grad.reshape(-1), P.W4.grad.reshape(-1), P.W5.grad.reshape(-1)]).numpy()
+    for got, ref in ((gs, f["grad_sigma_net"]), (gr, f["grad_rgb_net"])):
+        assert np.linalg.norm(got - ref) <= 1e-4 * np.linalg.norm(ref)
+    gt = P.table.grad.numpy()
+    np.testing.assert_allclose(np.linalg.norm(gt), f["grad_table_norm"], rtol=1e-4)
+    np.testing.assert_allclose(gt[f["grad_table_nz_idx"]], f["grad_table_nz"], rtol=1e-3, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["loss_cluster.npz", "loss_cluster_ramp.npz"])
+def test_loss_and_clustering(name):
+    f = _load(name)
+    R = f["depth"].shape[0]
+    x1, x2, x3 = losses_ref.patch_triangle_index(R)
+    d = torch.from_numpy(f["rays_d"])
+    depth = torch.from_numpy(f["depth"]).requires_grad_(True)
+    rgb = torch.from_numpy(f["rgb_pred"]).requires_grad_(True)
+    op = torch.from_numpy(f["opacity"]).requires_grad_(True)
+    n = losses_ref.normals_from_depth(d, d, depth, x1, x2, x3)  # rays_o := rays_d (quirk q1)
+    valid = losses_ref.valid_normals_mask(n.detach())
+    nv = n[valid]
+    np.testing.assert_allclose(nv.detach().numpy(), f["valid_normals"], atol=1e-6)
+    C, a = losses_ref.spherical_kmeans(nv.detach().numpy(), K=20, niter=20, seed=1234)
+    np.testing.assert_allclose(C, f["kmeans_centroids"], atol=1e-6)
+    assert np.array_equal(a, f["kmeans_assign"])
+    lab, cn = losses_ref.cluster_select(C, a, 0.99)
+    assert np.array_equal(lab, f["clust_ass_new"])
+    np.testing.assert_allclose(cn, f["centrs_new"], atol=1e-7)
+    step = int(f["step"])
+    w = losses_ref.w_sched(2e-3, step)
+    ort, cdot, cl1 = losses_ref.cluster_losses(nv, torch.from_numpy(lab))
+    rgb_l = ((rgb - torch.from_numpy(f["rgb_target"])) ** 2).mean()
+    o = op + 1e-10
+    op_l = 1e-3 * (-o * torch.log(o)).mean()
+    terms = {"rgb": rgb_l, "opacity": op_l, "norm_D_C_ort_dot": w * ort, "norm_D_C_centr_dot": w * cdot,
+             "norm_D_C_centr_L1": w * cl1}
+    for k, v in terms.items():
+        np.testing.assert_allclose(float(v), float(f["loss_" + k]), rtol=2e-6, atol=1e-9, err_msg=k)
+    total = sum(terms.values())
+    np.testing.assert_allclose(float(total), float(f["loss_total"]), rtol=2e-6)
+    total.backward()
+    for got, key in ((depth.grad, "grad_depth"), (rgb.grad, "grad_rgb"), (op.grad, "grad_opacity")):
+        ref = f[key]
+        assert np.linalg.norm(got.numpy() - ref) <= 1e-4 * np.linalg.norm(ref), key
+
+
+def test_cluster_selection_cases():
+    """losses.py:75-166 restatement vs the reference on crafted sets (opposites, merges, noise)."""
+    f = _load("cluster_select.npz")
+    for i in range(3):
+        X = f[f"x{i}"]
+        C, a = losses_ref.spherical_kmeans(X, K=20, niter=20, seed=1234)
+        lab, cn = losses_ref.cluster_select(C, a, 0.99)
+        assert np.array_equal(lab, f[f"labels{i}"]), i
+        np.testing.assert_allclose(cn, f[f"centrs{i}"], atol=1e-7)
