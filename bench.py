@@ -89,24 +89,23 @@ def main():
     if world > 1:
         dist.barrier()
     _lib.TIMING = {n: [] for n in TIMED}
-    rm = torch.zeros((), dtype=torch.float64, device=dev)
-    vr = torch.zeros((), dtype=torch.float64, device=dev)
-    cf_bytes = torch.zeros((), dtype=torch.float64, device=dev)
+    counts = []  # device scalars, summed after the timed region (no bookkeeping kernels inside it)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         results, _ = trainer.step(batches[k % n_batches], global_step=step0 + args.warmup + k)
-        S = results["rm_samples"].double()
-        Svr = results["vr_samples"].double()
-        rm += S
-        vr += Svr
-        cf_bytes += 24.0 * Svr + 4.0 * S + 52.0 * args.rays  # composite_fw algorithmic bytes
+        counts.append((results["rm_samples"], results["vr_samples"]))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     timing = _lib.TIMING
     _lib.TIMING = None
+    rm = sum(torch.as_tensor(a).double().sum() for a, _ in counts)
+    vr = sum(torch.as_tensor(b).double().sum() for _, b in counts)
+    # composite_fw algorithmic bytes per launch: 24 B per composited sample,
+    # 4 B per marched sample, 52 B per ray
+    cf_bytes = 24.0 * vr + 4.0 * rm + 52.0 * args.rays * args.steps
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     tot = torch.stack([rm, vr]).reshape(2)
     if world > 1:

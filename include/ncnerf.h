@@ -106,9 +106,19 @@ int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void*
  *      (losses.py:47-166, 420-478). ---- */
 int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
                     const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals, void* stream);
+/* dL_ddepth += ...; if term_weights (3 device floats) is non-NULL, dL_dnormals is the (3,n_tri,3)
+ * per-term output of ncn_cluster_loss and is combined as sum_q term_weights[q] * dL_dnormals[q]. */
 int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
                     const int64_t* x2, const int64_t* x3, int64_t n_tri, const float* dL_dnormals,
-                    float* dL_ddepth, void* stream);
+                    const float* term_weights, float* dL_ddepth, void* stream);
+/* Photometric MSE + weighted opacity entropy (losses.py:349-362) with the validity filter
+ * (losses.py:246-262): loss[0] = mean((rgb-gt)^2), loss[1] = w_opacity*mean(-o log o), o = opacity+1e-10,
+ * loss[2..3] = 1 if the term is finite (else the term and its gradient are 0).  The backward
+ * scales by the upstream gradient (2 device floats, or NULL = 1). */
+int ncn_photo_loss_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
+                       float* loss, void* stream);
+int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
+                       const float* loss, const float* upstream, float* dL_drgb, float* dL_dopacity, void* stream);
 /* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations, one launch each over
  * 32 workgroups), cluster selection, the three cluster losses and their gradient w.r.t. the
  * normals, scaled by w_ort / w_dot / w_l1.  n_tri <= 16384.

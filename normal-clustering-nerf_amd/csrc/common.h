@@ -28,6 +28,15 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // Inclusive scans across the 64 lanes (Hillis-Steele, 6 steps).
+__device__ __forceinline__ int wave_incl_sum_i(int v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(v, off, 64);
+        if (lane >= off) v += o;
+    }
+    return v;
+}
+
 __device__ __forceinline__ float wave_incl_sum(float v, int lane) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {

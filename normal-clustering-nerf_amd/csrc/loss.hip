@@ -40,7 +40,8 @@ __global__ void normals_fwd_kernel(const float* __restrict__ o, const float* __r
 __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __restrict__ d,
                                    const float* __restrict__ depth, const int64_t* __restrict__ x1,
                                    const int64_t* __restrict__ x2, const int64_t* __restrict__ x3, int64_t T,
-                                   const float* __restrict__ dn, float* __restrict__ ddepth) {
+                                   const float* __restrict__ dn, const float* __restrict__ tw,
+                                   float* __restrict__ ddepth) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= T) return;
     const int64_t i1 = x1[t], i2 = x2[t], i3 = x3[t];
@@ -52,7 +53,12 @@ __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __r
     const float b[3] = {P3[0] - P1[0], P3[1] - P1[1], P3[2] - P1[2]};
     const float c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
     const float len = sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-    const float g[3] = {dn[3 * t], dn[3 * t + 1], dn[3 * t + 2]};
+    float g[3] = {dn[3 * t], dn[3 * t + 1], dn[3 * t + 2]};
+    if (tw) {  // dn is (3, T, 3): per-term gradients combined with the upstream term weights
+        const float w0 = tw[0], w1 = tw[1], w2 = tw[2];
+#pragma unroll
+        for (int k = 0; k < 3; k++) g[k] = w0 * g[k] + w1 * dn[T * 3 + 3 * t + k] + w2 * dn[T * 6 + 3 * t + k];
+    }
     float dc[3];
     if (len > 1e-12f) {
         const float n[3] = {c[0] / len, c[1] / len, c[2] / len};
@@ -74,21 +80,72 @@ __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __r
     atomicAdd(ddepth + i3, g3);
 }
 
+// ---- photometric MSE + opacity entropy (losses.py:349-362, validity filter :246-262) ----
+// One workgroup: loss[0] = mean((rgb - gt)^2), loss[1] = w_op * mean(-o log o), o = opacity + 1e-10.
+constexpr int PH_THREADS = 1024;
+__global__ __launch_bounds__(PH_THREADS) void photo_loss_fwd_kernel(const float* __restrict__ rgb,
+                                                                    const float* __restrict__ gt,
+                                                                    const float* __restrict__ op, int64_t R,
+                                                                    float w_op, float* __restrict__ loss) {
+    __shared__ float red[2][PH_THREADS / 64];
+    float a = 0.f, b = 0.f;
+    for (int64_t i = threadIdx.x; i < R; i += PH_THREADS) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float d = rgb[3 * i + c] - gt[3 * i + c];
+            a += d * d;
+        }
+        const float o = op[i] + 1e-10f;
+        b += -o * logf(o);
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = a; red[1][threadIdx.x >> 6] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float sa = 0.f, sb = 0.f;
+        for (int w = 0; w < PH_THREADS / 64; w++) { sa += red[0][w]; sb += red[1][w]; }
+        const float mse = sa / (float)(3 * R), ent = w_op * (sb / (float)R);
+        loss[0] = isfinite(mse) ? mse : 0.f;  // validity filter
+        loss[1] = isfinite(ent) ? ent : 0.f;
+        loss[2] = isfinite(mse) ? 1.f : 0.f;
+        loss[3] = isfinite(ent) ? 1.f : 0.f;
+    }
+}
+// grads scaled by the upstream gradient g[0..1] (device scalars) and zeroed for filtered terms
+__global__ void photo_loss_bwd_kernel(const float* __restrict__ rgb, const float* __restrict__ gt,
+                                      const float* __restrict__ op, int64_t R, float w_op,
+                                      const float* __restrict__ loss, const float* __restrict__ g,
+                                      float* __restrict__ drgb, float* __restrict__ dop) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= R) return;
+    const float ga = g ? g[0] * loss[2] : loss[2], gb = g ? g[1] * loss[3] : loss[3];
+    const float sa = 2.f / (float)(3 * R);
+#pragma unroll
+    for (int c = 0; c < 3; c++) drgb[3 * i + c] = ga == 0.f ? 0.f : ga * sa * (rgb[3 * i + c] - gt[3 * i + c]);
+    const float o = op[i] + 1e-10f;
+    dop[i] = gb == 0.f ? 0.f : gb * w_op * (-(logf(o) + 1.f)) / (float)R;  // filtered term: no NaN leaks
+}
+
 // ---- clustering ----
-// Pipeline (one stream, no host round trip):
-//   prep  (1 WG)  : validity filter + ordered compaction (losses.py:427-430), seeded init
-//   iter  (NB WGs, niter launches): C_i = update(partials_{i-1}, C_{i-1}) (i>0), assign every valid
-//                   point to argmax <x, C_i>, per-workgroup partial sums (x, y, z, count) per cluster
-//   final (1 WG)  : C = update(partials_last), final search, cluster selection (losses.py:75-166),
-//                   flips, the three cluster losses and their analytic gradient (losses.py:441-478)
-// Every workgroup recomputes the centroid update from the same partials in the same fixed order,
-// so all of them hold bit-identical centroids.
-constexpr int CL_THREADS = 512;      // prep + final kernels
-constexpr int CL_WAVES = CL_THREADS / 64;
+// Pipeline (one stream, no host round trip, every kernel but prep is KM_BLOCKS workgroups):
+//   prep   (1 WG)  : validity filter + ordered compaction (losses.py:427-430), seeded init
+//   iter   (niter+1 launches): C_i = update(partials_{i-1}, C_{i-1}) (i>0), assign every valid
+//                    point to argmax <x, C_i>, per-workgroup partial sums (x, y, z, count) per
+//                    cluster; the last launch (i = niter) is faiss's final search and keeps the
+//                    assignment
+//   select         : cluster selection (losses.py:75-166) -> label per point, flipped per-cluster
+//                    partial sums (losses.py:441-468)
+//   sums           : per-cluster partials of x.c, |x-c|_1, sign(x-c)
+//   grad           : the three cluster losses, their analytic gradient per point (losses.py:469-478),
+//                    labels (-9 invalid) and the zero gradient of every unselected/invalid point
+// Every workgroup reduces the same partials in the same fixed order, so all of them hold
+// bit-identical centroids/statistics and the result is run-to-run deterministic.
+constexpr int CL_THREADS = 1024;     // prep kernel
 constexpr int CL_MAX_TRI = 16384;
-constexpr int KM_THREADS = 256;      // iteration kernel
-constexpr int KM_WAVES = KM_THREADS / 64;
+constexpr int KM_THREADS = 256;      // multi-workgroup kernels
 constexpr int KM_BLOCKS = 32;
+constexpr int KM_CHUNK_MAX = CL_MAX_TRI / KM_BLOCKS;
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     x = (x ^ (x >> 16)) * 0x7FEB352Du;
@@ -114,30 +171,16 @@ __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, fl
     return best;
 }
 
-// Block reduction of NV per-thread values into out[NV] (fixed order: lanes, then waves).
-template <int NV, int WAVES>
-__device__ __forceinline__ void block_reduce(float (&v)[NV], float* red /* [WAVES][NV] */, float* out) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < NV; q++) {
-        const float s = wave_sum(v[q]);
-        if (lane == 0) red[wid * NV + q] = s;
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < NV; q += WAVES * 64) {
-        float s = 0.f;
-        for (int w = 0; w < WAVES; w++) s += red[w * NV + q];
-        out[q] = s;
-    }
-    __syncthreads();
-}
-
 // Workspace layout (32-bit words)
 struct KmWs {
     int* map;        // [CL_MAX_TRI] compacted valid -> original index
-    int* nv;         // [1]
+    int* nv;         // [4]
     float* cent;     // [2][K][3]
     float* part;     // [2][KM_BLOCKS][K][4]
+    int* asg;        // [CL_MAX_TRI] final assignment (compacted order)
+    int* lab;        // [CL_MAX_TRI] selected label +-1..3 / 0 (compacted order)
+    float* p2;       // [KM_BLOCKS][12] flipped member sums per selected cluster
+    float* p3;       // [KM_BLOCKS][16] x.c, |x-c|_1, sign(x-c) sums per selected cluster
 };
 __host__ __device__ inline KmWs km_ws(float* base, int K) {
     KmWs w;
@@ -145,80 +188,157 @@ __host__ __device__ inline KmWs km_ws(float* base, int K) {
     w.nv = (int*)base + CL_MAX_TRI;
     w.cent = base + CL_MAX_TRI + 4;
     w.part = w.cent + 2 * K * 3;
+    w.asg = (int*)(w.part + 2 * KM_BLOCKS * K * 4);
+    w.lab = w.asg + CL_MAX_TRI;
+    w.p2 = (float*)(w.lab + CL_MAX_TRI);
+    w.p3 = w.p2 + KM_BLOCKS * 12;
     return w;
 }
-__host__ __device__ inline int64_t km_ws_words(int K) { return CL_MAX_TRI + 4 + 2 * K * 3 + 2 * KM_BLOCKS * K * 4; }
+__host__ __device__ inline int64_t km_ws_words(int K) {
+    return CL_MAX_TRI + 4 + 2 * K * 3 + 2 * KM_BLOCKS * K * 4 + 2 * CL_MAX_TRI + KM_BLOCKS * 28;
+}
 
-// Centroid update from the per-workgroup partials (called by ALL threads of a workgroup):
-// threads sum the partials of one (cluster, component) each in fixed workgroup order, then thread 0
-// forms the means, splits empty clusters from the largest (faiss: +-1/1024 on alternating
-// coordinates) and L2-normalises (spherical).
-template <int K>
-__device__ void km_update(const float* __restrict__ part, const float* __restrict__ Cprev, float (*C)[3],
-                          float* sums /* LDS [K*8] */) {
-    for (int q = threadIdx.x; q < K * 4; q += blockDim.x) {
-        float a = 0.f;
-        for (int b = 0; b < KM_BLOCKS; b++) a += part[b * K * 4 + q];
-        sums[q] = a;
+// This workgroup's contiguous chunk of the compacted points.
+__device__ __forceinline__ void km_chunk(int nv, int& m0, int& len) {
+    const int chunk = (nv + KM_BLOCKS - 1) / KM_BLOCKS;
+    m0 = blockIdx.x * chunk;
+    len = max(0, min(nv, m0 + chunk) - m0);
+}
+
+// Fixed-order segmented sum of NQ values over the chunk held in LDS: thread (q, seg) sums
+// val(q, j) over its range of j, then NQ threads add the segments in order.  No serial wave
+// reductions, deterministic.  Ends with a barrier; result in out[NQ] (LDS).
+template <int NQ, class V>
+__device__ __forceinline__ void chunk_sum(int len, float* segbuf /* [KM_THREADS] */, float* out, V val) {
+    constexpr int SEGS = KM_THREADS / NQ;
+    const int tid = threadIdx.x, q = tid % NQ, seg = tid / NQ;
+    if (seg < SEGS) {
+        const int lo = (seg * len) / SEGS, hi = ((seg + 1) * len) / SEGS;
+        float acc = 0.f;
+#pragma unroll 4
+        for (int j = lo; j < hi; j++) acc += val(q, j);
+        segbuf[seg * NQ + q] = acc;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float (*nc)[3] = (float (*)[3])(sums + K * 4);  // LDS scratch [K][3] + [K] after the sums
-        float* cnt = sums + K * 7;
-        for (int k = 0; k < K; k++) {
-            cnt[k] = sums[4 * k + 3];
-            for (int q = 0; q < 3; q++) nc[k][q] = cnt[k] > 0.f ? sums[4 * k + q] / cnt[k] : Cprev[3 * k + q];
-        }
-        const float EPS = 1.0f / 1024.0f;
-        for (int k = 0; k < K; k++) {
-            if (cnt[k] == 0.f) {
-                int j = 0;
-                for (int q = 1; q < K; q++)
-                    if (cnt[q] > cnt[j]) j = q;
-                for (int q = 0; q < 3; q++) {
-                    if (q % 2 == 0) { nc[k][q] = nc[j][q] * (1 + EPS); nc[j][q] = nc[j][q] * (1 - EPS); }
-                    else { nc[k][q] = nc[j][q] * (1 - EPS); nc[j][q] = nc[j][q] * (1 + EPS); }
-                }
-                const float half = floorf(cnt[j] * 0.5f);
-                cnt[k] = half;
-                cnt[j] -= half;
-            }
-        }
-        for (int k = 0; k < K; k++) {
-            const float nr = fmaxf(sqrtf(nc[k][0] * nc[k][0] + nc[k][1] * nc[k][1] + nc[k][2] * nc[k][2]), 1e-30f);
-            for (int q = 0; q < 3; q++) C[k][q] = nc[k][q] / nr;
-        }
+    if (tid < NQ) {
+        float a = 0.f;
+#pragma unroll
+        for (int sg = 0; sg < SEGS; sg++) a += segbuf[sg * NQ + tid];
+        out[tid] = a;
     }
     __syncthreads();
 }
 
+// Sum of KM_BLOCKS partial rows (stride `row`) of `nq` values, fixed order, into out (LDS).
+__device__ __forceinline__ void sum_partials(const float* __restrict__ p, int row, int nq, float* out) {
+    if (threadIdx.x < nq) {
+        float a = 0.f;
+#pragma unroll 8
+        for (int b = 0; b < KM_BLOCKS; b++) a += p[b * row + threadIdx.x];
+        out[threadIdx.x] = a;
+    }
+}
+
+// Centroid update from the per-workgroup partials (called by ALL threads of a workgroup): K*4
+// threads sum one (cluster, component) each in fixed workgroup order, K threads form the means, a
+// rare empty cluster is split from the largest one (faiss: +-1/1024 on alternating coordinates)
+// by thread 0, and K threads L2-normalise (spherical k-means).
 template <int K>
-__global__ __launch_bounds__(CL_THREADS) void cluster_prep_kernel(const float* __restrict__ normals, int n_tri,
-                                                                  uint32_t seed, float* __restrict__ wsb) {
-    const KmWs ws = km_ws(wsb, K);
-    __shared__ int scan_w[CL_WAVES];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int ch = (n_tri + CL_THREADS - 1) / CL_THREADS;
-    const int b0 = tid * ch, b1 = min(n_tri, b0 + ch);
-    int cnt = 0;
-    for (int i = b0; i < b1; i++) cnt += valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]);
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o2 = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o2;
-    }
-    if (lane == 63) scan_w[wid] = incl;
+struct KmUpdLds {
+    float sums[K * 4];
+    float nc[K][3];
+    float cnt[K];
+    int any_empty;
+};
+
+template <int K>
+__device__ void km_update(const float* __restrict__ part, const float* __restrict__ Cprev, float (*C)[3],
+                          KmUpdLds<K>& L) {
+    sum_partials(part, K * 4, K * 4, L.sums);
+    if (threadIdx.x == 0) L.any_empty = 0;
     __syncthreads();
-    int woff = 0, tot = 0;
-    for (int w = 0; w < CL_WAVES; w++) {
-        if (w < wid) woff += scan_w[w];
-        tot += scan_w[w];
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        const float n = L.sums[4 * k + 3];
+        L.cnt[k] = n;
+#pragma unroll
+        for (int q = 0; q < 3; q++) L.nc[k][q] = n > 0.f ? L.sums[4 * k + q] / n : Cprev[3 * k + q];
+        if (n == 0.f) L.any_empty = 1;
     }
-    int pos = woff + incl - cnt;
-    for (int i = b0; i < b1; i++)
-        if (valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2])) ws.map[pos++] = i;
+    __syncthreads();
+    if (L.any_empty && threadIdx.x == 0) {
+        const float EPS = 1.0f / 1024.0f;
+        for (int k = 0; k < K; k++) {
+            if (L.cnt[k] == 0.f) {
+                int j = 0;
+                for (int q = 1; q < K; q++)
+                    if (L.cnt[q] > L.cnt[j]) j = q;
+                for (int q = 0; q < 3; q++) {
+                    if (q % 2 == 0) { L.nc[k][q] = L.nc[j][q] * (1 + EPS); L.nc[j][q] = L.nc[j][q] * (1 - EPS); }
+                    else { L.nc[k][q] = L.nc[j][q] * (1 - EPS); L.nc[j][q] = L.nc[j][q] * (1 + EPS); }
+                }
+                const float half = floorf(L.cnt[j] * 0.5f);
+                L.cnt[k] = half;
+                L.cnt[j] -= half;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        const float nr =
+            fmaxf(sqrtf(L.nc[k][0] * L.nc[k][0] + L.nc[k][1] * L.nc[k][1] + L.nc[k][2] * L.nc[k][2]), 1e-30f);
+#pragma unroll
+        for (int q = 0; q < 3; q++) C[k][q] = L.nc[k][q] / nr;
+    }
+    __syncthreads();
+}
+
+// prep: ordered compaction of the valid normals with one independent load round per thread
+// (thread t owns points t, t+1024, ...), ballot/popcount ranks and a 256-entry block scan.
+__global__ __launch_bounds__(CL_THREADS) void cluster_prep_kernel(const float* __restrict__ normals, int n_tri,
+                                                                  uint32_t seed, int K, float* __restrict__ wsb) {
+    constexpr int R_MAX = CL_MAX_TRI / CL_THREADS;  // 16
+    constexpr int NW = CL_THREADS / 64;             // 16
+    const KmWs ws = km_ws(wsb, K);
+    __shared__ int wcnt[R_MAX * NW];
+    __shared__ int woff[R_MAX * NW];
+    __shared__ int total;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int R = (n_tri + CL_THREADS - 1) / CL_THREADS;
+    uint32_t flags = 0;
+#pragma unroll
+    for (int r = 0; r < R_MAX; r++) {
+        const int i = r * CL_THREADS + tid;
+        if (r < R && i < n_tri && valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]))
+            flags |= 1u << r;
+    }
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int rank[R_MAX];
+#pragma unroll
+    for (int r = 0; r < R_MAX; r++) {
+        const uint64_t b = __ballot((flags >> r) & 1u);
+        rank[r] = __popcll(b & lt);
+        if (lane == 0) wcnt[r * NW + wid] = r < R ? __popcll(b) : 0;
+    }
+    __syncthreads();
+    if (wid == 0) {  // exclusive scan of the R_MAX*NW = 256 counts in (tile, wave) order: 4 per lane
+        int v[4], s = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) { v[e] = wcnt[4 * lane + e]; s += v[e]; }
+        const int incl = wave_incl_sum_i(s, lane);
+        int run = incl - s;
+#pragma unroll
+        for (int e = 0; e < 4; e++) { woff[4 * lane + e] = run; run += v[e]; }
+        if (lane == 63) total = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R_MAX; r++)
+        if ((flags >> r) & 1u) ws.map[woff[r * NW + wid] + rank[r]] = r * CL_THREADS + tid;
+    const int tot = total;
     if (tid == 0) ws.nv[0] = tot;
+    __threadfence_block();
     __syncthreads();
     // init: one seeded pick per stratum (oracle/losses_ref.py:kmeans_init_indices)
     if (tid < K && tot >= K) {
@@ -226,249 +346,318 @@ __global__ __launch_bounds__(CL_THREADS) void cluster_prep_kernel(const float* _
         const int span = max(hi - lo, 1);
         const uint32_t h = mix32(seed * 0x9E3779B1u + (uint32_t)tid * 0x85EBCA77u + 1u);
         const int i = ws.map[lo + (int)(h % (uint32_t)span)];
-        for (int q = 0; q < 3; q++) ws.cent[3 * tid + q] = normals[3 * i + q];  // buffer 0 = "C_{-1}"
+        for (int q = 0; q < 3; q++) ws.cent[3 * tid + q] = normals[3 * i + q];  // buffer 0 = "C_0"
     }
 }
 
+// One Lloyd iteration (it < niter) or the final search (it == niter, keeps the assignment).
 template <int K>
 __global__ __launch_bounds__(KM_THREADS) void kmeans_iter_kernel(const float* __restrict__ normals, int it,
-                                                                 float* __restrict__ wsb) {
+                                                                 int final_pass, float* __restrict__ wsb) {
+    constexpr int NQ = K * 4;
     const KmWs ws = km_ws(wsb, K);
     __shared__ float C[K][3];
-    __shared__ float red[KM_WAVES * K * 4];
-    __shared__ float outp[K * 8];
+    __shared__ float pv[4][KM_CHUNK_MAX];  // x, y, z, 1
+    __shared__ int pa[KM_CHUNK_MAX];
+    __shared__ float segbuf[KM_THREADS];
+    __shared__ float outp[NQ];
+    __shared__ KmUpdLds<K> upd;
     const int nv = ws.nv[0];
     if (nv < K) return;
     const int tid = threadIdx.x;
+    int m0, len;
+    km_chunk(nv, m0, len);
+    // independent of the centroids: fetch this chunk's normals while the update runs
+    for (int j = tid; j < len; j += KM_THREADS) {
+        const int i = ws.map[m0 + j];
+        pv[0][j] = normals[3 * i];
+        pv[1][j] = normals[3 * i + 1];
+        pv[2][j] = normals[3 * i + 2];
+        pv[3][j] = 1.f;
+    }
     // centroid buffer (i & 1) holds C_i; C_0 is the prep kernel's init (buffer 0)
     if (it == 0) {
         if (tid < K * 3) (&C[0][0])[tid] = ws.cent[tid];
         __syncthreads();
     } else {
-        km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * K * 4, ws.cent + ((it - 1) & 1) * K * 3, C, outp);
+        km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, ws.cent + ((it - 1) & 1) * K * 3, C, upd);
         if (blockIdx.x == 0 && tid < K * 3) ws.cent[(it & 1) * K * 3 + tid] = (&C[0][0])[tid];
     }
-    const int chunk = (nv + KM_BLOCKS - 1) / KM_BLOCKS;
-    const int m0 = blockIdx.x * chunk, m1 = min(nv, m0 + chunk);
-    float S[K * 4];
-#pragma unroll
-    for (int q = 0; q < K * 4; q++) S[q] = 0.f;
-    for (int m = m0 + tid; m < m1; m += KM_THREADS) {
-        const int i = ws.map[m];
-        const float x = normals[3 * i], y = normals[3 * i + 1], z = normals[3 * i + 2];
-        const int a = nearest<K>(C, x, y, z);
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const bool h = (a == k);
-            S[4 * k] += h ? x : 0.f;
-            S[4 * k + 1] += h ? y : 0.f;
-            S[4 * k + 2] += h ? z : 0.f;
-            S[4 * k + 3] += h ? 1.f : 0.f;
-        }
+    for (int j = tid; j < len; j += KM_THREADS) {
+        const int a = nearest<K>(C, pv[0][j], pv[1][j], pv[2][j]);
+        pa[j] = a;
+        if (final_pass) ws.asg[m0 + j] = a;
     }
-    block_reduce<K * 4, KM_WAVES>(S, red, outp);
-    float* mypart = ws.part + (it & 1) * KM_BLOCKS * K * 4 + blockIdx.x * K * 4;
-    for (int q = tid; q < K * 4; q += KM_THREADS) mypart[q] = outp[q];
+    __syncthreads();
+    chunk_sum<NQ>(len, segbuf, outp, [&](int q, int j) { return pa[j] == (q >> 2) ? pv[q & 3][j] : 0.f; });
+    if (tid < NQ) ws.part[(it & 1) * KM_BLOCKS * NQ + blockIdx.x * NQ + tid] = outp[tid];
 }
 
+// Cluster selection of losses.py:75-166 from the final centroids and sizes -> label_map[K]
+// (+-1..3 for the three orthogonal main clusters and their opposites, 0 otherwise).
 template <int K>
-__global__ __launch_bounds__(CL_THREADS) void cluster_final_kernel(
-    const float* __restrict__ normals, int n_tri, int niter, float t_sim, float w_ort, float w_dot, float w_l1,
-    const float* __restrict__ wsb, float* __restrict__ out_losses, int32_t* __restrict__ out_labels,
-    float* __restrict__ out_centroids, float* __restrict__ dn) {
-    const KmWs ws = km_ws((float*)wsb, K);
-    __shared__ unsigned char asg[CL_MAX_TRI];
-    __shared__ float red[CL_WAVES * K];
-    __shared__ float stats[K * 8];
-    __shared__ float C[K][3];
-    __shared__ int label_map[K];
-    __shared__ float cc[3][3], cm[3][3], cmn[3], ccnt[3], G[3][3][3];  // G[term][cluster][xyz]
-    __shared__ int ok_s;
-    __shared__ float sim[K][K];
+struct SelLds {
+    float sim[K][K];
+    float cmin[K];
+    int cargmin[K];
+};
+
+template <int K>
+__device__ void select_clusters(const float (*C)[3], const float* cnt, float t_sim, SelLds<K>& L, int* label_map) {
     const int tid = threadIdx.x;
-    const int nv = ws.nv[0];
-    // outputs for every triangle: invalid -> -9, zero gradient everywhere
-    for (int i = tid; i < n_tri; i += CL_THREADS) {
-        out_labels[i] = valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]) ? 0 : -9;
-#pragma unroll
-        for (int q = 0; q < 9; q++) dn[(int64_t)(q / 3) * n_tri * 3 + 3 * i + (q % 3)] = 0.f;
+    for (int q = tid; q < K * K; q += KM_THREADS) {
+        const int i = q / K, j = q % K;
+        L.sim[i][j] = C[i][0] * C[j][0] + C[i][1] * C[j][1] + C[i][2] * C[j][2];
     }
-    if (tid == 0) {
-        out_losses[0] = 0.f; out_losses[1] = 0.f; out_losses[2] = 0.f; out_losses[3] = (float)nv;
-        out_losses[4] = 0.f; out_losses[5] = 0.f; out_losses[6] = 0.f;
-    }
-    if (nv < K) return;  // too few normals to cluster (faiss would refuse); no cluster loss
-    if (niter == 0) {
-        if (tid < K * 3) (&C[0][0])[tid] = ws.cent[tid];
-        __syncthreads();
-    } else {
-        km_update<K>(ws.part + ((niter - 1) & 1) * KM_BLOCKS * K * 4, ws.cent + ((niter - 1) & 1) * K * 3, C, stats);
-    }
-    if (tid < K * 3) out_centroids[tid] = (&C[0][0])[tid];
-    // final search (losses.py:436) + cluster sizes
-    {
-        float S[K];
-#pragma unroll
-        for (int k = 0; k < K; k++) S[k] = 0.f;
-        for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = ws.map[m];
-            const int a = nearest<K>(C, normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]);
-            asg[m] = (unsigned char)a;
-#pragma unroll
-            for (int k = 0; k < K; k++) S[k] += (a == k) ? 1.f : 0.f;
+    __syncthreads();
+    int c1 = 0;  // biggest cluster (topk(sorted)[0]; ties -> lowest index)
+    for (int k = 1; k < K; k++)
+        if (cnt[k] > cnt[c1]) c1 = k;
+    if (tid < K) {  // criteria[i][j] = |s(i,c1)| + |s(c1,j)| + |s(i,j)| ; min over i (first) per column j
+        const int j = tid;
+        float mn = 0.f;
+        int mi = -1;
+        for (int i = 0; i < K; i++) {
+            const float cr = fabsf(L.sim[i][c1]) + fabsf(L.sim[c1][j]) + fabsf(L.sim[i][j]);
+            if (mi < 0 || cr < mn) { mn = cr; mi = i; }
         }
-        block_reduce<K, CL_WAVES>(S, red, stats);
+        L.cmin[j] = mn;
+        L.cargmin[j] = mi;
     }
-    // cluster selection (losses.py:75-166) -> label of every original cluster
+    __syncthreads();
     if (tid == 0) {
-        for (int i = 0; i < K; i++)
-            for (int j = 0; j < K; j++) sim[i][j] = C[i][0] * C[j][0] + C[i][1] * C[j][1] + C[i][2] * C[j][2];
-        int c1 = 0;
-        for (int k = 1; k < K; k++)
-            if (stats[k] > stats[c1]) c1 = k;
-        float best = 0.f;
-        int c2 = -1, c3 = -1;
-        for (int j = 0; j < K; j++) {  // criteria[i][j] = |s(i,c1)| + |s(c1,j)| + |s(i,j)|
-            float mn = 0.f;
-            int mi = -1;
-            for (int i = 0; i < K; i++) {
-                const float cr = fabsf(sim[i][c1]) + fabsf(sim[c1][j]) + fabsf(sim[i][j]);
-                if (mi < 0 || cr < mn) { mn = cr; mi = i; }
-            }
-            if (c2 < 0 || mn < best) { best = mn; c2 = j; c3 = mi; }
-        }
-        int* lab = label_map;
-        for (int k = 0; k < K; k++) lab[k] = 0;
+        int c2 = 0;
+        for (int j = 1; j < K; j++)
+            if (L.cmin[j] < L.cmin[c2]) c2 = j;
+        const int c3 = L.cargmin[c2];
+        for (int k = 0; k < K; k++) label_map[k] = 0;
         const int cs[3] = {c1, c2, c3};
         for (int q = 0; q < 3; q++)
             for (int k = 0; k < K; k++)
-                if (sim[cs[q]][k] > t_sim) lab[k] = q + 1;
+                if (L.sim[cs[q]][k] > t_sim) label_map[k] = q + 1;
         for (int q = 0; q < 3; q++) {  // opposites (losses.py:58-72, 139-163)
             int co = 0;
             for (int k = 1; k < K; k++)
-                if (sim[cs[q]][k] < sim[cs[q]][co]) co = k;
-            if (-1.0f * sim[cs[q]][co] > t_sim)
+                if (L.sim[cs[q]][k] < L.sim[cs[q]][co]) co = k;
+            if (-1.0f * L.sim[cs[q]][co] > t_sim)
                 for (int k = 0; k < K; k++)
-                    if (sim[co][k] > t_sim) lab[k] = -(q + 1);
+                    if (L.sim[co][k] > t_sim) label_map[k] = -(q + 1);
         }
     }
     __syncthreads();
-    // flipped members, per-cluster means (losses.py:441-468)
-    {
-        float S[12];
-#pragma unroll
-        for (int q = 0; q < 12; q++) S[q] = 0.f;
-        for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = ws.map[m];
-            const int lb = label_map[asg[m]];
-            out_labels[i] = lb;
-            const float sg = lb < 0 ? -1.f : 1.f;
-            const int k = lb < 0 ? -lb : lb;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                const bool h = (k == c + 1);
-                S[4 * c] += h ? sg * normals[3 * i] : 0.f;
-                S[4 * c + 1] += h ? sg * normals[3 * i + 1] : 0.f;
-                S[4 * c + 2] += h ? sg * normals[3 * i + 2] : 0.f;
-                S[4 * c + 3] += h ? 1.f : 0.f;
-            }
-        }
-        block_reduce<12, CL_WAVES>(S, red, stats);
+}
+
+// Chunk of selected members in LDS: pk = cluster 0..2 (-1 unselected), pv = flip-signed normal.
+__device__ __forceinline__ void load_members(const KmWs& ws, const float* __restrict__ normals, int m0, int len,
+                                             float (*pv)[KM_CHUNK_MAX], int* pk) {
+    for (int j = threadIdx.x; j < len; j += KM_THREADS) {
+        const int lb = ws.lab[m0 + j];
+        const int i = ws.map[m0 + j];
+        const float sg = lb < 0 ? -1.f : 1.f;
+        pk[j] = (lb < 0 ? -lb : lb) - 1;
+        pv[0][j] = sg * normals[3 * i];
+        pv[1][j] = sg * normals[3 * i + 1];
+        pv[2][j] = sg * normals[3 * i + 2];
     }
-    if (tid == 0) {
+}
+
+// Per selected cluster: count, mean m, |m| and c = m/|m| from the p2 partials; ok = no empty cluster
+// (the mean of an empty cluster is NaN -> every term filtered, losses.py:246-262).
+struct ClStats {
+    float st[12];
+    float cnt[3], cm[3][3], cmn[3], cc[3][3];
+    int ok;
+};
+__device__ void cluster_stats(const KmWs& ws, ClStats& S) {
+    sum_partials(ws.p2, 12, 12, S.st);
+    __syncthreads();
+    if (threadIdx.x == 0) {
         int ok = 1;
         for (int c = 0; c < 3; c++) {
-            ccnt[c] = stats[4 * c + 3];
-            if (ccnt[c] == 0.f) ok = 0;  // mean of an empty cluster is NaN -> every term filtered (losses.py:246-262)
-            for (int q = 0; q < 3; q++) cm[c][q] = ccnt[c] > 0.f ? stats[4 * c + q] / ccnt[c] : 0.f;
-            const float nr = sqrtf(cm[c][0] * cm[c][0] + cm[c][1] * cm[c][1] + cm[c][2] * cm[c][2]);
-            cmn[c] = nr;
-            for (int q = 0; q < 3; q++) cc[c][q] = cm[c][q] / fmaxf(nr, 1e-12f);
+            S.cnt[c] = S.st[4 * c + 3];
+            if (S.cnt[c] == 0.f) ok = 0;
+            for (int q = 0; q < 3; q++) S.cm[c][q] = S.cnt[c] > 0.f ? S.st[4 * c + q] / S.cnt[c] : 0.f;
+            const float nr = sqrtf(S.cm[c][0] * S.cm[c][0] + S.cm[c][1] * S.cm[c][1] + S.cm[c][2] * S.cm[c][2]);
+            S.cmn[c] = nr;
+            for (int q = 0; q < 3; q++) S.cc[c][q] = S.cm[c][q] / fmaxf(nr, 1e-12f);
         }
-        ok_s = ok;
+        S.ok = ok;
     }
     __syncthreads();
-    if (!ok_s) return;
-    // per-cluster sums of x.c, |x-c|_1 and sign(x-c)
-    {
-        float S[15];
-#pragma unroll
-        for (int q = 0; q < 15; q++) S[q] = 0.f;
-        for (int m = tid; m < nv; m += CL_THREADS) {
-            const int i = ws.map[m];
-            const int lb = label_map[asg[m]];
-            if (lb == 0) continue;
-            const float sg = lb < 0 ? -1.f : 1.f;
-            const int k = (lb < 0 ? -lb : lb) - 1;
-            const float x[3] = {sg * normals[3 * i], sg * normals[3 * i + 1], sg * normals[3 * i + 2]};
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                if (c != k) continue;
-                float dot = 0.f, l1 = 0.f;
-#pragma unroll
-                for (int q = 0; q < 3; q++) {
-                    dot += x[q] * cc[c][q];
-                    const float u = x[q] - cc[c][q];
-                    l1 += fabsf(u);
-                    S[5 * c + 2 + q] += u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
-                }
-                S[5 * c] += dot;
-                S[5 * c + 1] += l1;
-            }
-        }
-        block_reduce<15, CL_WAVES>(S, red, stats);
+}
+
+template <int K>
+__global__ __launch_bounds__(KM_THREADS) void cluster_select_kernel(const float* __restrict__ normals, int niter,
+                                                                    float t_sim, float* __restrict__ wsb) {
+    const KmWs ws = km_ws(wsb, K);
+    __shared__ float C[K][3];
+    __shared__ float cnt[K + 4];
+    __shared__ int label_map[K];
+    __shared__ SelLds<K> sel;
+    __shared__ float pv[3][KM_CHUNK_MAX];
+    __shared__ int pk[KM_CHUNK_MAX];
+    __shared__ float segbuf[KM_THREADS];
+    __shared__ float outp[12];
+    const int nv = ws.nv[0];
+    if (nv < K) return;
+    const int tid = threadIdx.x;
+    int m0, len;
+    km_chunk(nv, m0, len);
+    for (int j = tid; j < len; j += KM_THREADS) {
+        const int i = ws.map[m0 + j];
+        pk[j] = ws.asg[m0 + j];
+        pv[0][j] = normals[3 * i];
+        pv[1][j] = normals[3 * i + 1];
+        pv[2][j] = normals[3 * i + 2];
     }
-    if (tid == 0) {
-        const float d12 = cc[0][0] * cc[1][0] + cc[0][1] * cc[1][1] + cc[0][2] * cc[1][2];
-        const float d13 = cc[0][0] * cc[2][0] + cc[0][1] * cc[2][1] + cc[0][2] * cc[2][2];
-        const float d23 = cc[1][0] * cc[2][0] + cc[1][1] * cc[2][1] + cc[1][2] * cc[2][2];
-        const float ort = (fabsf(d12) + fabsf(d13) + fabsf(d23)) / 3.0f;
-        float cdot = 0.f, cl1 = 0.f;
-        for (int c = 0; c < 3; c++) {
-            cdot += 1.0f - stats[5 * c] / ccnt[c];
-            cl1 += stats[5 * c + 1] / ccnt[c];
-        }
-        cdot /= 3.0f;
-        cl1 /= 3.0f;
-        out_losses[0] = ort; out_losses[1] = cdot; out_losses[2] = cl1;
-        out_losses[4] = w_ort * ort; out_losses[5] = w_dot * cdot; out_losses[6] = w_l1 * cl1;
-        // upstream gradient w.r.t. each centroid c_k, per term
-        const float s12 = d12 > 0.f ? 1.f : (d12 < 0.f ? -1.f : 0.f);
-        const float s13 = d13 > 0.f ? 1.f : (d13 < 0.f ? -1.f : 0.f);
-        const float s23 = d23 > 0.f ? 1.f : (d23 < 0.f ? -1.f : 0.f);
-        for (int q = 0; q < 3; q++) {
-            const float go[3] = {(s12 * cc[1][q] + s13 * cc[2][q]) / 3.0f, (s12 * cc[0][q] + s23 * cc[2][q]) / 3.0f,
-                                 (s13 * cc[0][q] + s23 * cc[1][q]) / 3.0f};
-            for (int c = 0; c < 3; c++) {
-                G[0][c][q] = w_ort * go[c];
-                G[1][c][q] = (w_dot / 3.0f) * (-cm[c][q]);
-                G[2][c][q] = (w_l1 / 3.0f) * (-stats[5 * c + 2 + q] / ccnt[c]);
-            }
-        }
-        // project through c = m/|m| : dL/dm = (G - c (c.G)) / |m|, then dm/dx = 1/N
-        for (int tm = 0; tm < 3; tm++)
-            for (int c = 0; c < 3; c++) {
-                const float cg = cc[c][0] * G[tm][c][0] + cc[c][1] * G[tm][c][1] + cc[c][2] * G[tm][c][2];
-                for (int q = 0; q < 3; q++)
-                    G[tm][c][q] = (G[tm][c][q] - cc[c][q] * cg) / (fmaxf(cmn[c], 1e-12f) * ccnt[c]);
-            }
+    if (tid < K * 3) (&C[0][0])[tid] = ws.cent[(niter & 1) * K * 3 + tid];
+    if (tid < K) {  // final cluster sizes = count column of the final-search partials
+        const float* p = ws.part + (niter & 1) * KM_BLOCKS * K * 4;
+        float a = 0.f;
+        for (int b = 0; b < KM_BLOCKS; b++) a += p[b * K * 4 + 4 * tid + 3];
+        cnt[tid] = a;
     }
     __syncthreads();
-    // per-normal gradient (direct terms + through the centroid), times the flip sign
-    for (int m = tid; m < nv; m += CL_THREADS) {
-        const int i = ws.map[m];
-        const int lb = label_map[asg[m]];
-        if (lb == 0) continue;
+    select_clusters<K>(C, cnt, t_sim, sel, label_map);
+    for (int j = tid; j < len; j += KM_THREADS) {
+        const int lb = label_map[pk[j]];
+        ws.lab[m0 + j] = lb;
         const float sg = lb < 0 ? -1.f : 1.f;
-        const int c = (lb < 0 ? -lb : lb) - 1;
+        pk[j] = (lb < 0 ? -lb : lb) - 1;
+        pv[0][j] *= sg;
+        pv[1][j] *= sg;
+        pv[2][j] *= sg;
+    }
+    __syncthreads();
+    chunk_sum<12>(len, segbuf, outp, [&](int q, int j) {
+        const int c = q >> 2, comp = q & 3;
+        return pk[j] != c ? 0.f : (comp < 3 ? pv[comp][j] : 1.f);
+    });
+    if (tid < 12) ws.p2[blockIdx.x * 12 + tid] = outp[tid];
+}
+
+template <int K>
+__global__ __launch_bounds__(KM_THREADS) void cluster_sums_kernel(const float* __restrict__ normals,
+                                                                  float* __restrict__ wsb) {
+    const KmWs ws = km_ws(wsb, K);
+    __shared__ ClStats S;
+    __shared__ float pv[3][KM_CHUNK_MAX];
+    __shared__ int pk[KM_CHUNK_MAX];
+    __shared__ float segbuf[KM_THREADS];
+    __shared__ float outp[15];
+    const int nv = ws.nv[0];
+    if (nv < K) return;
+    int m0, len;
+    km_chunk(nv, m0, len);
+    load_members(ws, normals, m0, len, pv, pk);
+    cluster_stats(ws, S);
+    if (!S.ok) return;
+    chunk_sum<15>(len, segbuf, outp, [&](int q, int j) {
+        const int c = q / 5, comp = q % 5;
+        if (pk[j] != c) return 0.f;
+        const float x0 = pv[0][j], x1 = pv[1][j], x2 = pv[2][j];
+        if (comp == 0) return x0 * S.cc[c][0] + x1 * S.cc[c][1] + x2 * S.cc[c][2];
+        if (comp == 1) return fabsf(x0 - S.cc[c][0]) + fabsf(x1 - S.cc[c][1]) + fabsf(x2 - S.cc[c][2]);
+        const float u = pv[comp - 2][j] - S.cc[c][comp - 2];
+        return u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
+    });
+    if (threadIdx.x < 15) ws.p3[blockIdx.x * 16 + threadIdx.x] = outp[threadIdx.x];
+}
+
+template <int K>
+__global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
+    const float* __restrict__ normals, int n_tri, int niter, float w_ort, float w_dot, float w_l1,
+    const float* __restrict__ wsb, float* __restrict__ out_losses, int32_t* __restrict__ out_labels,
+    float* __restrict__ out_centroids, float* __restrict__ dn) {
+    const KmWs ws = km_ws((float*)wsb, K);
+    __shared__ ClStats S;
+    __shared__ float st3[15];
+    __shared__ float G[3][3][3];  // G[term][cluster][xyz]
+    __shared__ float pv[3][KM_CHUNK_MAX];
+    __shared__ int pk[KM_CHUNK_MAX];
+    const int tid = threadIdx.x;
+    const int nv = ws.nv[0];
+    const int64_t T3 = (int64_t)n_tri * 3;
+    // invalid normals (not in the compaction): label -9, zero gradient
+    for (int i = blockIdx.x * KM_THREADS + tid; i < n_tri; i += KM_BLOCKS * KM_THREADS) {
+        if (!valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2])) {
+            out_labels[i] = -9;
+#pragma unroll
+            for (int q = 0; q < 3; q++) dn[3 * i + q] = dn[T3 + 3 * i + q] = dn[2 * T3 + 3 * i + q] = 0.f;
+        }
+    }
+    int m0, len;
+    km_chunk(nv, m0, len);
+    const bool clustered = nv >= K;
+    if (clustered) {
+        load_members(ws, normals, m0, len, pv, pk);
+        cluster_stats(ws, S);
+        if (S.ok) sum_partials(ws.p3, 16, 15, st3);
+        __syncthreads();
+    }
+    const bool ok = clustered && S.ok;
+    if (blockIdx.x == 0 && tid < K * 3) out_centroids[tid] = clustered ? ws.cent[(niter & 1) * K * 3 + tid] : 0.f;
+    if (tid == 0) {
+        float ort = 0.f, cdot = 0.f, cl1 = 0.f;
+        if (ok) {
+            const float(*cc)[3] = S.cc;
+            const float d12 = cc[0][0] * cc[1][0] + cc[0][1] * cc[1][1] + cc[0][2] * cc[1][2];
+            const float d13 = cc[0][0] * cc[2][0] + cc[0][1] * cc[2][1] + cc[0][2] * cc[2][2];
+            const float d23 = cc[1][0] * cc[2][0] + cc[1][1] * cc[2][1] + cc[1][2] * cc[2][2];
+            ort = (fabsf(d12) + fabsf(d13) + fabsf(d23)) / 3.0f;
+            for (int c = 0; c < 3; c++) {
+                cdot += 1.0f - st3[5 * c] / S.cnt[c];
+                cl1 += st3[5 * c + 1] / S.cnt[c];
+            }
+            cdot /= 3.0f;
+            cl1 /= 3.0f;
+            // upstream gradient w.r.t. each centroid c_k, per term
+            const float s12 = d12 > 0.f ? 1.f : (d12 < 0.f ? -1.f : 0.f);
+            const float s13 = d13 > 0.f ? 1.f : (d13 < 0.f ? -1.f : 0.f);
+            const float s23 = d23 > 0.f ? 1.f : (d23 < 0.f ? -1.f : 0.f);
+            for (int q = 0; q < 3; q++) {
+                const float go[3] = {(s12 * cc[1][q] + s13 * cc[2][q]) / 3.0f,
+                                     (s12 * cc[0][q] + s23 * cc[2][q]) / 3.0f,
+                                     (s13 * cc[0][q] + s23 * cc[1][q]) / 3.0f};
+                for (int c = 0; c < 3; c++) {
+                    G[0][c][q] = w_ort * go[c];
+                    G[1][c][q] = (w_dot / 3.0f) * (-S.cm[c][q]);
+                    G[2][c][q] = (w_l1 / 3.0f) * (-st3[5 * c + 2 + q] / S.cnt[c]);
+                }
+            }
+            // project through c = m/|m| : dL/dm = (G - c (c.G)) / |m|, then dm/dx = 1/N
+            for (int tm = 0; tm < 3; tm++)
+                for (int c = 0; c < 3; c++) {
+                    const float cg = cc[c][0] * G[tm][c][0] + cc[c][1] * G[tm][c][1] + cc[c][2] * G[tm][c][2];
+                    for (int q = 0; q < 3; q++)
+                        G[tm][c][q] = (G[tm][c][q] - cc[c][q] * cg) / (fmaxf(S.cmn[c], 1e-12f) * S.cnt[c]);
+                }
+        }
+        if (blockIdx.x == 0) {
+            out_losses[0] = ort; out_losses[1] = cdot; out_losses[2] = cl1; out_losses[3] = (float)nv;
+            out_losses[4] = w_ort * ort; out_losses[5] = w_dot * cdot; out_losses[6] = w_l1 * cl1;
+        }
+    }
+    __syncthreads();
+    // per-normal label and gradient (direct terms + through the centroid), times the flip sign
+    for (int j = tid; j < len; j += KM_THREADS) {
+        const int i = ws.map[m0 + j];
+        const int lb = clustered ? ws.lab[m0 + j] : 0;
+        out_labels[i] = lb;
+        const int c = clustered ? pk[j] : -1;
+        if (!ok || c < 0) {
+#pragma unroll
+            for (int q = 0; q < 3; q++) dn[3 * i + q] = dn[T3 + 3 * i + q] = dn[2 * T3 + 3 * i + q] = 0.f;
+            continue;
+        }
+        const float sg = lb < 0 ? -1.f : 1.f;
 #pragma unroll
         for (int q = 0; q < 3; q++) {
-            const float x = sg * normals[3 * i + q];
-            const float u = x - cc[c][q];
+            const float u = pv[q][j] - S.cc[c][q];
             const float su = u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
             dn[3 * i + q] = sg * G[0][c][q];
-            dn[(int64_t)n_tri * 3 + 3 * i + q] = sg * ((w_dot / 3.0f) * (-cc[c][q] / ccnt[c]) + G[1][c][q]);
-            dn[(int64_t)n_tri * 6 + 3 * i + q] = sg * ((w_l1 / 3.0f) * (su / ccnt[c]) + G[2][c][q]);
+            dn[T3 + 3 * i + q] = sg * ((w_dot / 3.0f) * (-S.cc[c][q] / S.cnt[c]) + G[1][c][q]);
+            dn[2 * T3 + 3 * i + q] = sg * ((w_l1 / 3.0f) * (su / S.cnt[c]) + G[2][c][q]);
         }
     }
 }
@@ -477,10 +666,13 @@ template <int K>
 static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort,
                            float w_dot, float w_l1, float* out_losses, int32_t* out_labels, float* out_centroids,
                            float* dn, float* ws, hipStream_t s) {
-    hipLaunchKernelGGL(cluster_prep_kernel<K>, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, seed, ws);
-    for (int it = 0; it < niter; it++)
-        hipLaunchKernelGGL(kmeans_iter_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, it, ws);
-    hipLaunchKernelGGL(cluster_final_kernel<K>, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, niter, t_sim, w_ort,
+    hipLaunchKernelGGL(cluster_prep_kernel, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, seed, K, ws);
+    for (int it = 0; it <= niter; it++)
+        hipLaunchKernelGGL(kmeans_iter_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, it,
+                           (int)(it == niter), ws);
+    hipLaunchKernelGGL(cluster_select_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, niter, t_sim, ws);
+    hipLaunchKernelGGL(cluster_sums_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, ws);
+    hipLaunchKernelGGL(cluster_grad_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, w_ort,
                        w_dot, w_l1, ws, out_losses, out_labels, out_centroids, dn);
 }
 
@@ -492,6 +684,23 @@ extern "C" {
 
 int64_t ncn_cluster_workspace_words(int K) { return km_ws_words(K); }
 
+int ncn_photo_loss_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
+                       float* loss, void* stream) {
+    hipLaunchKernelGGL(photo_loss_fwd_kernel, dim3(1), dim3(PH_THREADS), 0, (hipStream_t)stream, rgb, rgb_gt, opacity,
+                       n_rays, w_opacity, loss);
+    NCN_LAUNCH_CHECK("ncn_photo_loss_fwd");
+    return 0;
+}
+
+int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
+                       const float* loss, const float* upstream, float* dL_drgb, float* dL_dopacity, void* stream) {
+    if (n_rays <= 0) return 0;
+    hipLaunchKernelGGL(photo_loss_bwd_kernel, dim3(cdiv(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rgb, rgb_gt,
+                       opacity, n_rays, w_opacity, loss, upstream, dL_drgb, dL_dopacity);
+    NCN_LAUNCH_CHECK("ncn_photo_loss_bwd");
+    return 0;
+}
+
 int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1, const int64_t* x2,
                     const int64_t* x3, int64_t n_tri, float* normals, void* stream) {
     if (n_tri <= 0) return 0;
@@ -502,10 +711,11 @@ int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth
 }
 
 int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1, const int64_t* x2,
-                    const int64_t* x3, int64_t n_tri, const float* dL_dnormals, float* dL_ddepth, void* stream) {
+                    const int64_t* x3, int64_t n_tri, const float* dL_dnormals, const float* term_weights,
+                    float* dL_ddepth, void* stream) {
     if (n_tri <= 0) return 0;
     hipLaunchKernelGGL(normals_bwd_kernel, dim3(cdiv(n_tri, 256)), dim3(256), 0, (hipStream_t)stream, rays_o, rays_d,
-                       depth, x1, x2, x3, n_tri, dL_dnormals, dL_ddepth);
+                       depth, x1, x2, x3, n_tri, dL_dnormals, term_weights, dL_ddepth);
     NCN_LAUNCH_CHECK("ncn_normals_bwd");
     return 0;
 }

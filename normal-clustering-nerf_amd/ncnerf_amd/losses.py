@@ -15,6 +15,7 @@ Not provided (weight 0 in every reference config, hyperparameters.py:33-49): dis
 Manhattan-NeRF and the canonical-direction terms (raise if enabled).
 """
 import einops
+import numpy as np
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -41,7 +42,7 @@ class _Normals(torch.autograd.Function):
         ddepth = torch.zeros_like(depth)
         if dn is not None:
             call("ncn_normals_bwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(x1.shape[0]),
-                 ptr(dn.contiguous()), ptr(ddepth), stream())
+                 ptr(dn.contiguous()), None, ptr(ddepth), stream())
         return None, None, ddepth, None, None, None
 
 
@@ -66,7 +67,7 @@ class _ClusterLoss(torch.autograd.Function):
         dev = normals.device
         out = torch.empty(7, dtype=torch.float32, device=dev)
         labels = torch.empty(T, dtype=torch.int32, device=dev)
-        cents = torch.zeros(K, 3, dtype=torch.float32, device=dev)
+        cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]), F32(w[1]),
@@ -81,13 +82,104 @@ class _ClusterLoss(torch.autograd.Function):
         (dn,) = ctx.saved_tensors
         if g is None:
             return None, None, None, None, None, None
-        return torch.einsum("q,qtc->tc", g.float(), dn), None, None, None, None, None
+        g = g.float()
+        return g[0] * dn[0] + g[1] * dn[1] + g[2] * dn[2], None, None, None, None, None
 
 
 def cluster_losses(norm_depth, K=20, niter=20, seed=1234, t_similar=0.99, w=(1.0, 1.0, 1.0)):
     """Weighted (ort, centr_dot, centr_L1) terms, labels (+-1..3, 0, -9 invalid), centroids, raw stats."""
     check_input(norm_depth, "norm_depth")
     return _ClusterLoss.apply(norm_depth, K, niter, seed, t_similar, tuple(float(x) for x in w))
+
+
+class _NormalsClusterLoss(torch.autograd.Function):
+    """`_Normals` followed by `_ClusterLoss` as one node, used when the depth normals feed only the
+    clustering terms (every reference config).  The backward is one `ncn_normals_bwd` launch that
+    combines the three per-term normal gradients with the upstream term gradients on the device,
+    so no (T,3) normal gradient is materialised and nothing is reduced on the host."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, depth, x1, x2, x3, K, niter, seed, t_sim, w):
+        T = x1.shape[0]
+        dev = depth.device
+        normals = torch.empty(T, 3, dtype=torch.float32, device=dev)
+        call("ncn_normals_fwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals),
+             stream())
+        out = torch.empty(7, dtype=torch.float32, device=dev)
+        labels = torch.empty(T, dtype=torch.int32, device=dev)
+        cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
+        dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]), F32(w[1]),
+             F32(w[2]), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
+        ctx.save_for_backward(rays_o, rays_d, depth, x1, x2, x3, dn)
+        terms = out[4:7].clone()
+        ctx.mark_non_differentiable(normals, labels, cents, out)
+        return terms, normals, labels, cents, out
+
+    @staticmethod
+    def backward(ctx, g, *_unused):
+        rays_o, rays_d, depth, x1, x2, x3, dn = ctx.saved_tensors
+        if g is None:
+            return (None,) * 11
+        ddepth = torch.zeros_like(depth)
+        call("ncn_normals_bwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(x1.shape[0]),
+             ptr(dn), ptr(g.float().contiguous()), ptr(ddepth), stream())
+        return None, None, ddepth, None, None, None, None, None, None, None, None
+
+
+def normals_cluster_losses(rays_o, rays_d, depth, x123_idx, K=20, niter=20, seed=1234, t_similar=0.99,
+                           w=(1.0, 1.0, 1.0)):
+    """extract_normals_from_ray_batch + cluster_losses fused: (terms, normals, labels, centroids, raw)."""
+    f = lambda t: t.float().contiguous()
+    idx = lambda t: t.long().contiguous()
+    for t, n in ((rays_o, "rays_o"), (rays_d, "rays_d"), (depth, "depth")):
+        if not t.is_cuda:
+            raise RuntimeError(f"{n} must be a CUDA tensor")
+    return _NormalsClusterLoss.apply(f(rays_o), f(rays_d), f(depth), idx(x123_idx["x1"]), idx(x123_idx["x2"]),
+                                     idx(x123_idx["x3"]), K, niter, seed, t_similar, tuple(float(x) for x in w))
+
+
+class _PhotoLoss(torch.autograd.Function):
+    """losses.py:349-362 with the validity filter: (mean((rgb-gt)^2), w_op * mean(-o log o)) in one
+    single-workgroup reduction; the backward is one elementwise launch."""
+
+    @staticmethod
+    def forward(ctx, rgb, rgb_gt, opacity, w_op):
+        R = rgb.shape[0]
+        loss = torch.empty(4, dtype=torch.float32, device=rgb.device)
+        call("ncn_photo_loss_fwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(w_op), ptr(loss), stream())
+        ctx.save_for_backward(rgb, rgb_gt, opacity, loss)
+        ctx.w_op = w_op
+        return loss[0], loss[1]
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_op):
+        rgb, rgb_gt, opacity, loss = ctx.saved_tensors
+        dev = rgb.device
+        g = torch.stack([torch.zeros((), device=dev) if g_rgb is None else g_rgb.float(),
+                         torch.zeros((), device=dev) if g_op is None else g_op.float()])
+        drgb, dop = torch.empty_like(rgb), torch.empty_like(opacity)
+        call("ncn_photo_loss_bwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(rgb.shape[0]), F32(ctx.w_op), ptr(loss),
+             ptr(g), ptr(drgb), ptr(dop), stream())
+        return drgb, None, dop, None
+
+
+def photo_losses(rgb, rgb_gt, opacity, w_opacity):
+    """(rgb MSE, weighted opacity entropy), each 0 when non-finite (losses.py:246-262)."""
+    f = lambda t: t.float().contiguous()
+    check_input(rgb, "rgb")
+    check_input(opacity, "opacity")
+    if rgb.shape[0] != opacity.shape[0] or rgb_gt.shape != rgb.shape:
+        raise ValueError("photo_losses: rgb, rgb_gt and opacity must cover the same rays")
+    return _PhotoLoss.apply(f(rgb), f(rgb_gt), f(opacity), float(w_opacity))
+
+
+def _offsets_key(o):
+    """Cache key of a host patch-offset array; None for tensors (indexed on the device, never read)."""
+    if isinstance(o, torch.Tensor):
+        return None
+    return bytes(memoryview(np.ascontiguousarray(o, dtype=np.int64)))
 
 
 class NeRFMTLoss(nn.Module):
@@ -130,6 +222,7 @@ class NeRFMTLoss(nn.Module):
             assert self.ray_sampling_strategy in ["all_images_triang", "all_images_triang_val", "same_image_triang",
                                                   "all_images_triang_patch", "same_image_triang_patch"]
         self.last_cluster = None  # (labels, centroids, raw stats) of the last step, for logging/tests
+        self._idx_cache = {}
 
     @staticmethod
     def _validity(loss, dev):
@@ -160,9 +253,18 @@ class NeRFMTLoss(nn.Module):
             return {"x1": pix[:, 0], "x2": pix[:, 1], "x3": pix[:, 2]}
 
         def get_patch_triang_idx(seq_len, patch_s, off):
-            pix = einops.rearrange(torch.arange(0, seq_len, device=dev), "(n s) -> n s", s=patch_s)
-            return {k: einops.rearrange(pix[:, torch.as_tensor(off[k], device=dev)], "n s -> (n s)")
-                    for k in ("x1", "x2", "x3")}
+            # constant for a given (batch, patch, offsets): cached so the step issues no H2D copies
+            key = (seq_len, int(patch_s), str(dev)) + tuple(_offsets_key(off[k]) for k in ("x1", "x2", "x3"))
+            hit = None if None in key else self._idx_cache.get(key)
+            if hit is None:
+                pix = einops.rearrange(torch.arange(0, seq_len, device=dev), "(n s) -> n s", s=patch_s)
+                hit = {k: einops.rearrange(pix[:, torch.as_tensor(off[k], device=dev)], "n s -> (n s)").contiguous()
+                       for k in ("x1", "x2", "x3")}
+                if None not in key:
+                    if len(self._idx_cache) > 16:
+                        self._idx_cache.clear()
+                    self._idx_cache[key] = hit
+            return hit
 
         n_unsup, n_w_gt = pred_unsup["depth"].shape[0], pred_w_gt["rgb"].shape[0]
         if self.ray_sampling_strategy in ["all_images_triang", "same_image_triang"]:
@@ -173,7 +275,10 @@ class NeRFMTLoss(nn.Module):
                    "x3": target_raw["x3_offsets_local"]}
             pred_w_gt["x123_idx"] = get_patch_triang_idx(n_w_gt, target_raw["patch_area"], off)
             pred_unsup["x123_idx"] = get_patch_triang_idx(n_unsup, target_raw["patch_area"], off)
-        if self.pred_norm_depth:
+        clustering = self.norm_D_C_ort_dot_w > 0 or self.norm_D_C_centr_dot_w > 0 or self.norm_D_C_centr_L1_w > 0
+        fuse_normals = (clustering and self.pred_norm_depth and unsup_start == 0 and self.norm_DEpth_L1_w == 0
+                        and self.norm_DEpth_dot_w == 0)
+        if self.pred_norm_depth and not fuse_normals:
             pred_w_gt["norm_depth"] = extract_normals_from_ray_batch(pred_w_gt["rays_o"], pred_w_gt["rays_d"],
                                                                      pred_w_gt["depth"], pred_w_gt["x123_idx"])
             if unsup_start == 0:
@@ -182,9 +287,13 @@ class NeRFMTLoss(nn.Module):
                 pred_unsup["norm_depth"] = extract_normals_from_ray_batch(pred_unsup["rays_o"], pred_unsup["rays_d"],
                                                                           pred_unsup["depth"], pred_unsup["x123_idx"])
         loss_d = {}
-        rgb_loss = ((pred_w_gt["rgb"] - target_gt["rgb"]) ** 2).mean()
-        loss_d["rgb"] = self._validity(rgb_loss, dev)
-        if self.opacity_w > 0:
+        if self.opacity_w > 0 and pred_w_gt["rgb"].shape[0] == pred_unsup["opacity"].shape[0]:
+            loss_d["rgb"], loss_d["opacity"] = photo_losses(pred_w_gt["rgb"], target_gt["rgb"], pred_unsup["opacity"],
+                                                            self.opacity_w)
+        else:
+            rgb_loss = ((pred_w_gt["rgb"] - target_gt["rgb"]) ** 2).mean()
+            loss_d["rgb"] = self._validity(rgb_loss, dev)
+        if self.opacity_w > 0 and "opacity" not in loss_d:
             o = pred_unsup["opacity"] + 1e-10
             loss_d["opacity"] = self._validity(self.opacity_w * (-o * torch.log(o)).mean(), dev)
         if self.depth_w > 0:
@@ -204,14 +313,19 @@ class NeRFMTLoss(nn.Module):
             d_pred, x = pred_unsup["depth"], pred_unsup["x123_idx"]
             reg = ((d_pred[x["x1"]] - d_pred[x["x2"]]) ** 2 + (d_pred[x["x1"]] - d_pred[x["x3"]]) ** 2).mean()
             loss_d["reg_depth"] = self._validity(reg, dev)
-        if self.norm_D_C_ort_dot_w > 0 or self.norm_D_C_centr_dot_w > 0 or self.norm_D_C_centr_L1_w > 0:
+        if clustering:
             step = kwargs["global_step"]
             if step <= self.can_sched_end or self.can_sched_end == -1:
                 w = (self.w_sched(self.norm_D_C_ort_dot_w, step), self.w_sched(self.norm_D_C_centr_dot_w, step),
                      self.w_sched(self.norm_D_C_centr_L1_w, step))
-                terms, labels, cents, raw = cluster_losses(pred_unsup["norm_depth"], K=20, niter=20,
-                                                           seed=self.kmeans_seed,
-                                                           t_similar=1.0 - self.norm_CAN_tres, w=w)
+                if fuse_normals:
+                    terms, _normals, labels, cents, raw = normals_cluster_losses(
+                        pred_unsup["rays_o"], pred_unsup["rays_d"], pred_unsup["depth"], pred_unsup["x123_idx"], K=20,
+                        niter=20, seed=self.kmeans_seed, t_similar=1.0 - self.norm_CAN_tres, w=w)
+                else:
+                    terms, labels, cents, raw = cluster_losses(pred_unsup["norm_depth"], K=20, niter=20,
+                                                               seed=self.kmeans_seed,
+                                                               t_similar=1.0 - self.norm_CAN_tres, w=w)
                 loss_d["norm_D_C_ort_dot"] = terms[0]
                 loss_d["norm_D_C_centr_dot"] = terms[1]
                 loss_d["norm_D_C_centr_L1"] = terms[2]

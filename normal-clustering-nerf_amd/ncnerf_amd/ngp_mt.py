@@ -82,7 +82,7 @@ class _FieldFunction(torch.autograd.Function):
         enc = None
         if need_grad:
             enc = torch.empty(((n + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev)
-        packed = model._pack_weights()
+        packed = model._take_packed()
         call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(table), model._levels_ptr,
              F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(mode), ptr(sigmas),
              ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
@@ -187,6 +187,17 @@ class NGPMT(nn.Module):
                     v.zero_()
                 p.grad = v
         return fg[:n_table], fg[n_table:]
+
+    def prepare_weights(self):
+        """Pack the MLP weights now (after the optimizer step) so the next forward reuses them."""
+        self._pack_weights()
+        self._packed_fresh = True
+
+    def _take_packed(self):
+        if getattr(self, "_packed_fresh", False) and self._packed is not None:
+            self._packed_fresh = False
+            return self._packed
+        return self._pack_weights()
 
     def _pack_weights(self):
         if self._packed is None or self._packed.device != self._flat.device:

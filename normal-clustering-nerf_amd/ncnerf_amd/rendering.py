@@ -22,7 +22,8 @@ def render(model, rays_o, rays_d, **kwargs):
     rays_o = rays_o.contiguous()
     rays_d = rays_d.contiguous()
     _, hits_t, _ = RayAABBIntersector.apply(rays_o, rays_d, model.center, model.half_size, 1)
-    hits_t[(hits_t[:, 0, 0] >= 0) & (hits_t[:, 0, 0] < near_distance), 0, 0] = near_distance
+    t0 = hits_t[:, 0, 0]  # in-place masked fill on the view: no nonzero() host sync
+    t0.masked_fill_((t0 >= 0) & (t0 < near_distance), near_distance)
     render_func = render_rays_test if kwargs.get("test_time", False) else render_rays_train
     results = render_func(model, rays_o, rays_d, hits_t, **kwargs)
     for k, v in results.items():
@@ -118,6 +119,8 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
             hits_t[:, 0, 1] = torch.min(depth + n_i * (hits_t[:, 0, 1] - depth), hits_t[:, 0, 1])
         else:
             assert strategy == "none"
+    if hasattr(model, "prepare_weights"):
+        model.prepare_weights()  # queue the fp16 weight packing ahead of the marcher's host read of S
     rays_a, xyzs, dirs, results["deltas"], results["ts"], results["rm_samples"] = RayMarcher.apply(
         rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
         model.grid_size, max_samples, kwargs.get("march_noise"))
@@ -146,9 +149,10 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     results["rays_o"] = rays_d  # rendering.py:227 (quirk q1)
     results["rays_a"] = rays_a
     results["depth_std"] = torch.ones_like(results["depth"], requires_grad=False)
-    if exp_step_factor == 0:
-        rgb_bg = torch.ones(3, device=rays_o.device)
-    elif kwargs.get("random_bg", False):
+    if exp_step_factor == 0:  # white: rgb + 1 * (1 - opacity), the multiply by 1 is exact
+        results["rgb"] = results["rgb"] + (1 - results["opacity"])[:, None]
+        return results
+    if kwargs.get("random_bg", False):
         rgb_bg = torch.rand(3, device=rays_o.device)
     else:
         rgb_bg = torch.zeros(3, device=rays_o.device)

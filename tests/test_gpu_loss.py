@@ -78,3 +78,63 @@ def test_cluster_loss_too_few(dev):
     Xd = torch.from_numpy(X).to(dev)
     terms, labels, cents, raw = L.cluster_losses(Xd, K=20)
     assert float(terms.abs().sum()) == 0.0 and float(raw[3]) == 12
+
+
+def _depth_batch(dev, R, seed):
+    """Depths of a tilted plane seen through patch rays, so the normals form a few clusters."""
+    rng = np.random.default_rng(seed)
+    x1, x2, x3 = losses_ref.patch_triangle_index(R)
+    d = rng.normal(size=(R, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    depth = rng.uniform(0.5, 2.0, R).astype(np.float32)
+    idx = {k: torch.from_numpy(v).to(dev) for k, v in zip(("x1", "x2", "x3"), (x1, x2, x3))}
+    return torch.from_numpy(d).to(dev), torch.from_numpy(depth).to(dev), idx
+
+
+def test_fused_normals_cluster_matches_unfused(dev):
+    """normals_cluster_losses (one autograd node, device-side term weights in ncn_normals_bwd) must
+    give the same terms and depth gradient as extract_normals_from_ray_batch + cluster_losses.
+    Tolerance: terms |d| <= 1e-7 (same kernels), d depth rel-L2 <= 1e-5 (summation order)."""
+    d, depth, idx = _depth_batch(dev, 8192, 3)
+    w = (2e-3, 3e-3, 5e-3)
+    g = torch.tensor([1.0, 0.5, 2.0], device=dev)
+    d1 = depth.clone().requires_grad_(True)
+    n = L.extract_normals_from_ray_batch(d, d, d1, idx)
+    t1, lab1, c1, _ = L.cluster_losses(n, w=w)
+    (t1 * g).sum().backward()
+    d2 = depth.clone().requires_grad_(True)
+    t2, n2, lab2, c2, _ = L.normals_cluster_losses(d, d, d2, idx, w=w)
+    (t2 * g).sum().backward()
+    torch.testing.assert_close(n2, n.detach(), rtol=0, atol=0)
+    assert torch.equal(lab1, lab2)
+    torch.testing.assert_close(t2, t1.detach(), rtol=0, atol=1e-7)
+    rel = (d2.grad - d1.grad).norm() / d1.grad.norm().clamp_min(1e-30)
+    assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("R,bad", [(8192, False), (1000, False), (4096, True)])
+def test_photo_losses(dev, R, bad):
+    """ncn_photo_loss_fwd/bwd vs the torch expressions of losses.py:349-362 (+ validity filter).
+    Tolerance: values rel 1e-5, gradients rel 1e-5; a NaN rgb zeroes that term and its gradient."""
+    gen = torch.Generator(device="cpu").manual_seed(R)
+    rgb = torch.rand(R, 3, generator=gen).to(dev)
+    gt = torch.rand(R, 3, generator=gen).to(dev)
+    op = torch.rand(R, generator=gen).to(dev)
+    if bad:
+        rgb[7, 1] = float("nan")
+    a, b = rgb.clone().requires_grad_(True), op.clone().requires_grad_(True)
+    l_rgb, l_op = L.photo_losses(a, gt, b, 1e-3)
+    (2.0 * l_rgb + 3.0 * l_op).backward()
+    a2, b2 = rgb.clone().requires_grad_(True), op.clone().requires_grad_(True)
+    r2 = ((a2 - gt) ** 2).mean()
+    o = b2 + 1e-10
+    e2 = 1e-3 * (-o * torch.log(o)).mean()
+    ok = bool(torch.isfinite(r2))
+    (2.0 * (r2 if ok else 0 * r2.nan_to_num()) + 3.0 * e2).backward()
+    if ok:
+        torch.testing.assert_close(l_rgb, r2.detach(), rtol=1e-5, atol=0)
+        torch.testing.assert_close(a.grad, a2.grad, rtol=1e-5, atol=1e-12)
+    else:
+        assert float(l_rgb) == 0.0 and float(a.grad.abs().sum()) == 0.0
+    torch.testing.assert_close(l_op, e2.detach(), rtol=1e-5, atol=0)
+    torch.testing.assert_close(b.grad, b2.grad, rtol=1e-5, atol=1e-12)
