@@ -92,13 +92,17 @@ int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void
 int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* table, const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int mode,
                   float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
-/* Backward: accumulates (+=) into grad_table (n_entries,2) with f32 atomics and writes per-block
- * weight-gradient slabs (n_blocks x NCN_FIELD_NW) into `slab`; ncn_field_reduce_wgrad sums them
- * into grad_w (+=).  n_blocks is returned by ncn_field_bwd_blocks(n). */
+/* Backward: accumulates (+=) into grad_table (n_entries,2) and writes per-block weight-gradient
+ * slabs (n_blocks x NCN_FIELD_NW) into `slab`; ncn_field_reduce_wgrad sums them into grad_w (+=).
+ * n_blocks is returned by ncn_field_bwd_blocks(n).  dE_ws is a device workspace of
+ * ncn_field_bwd_dE_floats(n) floats (the level-major encoding gradient between the MLP pass and the
+ * LDS-aggregating table scatter pass). */
 int ncn_field_bwd_blocks(int64_t n);
+int64_t ncn_field_bwd_dE_floats(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_t* levels, float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
-                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, void* stream);
+                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
+                  void* stream);
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream);
 
 /* ---- normal clustering loss path: replaces _extract_normals_from_ray_batch

@@ -99,7 +99,10 @@ __device__ __forceinline__ uint32_t grid_index(uint32_t params, uint32_t res, ui
     if (stride <= params) { index += y * stride; stride *= res; }
     if (stride <= params) { index += z * stride; stride *= res; }
     if (params < stride) index = x ^ (y * 2654435761u) ^ (z * 805459861u);
-    return index % params;
+    // index % params without a 32-bit division: a hashed level always has params = 2^log2_T (a
+    // power of two), a dense level has index < res^3 <= params.  Same result as the modulo.
+    if ((params & (params - 1)) == 0) return index & (params - 1);
+    return index < params ? index : index % params;
 }
 
 struct LevelPos {
@@ -141,17 +144,7 @@ __device__ __forceinline__ float2 encode_level(const float2* __restrict__ tab, c
     return acc;
 }
 
-// Backward scatter of one level for the 16 samples of a lane group (lanes 16g..16g+15 hold 16
-// consecutive samples, i.e. mostly consecutive points of one ray).
-//  1. Runs: lanes whose samples fall in the same base cell form runs; a segmented suffix sum over
-//     each run (4 doubling steps with DPP row shifts inside the 16-lane row) leaves the run total in
-//     its head lane.  At the coarse levels a group usually shares one cell: up to 16x fewer atomics
-//     on the few thousand hot entries.
-//  2. Coalescing: the two corners that differ only in x (tcnn's hash multiplies x by 1, so their
-//     entries are adjacent for dense levels and share a 64-B line 7/8 of the time for hashed ones)
-//     x 2 features = 16 contiguous bytes.  A quad of lanes takes one source lane's 4 values
-//     (quad_perm broadcast), so each f32-atomic instruction touches ~16 lines instead of 64:
-//     scattered single-lane atomics run ~17x below the coalesced atomic rate on MI355X.
+// DPP helpers (16-lane rows)
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -162,62 +155,11 @@ __device__ __forceinline__ int dppi(int v) {
 }
 constexpr int DPP_ROW_SL(int k) { return 0x100 + k; }  // dst[r] = src[r+k] inside a 16-lane row
 constexpr int DPP_ROW_SR(int k) { return 0x110 + k; }  // dst[r] = src[r-k]
-constexpr int DPP_QUAD_BCAST(int t) { return t * 0x55; }  // quad_perm [t,t,t,t]
 
 template <int K>
 __device__ __forceinline__ void run_sum(float& v, const int (&link)[4]) {
     const float t = dppf<DPP_ROW_SL(1 << K)>(v);
     if (link[K]) v += t;
-}
-
-template <int T>
-__device__ __forceinline__ void quad_atomics(float* __restrict__ grad, int j, bool head, const float (&V)[4],
-                                             uint32_t i0, uint32_t i1) {
-    const int bh = dppi<DPP_QUAD_BCAST(T)>((int)head);
-    const float b0 = dppf<DPP_QUAD_BCAST(T)>(V[0]), b1 = dppf<DPP_QUAD_BCAST(T)>(V[1]);
-    const float b2 = dppf<DPP_QUAD_BCAST(T)>(V[2]), b3 = dppf<DPP_QUAD_BCAST(T)>(V[3]);
-    const uint32_t e0 = (uint32_t)dppi<DPP_QUAD_BCAST(T)>((int)i0), e1 = (uint32_t)dppi<DPP_QUAD_BCAST(T)>((int)i1);
-    const float val = j == 0 ? b0 : (j == 1 ? b1 : (j == 2 ? b2 : b3));
-    const uint32_t e = j < 2 ? e0 : e1;
-    if (bh) atomicAdd(grad + 2 * (size_t)e + (j & 1), val);
-}
-
-__device__ __forceinline__ void scatter_level(float* __restrict__ grad, const LevelTable& L, int l, float x, float y,
-                                              float z, float g0, float g1, bool valid, int r, int lane) {
-    const LevelPos p = level_pos(L.scale[l], x, y, z);
-    const uint32_t params = L.params[l], res = L.res[l], off = L.offset[l];
-    // run structure from the base cell (a sample outside [0,n) gets a key no valid sample has)
-    const int key = valid ? (int)(p.px + res * (p.py + res * p.pz)) : (int)(0xFFFFFFF0u - (uint32_t)r);
-    const int key_next = dppi<DPP_ROW_SL(1)>(key);
-    const int key_prev = dppi<DPP_ROW_SR(1)>(key);
-    int link[4];
-    link[0] = (r < 15) && (key_next == key);
-    link[1] = link[0] && dppi<DPP_ROW_SL(1)>(link[0]);
-    link[2] = link[1] && dppi<DPP_ROW_SL(2)>(link[1]);
-    link[3] = link[2] && dppi<DPP_ROW_SL(4)>(link[2]);
-    const bool head = valid && (r == 0 || key_prev != key);
-    const int j = lane & 3;
-#pragma unroll
-    for (int cp = 0; cp < 4; cp++) {  // corner pair: (x, x+1) at (y + (cp&1), z + (cp>>1))
-        const uint32_t cy = p.py + (cp & 1), cz = p.pz + (cp >> 1);
-        const float wy = (cp & 1) ? p.fy : 1.0f - p.fy;
-        const float wz = (cp & 2) ? p.fz : 1.0f - p.fz;
-        const float w0 = ((1.0f - p.fx) * wy) * wz, w1 = (p.fx * wy) * wz;
-        float V[4] = {valid ? w0 * g0 : 0.f, valid ? w0 * g1 : 0.f, valid ? w1 * g0 : 0.f, valid ? w1 * g1 : 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            run_sum<0>(V[q], link);
-            run_sum<1>(V[q], link);
-            run_sum<2>(V[q], link);
-            run_sum<3>(V[q], link);
-        }
-        const uint32_t i0 = off + grid_index(params, res, p.px, cy, cz);
-        const uint32_t i1 = off + grid_index(params, res, p.px + 1, cy, cz);
-        quad_atomics<0>(grad, j, head, V, i0, i1);
-        quad_atomics<1>(grad, j, head, V, i0, i1);
-        quad_atomics<2>(grad, j, head, V, i0, i1);
-        quad_atomics<3>(grad, j, head, V, i0, i1);
-    }
 }
 
 __device__ __forceinline__ half4_t frag(const half4_t* __restrict__ lds_frags, int f, int lane) {
@@ -389,21 +331,18 @@ __device__ __forceinline__ half4_t transpose_tile_h(_Float16* slot, int lane, ha
 }
 
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
-    const float* __restrict__ xyzs, const float* __restrict__ dirs, int64_t n, LevelTable Lt, float xyz_min,
-    float xyz_extent, const half4_t* __restrict__ wpacked, const half4_t* __restrict__ enc_cache,
-    const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb, float* __restrict__ grad_table,
-    float* __restrict__ slab) {
+    const float* __restrict__ dirs, int64_t n, const half4_t* __restrict__ wpacked,
+    const half4_t* __restrict__ enc_cache, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
+    float* __restrict__ dE_out, float* __restrict__ slab) {
     // One LDS arena: [fragments | transpose slots] during the loop, reused as the fp32 dW
     // reduction buffer afterwards (43 KB total -> several workgroups per CU).
     constexpr int FRAG_BYTES = N_FRAGS * 64 * 8, SLOT_BYTES = 4 * 2 * 256 * 2;
     static_assert(FRAG_BYTES + SLOT_BYTES >= NCN_FIELD_NW * 4, "arena too small for the dW reduction");
     __shared__ __attribute__((aligned(16))) char arena[FRAG_BYTES + SLOT_BYTES];
-    __shared__ LevelTable L;
     half4_t* F = (half4_t*)arena;
     _Float16* tslots = (_Float16*)(arena + FRAG_BYTES);
     float* red = (float*)arena;
     for (int i = threadIdx.x; i < N_FRAGS * 64; i += BWD_THREADS) F[i] = wpacked[i];
-    load_levels(L, Lt);
     __syncthreads();
     const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, wid = threadIdx.x >> 6;
     _Float16* sA = tslots + wid * 512;
@@ -495,18 +434,15 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             for (int ks = 0; ks < 4; ks++) v = mfma16(frag(F, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
             dE[t] = v;
         }
-        {
-            float x = 0.f, y = 0.f, z = 0.f;
-            if (valid) {
-                x = (xyzs[3 * s] - xyz_min) / xyz_extent;
-                y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
-                z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
-            }
-            scatter_level(grad_table, L, 2 * g, x, y, z, dE[0][0], dE[0][1], valid, r, lane);
-            scatter_level(grad_table, L, 2 * g + 1, x, y, z, dE[0][2], dE[0][3], valid, r, lane);
-            scatter_level(grad_table, L, 8 + 2 * g, x, y, z, dE[1][0], dE[1][1], valid, r, lane);
-            scatter_level(grad_table, L, 9 + 2 * g, x, y, z, dE[1][2], dE[1][3], valid, r, lane);
+        // encoding gradient -> level-major [16][n] float2 for the scatter pass
+        if (valid) {
+            float2* o = (float2*)dE_out;
+            o[(int64_t)(2 * g) * n + s] = make_float2(dE[0][0], dE[0][1]);
+            o[(int64_t)(2 * g + 1) * n + s] = make_float2(dE[0][2], dE[0][3]);
+            o[(int64_t)(8 + 2 * g) * n + s] = make_float2(dE[1][0], dE[1][1]);
+            o[(int64_t)(9 + 2 * g) * n + s] = make_float2(dE[1][2], dE[1][3]);
         }
+#ifndef NCN_DIAG_NO_DW
         // ---- weight gradients: dW[out][in] += sum_s dY[out][s] X[in][s] ----
         // A operand = dY^T rows (out, lane r) over K = samples; B operand = X over K = samples.
         {   // L5: dY = dy5 (1 out tile), X = x5 (4 in tiles)
@@ -550,6 +486,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
                 acc.w1[a][1] = mfma16(A, X1, acc.w1[a][1]);
             }
         }
+#endif
     }
     // ---- workgroup reduction of the 40 tiles into LDS (C layout: row 4g+i, col r) ----
     __syncthreads();  // every wave is done with the fragments / slots: reuse the arena
@@ -605,6 +542,304 @@ __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb, floa
     atomicAdd(gw + i, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Scatter of the encoding gradient into the fp32 table gradient (tcnn kernel_grid_backward).
+// Hash-grid gradients are extremely local: the rays of a patch re-touch the same few entries per
+// level hundreds of times, so a workgroup owns one span of consecutive samples
+// (~1/4 patch) and, level by level, aggregates every contribution in an LDS hash table before
+// anything reaches memory (4096 direct-mapped slots: 16 KB keys + 64 KB int64 sums):
+//  1. consecutive samples (lanes) in the same base cell are merged first with DPP run sums inside
+//     each 16-lane row (all 8 corners shared);
+//  2. run heads look up their 8 corners (one ds_read round trip, ds_cmpst_b32 to claim an empty
+//     slot) and add with ds_add_u64 into 64-bit FIXED-POINT sums: on gfx950 an LDS f32 atomic
+//     costs ~3 cycles per active lane (193 cycles per wave-instruction, tools/lds_atomic_bench),
+//     an LDS u64 atomic add ~13 cycles per wave-instruction.  The fixed point is exact integer
+//     arithmetic (order-independent, reproducible): per (workgroup, level) the scale is 2^k with
+//     k = 46 - e, max|dE| < 2^e, so a value within 2^23 of the level's maximum converts exactly
+//     and the LDS sum (< 2^15 contributions) cannot overflow;
+//  3. at the end of a level (or when a quarter of the slots are taken) the table is flushed: two
+//     lanes per slot, each converts its sum back to f32 and issues one f32 global atomic.
+// A contribution whose slot holds another entry (collision) goes straight to a global atomic, as
+// does a whole level whose gradient is not finite (NaN/Inf propagate as in the f32 path).
+#ifdef NCN_DIAG_PHASES
+__device__ unsigned long long ncn_sc_phase[8];
+#define SC_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define SC_ACC(i, a, b) ph[i] += (b) - (a)
+#else
+#define SC_T(v)
+#define SC_ACC(i, a, b)
+#endif
+constexpr int SC_THREADS = 1024;
+constexpr int SC_LOG2_TS = 12;
+constexpr int SC_TS = 1 << SC_LOG2_TS;
+constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
+#ifndef SC_MERGE_LEVELS
+#define SC_MERGE_LEVELS 16
+#endif
+
+__device__ __forceinline__ uint32_t sc_pair(uint32_t e) { return (e * 0x9E3779B1u) >> (33 - SC_LOG2_TS); }
+
+// round(v * 2^k) as int64 for |v * 2^k| < 2^46 without f64: split at 2^23 into two exact int32s
+__device__ __forceinline__ long long sc_fix(float v, int k) {
+    const float x = ldexpf(v, k - 23);   // |x| < 2^23
+    const float hi = truncf(x);          // exact
+    const float lo = ldexpf(x - hi, 23); // exact fraction, |lo| < 2^23
+    return ((long long)(int)hi << 23) + (long long)(int)rintf(lo);
+}
+
+// Flush: two lanes per slot (x and y of one entry are adjacent floats, so an atomic instruction
+// writes 8-B pieces), every lane's keys and sums read in one LDS round trip, one f32 global
+// atomic per non-zero sum; the slots are then reset.
+__device__ __forceinline__ void sc_flush(uint32_t* keys, long long* valx, long long* valy, int* fill,
+                                         float* __restrict__ grad, uint32_t off, int k) {
+    constexpr int PER = 2 * SC_TS / SC_THREADS;
+    uint32_t key[PER];
+    long long q[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int i = threadIdx.x + j * SC_THREADS, slot = i >> 1;
+        key[j] = keys[slot];
+        q[j] = (i & 1) ? valy[slot] : valx[slot];
+    }
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int i = threadIdx.x + j * SC_THREADS;
+#ifdef NCN_DIAG_SC_NO_GATOMIC
+        if (key[j] != SC_EMPTY && q[j] == 12345) grad[2 * (size_t)(off + key[j]) + (i & 1)] = 1.f;
+#else
+        if (key[j] != SC_EMPTY && q[j] != 0)
+            atomicAdd(grad + 2 * (size_t)(off + key[j]) + (i & 1), (float)ldexp((double)q[j], -k));
+#endif
+    }
+    __syncthreads();  // every lane has read its slots
+    for (int i = threadIdx.x; i < SC_TS; i += SC_THREADS) {
+        keys[i] = SC_EMPTY;
+        valx[i] = 0;
+        valy[i] = 0;
+    }
+    if (threadIdx.x == 0) *fill = 0;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                                   LevelTable Lt, float xyz_min, float xyz_extent,
+                                                                   const float2* __restrict__ dE, int64_t span,
+                                                                   float* __restrict__ grad) {
+    __shared__ uint32_t keys[SC_TS];
+    __shared__ long long valx[SC_TS], valy[SC_TS];
+    __shared__ int fill;
+    __shared__ float wmax[SC_THREADS / 64][16];
+    __shared__ float lmax[16];
+    for (int i = threadIdx.x; i < SC_TS; i += SC_THREADS) {
+        keys[i] = SC_EMPTY;
+        valx[i] = 0;
+        valy[i] = 0;
+    }
+    if (threadIdx.x == 0) fill = 0;
+    const int lane = threadIdx.x & 63, r = lane & 15, wid = threadIdx.x >> 6;
+    const int64_t s0 = (int64_t)blockIdx.x * span, s1 = min(n, s0 + span);
+    // fixed-point scale per level: max |dE| over the span, all 16 levels in one load round
+    {
+        float m[16];
+#pragma unroll
+        for (int l = 0; l < 16; l++) m[l] = 0.f;
+        for (int64_t s = s0 + threadIdx.x; s < s1; s += SC_THREADS) {
+#pragma unroll
+            for (int l = 0; l < 16; l++) {
+                const float2 g = dE[(int64_t)l * n + s];
+                const float a = fmaxf(fabsf(g.x), fabsf(g.y));
+                m[l] = (isfinite(g.x) && isfinite(g.y)) ? fmaxf(m[l], a) : INFINITY;
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < 16; l++) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m[l] = fmaxf(m[l], __shfl_xor(m[l], o, 64));
+        }
+        if (lane < 16) {
+            float v = m[0];
+#pragma unroll
+            for (int l = 1; l < 16; l++) v = lane == l ? m[l] : v;
+            wmax[wid][lane] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            float v = 0.f;
+            for (int w = 0; w < SC_THREADS / 64; w++) v = fmaxf(v, wmax[w][threadIdx.x]);
+            lmax[threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    // the span is cut into nchunk EQUAL chunks (<= SC_THREADS samples each) so that no chunk
+    // leaves most waves idle at its barrier
+    const int nchunk = (int)((s1 - s0 + SC_THREADS - 1) / SC_THREADS);
+    const int64_t len = s1 - s0;
+    const int total = 16 * max(nchunk, 0);
+    // software pipeline over (level, chunk): the next item's loads are in flight while this one
+    // is aggregated
+    auto load = [&](int it, float& x, float& y, float& z, float2& g) {
+        const int l = it / nchunk, ch = it - l * nchunk;
+        const int64_t c0 = s0 + len * ch / nchunk, c1 = s0 + len * (ch + 1) / nchunk;
+        const int64_t s = c0 + threadIdx.x;
+        x = y = z = 0.f;
+        g = make_float2(0.f, 0.f);
+        if (s < c1) {
+            x = xyzs[3 * s];
+            y = xyzs[3 * s + 1];
+            z = xyzs[3 * s + 2];
+            g = dE[(int64_t)l * n + s];
+        }
+    };
+    float nx, ny, nz;
+    float2 ng;
+    if (total > 0) load(0, nx, ny, nz, ng);
+#ifdef NCN_DIAG_PHASES
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    for (int it = 0; it < total; it++) {
+        SC_T(t0);
+        const int l = it / nchunk, ch = it - l * nchunk;
+        const float m = lmax[l];
+        if (m == 0.f) {  // uniform: nothing at this level; keep the pipeline moving
+            if (it + 1 < total) load(it + 1, nx, ny, nz, ng);
+            continue;
+        }
+        const float scale = Lt.scale[l];
+        const uint32_t res = Lt.res[l], params = Lt.params[l], off = Lt.offset[l];
+        const bool dense = (uint64_t)res * res * res <= params;  // tcnn: stride stays <= params
+        const bool direct = !isfinite(m);
+        int e2 = 0;
+        (void)frexpf(direct ? 1.f : m, &e2);  // m < 2^e2
+        const int k = 46 - e2;
+        const int64_t c1 = s0 + len * (ch + 1) / nchunk;
+        const int64_t s = s0 + len * ch / nchunk + threadIdx.x;
+        const float x = (nx - xyz_min) / xyz_extent, y = (ny - xyz_min) / xyz_extent, z = (nz - xyz_min) / xyz_extent;
+        const float2 gv = ng;
+        if (it + 1 < total) load(it + 1, nx, ny, nz, ng);
+        const bool valid = s < c1 && ((gv.x != 0.f) || (gv.y != 0.f));
+        const LevelPos p = level_pos(scale, x, y, z);
+        // corner weights in the forward's association ((wx * wy) * wz) and entry indices without
+        // per-corner grid_index branches: dense = base + dx + dy*res + dz*res^2, hashed =
+        // ((x+dx) ^ (y+dy)*P1 ^ (z+dz)*P2) & (params-1) (params is 2^19 on every hashed level)
+        const float wx[2] = {1.0f - p.fx, p.fx}, wy[2] = {1.0f - p.fy, p.fy}, wz[2] = {1.0f - p.fz, p.fz};
+        uint32_t e[8];
+        if (dense) {
+            const uint32_t b0 = p.px + res * p.py + res * res * p.pz;
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                e[c] = b0 + (c & 1) + ((c >> 1) & 1) * res + ((c >> 2) & 1) * res * res;
+                e[c] = e[c] < params ? e[c] : e[c] % params;  // as grid_index (boundary corner)
+            }
+        } else {
+            const uint32_t hy0 = p.py * 2654435761u, hy1 = (p.py + 1) * 2654435761u;
+            const uint32_t hz0 = p.pz * 805459861u, hz1 = (p.pz + 1) * 805459861u;
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+                e[c] = ((p.px + (c & 1)) ^ ((c & 2) ? hy1 : hy0) ^ ((c & 4) ? hz1 : hz0)) & (params - 1);
+        }
+        // runs of lanes in the same base cell, merged with DPP suffix sums inside each 16-lane row
+        // (an inactive lane gets a key nobody else has).  Coarse levels only: from level
+        // SC_MERGE_LEVELS on most lanes head their own run and the merge would cost more VALU
+        // than the LDS traffic it saves.
+        bool head = valid;
+        float v0[8], v1[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+            v0[c] = valid ? w * gv.x : 0.f;
+            v1[c] = valid ? w * gv.y : 0.f;
+        }
+        if (l < SC_MERGE_LEVELS) {
+            const int key = valid ? (int)(p.px + res * (p.py + res * p.pz)) : (int)(0xFFFFFFF0u - (uint32_t)r);
+            const int key_next = dppi<DPP_ROW_SL(1)>(key);
+            const int key_prev = dppi<DPP_ROW_SR(1)>(key);
+            int link[4];
+            link[0] = (r < 15) && (key_next == key);
+            link[1] = link[0] && dppi<DPP_ROW_SL(1)>(link[0]);
+            link[2] = link[1] && dppi<DPP_ROW_SL(2)>(link[1]);
+            link[3] = link[2] && dppi<DPP_ROW_SL(4)>(link[2]);
+            head = valid && (r == 0 || key_prev != key);
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                run_sum<0>(v0[c], link); run_sum<0>(v1[c], link);
+                run_sum<1>(v0[c], link); run_sum<1>(v1[c], link);
+                run_sum<2>(v0[c], link); run_sum<2>(v1[c], link);
+                run_sum<3>(v0[c], link); run_sum<3>(v1[c], link);
+            }
+        }
+        int inserted = 0;
+        if (head && direct) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                atomicAdd(grad + 2 * (size_t)(off + e[c]), v0[c]);
+                atomicAdd(grad + 2 * (size_t)(off + e[c]) + 1, v1[c]);
+            }
+        }
+        SC_T(t1);
+        if (head && !direct) {
+            // 2-way set-associative lookup: both keys of the aligned slot pair in one ds_read_b64
+            uint2 kk[8];
+            int slot[8];
+#pragma unroll
+            for (int c = 0; c < 8; c++) kk[c] = *(const uint2*)&keys[2 * sc_pair(e[c])];
+            int claim[8];
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const int p0 = 2 * sc_pair(e[c]);
+                slot[c] = kk[c].x == e[c] ? p0 : (kk[c].y == e[c] ? p0 + 1 : -1);
+                // claim the first slot of the pair seen empty
+                claim[c] = slot[c] >= 0 ? -1 : (kk[c].x == SC_EMPTY ? p0 : (kk[c].y == SC_EMPTY ? p0 + 1 : -1));
+            }
+            uint32_t got[8];
+#pragma unroll
+            for (int c = 0; c < 8; c++) got[c] = claim[c] >= 0 ? atomicCAS(&keys[claim[c]], SC_EMPTY, e[c]) : 0u;
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                if (claim[c] >= 0) {
+                    if (got[c] == SC_EMPTY) { slot[c] = claim[c]; inserted++; }
+                    else if (got[c] == e[c]) slot[c] = claim[c];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                if (slot[c] >= 0) {
+                    atomicAdd((unsigned long long*)&valx[slot[c]], (unsigned long long)sc_fix(v0[c], k));
+                    atomicAdd((unsigned long long*)&valy[slot[c]], (unsigned long long)sc_fix(v1[c], k));
+                } else {
+#ifdef NCN_DIAG_SC_NO_FALLBACK
+                    if (v0[c] == 1234.5f) grad[c] = v1[c];
+#else
+                    atomicAdd(grad + 2 * (size_t)(off + e[c]), v0[c]);
+                    atomicAdd(grad + 2 * (size_t)(off + e[c]) + 1, v1[c]);
+#endif
+                }
+            }
+        }
+        SC_T(t2);
+        const int wins = (int)wave_sum((float)inserted);
+        if (lane == 0 && wins) atomicAdd(&fill, wins);
+        __syncthreads();
+        SC_T(t3);
+        if (ch == nchunk - 1 || fill > SC_TS / 4) sc_flush(keys, valx, valy, &fill, grad, off, k);
+        SC_T(t4);
+        SC_ACC(0, t0, t1);
+        SC_ACC(1, t1, t2);
+        SC_ACC(2, t2, t3);
+        SC_ACC(3, t3, t4);
+    }
+#ifdef NCN_DIAG_PHASES
+    if (threadIdx.x == 0 && blockIdx.x == 7)
+        for (int i = 0; i < 4; i++) ncn_sc_phase[i] = ph[i];
+#endif
+}
+
+static int64_t scatter_span(int64_t n) {
+    // one workgroup per CU (80 KB LDS): n/256 samples, at least 1024, at most 2048 (the fixed-point
+    // headroom assumes < 2^15 contributions per slot), a multiple of 64
+    int64_t sp = std::min<int64_t>(2048, std::max<int64_t>(1024, (n + 255) / 256));
+    return (sp + 63) / 64 * 64;
+}
+
 static LevelTable make_table(const uint32_t* levels) {
     LevelTable t;
     for (int l = 0; l < 16; l++) {
@@ -656,17 +891,31 @@ int ncn_field_bwd_blocks(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(512, (groups + 15) / 16));
 }
 
+int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * n : 0; }
+
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_t* levels, float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
-                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, void* stream) {
+                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
+                  void* stream) {
     if (n <= 0) return 0;
+    NCN_REQUIRE(((uintptr_t)dE_ws & 7) == 0, hipErrorInvalidValue, "ncn_field_bwd: dE_ws must be 8-byte aligned");
     const LevelTable Lt = make_table(levels);
     hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
-                       xyzs, dirs, n, Lt, xyz_min, xyz_extent, (const half4_t*)weights_packed,
-                       (const half4_t*)enc_cache, dL_dsigmas, dL_drgbs, grad_table, slab);
+                       dirs, n, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas, dL_drgbs,
+                       dE_ws, slab);
     NCN_LAUNCH_CHECK("ncn_field_bwd");
+    const int64_t span = scatter_span(n);
+    hipLaunchKernelGGL(field_scatter_kernel, dim3((unsigned)((n + span - 1) / span)), dim3(SC_THREADS), 0,
+                       (hipStream_t)stream, xyzs, n, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, span, grad_table);
+    NCN_LAUNCH_CHECK("ncn_field_bwd (scatter)");
     return 0;
 }
+
+#ifdef NCN_DIAG_PHASES
+int ncn_diag_read_phases(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_phase), 8 * sizeof(unsigned long long));
+}
+#endif
 
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream) {
     if (n_blocks <= 0) return 0;

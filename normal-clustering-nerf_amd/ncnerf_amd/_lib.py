@@ -34,7 +34,8 @@ SIGNATURES = {
     "ncn_field_pack_weights": [P, P, P],
     "ncn_field_fwd": [P, P, I64, P, P, F32, F32, P, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
-    "ncn_field_bwd": [P, P, I64, P, F32, F32, P, P, P, P, P, P, P],
+    "ncn_field_bwd_dE_floats": [I64],
+    "ncn_field_bwd": [P, P, I64, P, F32, F32, P, P, P, P, P, P, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],
@@ -71,6 +72,7 @@ def lib():
             fn.argtypes = args
             fn.restype = ctypes.c_int
         L.ncn_cluster_workspace_words.restype = ctypes.c_int64
+        L.ncn_field_bwd_dE_floats.restype = ctypes.c_int64
         L.ncn_last_error.argtypes = []
         L.ncn_last_error.restype = ctypes.c_char_p
         L.ncn_version.restype = ctypes.c_int

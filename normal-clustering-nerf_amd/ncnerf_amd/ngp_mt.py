@@ -102,10 +102,11 @@ class _FieldFunction(torch.autograd.Function):
         g_table, g_w = model._grad_views()
         nb = _lib.lib().ncn_field_bwd_blocks(I64(n))
         slab = torch.empty(nb * N_W, dtype=torch.float32, device=x.device)
+        dE_ws = torch.empty(int(_lib.lib().ncn_field_bwd_dE_floats(I64(n))), dtype=torch.float32, device=x.device)
         c = lambda t: None if t is None else t.contiguous().float()
         dsig, drgb = c(dL_dsigmas), c(dL_drgbs)
         call("ncn_field_bwd", ptr(x), ptr(d), I64(n), model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent),
-             ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), stream())
+             ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), ptr(dE_ws), stream())
         call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
         return None, None, None, None, None, None, None
 
