@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--rays", type=int, default=8192, help="rays per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grid-update", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager (Python-launched) step instead of a HIP graph")
     args = ap.parse_args()
 
     from ncnerf_amd import _lib, distributed
@@ -77,7 +78,7 @@ def main():
     with torch.no_grad():
         model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
         model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
-    trainer = Trainer(model, update_grid=not args.no_grid_update)
+    trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph)
     n_batches = 8
     batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
     step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
@@ -88,24 +89,39 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    _lib.TIMING = {n: [] for n in TIMED}
-    counts = []  # device scalars, summed after the timed region (no bookkeeping kernels inside it)
+    counts = []  # per-step device counts (copied: graph outputs are overwritten by the next replay)
+    if args.no_graph:
+        _lib.TIMING = {n: [] for n in TIMED}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         results, _ = trainer.step(batches[k % n_batches], global_step=step0 + args.warmup + k)
-        counts.append((results["rm_samples"], results["vr_samples"]))
+        counts.append((results["rm_samples"].clone(), results["vr_samples"].clone()))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    kcounts = counts
+    if not args.no_graph:
+        # Per-kernel durations: a graph replay has no host launch to bracket, so the same kernel
+        # sequence (the captured body) is run eagerly for `steps` more steps with HIP events on the
+        # launch stream around each hot kernel; the roofline uses those launches and their counts.
+        _lib.TIMING = {n: [] for n in TIMED}
+        kcounts = []
+        for k in range(args.steps):
+            b = batches[k % n_batches]
+            res, _ = trainer._body(b, torch.full((), step0, dtype=torch.int64, device=dev), True)
+            kcounts.append((res["rm_samples"].clone(), res["vr_samples"].clone()))
+        torch.cuda.synchronize()
     timing = _lib.TIMING
     _lib.TIMING = None
+    krm = sum(torch.as_tensor(a).double().sum() for a, _ in kcounts)
+    kvr = sum(torch.as_tensor(b).double().sum() for _, b in kcounts)
     rm = sum(torch.as_tensor(a).double().sum() for a, _ in counts)
     vr = sum(torch.as_tensor(b).double().sum() for _, b in counts)
     # composite_fw algorithmic bytes per launch: 24 B per composited sample,
     # 4 B per marched sample, 52 B per ray
-    cf_bytes = 24.0 * vr + 4.0 * rm + 52.0 * args.rays * args.steps
+    cf_bytes = 24.0 * kvr + 4.0 * krm + 52.0 * args.rays * len(kcounts)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     tot = torch.stack([rm, vr]).reshape(2)
     if world > 1:
@@ -118,7 +134,7 @@ def main():
             ms = [a.elapsed_time(b) for a, b in evs]
             kern[name] = {"avg_us": round(1e3 * float(np.mean(ms)), 2), "launches": len(ms)}
     cf_avg_s = kern["ncn_composite_train_fw"]["avg_us"] * 1e-6
-    cf_bytes_per_launch = float(cf_bytes.item()) / args.steps
+    cf_bytes_per_launch = float(cf_bytes.item()) / len(kcounts)
     achieved = cf_bytes_per_launch / cf_avg_s / 1e9
     if rank != 0:
         if world > 1:
@@ -142,7 +158,8 @@ def main():
                 "random-init NGPMT",
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
-                   "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update},
+                   "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
+                   "step": "eager" if args.no_graph else "hip_graph"},
         "samples_per_s": round(float(tot[0].item()) / el, 1),
         "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),

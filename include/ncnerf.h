@@ -84,12 +84,16 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
  *   W1 (64,32) W2 (16,64) W3 (64,19) W4 (64,64) W5 (3,64) concatenated (size NCN_FIELD_NW floats).
  * enc_cache: fp16 encoding cache for the backward, NCN_ENC_BYTES_PER_SAMPLE bytes per sample
  *   (rounded up to 16 samples); may be NULL for inference.
- * mode 0: full (sigmas + rgbs), mode 1: density only (sigmas; dirs/rgbs ignored). ---- */
+ * mode 0: full (sigmas + rgbs), mode 1: density only (sigmas; dirs/rgbs ignored).
+ * n_dev: NULL, or a device int32 holding the real sample count (<= n): then n is the capacity of
+ *   the buffers (static-shape / graph-captured step, where the host never reads the marcher's
+ *   counter); grids are sized from n, the kernels stop at *n_dev. ---- */
 #define NCN_FIELD_NW (64 * 32 + 16 * 64 + 64 * 19 + 64 * 64 + 3 * 64)
 #define NCN_FIELD_PACKED_HALVES 19456
 #define NCN_ENC_BYTES_PER_SAMPLE 64
 int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void* stream);
-int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* table, const uint32_t* levels,
+int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const float* table,
+                  const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int mode,
                   float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
 /* Backward: accumulates (+=) into grad_table (n_entries,2) and writes per-block weight-gradient
@@ -99,7 +103,8 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* 
  * LDS-aggregating table scatter pass). */
 int ncn_field_bwd_blocks(int64_t n);
 int64_t ncn_field_bwd_dE_floats(int64_t n);
-int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_t* levels, float xyz_min,
+int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
+                  float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
                   const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
                   void* stream);
@@ -130,17 +135,22 @@ int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opaci
  * [4..6] = the weighted terms; out_labels (n_tri) int32 in {0,+-1,+-2,+-3} (-9 = invalid normal);
  * out_centroids (K,3); dL_dnormals (3,n_tri,3) fully written: the gradient of w_ort*ort, w_dot*centr_dot and w_l1*centr_L1
  * separately, so any upstream weighting of the three terms is a 3-term combination.
+ * w_dev: NULL, or 3 device floats that replace (w_ort, w_dot, w_l1) (the step-dependent weight
+ *   schedule of losses.py:217 evaluated on the device, for a graph-captured step).
  * workspace: ncn_cluster_workspace_words(K) 32-bit words of device scratch. */
 int64_t ncn_cluster_workspace_words(int K);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
-                     float w_ort, float w_dot, float w_l1, float* out_losses, int32_t* out_labels,
+                     float w_ort, float w_dot, float w_l1, const float* w_dev, float* out_losses, int32_t* out_labels,
                      float* out_centroids, float* dL_dnormals, float* workspace, void* stream);
 
 /* ---- optimizer (train_nerf.py:262-291, 954-955): global-norm clip + Adam over a flat buffer. ---- */
-int ncn_sumsq(const float* x, int64_t n, float* out_partial /* >= 1024 floats */, void* stream);
+/* step_inc: NULL, or a device int incremented once (the optimizer step counter of a captured step) */
+int ncn_sumsq(const float* x, int64_t n, float* out_partial /* >= 1024 floats */, int* step_inc, void* stream);
+/* lr_dev / step_dev: NULL, or device scalars that override lr / step (step_dev: bias corrections
+ * 1 - beta^step are formed on the device), so a graph-captured step needs no host values. */
 int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
              const float* sumsq_partial, float max_norm, float lr, float beta1, float beta2, float eps,
-             float weight_decay, int step, void* stream);
+             float weight_decay, int step, const float* lr_dev, const int* step_dev, void* stream);
 
 #ifdef __cplusplus
 }

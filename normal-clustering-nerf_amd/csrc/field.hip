@@ -244,13 +244,15 @@ __device__ __forceinline__ void load_levels(LevelTable& Ls, const LevelTable& La
 // ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
 __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
-                                                        int64_t n, const float2* __restrict__ table, LevelTable Lt,
+                                                        int64_t n, const int32_t* __restrict__ n_dev,
+                                                        const float2* __restrict__ table, LevelTable Lt,
                                                         float xyz_min, float xyz_extent,
                                                         const half4_t* __restrict__ wpacked, int mode,
                                                         float* __restrict__ sigmas, float* __restrict__ rgbs,
                                                         half4_t* __restrict__ enc_cache) {
     __shared__ half4_t F[N_FWD_FRAGS * 64];
     __shared__ LevelTable L;
+    if (n_dev) n = min<int64_t>(n, *n_dev);  // device-resident count (static-capacity buffers)
     for (int i = threadIdx.x; i < N_FWD_FRAGS * 64; i += 256) F[i] = wpacked[i];
     load_levels(L, Lt);
     __syncthreads();
@@ -331,9 +333,11 @@ __device__ __forceinline__ half4_t transpose_tile_h(_Float16* slot, int lane, ha
 }
 
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
-    const float* __restrict__ dirs, int64_t n, const half4_t* __restrict__ wpacked,
+    const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const half4_t* __restrict__ wpacked,
     const half4_t* __restrict__ enc_cache, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
     float* __restrict__ dE_out, float* __restrict__ slab) {
+    const int64_t n_stride = n;  // dE layout [16][n_stride]
+    if (n_dev) n = min<int64_t>(n, *n_dev);
     // One LDS arena: [fragments | transpose slots] during the loop, reused as the fp32 dW
     // reduction buffer afterwards (43 KB total -> several workgroups per CU).
     constexpr int FRAG_BYTES = N_FRAGS * 64 * 8, SLOT_BYTES = 4 * 2 * 256 * 2;
@@ -437,10 +441,10 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         // encoding gradient -> level-major [16][n] float2 for the scatter pass
         if (valid) {
             float2* o = (float2*)dE_out;
-            o[(int64_t)(2 * g) * n + s] = make_float2(dE[0][0], dE[0][1]);
-            o[(int64_t)(2 * g + 1) * n + s] = make_float2(dE[0][2], dE[0][3]);
-            o[(int64_t)(8 + 2 * g) * n + s] = make_float2(dE[1][0], dE[1][1]);
-            o[(int64_t)(9 + 2 * g) * n + s] = make_float2(dE[1][2], dE[1][3]);
+            o[(int64_t)(2 * g) * n_stride + s] = make_float2(dE[0][0], dE[0][1]);
+            o[(int64_t)(2 * g + 1) * n_stride + s] = make_float2(dE[0][2], dE[0][3]);
+            o[(int64_t)(8 + 2 * g) * n_stride + s] = make_float2(dE[1][0], dE[1][1]);
+            o[(int64_t)(9 + 2 * g) * n_stride + s] = make_float2(dE[1][2], dE[1][3]);
         }
 #ifndef NCN_DIAG_NO_DW
         // ---- weight gradients: dW[out][in] += sum_s dY[out][s] X[in][s] ----
@@ -621,9 +625,17 @@ __device__ __forceinline__ void sc_flush(uint32_t* keys, long long* valx, long l
     __syncthreads();
 }
 
-__global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n,
-                                                                   LevelTable Lt, float xyz_min, float xyz_extent,
-                                                                   const float2* __restrict__ dE, int64_t span,
+__device__ __forceinline__ int64_t scatter_span_of(int64_t n) {
+    // ~one span per CU: n/256 samples, at least 1024, a multiple of 64; at most 2^16 so that the
+    // fixed-point sums keep their headroom (each sample adds at most once to an entry)
+    int64_t sp = min<int64_t>(65536, max<int64_t>(1024, (n + 255) / 256));
+    return (sp + 63) / 64 * 64;
+}
+
+__global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
+                                                                   const int32_t* __restrict__ n_dev, LevelTable Lt,
+                                                                   float xyz_min, float xyz_extent,
+                                                                   const float2* __restrict__ dE,
                                                                    float* __restrict__ grad) {
     __shared__ uint32_t keys[SC_TS];
     __shared__ long long valx[SC_TS], valy[SC_TS];
@@ -637,7 +649,10 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     }
     if (threadIdx.x == 0) fill = 0;
     const int lane = threadIdx.x & 63, r = lane & 15, wid = threadIdx.x >> 6;
-    const int64_t s0 = (int64_t)blockIdx.x * span, s1 = min(n, s0 + span);
+    const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
+    const int64_t span = scatter_span_of(n), nspans = (n + span - 1) / span;
+    for (int64_t sp = blockIdx.x; sp < nspans; sp += gridDim.x) {
+    const int64_t s0 = sp * span, s1 = min(n, s0 + span);
     // fixed-point scale per level: max |dE| over the span, all 16 levels in one load round
     {
         float m[16];
@@ -646,7 +661,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         for (int64_t s = s0 + threadIdx.x; s < s1; s += SC_THREADS) {
 #pragma unroll
             for (int l = 0; l < 16; l++) {
-                const float2 g = dE[(int64_t)l * n + s];
+                const float2 g = dE[(int64_t)l * n_stride + s];
                 const float a = fmaxf(fabsf(g.x), fabsf(g.y));
                 m[l] = (isfinite(g.x) && isfinite(g.y)) ? fmaxf(m[l], a) : INFINITY;
             }
@@ -687,7 +702,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
             x = xyzs[3 * s];
             y = xyzs[3 * s + 1];
             z = xyzs[3 * s + 2];
-            g = dE[(int64_t)l * n + s];
+            g = dE[(int64_t)l * n_stride + s];
         }
     };
     float nx, ny, nz;
@@ -831,13 +846,12 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     if (threadIdx.x == 0 && blockIdx.x == 7)
         for (int i = 0; i < 4; i++) ncn_sc_phase[i] = ph[i];
 #endif
+    __syncthreads();  // lmax / wmax are rewritten by the next span
+    }
 }
 
-static int64_t scatter_span(int64_t n) {
-    // one workgroup per CU (80 KB LDS): n/256 samples, at least 1024, at most 2048 (the fixed-point
-    // headroom assumes < 2^15 contributions per slot), a multiple of 64
-    int64_t sp = std::min<int64_t>(2048, std::max<int64_t>(1024, (n + 255) / 256));
-    return (sp + 63) / 64 * 64;
+static int scatter_grid(int64_t n_cap) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(256, (n_cap + 1023) / 1024));  // one per CU
 }
 
 static LevelTable make_table(const uint32_t* levels) {
@@ -870,7 +884,8 @@ int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void
 }
 
 // `levels` is a HOST array of 16 x {scale f32 bits, resolution, params, offset}.
-int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* table, const uint32_t* levels,
+int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const float* table,
+                  const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int mode, float* sigmas,
                   float* rgbs, uint16_t* enc_cache, void* stream) {
     if (n <= 0) return 0;
@@ -878,7 +893,7 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const float* 
     NCN_REQUIRE(((uintptr_t)table & 7) == 0 && ((uintptr_t)enc_cache & 7) == 0, hipErrorInvalidValue,
                 "ncn_field_fwd: table / enc_cache must be 8-byte aligned");
     const LevelTable Lt = make_table(levels);
-    hipLaunchKernelGGL(field_fwd_kernel, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs, n,
+    hipLaunchKernelGGL(field_fwd_kernel, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs, n, n_dev,
                        (const float2*)table, Lt, xyz_min, xyz_extent, (const half4_t*)weights_packed, mode, sigmas,
                        rgbs, (half4_t*)enc_cache);
     NCN_LAUNCH_CHECK("ncn_field_fwd");
@@ -893,7 +908,8 @@ int ncn_field_bwd_blocks(int64_t n) {
 
 int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * n : 0; }
 
-int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_t* levels, float xyz_min,
+int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
+                  float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
                   const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
                   void* stream) {
@@ -901,12 +917,11 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const uint32_
     NCN_REQUIRE(((uintptr_t)dE_ws & 7) == 0, hipErrorInvalidValue, "ncn_field_bwd: dE_ws must be 8-byte aligned");
     const LevelTable Lt = make_table(levels);
     hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
-                       dirs, n, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas, dL_drgbs,
-                       dE_ws, slab);
+                       dirs, n, n_dev, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas,
+                       dL_drgbs, dE_ws, slab);
     NCN_LAUNCH_CHECK("ncn_field_bwd");
-    const int64_t span = scatter_span(n);
-    hipLaunchKernelGGL(field_scatter_kernel, dim3((unsigned)((n + span - 1) / span)), dim3(SC_THREADS), 0,
-                       (hipStream_t)stream, xyzs, n, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, span, grad_table);
+    hipLaunchKernelGGL(field_scatter_kernel, dim3(scatter_grid(n)), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n,
+                       n_dev, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, grad_table);
     NCN_LAUNCH_CHECK("ncn_field_bwd (scatter)");
     return 0;
 }

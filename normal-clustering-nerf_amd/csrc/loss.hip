@@ -567,9 +567,10 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_sums_kernel(const float* _
 template <int K>
 __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
     const float* __restrict__ normals, int n_tri, int niter, float w_ort, float w_dot, float w_l1,
-    const float* __restrict__ wsb, float* __restrict__ out_losses, int32_t* __restrict__ out_labels,
-    float* __restrict__ out_centroids, float* __restrict__ dn) {
+    const float* __restrict__ w_dev, const float* __restrict__ wsb, float* __restrict__ out_losses,
+    int32_t* __restrict__ out_labels, float* __restrict__ out_centroids, float* __restrict__ dn) {
     const KmWs ws = km_ws((float*)wsb, K);
+    if (w_dev) { w_ort = w_dev[0]; w_dot = w_dev[1]; w_l1 = w_dev[2]; }
     __shared__ ClStats S;
     __shared__ float st3[15];
     __shared__ float G[3][3][3];  // G[term][cluster][xyz]
@@ -664,7 +665,7 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
 
 template <int K>
 static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort,
-                           float w_dot, float w_l1, float* out_losses, int32_t* out_labels, float* out_centroids,
+                           float w_dot, float w_l1, const float* w_dev, float* out_losses, int32_t* out_labels, float* out_centroids,
                            float* dn, float* ws, hipStream_t s) {
     hipLaunchKernelGGL(cluster_prep_kernel, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, seed, K, ws);
     for (int it = 0; it <= niter; it++)
@@ -673,7 +674,7 @@ static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t 
     hipLaunchKernelGGL(cluster_select_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, niter, t_sim, ws);
     hipLaunchKernelGGL(cluster_sums_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, ws);
     hipLaunchKernelGGL(cluster_grad_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, w_ort,
-                       w_dot, w_l1, ws, out_losses, out_labels, out_centroids, dn);
+                       w_dot, w_l1, w_dev, ws, out_losses, out_labels, out_centroids, dn);
 }
 
 }  // namespace ncn
@@ -721,17 +722,18 @@ int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth
 }
 
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
-                     float w_ort, float w_dot, float w_l1, float* out_losses, int32_t* out_labels,
-                     float* out_centroids, float* dL_dnormals, float* workspace, void* stream) {
+                     float w_ort, float w_dot, float w_l1, const float* w_dev, float* out_losses,
+                     int32_t* out_labels, float* out_centroids, float* dL_dnormals, float* workspace,
+                     void* stream) {
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
                 "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
     NCN_REQUIRE(niter >= 0, hipErrorInvalidValue, "ncn_cluster_loss: niter < 0");
     hipStream_t s = (hipStream_t)stream;
     if (K == 20)
-        launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, out_losses, out_labels,
+        launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, out_losses, out_labels,
                            out_centroids, dL_dnormals, workspace, s);
     else if (K == 10)
-        launch_cluster<10>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, out_losses, out_labels,
+        launch_cluster<10>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, out_losses, out_labels,
                            out_centroids, dL_dnormals, workspace, s);
     else
         NCN_REQUIRE(false, hipErrorInvalidValue, "ncn_cluster_loss: K must be 10 or 20 (got %d)", K);

@@ -32,19 +32,19 @@ SIGNATURES = {
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, P],
-    "ncn_field_fwd": [P, P, I64, P, P, F32, F32, P, I32, P, P, P, P],
+    "ncn_field_fwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
     "ncn_field_bwd_dE_floats": [I64],
-    "ncn_field_bwd": [P, P, I64, P, F32, F32, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd": [P, P, I64, P, P, F32, F32, P, P, P, P, P, P, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],
     "ncn_photo_loss_fwd": [P, P, P, I64, F32, P, P],
     "ncn_photo_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P],
     "ncn_cluster_workspace_words": [I32],
-    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, P, P, P, P],
-    "ncn_sumsq": [P, I64, P, P],
-    "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P],
+    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, P, P, P, P, P],
+    "ncn_sumsq": [P, I64, P, P, P],
+    "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
 }
 
 _lib = None

@@ -28,21 +28,24 @@ class RayMarcher(torch.autograd.Function):
     @staticmethod
     @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, grid_size,
-                max_samples, noise=None):
+                max_samples, noise=None, static_capacity=False):
         if noise is None:
             noise = torch.rand_like(rays_o[:, 0])
         rays_a, xyzs, dirs, deltas, ts, counter = vren.raymarching_train(
             rays_o, rays_d, hits_t.contiguous(), density_bitfield, cascades, scale, exp_step_factor, noise.contiguous(),
-            grid_size, max_samples)
-        total_samples = counter[0]
+            grid_size, max_samples, static_capacity=static_capacity)
+        total_samples = counter[0]  # with static_capacity: THE device count (n_samples_dev) of the arrays
         ctx.save_for_backward(rays_a, ts)
         ctx.n_rays = rays_o.shape[0]
+        ctx.static_capacity = static_capacity
         return rays_a, xyzs, dirs, deltas, ts, total_samples
 
     @staticmethod
     @custom_bwd(device_type="cuda")
     def backward(ctx, dL_drays_a, dL_dxyzs, dL_ddirs, dL_ddeltas, dL_dts, dL_dtotal_samples):
         rays_a, ts = ctx.saved_tensors
+        if ctx.static_capacity:
+            raise NotImplementedError("ray gradients are not available on the static-capacity (graph) path")
         seg = torch.repeat_interleave(rays_a[:, 0], rays_a[:, 2])
         dev, R = ts.device, ctx.n_rays
         dL_drays_o = torch.zeros(R, 3, device=dev)
@@ -52,7 +55,7 @@ class RayMarcher(torch.autograd.Function):
             dL_drays_d.index_add_(0, seg, dL_dxyzs * ts[:, None])
         if dL_ddirs is not None:
             dL_drays_d.index_add_(0, seg, dL_ddirs)
-        return dL_drays_o, dL_drays_d, None, None, None, None, None, None, None, None
+        return dL_drays_o, dL_drays_d, None, None, None, None, None, None, None, None, None
 
 
 class VolumeRenderer(torch.autograd.Function):

@@ -23,6 +23,10 @@ def init_from_env(backend=None):
     return dist.get_rank(), dist.get_world_size()
 
 
+def is_distributed():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
 def allreduce_grads(flat_grad):
     """Average the flat gradient over ranks (single bucket: the buffer is contiguous)."""
     if dist.is_initialized() and dist.get_world_size() > 1:

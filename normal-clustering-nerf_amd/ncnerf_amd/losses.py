@@ -70,8 +70,9 @@ class _ClusterLoss(torch.autograd.Function):
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
-        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]), F32(w[1]),
-             F32(w[2]), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
+        hw, w_dev = _split_weights(w)
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
+             F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(dn)
         terms = out[4:7].clone()
         ctx.mark_non_differentiable(labels, cents, out)
@@ -86,10 +87,22 @@ class _ClusterLoss(torch.autograd.Function):
         return g[0] * dn[0] + g[1] * dn[1] + g[2] * dn[2], None, None, None, None, None
 
 
+def _split_weights(w):
+    """(host weights, device weights or None): w is 3 floats or a device tensor of 3 (the
+    step-dependent schedule evaluated on the device)."""
+    if isinstance(w, torch.Tensor):
+        return (0.0, 0.0, 0.0), w.float().contiguous()
+    return tuple(float(x) for x in w), None
+
+
+def _weights_arg(w):
+    return w if isinstance(w, torch.Tensor) else tuple(float(x) for x in w)
+
+
 def cluster_losses(norm_depth, K=20, niter=20, seed=1234, t_similar=0.99, w=(1.0, 1.0, 1.0)):
     """Weighted (ort, centr_dot, centr_L1) terms, labels (+-1..3, 0, -9 invalid), centroids, raw stats."""
     check_input(norm_depth, "norm_depth")
-    return _ClusterLoss.apply(norm_depth, K, niter, seed, t_similar, tuple(float(x) for x in w))
+    return _ClusterLoss.apply(norm_depth, K, niter, seed, t_similar, _weights_arg(w))
 
 
 class _NormalsClusterLoss(torch.autograd.Function):
@@ -110,8 +123,9 @@ class _NormalsClusterLoss(torch.autograd.Function):
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
-        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]), F32(w[1]),
-             F32(w[2]), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
+        hw, w_dev = _split_weights(w)
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
+             F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(rays_o, rays_d, depth, x1, x2, x3, dn)
         terms = out[4:7].clone()
         ctx.mark_non_differentiable(normals, labels, cents, out)
@@ -137,7 +151,7 @@ def normals_cluster_losses(rays_o, rays_d, depth, x123_idx, K=20, niter=20, seed
         if not t.is_cuda:
             raise RuntimeError(f"{n} must be a CUDA tensor")
     return _NormalsClusterLoss.apply(f(rays_o), f(rays_d), f(depth), idx(x123_idx["x1"]), idx(x123_idx["x2"]),
-                                     idx(x123_idx["x3"]), K, niter, seed, t_similar, tuple(float(x) for x in w))
+                                     idx(x123_idx["x3"]), K, niter, seed, t_similar, _weights_arg(w))
 
 
 class _PhotoLoss(torch.autograd.Function):
@@ -216,6 +230,7 @@ class NeRFMTLoss(nn.Module):
         self.can_sched_end = h.get("loss_norm_can_end", -1)
         grow = h.get("loss_norm_can_grow", 1)
         self.w_sched = lambda w, step: max(0, min(w, (step - start) * (w / grow)))  # losses.py:217
+        self._grow = grow
         self.L1_norm = lambda x, y: ((torch.abs(x - y)).sum(-1)).mean()
         self.dot_prod = lambda x, y: (1.0 - torch.nn.CosineSimilarity(dim=-1)(x, y)).mean()
         if self.pred_norm_depth:
@@ -223,6 +238,7 @@ class NeRFMTLoss(nn.Module):
                                                   "all_images_triang_patch", "same_image_triang_patch"]
         self.last_cluster = None  # (labels, centroids, raw stats) of the last step, for logging/tests
         self._idx_cache = {}
+        self._wt = {}
 
     @staticmethod
     def _validity(loss, dev):
@@ -309,15 +325,28 @@ class NeRFMTLoss(nn.Module):
             if self.norm_DEpth_dot_w > 0:
                 loss_d["norm_D_dot"] = self._validity(self.norm_DEpth_dot_w * self.dot_prod(nd[valid], tgt[valid]),
                                                       dev)
+        step_t = isinstance(kwargs.get("global_step"), torch.Tensor)
+        if step_t and (self.reg_depth_w > 0 or self.can_sched_end != -1):
+            raise NotImplementedError("a device global_step needs step-independent control flow "
+                                      "(loss_reg_depth_w == 0 and loss_norm_can_end == -1)")
         if self.reg_depth_w > 0 and kwargs["global_step"] > self.can_sched_start:
             d_pred, x = pred_unsup["depth"], pred_unsup["x123_idx"]
             reg = ((d_pred[x["x1"]] - d_pred[x["x2"]]) ** 2 + (d_pred[x["x1"]] - d_pred[x["x3"]]) ** 2).mean()
             loss_d["reg_depth"] = self._validity(reg, dev)
         if clustering:
             step = kwargs["global_step"]
-            if step <= self.can_sched_end or self.can_sched_end == -1:
-                w = (self.w_sched(self.norm_D_C_ort_dot_w, step), self.w_sched(self.norm_D_C_centr_dot_w, step),
-                     self.w_sched(self.norm_D_C_centr_L1_w, step))
+            if step_t or step <= self.can_sched_end or self.can_sched_end == -1:
+                if step_t:  # the schedule on the device (graph-captured step): clamp((s-start)*w/grow, 0, w)
+                    wt = self._wt.get(dev)
+                    if wt is None:  # created once, before any capture (no H2D copy inside a graph)
+                        wt = torch.tensor([self.norm_D_C_ort_dot_w, self.norm_D_C_centr_dot_w,
+                                           self.norm_D_C_centr_L1_w], dtype=torch.float32, device=dev)
+                        self._wt[dev] = wt
+                    ramp = (step.float() - float(self.can_sched_start)) * (wt / float(self._grow))
+                    w = torch.minimum(torch.clamp_min(ramp, 0.0), wt)
+                else:
+                    w = (self.w_sched(self.norm_D_C_ort_dot_w, step), self.w_sched(self.norm_D_C_centr_dot_w, step),
+                         self.w_sched(self.norm_D_C_centr_L1_w, step))
                 if fuse_normals:
                     terms, _normals, labels, cents, raw = normals_cluster_losses(
                         pred_unsup["rays_o"], pred_unsup["rays_d"], pred_unsup["depth"], pred_unsup["x123_idx"], K=20,

@@ -73,8 +73,8 @@ class _FieldFunction(torch.autograd.Function):
     """Fused hash-grid + sigma_net + TruncExp + rgb_net (ncn_field_fwd / ncn_field_bwd)."""
 
     @staticmethod
-    def forward(ctx, x, d, table, w_sigma, w_rgb, model, mode):
-        n = x.shape[0]
+    def forward(ctx, x, d, table, w_sigma, w_rgb, model, mode, n_dev=None):
+        n = x.shape[0]  # capacity when n_dev (device int32 count) is given
         dev = x.device
         need_grad = any(ctx.needs_input_grad[2:5])  # grad mode is off inside Function.forward
         sigmas = torch.empty(n, dtype=torch.float32, device=dev)
@@ -83,11 +83,12 @@ class _FieldFunction(torch.autograd.Function):
         if need_grad:
             enc = torch.empty(((n + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev)
         packed = model._take_packed()
-        call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(table), model._levels_ptr,
+        call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(n_dev), ptr(table),
+             model._levels_ptr,
              F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(mode), ptr(sigmas),
              ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
         if need_grad:
-            ctx.save_for_backward(x, d, enc, packed)
+            ctx.save_for_backward(x, d, enc, packed, n_dev)
             ctx.model = model
         if mode != 0:
             ctx.mark_non_differentiable(rgbs)
@@ -96,7 +97,7 @@ class _FieldFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dL_dsigmas, dL_drgbs):
-        x, d, enc, packed = ctx.saved_tensors
+        x, d, enc, packed, n_dev = ctx.saved_tensors
         model = ctx.model
         n = x.shape[0]
         g_table, g_w = model._grad_views()
@@ -105,10 +106,11 @@ class _FieldFunction(torch.autograd.Function):
         dE_ws = torch.empty(int(_lib.lib().ncn_field_bwd_dE_floats(I64(n))), dtype=torch.float32, device=x.device)
         c = lambda t: None if t is None else t.contiguous().float()
         dsig, drgb = c(dL_dsigmas), c(dL_drgbs)
-        call("ncn_field_bwd", ptr(x), ptr(d), I64(n), model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent),
+        call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
+             F32(model._xyz_extent),
              ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), ptr(dE_ws), stream())
         call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
-        return None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None
 
 
 class NGPMT(nn.Module):
@@ -218,13 +220,17 @@ class NGPMT(nn.Module):
         return sigmas
 
     def forward(self, x, d, **kwargs):
-        """ngp_mt.py:196-229 -> {'sigmas': (N,), 'rgbs': (N,3)} (fp32)."""
+        """ngp_mt.py:196-229 -> {'sigmas': (N,), 'rgbs': (N,3)} (fp32).
+
+        kwargs['n_samples_dev'] (extension): a device int32 sample count <= len(x); x/d are then
+        static-capacity buffers and only the first *n_samples_dev rows are evaluated."""
         x = x.float().contiguous()
         d = d.float().contiguous()
         _lib.check_input(x, "x")
         _lib.check_input(d, "d")
+        n_dev = kwargs.get("n_samples_dev")
         sigmas, rgbs = _FieldFunction.apply(x, d, self.xyz_encoder.params, self.sigma_net.params,
-                                            self.rgb_net.params, self, 0)
+                                            self.rgb_net.params, self, 0, n_dev)
         return {"sigmas": sigmas, "rgbs": rgbs}
 
     # -- occupancy grid maintenance (ngp_mt.py:231-368) --------------------------------------------

@@ -23,6 +23,10 @@ class FlatAdam:
         self.v = torch.zeros_like(flat)
         self.part = torch.empty(1024, dtype=torch.float32, device=flat.device)
         self.step_count = 0
+        # device-side step counter and learning rate: the step kernels read them, so the optimizer
+        # step can sit inside a captured HIP graph (the counter is bumped by the sum-of-squares kernel)
+        self.step_dev = torch.zeros((), dtype=torch.int32, device=flat.device)
+        self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device)
         self.num_epochs = num_epochs
         self.n_table = model._n_table
 
@@ -33,15 +37,20 @@ class FlatAdam:
         """CosineAnnealingLR(T_max=num_epochs, eta_min=0) stepped per epoch (train_nerf.py:286-288)."""
         if self.num_epochs:
             self.lr = 0.5 * self.base_lr * (1 + math.cos(math.pi * epoch / self.num_epochs))
+            self.lr_dev.fill_(self.lr)
 
     def step(self):
         self.step_count += 1
         p = self.model.flat_params()
         g = self.model.flat_grad()
         s = stream()
-        call("ncn_sumsq", ptr(g), I64(g.numel()), ptr(self.part), s)
+        call("ncn_sumsq", ptr(g), I64(g.numel()), ptr(self.part), ptr(self.step_dev), s)
         b1, b2 = self.betas
         for lo, hi, wd in ((0, self.n_table, self.wd[0]), (self.n_table, p.numel(), self.wd[1])):
             call("ncn_adam", ptr(p[lo:hi]), ptr(g[lo:hi]), ptr(self.m[lo:hi]), ptr(self.v[lo:hi]), I64(hi - lo),
                  ptr(self.part), F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(wd),
-                 I32(self.step_count), s)
+                 I32(self.step_count), ptr(self.lr_dev), ptr(self.step_dev), s)
+
+    def state_tensors(self):
+        """Every tensor the step mutates (parameters, moments, device counters)."""
+        return [self.model.flat_params(), self.m, self.v, self.step_dev, self.lr_dev]

@@ -6,7 +6,9 @@ output dict, including the reference quirks that downstream losses depend on:
   * results['rays_o'] = rays_d  (rendering.py:226-227, quirk q1)
   * white background when exp_step_factor == 0 (rendering.py:232-240, quirk q2)
 Removed: the dead `(rays_a[:,2]==0).any()` host sync (rendering.py:195-196).
-Extension (test hook, not in the reference): kwargs['march_noise'] injects the marcher noise.
+Extensions (not in the reference): kwargs['march_noise'] injects the marcher noise (test hook);
+kwargs['static_shapes']=True keeps every shape independent of the marched sample count (no host
+read of the counter), which is what lets Trainer capture the whole step in one HIP graph.
 """
 import torch
 from einops import rearrange
@@ -121,12 +123,17 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
             assert strategy == "none"
     if hasattr(model, "prepare_weights"):
         model.prepare_weights()  # queue the fp16 weight packing ahead of the marcher's host read of S
+    static = bool(kwargs.get("static_shapes", False))
     rays_a, xyzs, dirs, results["deltas"], results["ts"], results["rm_samples"] = RayMarcher.apply(
         rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
-        model.grid_size, max_samples, kwargs.get("march_noise"))
+        model.grid_size, max_samples, kwargs.get("march_noise"), static)
     for k, v in list(kwargs.items()):  # rendering.py:198-200
         if isinstance(v, torch.Tensor) and k not in ("march_noise",):
+            if static:
+                raise NotImplementedError(f"per-ray tensor kwarg {k!r} on the static-shape path")
             kwargs[k] = torch.repeat_interleave(v[rays_a[:, 0]], rays_a[:, 2], 0)
+    if static:  # capacity-sized sample arrays; the field stops at the device count
+        kwargs["n_samples_dev"] = results["rm_samples"]
     output = model(xyzs, dirs, **kwargs)
     sigmas = output["sigmas"]
     raws = output["rgbs"]

@@ -25,7 +25,7 @@ class Trainer:
     warmup_steps = 256
     update_interval = 16
 
-    def __init__(self, model, hparams=None, update_grid=False):
+    def __init__(self, model, hparams=None, update_grid=False, use_graph=False):
         self.h = dict(HYPERSIM_HPARAMS, **(hparams or {}))
         self.model = model
         self.loss = NeRFMTLoss(self.h)
@@ -33,13 +33,80 @@ class Trainer:
         self.update_grid = update_grid
         self.render_kwargs = dict(near_distance=self.h["rend_near_dist"], max_samples=self.h["rend_max_samples"],
                                   test_time=False, random_bg=False, anneal_strategy="none", anneal_steps=0)
+        self.use_graph = use_graph
+        self.graph = None
 
-    def step(self, batch, global_step):
+    def _maybe_update_grid(self, global_step):
         m = self.model
         if self.update_grid and global_step % self.update_interval == 0:
             thr = 0.01 * self.h["rend_max_samples"] / 3 ** 0.5 * self.h["density_tresh_decay"]
             m.update_density_grid(thr, warmup=global_step < self.warmup_steps)
             distributed.broadcast_occupancy(m)
+
+    # -- graph-captured step ---------------------------------------------------------------------
+    # The whole step (zero_grad, render with static shapes, losses, backward, [optimizer]) is one
+    # HIP graph: the marcher's sample count stays on the device (static_shapes), the loss-weight
+    # schedule and Adam's step/lr are device scalars, so nothing in the step reads the host.  A
+    # replay costs one launch instead of ~150 Python-driven ones.  Inputs are copied into the
+    # graph's static batch buffers; the occupancy-grid refresh and the RCCL all-reduce (N > 1)
+    # run eagerly around it.
+    def _body(self, batch, step_dev, with_opt):
+        m = self.model
+        self.opt.zero_grad()
+        kw = dict(self.render_kwargs, global_step=0, static_shapes=True)
+        if "march_noise" in batch:
+            kw["march_noise"] = batch["march_noise"]
+        results = render(m, batch["rays_o"], batch["rays_d"], **kw)
+        loss_d = self.loss(results, batch, global_step=step_dev)
+        loss_d["total"].backward()
+        if with_opt:
+            self.opt.step()
+        return results, loss_d
+
+    def _capture(self, batch):
+        import torch
+        dev = batch["rays_o"].device
+        if self.render_kwargs.get("anneal_steps", 0) > 0:
+            raise NotImplementedError("ray-range annealing is step-dependent host control flow")
+        self._static = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in batch.items()}
+        self._step_dev = torch.zeros((), dtype=torch.int64, device=dev)
+        self._with_opt = not distributed.is_distributed()
+        state = self.opt.state_tensors()
+        saved = [t.clone() for t in state]  # warm-up steps must not advance training
+        saved_count = self.opt.step_count
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self._body(self._static, self._step_dev, self._with_opt)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._out = self._body(self._static, self._step_dev, self._with_opt)
+        for t, v in zip(state, saved):
+            t.copy_(v)
+        self.opt.step_count = saved_count
+
+    def _graph_step(self, batch, global_step):
+        if self.graph is None:
+            self._capture(batch)
+        for k, v in batch.items():
+            if k in self._static and hasattr(v, "copy_") and v is not self._static[k]:
+                self._static[k].copy_(v, non_blocking=True)
+        self._step_dev.fill_(global_step)
+        self.graph.replay()
+        if not self._with_opt:
+            distributed.allreduce_grads(self.model.flat_grad())
+            self.opt.step()
+        else:
+            self.opt.step_count += 1
+        return self._out
+
+    def step(self, batch, global_step):
+        m = self.model
+        self._maybe_update_grid(global_step)
+        if self.use_graph:
+            return self._graph_step(batch, global_step)
         self.opt.zero_grad()
         kw = dict(self.render_kwargs, global_step=global_step)
         if "march_noise" in batch:

@@ -69,10 +69,13 @@ def packbits(density_grid, density_threshold, density_bitfield):
 
 
 def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, noise,
-                      grid_size, max_samples):
+                      grid_size, max_samples, static_capacity=False):
     """raymarching.cu:283-332 -> [rays_a i64 (R,3), xyzs (S,3), dirs (S,3), deltas (S), ts (S), counter i32 (2)].
 
-    Walk -> scan -> (read S, the reference's own sync point custom_functions.py:91) -> pack."""
+    Walk -> scan -> (read S, the reference's own sync point custom_functions.py:91) -> pack.
+    static_capacity=True (extension): the host never reads S; the sample arrays have the capacity
+    R*max_samples, rows >= counter[0] are unspecified, and consumers take counter[0:1] as the
+    device-resident count (the graph-captured training step)."""
     for t, n in ((rays_o, "rays_o"), (rays_d, "rays_d"), (hits_t, "hits_t"), (density_bitfield, "density_bitfield"),
                  (noise, "noise")):
         check_input(t, n)
@@ -90,7 +93,7 @@ def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
          I32(int(cascades)), F32(float(scale)), F32(float(exp_step_factor)), I32(int(grid_size)), I32(ms),
          ptr(counts), ptr(slab_xyz), ptr(slab_t), ptr(slab_dt), s)
     call("ncn_march_train_scan", ptr(counts), I64(R), ptr(rays_a), ptr(counter), s)
-    S = int(counter[0].item())
+    S = R * ms if static_capacity else int(counter[0].item())
     xyzs = torch.empty(S, 3, dtype=torch.float32, device=dev)
     dirs = torch.empty(S, 3, dtype=torch.float32, device=dev)
     deltas = torch.empty(S, dtype=torch.float32, device=dev)
