@@ -54,6 +54,38 @@ __device__ __forceinline__ float wave_incl_prod(float v, int lane) {
     return v;
 }
 
+// DPP wave scans (GFX9 DPP: row_shr within 16-lane rows, then row_bcast:15 / row_bcast:31 across
+// rows): 6 DPP ops with ~no latency, no LDS crossbar traffic (unlike __shfl_* = ds_bpermute).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROW_MASK, 0xF,
+                                                      false));
+}
+__device__ __forceinline__ float wave_incl_prod_dpp(float v) {
+    v *= dpp_f<0x111, 0xF>(1.0f, v);  // row_shr:1
+    v *= dpp_f<0x112, 0xF>(1.0f, v);  // row_shr:2
+    v *= dpp_f<0x114, 0xF>(1.0f, v);  // row_shr:4
+    v *= dpp_f<0x118, 0xF>(1.0f, v);  // row_shr:8
+    v *= dpp_f<0x142, 0xA>(1.0f, v);  // row_bcast:15 into rows 1, 3
+    v *= dpp_f<0x143, 0xC>(1.0f, v);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ __forceinline__ float wave_incl_sum_dpp(float v) {
+    v += dpp_f<0x111, 0xF>(0.0f, v);
+    v += dpp_f<0x112, 0xF>(0.0f, v);
+    v += dpp_f<0x114, 0xF>(0.0f, v);
+    v += dpp_f<0x118, 0xF>(0.0f, v);
+    v += dpp_f<0x142, 0xA>(0.0f, v);
+    v += dpp_f<0x143, 0xC>(0.0f, v);
+    return v;
+}
+// value of lane (l - 1), `first` for lane 0 (DPP wave_shr:1)
+__device__ __forceinline__ float wave_shr1_dpp(float v, float first) { return dpp_f<0x138, 0xF>(first, v); }
+// wave total via the inclusive DPP scan, read from lane 63 (uniform result)
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_incl_sum_dpp(v)), 63));
+}
+
 }  // namespace ncn
 
 #define NCN_LAUNCH_CHECK(name)                                                         \

@@ -222,7 +222,8 @@ __global__ __launch_bounds__(256) void march_train_pack_kernel(
     const float* __restrict__ slab_xyz, const float* __restrict__ slab_t, const float* __restrict__ slab_dt,
     float* __restrict__ xyzs, float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts) {
     const int lane = threadIdx.x & 63;
-    const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
+    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (n >= R) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
     const int cnt = (int)rays_a[3 * n + 2];
@@ -368,6 +369,7 @@ struct RendAcc {
     float v[C];
 };
 
+#ifdef NCN_COMPOSITE_V1
 // volumerendering.cu:97-137
 template <int C>
 __global__ __launch_bounds__(256) void composite_fw_kernel(
@@ -376,7 +378,8 @@ __global__ __launch_bounds__(256) void composite_fw_kernel(
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
     float* __restrict__ rend, float* __restrict__ ws) {
     const int lane = threadIdx.x & 63;
-    const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
+    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (n >= R) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
     const int N = (int)rays_a[3 * n + 2];
@@ -458,6 +461,102 @@ __global__ __launch_bounds__(256) void composite_fw_kernel(
     }
 }
 
+#else
+// volumerendering.cu:97-137.  One wave per ray; the ray's samples are taken in rows of 64
+// consecutive samples (lane l holds sample row*64 + l, so every load instruction is one contiguous
+// 256-B piece), up to 4 rows per round with all loads in flight before the first scan.  Per row:
+// an inclusive DPP prefix product of (1 - a) gives the transmittance in front of each sample, the
+// first sample whose transmittance after it falls to T_threshold stops the ray (it is composited
+// but not counted, quirk q6), and the row's last transmittance carries to the next row.
+template <int C>
+__global__ __launch_bounds__(256) void composite_fw_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
+    int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
+    float* __restrict__ rend, float* __restrict__ ws) {
+    constexpr int ROWS = 4;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
+    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (n >= R) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
+    const int N = (int)rays_a[3 * n + 2];
+#if defined(NCN_DIAG_CF_STAGE) && NCN_DIAG_CF_STAGE == 1
+    if (lane == 0) opacity[ray] = (float)N;
+    return;
+#endif
+    float Tc = 1.0f, acc_o = 0.f, acc_d = 0.f;
+    float acc_r[C];
+#pragma unroll
+    for (int i = 0; i < C; i++) acc_r[i] = 0.f;
+    int total = N;
+    bool done = false;
+    for (int base = 0; base < N; base += 64 * ROWS) {
+        float sg[ROWS], dl[ROWS], tt[ROWS], rr[ROWS][C];
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {  // every load of the round issued before any use
+            const int k = base + r * 64 + lane;
+            const int64_t s = start + k;
+            const bool v = k < N && !done;
+            sg[r] = v ? sigmas[s] : 0.f;
+            dl[r] = v ? deltas[s] : 0.f;
+            tt[r] = v ? ts[s] : 0.f;
+#pragma unroll
+            for (int i = 0; i < C; i++) rr[r][i] = v ? raws[s * C + i] : 0.f;
+        }
+#if defined(NCN_DIAG_CF_STAGE) && NCN_DIAG_CF_STAGE == 2
+        {
+            float t = 0.f;
+            for (int r = 0; r < ROWS; r++) t += sg[r] + dl[r] + tt[r] + rr[r][0] + rr[r][1] + rr[r][C - 1];
+            if (t == 1234.5f) opacity[ray] = t;
+            continue;
+        }
+#endif
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            const int k = base + r * 64 + lane;
+            if (base + r * 64 >= N) break;  // uniform
+            const bool valid = k < N;
+            if (done) {
+                if (valid) ws[start + k] = 0.f;
+                continue;
+            }
+            const float a = 1.0f - __expf(-sg[r] * dl[r]);
+            const float om = 1.0f - a;
+            const float incl = wave_incl_prod_dpp(valid ? om : 1.0f);
+            const float Tb = Tc * wave_shr1_dpp(incl, 1.0f);  // transmittance in front of the sample
+            const float Ta = Tb * om;                         // ... and after it
+            const uint64_t stopm = __ballot(valid && Ta <= T_thr);
+            const int stop_lane = stopm ? __builtin_ctzll(stopm) : 64;
+            const bool inc = valid && lane <= stop_lane;
+            const float w = inc ? a * Tb : 0.f;
+            if (valid) ws[start + k] = w;
+#pragma unroll
+            for (int i = 0; i < C; i++) acc_r[i] = fmaf(w, rr[r][i], acc_r[i]);
+            acc_d = fmaf(w, tt[r], acc_d);
+            acc_o += w;
+            if (stopm) {
+                done = true;
+                total = base + r * 64 + stop_lane;
+            }
+            Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
+        }
+    }
+    acc_o = wave_sum_dpp(acc_o);
+    acc_d = wave_sum_dpp(acc_d);
+#pragma unroll
+    for (int i = 0; i < C; i++) acc_r[i] = wave_sum_dpp(acc_r[i]);
+    if (lane == 0) {
+        opacity[ray] = acc_o;
+        depth[ray] = acc_d;
+#pragma unroll
+        for (int i = 0; i < C; i++) rend[ray * C + i] = acc_r[i];
+        total_samples[ray] = total;
+    }
+}
+
+#endif
+
 // volumerendering.cu:297-364.  T is the post-update transmittance (quirk q10); d/r are inclusive
 // prefix sums of w*t and w*raw; (sum - pre[s]) is the suffix of dL_dws*ws over the WHOLE marched
 // segment (:331-335).  Evaluation order of dL_dsigmas follows :349-359.
@@ -470,7 +569,8 @@ __global__ __launch_bounds__(256) void composite_bw_kernel(
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
     float* __restrict__ dL_draws) {
     const int lane = threadIdx.x & 63;
-    const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
+    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (n >= R) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
     const int N = (int)rays_a[3 * n + 2];

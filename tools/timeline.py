@@ -4,10 +4,12 @@ import sys
 
 db = sys.argv[1]
 marker = sys.argv[2] if len(sys.argv) > 2 else "photo_loss_fwd"
+which = int(sys.argv[3]) if len(sys.argv) > 3 else -3  # occurrence index of the marker
 c = sqlite3.connect(db)
 rows = list(c.execute("select name,start,end from kernels order by start"))
 idx = [i for i, r in enumerate(rows) if marker in r[0]]
-i0, i1 = idx[-3], idx[-2]
+print("marker occurrences:", len(idx))
+i0, i1 = idx[which], idx[which + 1]
 t0 = rows[i0][1]
 busy = 0
 for r in rows[i0:i1]:
