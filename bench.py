@@ -12,6 +12,7 @@ scaling (8192 rays per rank), value = all ranks' rays / max-over-ranks time.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -29,6 +30,17 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 TIMED = ("ncn_composite_train_fw", "ncn_composite_train_bw", "ncn_march_train_walk", "ncn_field_fwd",
          "ncn_field_bwd", "ncn_cluster_loss")
+
+
+def pmc_traffic():
+    """HBM bytes per composite_fw launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2 +
+    WRITE_SIZE, separate passes; profiles/<round>/composite_fw_traffic.json), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "composite_fw_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
 def composite_fw_roofline(model, batch, dev, reps=50):
@@ -163,6 +175,7 @@ def main():
             ms = [a.elapsed_time(b) for a, b in evs]
             kern[name] = {"avg_us": round(1e3 * float(np.mean(ms)), 2), "launches": len(ms)}
     cf_bytes_per_launch, cf_us = composite_fw_roofline(model, batches[0], dev)
+    traffic, traffic_src = pmc_traffic()
     achieved = cf_bytes_per_launch / (cf_us * 1e-6) / 1e9
     if rank != 0:
         if world > 1:
@@ -193,7 +206,7 @@ def main():
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),
         "roofline": {"kernel": "composite_train_fw", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(cf_bytes_per_launch),
                      "avg_launch_us": round(cf_us, 2),
                      "method": "50 back-to-back launches on one bench batch between HIP events on the launch "
