@@ -591,36 +591,31 @@ __device__ __forceinline__ long long sc_fix(float v, int k) {
     return ((long long)(int)hi << 23) + (long long)(int)rintf(lo);
 }
 
-// Flush: two lanes per slot (x and y of one entry are adjacent floats, so an atomic instruction
-// writes 8-B pieces), every lane's keys and sums read in one LDS round trip, one f32 global
-// atomic per non-zero sum; the slots are then reset.
-__device__ __forceinline__ void sc_flush(uint32_t* keys, long long* valx, long long* valy, int* fill,
-                                         float* __restrict__ grad, uint32_t off, int k) {
-    constexpr int PER = 2 * SC_TS / SC_THREADS;
-    uint32_t key[PER];
-    long long q[PER];
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int i = threadIdx.x + j * SC_THREADS, slot = i >> 1;
-        key[j] = keys[slot];
-        q[j] = (i & 1) ? valy[slot] : valx[slot];
-    }
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int i = threadIdx.x + j * SC_THREADS;
+// Flush: only the slots claimed since the last flush (the `used` list), two lanes per slot (x and
+// y of one entry are adjacent floats: 8-B pieces per atomic instruction), one f32 global atomic per
+// non-zero sum; then exactly those slots are reset.  Cost proportional to the entries, not the table.
+__device__ __forceinline__ void sc_flush(uint32_t* keys, long long* valx, long long* valy,
+                                         const uint16_t* used, int* fill, float* __restrict__ grad, uint32_t off,
+                                         int k) {
+    const int nf = *fill;
+    for (int i = threadIdx.x; i < 2 * nf; i += SC_THREADS) {
+        const int slot = used[i >> 1];
+        const uint32_t key = keys[slot];
+        const long long q = (i & 1) ? valy[slot] : valx[slot];
 #ifdef NCN_DIAG_SC_NO_GATOMIC
-        if (key[j] != SC_EMPTY && q[j] == 12345) grad[2 * (size_t)(off + key[j]) + (i & 1)] = 1.f;
+        if (q == 12345) grad[2 * (size_t)(off + key) + (i & 1)] = 1.f;
 #else
-        if (key[j] != SC_EMPTY && q[j] != 0)
-            atomicAdd(grad + 2 * (size_t)(off + key[j]) + (i & 1), (float)ldexp((double)q[j], -k));
+        if (q != 0) atomicAdd(grad + 2 * (size_t)(off + key) + (i & 1), (float)ldexp((double)q, -k));
 #endif
     }
     __syncthreads();  // every lane has read its slots
-    for (int i = threadIdx.x; i < SC_TS; i += SC_THREADS) {
-        keys[i] = SC_EMPTY;
-        valx[i] = 0;
-        valy[i] = 0;
+    for (int i = threadIdx.x; i < nf; i += SC_THREADS) {
+        const int slot = used[i];
+        keys[slot] = SC_EMPTY;
+        valx[slot] = 0;
+        valy[slot] = 0;
     }
+    __syncthreads();
     if (threadIdx.x == 0) *fill = 0;
     __syncthreads();
 }
@@ -639,7 +634,8 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    float* __restrict__ grad) {
     __shared__ uint32_t keys[SC_TS];
     __shared__ long long valx[SC_TS], valy[SC_TS];
-    __shared__ int fill;
+    __shared__ uint16_t used[SC_TS];  // slots claimed since the last flush, in claim order
+    __shared__ int fill;              // == number of entries in `used`
     __shared__ float wmax[SC_THREADS / 64][16];
     __shared__ float lmax[16];
     for (int i = threadIdx.x; i < SC_TS; i += SC_THREADS) {
@@ -782,7 +778,8 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                 run_sum<3>(v0[c], link); run_sum<3>(v1[c], link);
             }
         }
-        int inserted = 0;
+        uint32_t newmask = 0;  // corners whose slot this lane claimed
+        int slot[8];
         if (head && direct) {
 #pragma unroll
             for (int c = 0; c < 8; c++) {
@@ -794,7 +791,6 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         if (head && !direct) {
             // 2-way set-associative lookup: both keys of the aligned slot pair in one ds_read_b64
             uint2 kk[8];
-            int slot[8];
 #pragma unroll
             for (int c = 0; c < 8; c++) kk[c] = *(const uint2*)&keys[2 * sc_pair(e[c])];
             int claim[8];
@@ -811,7 +807,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
 #pragma unroll
             for (int c = 0; c < 8; c++) {
                 if (claim[c] >= 0) {
-                    if (got[c] == SC_EMPTY) { slot[c] = claim[c]; inserted++; }
+                    if (got[c] == SC_EMPTY) { slot[c] = claim[c]; newmask |= 1u << c; }
                     else if (got[c] == e[c]) slot[c] = claim[c];
                 }
             }
@@ -831,11 +827,23 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
             }
         }
         SC_T(t2);
-        const int wins = (int)wave_sum((float)inserted);
-        if (lane == 0 && wins) atomicAdd(&fill, wins);
+        {   // append the claimed slots to `used`: one LDS atomic per wave
+            const int mine = __builtin_popcount(newmask);
+            const float incl = wave_incl_sum_dpp((float)mine);
+            const int wtot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+            int base = 0;
+            if (wtot) {
+                if (lane == 0) base = atomicAdd(&fill, wtot);
+                base = __builtin_amdgcn_readfirstlane(base);
+                int pos = base + (int)incl - mine;
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+                    if (newmask & (1u << c)) used[pos++] = (uint16_t)slot[c];
+            }
+        }
         __syncthreads();
         SC_T(t3);
-        if (ch == nchunk - 1 || fill > SC_TS / 4) sc_flush(keys, valx, valy, &fill, grad, off, k);
+        if (ch == nchunk - 1 || fill > SC_TS / 4) sc_flush(keys, valx, valy, used, &fill, grad, off, k);
         SC_T(t4);
         SC_ACC(0, t0, t1);
         SC_ACC(1, t1, t2);

@@ -42,7 +42,8 @@ table = model.flat_params()[: model._n_table]
 
 
 def fwd(lib):
-    return lib.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(table), model._levels_ptr, F32(model._xyz_min),
+    return lib.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(table), model._levels_ptr,
+                             F32(model._xyz_min),
                              F32(model._xyz_extent), ptr(packed), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
 
 
@@ -58,7 +59,7 @@ dE_ws = torch.empty(32 * n, device=dev)
 
 
 def bwd(lib):
-    return lib.ncn_field_bwd(ptr(xyzs), ptr(dirs), I64(n), model._levels_ptr, F32(model._xyz_min),
+    return lib.ncn_field_bwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), model._levels_ptr, F32(model._xyz_min),
                              F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(gtab), ptr(slab),
                              ptr(dE_ws), stream())
 
@@ -68,6 +69,7 @@ def timeit(f, lib, reps=20):
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, e in evs:
+        torch.cuda._sleep(60000)  # GPU busy while Python issues the launch
         a.record()
         assert f(lib) == 0
         e.record()
@@ -82,7 +84,19 @@ for so in sorted(glob.glob(os.path.join(ROOT, "tools", "_build", "field_*.so")))
         getattr(L, name).argtypes = _lib.SIGNATURES[name]
         getattr(L, name).restype = ctypes.c_int
     libs.append((os.path.basename(so)[6:-3], L))
+gref = None
 for name, L in libs:
+    gtab.zero_()
+    assert bwd(L) == 0
+    torch.cuda.synchronize()
+    g1 = gtab.clone()
+    if gref is None:
+        gref = g1
+    else:
+        rel = ((g1 - gref).norm() / gref.norm()).item()
+        big = gref.abs() > 1e-3 * gref.abs().max()
+        relb = ((g1 - gref)[big].abs() / gref[big].abs()).max().item()
+        print(f"   table-grad vs main: rel-L2 {rel:.3e}, max rel on entries > 1e-3 max: {relb:.3e}")
     print(f"{name:16s} fwd {timeit(fwd, L):8.1f} us   bwd {timeit(bwd, L):8.1f} us", flush=True)
     if hasattr(L, "ncn_diag_read_phases"):
         buf = (ctypes.c_ulonglong * 8)()
