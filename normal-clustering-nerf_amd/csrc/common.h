@@ -86,6 +86,82 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_incl_sum_dpp(v)), 63));
 }
 
+// Inclusive product scan as 6 fused v_mul_f32_dpp with the register as both sources and no
+// bound_ctrl: a lane without a DPP source is not written, i.e. keeps its value (x 1).  The
+// compiler's update_dpp form needs a v_mov of the identity + v_mov_dpp + v_mul per step.
+// `s_nop 1` covers the VALU-write -> DPP-read hazard (2 wait states) before every step.
+__device__ __forceinline__ float wave_incl_prod_dpp_fused(float v) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_mul_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(v));
+    return v;
+}
+
+// Wave totals of K values at once (CDNA4 permlane swaps): v_permlane32_swap pairs values so the
+// lower half-wave carries one and the upper half the other, v_permlane16_swap halves again, then
+// one 16-lane row total per register (row_ror 8/4/2/1).  ~3K+6 instructions instead of K full
+// 64-lane DPP reductions (~8K + s_nops).  Result i is returned uniform in v[i].
+__device__ __forceinline__ float swap32_sum(float a, float b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_sum(float a, float b) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_add_zero(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_total(float v) {
+    v = dpp_add_zero<0x128>(v);  // row_ror:8
+    v = dpp_add_zero<0x124>(v);  // row_ror:4
+    v = dpp_add_zero<0x122>(v);  // row_ror:2
+    v = dpp_add_zero<0x121>(v);  // row_ror:1
+    return v;
+}
+template <int K>
+__device__ __forceinline__ void wave_sum_multi(float (&v)[K]) {
+    constexpr int K1 = (K + 1) / 2, K2 = (K1 + 1) / 2;
+    float P[K1], Q[K2];
+#pragma unroll
+    for (int i = 0; i < K1; i++) P[i] = swap32_sum(v[2 * i], (2 * i + 1 < K) ? v[2 * i + 1] : v[2 * i]);
+#pragma unroll
+    for (int j = 0; j < K2; j++) Q[j] = row16_total(swap16_sum(P[2 * j], (2 * j + 1 < K1) ? P[2 * j + 1] : P[2 * j]));
+    // value m sits in P[m/2], half m%2 (lanes 0-31 / 32-63); P[i] sits in Q[i/2], rows (i%2) + 2*half
+#pragma unroll
+    for (int m = 0; m < K; m++) {
+        const int i = m / 2, h = (2 * i + 1 < K) ? (m & 1) : 0;
+        const int row = (((2 * (i / 2) + 1) < K1) ? (i & 1) : 0) + 2 * h;
+        v[m] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Q[i / 2]), row * 16));
+    }
+}
+
+// Raw buffer resources (T8): a descriptor sized to one segment makes the hardware bounds check
+// return 0 for loads past it and drop stores past it, so row bodies carry no masks or branches.
+// Build them from wave-uniform values only (scalar loads / kernargs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, byte_off, 0, 0);
+}
+
 }  // namespace ncn
 
 #define NCN_LAUNCH_CHECK(name)                                                         \

@@ -356,210 +356,116 @@ __global__ __launch_bounds__(256) void ray_aabb_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Compositing.  One wave per ray segment (rays are independent, the segment is contiguous in the
-// ray-ordered sample arrays).  Each lane owns 4 consecutive samples, so a 256-sample chunk costs
-// one set of loads per lane; the transmittance is a wave-level inclusive product scan of the
-// lane products, carried across chunks.  The early stop (T <= T_threshold, volumerendering.cu:133)
-// is found with a ballot; the stopping sample is composited and counted out (quirk q6).
-constexpr int SPL = 4;  // samples per lane
-constexpr int CHUNK = 64 * SPL;
+// Compositing (volumerendering.cu:97-176 forward, :297-418 backward).  One wave per ray segment;
+// the segment's samples are taken in rows of 64 consecutive samples (lane l holds sample
+// row*64 + l, so every load is one contiguous 256-B piece), up to ROWS rows per round with all of
+// the round's loads issued before the first use.  Per row an inclusive DPP product scan of (1 - a)
+// gives the transmittance in front of each sample; the first sample whose transmittance after it
+// falls to T_threshold stops the ray (it is composited but not counted, quirk q6); the row's last
+// transmittance carries to the next row.  Every per-sample array is addressed through a buffer
+// descriptor sized to the ray's segment (buf_rsrc): lanes past N read 0 (so a = 0, 1 - a = 1 and
+// w = 0 fall out without masks) and their stores are dropped.  Per-ray values are scalar loads.
+constexpr int CF_ROWS = 4;
 
-template <int C>
-struct RendAcc {
-    float v[C];
+// The ray handled by this wave and its segment.  The wave index is clamped instead of returning
+// early so the kernarg, rays_a and array-pointer loads issue as one scalar batch; `live` guards
+// the per-ray stores of the (at most 3) surplus waves of the last block.
+struct RaySeg {
+    int64_t ray, start;
+    int N;
+    bool live;
 };
-
-#ifdef NCN_COMPOSITE_V1
-// volumerendering.cu:97-137
-template <int C>
-__global__ __launch_bounds__(256) void composite_fw_kernel(
-    const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
-    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
-    int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
-    float* __restrict__ rend, float* __restrict__ ws) {
-    const int lane = threadIdx.x & 63;
-    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
-    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (n >= R) return;
-    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
-    const int N = (int)rays_a[3 * n + 2];
-    float Tc = 1.0f, acc_o = 0.f, acc_d = 0.f;
-    float acc_r[C];
-#pragma unroll
-    for (int i = 0; i < C; i++) acc_r[i] = 0.f;
-    int total = N;
-    bool done = false;
-    for (int base = 0; base < N; base += CHUNK) {
-        const int k0 = base + lane * SPL;
-        if (done) {
-#pragma unroll
-            for (int j = 0; j < SPL; j++)
-                if (k0 + j < N) ws[start + k0 + j] = 0.f;
-            continue;
-        }
-        float a[SPL], om[SPL], tt[SPL], rr[SPL][C];
-        bool valid[SPL];
-#pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            const int64_t s = start + k0 + j;
-            valid[j] = (k0 + j) < N;
-            const float sg = valid[j] ? sigmas[s] : 0.f;
-            const float dl = valid[j] ? deltas[s] : 0.f;
-            tt[j] = valid[j] ? ts[s] : 0.f;
-#pragma unroll
-            for (int i = 0; i < C; i++) rr[j][i] = valid[j] ? raws[s * C + i] : 0.f;
-            a[j] = 1.0f - __expf(-sg * dl);
-            om[j] = 1.0f - a[j];
-        }
-        float lp = om[0];
-#pragma unroll
-        for (int j = 1; j < SPL; j++) lp *= om[j];
-        const float incl = wave_incl_prod(lp, lane);
-        float excl = __shfl_up(incl, 1, 64);
-        if (lane == 0) excl = 1.0f;
-        float T = Tc * excl;
-        float Tb[SPL];
-        int my_stop = SPL;
-#pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            Tb[j] = T;
-            T *= om[j];
-            if (valid[j] && T <= T_thr && my_stop == SPL) my_stop = j;
-        }
-        const uint64_t mask = __ballot(my_stop < SPL);
-        int stop_lane = 64, stop_j = SPL;
-        if (mask) {
-            stop_lane = __builtin_ctzll(mask);
-            stop_j = __shfl(my_stop, stop_lane, 64);
-        }
-#pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            const bool inc = valid[j] && (lane < stop_lane || (lane == stop_lane && j <= stop_j));
-            const float w = inc ? a[j] * Tb[j] : 0.f;
-            if (valid[j]) ws[start + k0 + j] = w;
-#pragma unroll
-            for (int i = 0; i < C; i++) acc_r[i] = fmaf(w, rr[j][i], acc_r[i]);
-            acc_d = fmaf(w, tt[j], acc_d);
-            acc_o += w;
-        }
-        if (mask) {
-            done = true;
-            total = base + stop_lane * SPL + stop_j;
-        }
-        Tc = __shfl(T, 63, 64);
-    }
-    acc_o = wave_sum(acc_o);
-    acc_d = wave_sum(acc_d);
-#pragma unroll
-    for (int i = 0; i < C; i++) acc_r[i] = wave_sum(acc_r[i]);
-    if (lane == 0) {
-        opacity[ray] = acc_o;
-        depth[ray] = acc_d;
-#pragma unroll
-        for (int i = 0; i < C; i++) rend[ray * C + i] = acc_r[i];
-        total_samples[ray] = total;
-    }
+__device__ __forceinline__ RaySeg load_ray_seg(const int64_t* __restrict__ rays_a, int64_t R) {
+    const int64_t n0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int64_t n = n0 < R ? n0 : R - 1;
+    RaySeg s;
+    s.ray = rays_a[3 * n];
+    s.start = rays_a[3 * n + 1];
+    s.N = (int)rays_a[3 * n + 2];
+    s.live = n0 < R;
+    return s;
 }
 
-#else
-// volumerendering.cu:97-137.  One wave per ray; the ray's samples are taken in rows of 64
-// consecutive samples (lane l holds sample row*64 + l, so every load instruction is one contiguous
-// 256-B piece), up to 4 rows per round with all loads in flight before the first scan.  Per row:
-// an inclusive DPP prefix product of (1 - a) gives the transmittance in front of each sample, the
-// first sample whose transmittance after it falls to T_threshold stops the ray (it is composited
-// but not counted, quirk q6), and the row's last transmittance carries to the next row.
 template <int C>
 __global__ __launch_bounds__(256) void composite_fw_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
     float* __restrict__ rend, float* __restrict__ ws) {
-    constexpr int ROWS = 4;
     const int lane = threadIdx.x & 63;
-    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
-    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (n >= R) return;
-    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
-    const int N = (int)rays_a[3 * n + 2];
-#if defined(NCN_DIAG_CF_STAGE) && NCN_DIAG_CF_STAGE == 1
-    if (lane == 0) opacity[ray] = (float)N;
-    return;
-#endif
-    float Tc = 1.0f, acc_o = 0.f, acc_d = 0.f;
-    float acc_r[C];
+    const RaySeg g = load_ray_seg(rays_a, R);
+    const int N = g.N;
+    const uint32_t nb = (uint32_t)N * 4u;
+    const auto r_s = buf_rsrc(sigmas + g.start, nb), r_d = buf_rsrc(deltas + g.start, nb);
+    const auto r_t = buf_rsrc(ts + g.start, nb), r_r = buf_rsrc(raws + g.start * C, nb * C);
+    const auto r_w = buf_rsrc(ws + g.start, nb);
+    float Tc = 1.0f;
+    float acc[2 + C];  // opacity, depth, rend[C]
 #pragma unroll
-    for (int i = 0; i < C; i++) acc_r[i] = 0.f;
+    for (int i = 0; i < 2 + C; i++) acc[i] = 0.f;
     int total = N;
-    bool done = false;
-    for (int base = 0; base < N; base += 64 * ROWS) {
-        float sg[ROWS], dl[ROWS], tt[ROWS], rr[ROWS][C];
+    // base == 0 runs once even for N == 0 (all loads read 0): the loads then need only the
+    // segment, so the compiler issues them right behind the scalar batch
+    for (int base = 0; base == 0 || base < N; base += 64 * CF_ROWS) {
+        float sg[CF_ROWS], dl[CF_ROWS], tt[CF_ROWS], rr[CF_ROWS][C];
 #pragma unroll
-        for (int r = 0; r < ROWS; r++) {  // every load of the round issued before any use
-            const int k = base + r * 64 + lane;
-            const int64_t s = start + k;
-            const bool v = k < N && !done;
-            sg[r] = v ? sigmas[s] : 0.f;
-            dl[r] = v ? deltas[s] : 0.f;
-            tt[r] = v ? ts[s] : 0.f;
+        for (int r = 0; r < CF_ROWS; r++) {
+            const uint32_t k = (uint32_t)(base + r * 64 + lane);
+            if (r == 0 || base + r * 64 < N) {  // uniform
+                sg[r] = buf_load(r_s, k * 4u);
+                dl[r] = buf_load(r_d, k * 4u);
+                tt[r] = buf_load(r_t, k * 4u);
 #pragma unroll
-            for (int i = 0; i < C; i++) rr[r][i] = v ? raws[s * C + i] : 0.f;
-        }
-#if defined(NCN_DIAG_CF_STAGE) && NCN_DIAG_CF_STAGE == 2
-        {
-            float t = 0.f;
-            for (int r = 0; r < ROWS; r++) t += sg[r] + dl[r] + tt[r] + rr[r][0] + rr[r][1] + rr[r][C - 1];
-            if (t == 1234.5f) opacity[ray] = t;
-            continue;
-        }
-#endif
+                for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+            } else {
+                sg[r] = dl[r] = tt[r] = 0.f;
 #pragma unroll
-        for (int r = 0; r < ROWS; r++) {
-            const int k = base + r * 64 + lane;
-            if (base + r * 64 >= N) break;  // uniform
-            const bool valid = k < N;
-            if (done) {
-                if (valid) ws[start + k] = 0.f;
-                continue;
+                for (int i = 0; i < C; i++) rr[r][i] = 0.f;
             }
+        }
+        bool stopped = false;
+#pragma unroll
+        for (int r = 0; r < CF_ROWS; r++) {
+            const int kb = base + r * 64;
+            if (kb >= N) break;  // uniform
             const float a = 1.0f - __expf(-sg[r] * dl[r]);
             const float om = 1.0f - a;
-            const float incl = wave_incl_prod_dpp(valid ? om : 1.0f);
-            const float Tb = Tc * wave_shr1_dpp(incl, 1.0f);  // transmittance in front of the sample
-            const float Ta = Tb * om;                         // ... and after it
-            const uint64_t stopm = __ballot(valid && Ta <= T_thr);
+            const float Tb = Tc * wave_shr1_dpp(wave_incl_prod_dpp_fused(om), 1.0f);  // in front of the sample
+            const float Ta = Tb * om;                                                  // ... and after it
+            // lanes past N carry Ta of the last sample, so they can only match after a real one
+            const uint64_t stopm = __ballot(Ta <= T_thr);
             const int stop_lane = stopm ? __builtin_ctzll(stopm) : 64;
-            const bool inc = valid && lane <= stop_lane;
-            const float w = inc ? a * Tb : 0.f;
-            if (valid) ws[start + k] = w;
+            const float w = lane <= stop_lane ? a * Tb : 0.f;
+            buf_store(r_w, (uint32_t)(kb + lane) * 4u, w);
+            acc[0] += w;
+            acc[1] = fmaf(w, tt[r], acc[1]);
 #pragma unroll
-            for (int i = 0; i < C; i++) acc_r[i] = fmaf(w, rr[r][i], acc_r[i]);
-            acc_d = fmaf(w, tt[r], acc_d);
-            acc_o += w;
-            if (stopm) {
-                done = true;
-                total = base + r * 64 + stop_lane;
+            for (int i = 0; i < C; i++) acc[2 + i] = fmaf(w, rr[r][i], acc[2 + i]);
+            if (stopm) {  // rest of the segment: ws = 0 (volumerendering.cu:133 breaks, ws stays 0)
+                total = kb + stop_lane;
+                for (int k = kb + 64 + lane; k < N; k += 64) buf_store(r_w, (uint32_t)k * 4u, 0.f);
+                stopped = true;
+                break;
             }
             Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
         }
+        if (stopped) break;
     }
-    acc_o = wave_sum_dpp(acc_o);
-    acc_d = wave_sum_dpp(acc_d);
+    wave_sum_multi<2 + C>(acc);
+    if (g.live && lane == 0) {
+        opacity[g.ray] = acc[0];
+        depth[g.ray] = acc[1];
 #pragma unroll
-    for (int i = 0; i < C; i++) acc_r[i] = wave_sum_dpp(acc_r[i]);
-    if (lane == 0) {
-        opacity[ray] = acc_o;
-        depth[ray] = acc_d;
-#pragma unroll
-        for (int i = 0; i < C; i++) rend[ray * C + i] = acc_r[i];
-        total_samples[ray] = total;
+        for (int i = 0; i < C; i++) rend[g.ray * C + i] = acc[2 + i];
+        total_samples[g.ray] = total;
     }
 }
 
-#endif
-
 // volumerendering.cu:297-364.  T is the post-update transmittance (quirk q10); d/r are inclusive
 // prefix sums of w*t and w*raw; (sum - pre[s]) is the suffix of dL_dws*ws over the WHOLE marched
-// segment (:331-335).  Evaluation order of dL_dsigmas follows :349-359.
+// segment (:331-335).  Evaluation order of dL_dsigmas follows :349-359.  Same row structure as the
+// forward; the prefix sums are DPP scans carried across rows.  A NULL upstream gradient skips its
+// term (the reference's are zero tensors: dL_dws is always zero in training, quirk q5).
 template <int C>
 __global__ __launch_bounds__(256) void composite_bw_kernel(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
@@ -568,12 +474,11 @@ __global__ __launch_bounds__(256) void composite_bw_kernel(
     const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
     float* __restrict__ dL_draws) {
+    constexpr int ROWS = 2;
     const int lane = threadIdx.x & 63;
-    // wave-uniform ray index (readfirstlane: the per-ray loads below become scalar s_loads)
-    const int64_t n = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (n >= R) return;
-    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
-    const int N = (int)rays_a[3 * n + 2];
+    const RaySeg g = load_ray_seg(rays_a, R);
+    const int N = g.N;
+    const int64_t ray = g.ray;
     const float dO = dL_dopacity ? dL_dopacity[ray] : 0.f;
     const float dD = dL_ddepth ? dL_ddepth[ray] : 0.f;
     const float O = opacity[ray], D = depth[ray];
@@ -583,122 +488,83 @@ __global__ __launch_bounds__(256) void composite_bw_kernel(
         dR[i] = dL_drend ? dL_drend[ray * C + i] : 0.f;
         RE[i] = rend[ray * C + i];
     }
-    // total of dL_dws*ws over the segment
-    float tot = 0.f;
-    if (dL_dws) {
-        for (int k = lane; k < N; k += 64) tot = fmaf(dL_dws[start + k], ws[start + k], tot);
-        tot = wave_sum(tot);
+    const float gO = dO * (1 - O);
+    const uint32_t nb = (uint32_t)N * 4u;
+    const auto r_s = buf_rsrc(sigmas + g.start, nb), r_d = buf_rsrc(deltas + g.start, nb);
+    const auto r_t = buf_rsrc(ts + g.start, nb), r_r = buf_rsrc(raws + g.start * C, nb * C);
+    const auto r_gs = buf_rsrc(dL_dsigmas + g.start, nb), r_gr = buf_rsrc(dL_draws + g.start * C, nb * C);
+    const bool has_dws = dL_dws != nullptr;
+    const auto r_dw = buf_rsrc(has_dws ? dL_dws + g.start : dL_dsigmas, has_dws ? nb : 0u);
+    const auto r_ws = buf_rsrc(has_dws ? ws + g.start : dL_dsigmas, has_dws ? nb : 0u);
+    float tot = 0.f;  // sum of dL_dws * ws over the whole segment
+    if (has_dws) {
+        for (int k = lane; k < N; k += 64) tot = fmaf(buf_load(r_dw, k * 4u), buf_load(r_ws, k * 4u), tot);
+        tot = wave_sum_dpp(tot);
     }
-    float Tc = 1.0f, cd = 0.f, cpw = 0.f;
-    float cr[C];
+    float Tc = 1.0f, cd = 0.f, cpw = 0.f, cr[C];
 #pragma unroll
     for (int i = 0; i < C; i++) cr[i] = 0.f;
-    bool done = false;
-    for (int base = 0; base < N; base += CHUNK) {
-        const int k0 = base + lane * SPL;
-        if (done) {
+    for (int base = 0; base == 0 || base < N; base += 64 * ROWS) {
+        float sg[ROWS], dl[ROWS], tt[ROWS], rr[ROWS][C], dws[ROWS], pw[ROWS];
 #pragma unroll
-            for (int j = 0; j < SPL; j++)
-                if (k0 + j < N) {
-                    const int64_t s = start + k0 + j;
-                    dL_dsigmas[s] = 0.f;
+        for (int r = 0; r < ROWS; r++) {
+            const uint32_t k = (uint32_t)(base + r * 64 + lane);
+            if (r == 0 || base + r * 64 < N) {
+                sg[r] = buf_load(r_s, k * 4u);
+                dl[r] = buf_load(r_d, k * 4u);
+                tt[r] = buf_load(r_t, k * 4u);
 #pragma unroll
-                    for (int i = 0; i < C; i++) dL_draws[s * C + i] = 0.f;
-                }
-            continue;
-        }
-        float a[SPL], om[SPL], tt[SPL], dl[SPL], rr[SPL][C], pw[SPL];
-        bool valid[SPL];
+                for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+                dws[r] = has_dws ? buf_load(r_dw, k * 4u) : 0.f;
+                pw[r] = has_dws ? dws[r] * buf_load(r_ws, k * 4u) : 0.f;
+            } else {
+                sg[r] = dl[r] = tt[r] = dws[r] = pw[r] = 0.f;
 #pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            const int64_t s = start + k0 + j;
-            valid[j] = (k0 + j) < N;
-            const float sg = valid[j] ? sigmas[s] : 0.f;
-            dl[j] = valid[j] ? deltas[s] : 0.f;
-            tt[j] = valid[j] ? ts[s] : 0.f;
-#pragma unroll
-            for (int i = 0; i < C; i++) rr[j][i] = valid[j] ? raws[s * C + i] : 0.f;
-            pw[j] = (dL_dws && valid[j]) ? dL_dws[s] * ws[s] : 0.f;
-            a[j] = 1.0f - __expf(-sg * dl[j]);
-            om[j] = 1.0f - a[j];
-        }
-        float lp = om[0];
-#pragma unroll
-        for (int j = 1; j < SPL; j++) lp *= om[j];
-        const float inclP = wave_incl_prod(lp, lane);
-        float exclP = __shfl_up(inclP, 1, 64);
-        if (lane == 0) exclP = 1.0f;
-        float T = Tc * exclP;
-        float w[SPL], Ta[SPL];
-        int my_stop = SPL;
-#pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            w[j] = a[j] * T;
-            T *= om[j];
-            Ta[j] = T;
-            if (valid[j] && T <= T_thr && my_stop == SPL) my_stop = j;
-        }
-        const uint64_t mask = __ballot(my_stop < SPL);
-        int stop_lane = 64, stop_j = SPL;
-        if (mask) {
-            stop_lane = __builtin_ctzll(mask);
-            stop_j = __shfl(my_stop, stop_lane, 64);
-        }
-        bool inc[SPL];
-        float ld = 0.f, lpw = 0.f, lr[C];
-#pragma unroll
-        for (int i = 0; i < C; i++) lr[i] = 0.f;
-#pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            inc[j] = valid[j] && (lane < stop_lane || (lane == stop_lane && j <= stop_j));
-            if (!inc[j]) w[j] = 0.f;
-            ld = fmaf(w[j], tt[j], ld);
-#pragma unroll
-            for (int i = 0; i < C; i++) lr[i] = fmaf(w[j], rr[j][i], lr[i]);
-            lpw += pw[j];
-        }
-        // exclusive lane prefixes
-        const float id = wave_incl_sum(ld, lane), ipw = wave_incl_sum(lpw, lane);
-        float ed = __shfl_up(id, 1, 64), epw = __shfl_up(ipw, 1, 64);
-        if (lane == 0) { ed = 0.f; epw = 0.f; }
-        float run_d = cd + ed, run_pw = cpw + epw;
-        float run_r[C], ir[C];
-#pragma unroll
-        for (int i = 0; i < C; i++) {
-            ir[i] = wave_incl_sum(lr[i], lane);
-            float er = __shfl_up(ir[i], 1, 64);
-            if (lane == 0) er = 0.f;
-            run_r[i] = cr[i] + er;
-        }
-#pragma unroll
-        for (int j = 0; j < SPL; j++) {
-            run_d = fmaf(w[j], tt[j], run_d);
-            run_pw += pw[j];
-#pragma unroll
-            for (int i = 0; i < C; i++) run_r[i] = fmaf(w[j], rr[j][i], run_r[i]);
-            if (!valid[j]) continue;
-            const int64_t s = start + k0 + j;
-            if (!inc[j]) {
-                dL_dsigmas[s] = 0.f;
-#pragma unroll
-                for (int i = 0; i < C; i++) dL_draws[s * C + i] = 0.f;
-                continue;
+                for (int i = 0; i < C; i++) rr[r][i] = 0.f;
             }
-            const float dws = dL_dws ? dL_dws[s] : 0.f;
-            float g = dO * (1 - O) + dD * (tt[j] * Ta[j] - (D - run_d)) + Ta[j] * dws - (tot - run_pw);
+        }
+        bool stopped = false;
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            const int kb = base + r * 64;
+            if (kb >= N) break;
+            const float a = 1.0f - __expf(-sg[r] * dl[r]);
+            const float om = 1.0f - a;
+            const float Tb = Tc * wave_shr1_dpp(wave_incl_prod_dpp_fused(om), 1.0f);
+            const float Ta = Tb * om;
+            const uint64_t stopm = __ballot(Ta <= T_thr);
+            const int stop_lane = stopm ? __builtin_ctzll(stopm) : 64;
+            const bool inc = lane <= stop_lane;
+            const float w = inc ? a * Tb : 0.f;
+            // inclusive prefixes (this row + carry) of w*t, w*raw_i, dL_dws*ws
+            const float run_d = cd + wave_incl_sum_dpp(w * tt[r]);
+            const float run_pw = cpw + wave_incl_sum_dpp(pw[r]);
+            float run_r[C];
+#pragma unroll
+            for (int i = 0; i < C; i++) run_r[i] = cr[i] + wave_incl_sum_dpp(w * rr[r][i]);
+            float gs = gO + dD * (tt[r] * Ta - (D - run_d)) + Ta * dws[r] - (tot - run_pw);
 #pragma unroll
             for (int i = 0; i < C; i++) {
-                dL_draws[s * C + i] = dR[i] * w[j];
-                g += dR[i] * (rr[j][i] * Ta[j] - (RE[i] - run_r[i]));
+                gs += dR[i] * (rr[r][i] * Ta - (RE[i] - run_r[i]));
+                buf_store(r_gr, (uint32_t)(kb + lane) * (4u * C) + 4u * i, dR[i] * w);
             }
-            dL_dsigmas[s] = g * dl[j];
-        }
-        cd = __shfl(cd + id, 63, 64);
-        cpw = __shfl(cpw + ipw, 63, 64);
+            buf_store(r_gs, (uint32_t)(kb + lane) * 4u, inc ? gs * dl[r] : 0.f);
+            if (stopm) {
+                for (int k = kb + 64 + lane; k < N; k += 64) {
+                    buf_store(r_gs, (uint32_t)k * 4u, 0.f);
 #pragma unroll
-        for (int i = 0; i < C; i++) cr[i] = __shfl(cr[i] + ir[i], 63, 64);
-        if (mask) done = true;
-        Tc = __shfl(T, 63, 64);
+                    for (int i = 0; i < C; i++) buf_store(r_gr, (uint32_t)k * (4u * C) + 4u * i, 0.f);
+                }
+                stopped = true;
+                break;
+            }
+            Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
+            cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_d), 63));
+            cpw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_pw), 63));
+#pragma unroll
+            for (int i = 0; i < C; i++) cr[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_r[i]), 63));
+        }
+        if (stopped) break;
     }
 }
 

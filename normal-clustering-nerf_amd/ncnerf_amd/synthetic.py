@@ -97,7 +97,52 @@ def camera_directions():
 
 
 def _gt_color(rays_d):
+    """View-only target (gt="direction"): a smooth function of the ray direction."""
     return (0.5 + 0.4 * np.sin(3.0 * rays_d + np.array([0.0, 2.1, 4.2], np.float32))).astype(np.float32)
+
+
+_TEX = np.array([[11.0, 7.0, -5.0], [-6.0, 13.0, 8.0], [9.0, -4.0, 12.0]], np.float32)  # texture frequencies
+_TEX_PHASE = np.array([0.3, 2.2, 4.1], np.float32)
+
+
+def texture_rgb(p):
+    """Albedo of the room surfaces at points p (N,3): smooth procedural texture in [0.1, 0.9]."""
+    return (0.5 + 0.4 * np.sin(p @ _TEX.T + _TEX_PHASE)).astype(np.float32)
+
+
+def first_hit(occ, rays_o, rays_d, scale=0.5, step_vox=0.25, t_max=2.0, chunk=64):
+    """Distance to the first occupied voxel of `occ` along each ray (inf if none inside the
+    [-scale, scale]^3 box), by stepping a quarter voxel at a time from t = 0."""
+    G = occ.shape[0]
+    h = step_vox * 2 * scale / G
+    n = rays_o.shape[0]
+    t_hit = np.full(n, np.inf, np.float32)
+    alive = np.arange(n)
+    t0 = 0.0
+    while alive.size and t0 < t_max:
+        t = t0 + h * np.arange(chunk, dtype=np.float32)
+        p = rays_o[alive, None, :] + rays_d[alive, None, :] * t[None, :, None]  # (A, chunk, 3)
+        inside = np.all(np.abs(p) < scale, axis=-1)
+        v = np.clip(np.floor((p + scale) / (2 * scale) * G).astype(np.int64), 0, G - 1)
+        hit = inside & occ[v[..., 0], v[..., 1], v[..., 2]]
+        left = ~inside & (t[None, :] > 0)  # outside the box after starting: the ray has left
+        first = np.where(hit.any(1), hit.argmax(1), chunk)
+        gone = np.where(left.any(1), left.argmax(1), chunk)
+        found = first < gone
+        t_hit[alive[found]] = t[first[found]]
+        alive = alive[~found & (gone == chunk)]
+        t0 += h * chunk
+    return t_hit
+
+
+def surface_rgb(occ, rays_o, rays_d, scale=0.5):
+    """Target colour of a ray (gt="surface", default): texture_rgb at its first occupied voxel,
+    white (the reference's background, rendering.py:232-240) if it hits nothing."""
+    t = first_hit(occ, rays_o, rays_d, scale)
+    rgb = np.ones((rays_o.shape[0], 3), np.float32)
+    m = np.isfinite(t)
+    rgb[m] = texture_rgb(rays_o[m] + rays_d[m] * t[m, None])
+    return rgb
 
 
 class SyntheticScene:
@@ -113,8 +158,9 @@ class SyntheticScene:
         o1 = np.arange(PATCH * PATCH).reshape(PATCH, PATCH)
         self.x1_off, self.x2_off, self.x3_off = o1[1:, 1:].reshape(-1), o1[:-1, 1:].reshape(-1), o1[1:, :-1].reshape(-1)
 
-    def batch(self, n_rays, seed):
-        """A dict like BaseDataset.__getitem__ + get_rays: rays_o, rays_d (R,3) f32, rgb (R,3), patch info."""
+    def batch(self, n_rays, seed, gt="surface"):
+        """A dict like BaseDataset.__getitem__ + get_rays: rays_o, rays_d (R,3) f32, rgb (R,3), patch info.
+        gt: "surface" (textured room, the PSNR-parity target) or "direction" (view-only colour)."""
         assert n_rays % (PATCH * PATCH) == 0
         rng = np.random.default_rng(seed)
         n_p = n_rays // (PATCH * PATCH)
@@ -128,11 +174,12 @@ class SyntheticScene:
         P = self.poses[cam]
         rays_d = np.einsum("nij,nj->ni", P[:, :, :3], dcam).astype(np.float32)
         rays_o = P[:, :, 3].astype(np.float32)
-        return {"rays_o": rays_o, "rays_d": rays_d, "rgb": _gt_color(rays_d), "patch_area": PATCH * PATCH,
+        rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale) if gt == "surface" else _gt_color(rays_d)
+        return {"rays_o": rays_o, "rays_d": rays_d, "rgb": rgb, "patch_area": PATCH * PATCH,
                 "x1_offsets_local": self.x1_off, "x2_offsets_local": self.x2_off, "x3_offsets_local": self.x3_off}
 
-    def torch_batch(self, n_rays, seed, device):
-        b = self.batch(n_rays, seed)
+    def torch_batch(self, n_rays, seed, device, gt="surface"):
+        b = self.batch(n_rays, seed, gt)
         out = {}
         for k, v in b.items():
             out[k] = torch.from_numpy(np.ascontiguousarray(v)).to(device) if isinstance(v, np.ndarray) else v

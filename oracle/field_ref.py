@@ -71,28 +71,31 @@ def _grid_index(pg, res, params):
 
 
 def hash_encode(x01, table, levels):
-    """x01: (N,3) f32 in [0,1]; table: (n_entries, 2) f32 -> (N, 32) f32 (level-major, 2 feats)."""
-    feats = []
+    """x01: (N,3) f32 in [0,1]; table: (n_entries, 2) f32 -> (N, 32) f32 (level-major, 2 feats).
+
+    All 16 levels x 8 corners are gathered by ONE `table[idx]` (so autograd scatters the table
+    gradient once, not 128 times into dense zero tables)."""
+    n = x01.shape[0]
     xd = x01.double()
-    for lv in levels:
-        pos = (xd * lv["scale"] + 0.5).float()  # fma(scale, x, 0.5) in fp32 (exact product in f64)
-        fl = torch.floor(pos)
-        frac = pos - fl
-        pg = (fl.to(torch.int64)) & 0xFFFFFFFF  # (uint32)(int)floor
-        acc = torch.zeros(x01.shape[0], F_PER_LEVEL, dtype=torch.float32)
-        for c in range(8):
-            w = torch.ones(x01.shape[0], dtype=torch.float32)
-            pc = pg.clone()
-            for dim in range(3):
-                if c & (1 << dim):
-                    w = w * frac[:, dim]
-                    pc[:, dim] = (pc[:, dim] + 1) & 0xFFFFFFFF
-                else:
-                    w = w * (1 - frac[:, dim])
-            idx = _grid_index(pc, lv["res"], lv["params"]) + lv["offset"]
-            acc = acc + w[:, None] * table[idx]
-        feats.append(acc)
-    return torch.cat(feats, dim=1)
+    corner = torch.tensor([[(c >> dim) & 1 for dim in range(3)] for c in range(8)], dtype=torch.int64)  # (8,3)
+    idx_l, w_l = [], []
+    with torch.no_grad():
+        for lv in levels:
+            pos = (xd * lv["scale"] + 0.5).float()  # fma(scale, x, 0.5) in fp32 (exact product in f64)
+            fl = torch.floor(pos)
+            frac = pos - fl
+            pg = (fl.to(torch.int64)) & 0xFFFFFFFF  # (uint32)(int)floor
+            pc = (pg[:, None, :] + corner[None]) & 0xFFFFFFFF  # (N,8,3)
+            # trilinear weight, product over dims in order x, y, z (as tcnn)
+            wd = torch.where(corner[None].bool(), frac[:, None, :], 1 - frac[:, None, :])  # (N,8,3)
+            w = torch.ones(n, 8, dtype=torch.float32) * wd[..., 0] * wd[..., 1] * wd[..., 2]
+            idx_l.append(_grid_index(pc, lv["res"], lv["params"]) + lv["offset"])
+            w_l.append(w)
+    L = len(levels)
+    idx = torch.stack(idx_l, 1)  # (N, L*8), level-major, corner-minor
+    wts = torch.stack(w_l, 1).view(n, L, 8, 1)
+    g = table[idx].view(n, L, 8, F_PER_LEVEL)
+    return (wts * g).sum(2).reshape(n, L * F_PER_LEVEL)
 
 
 def _f16(t, on):

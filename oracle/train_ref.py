@@ -60,14 +60,15 @@ class CPUTrainer:
                                       {"params": self.params[1:], "weight_decay": 1e-6}], lr=lr, eps=1e-15)
         self.w_cluster, self.opacity_w = w_cluster, opacity_w
 
-    def step(self, batch, global_step=3000):
+    def step(self, batch, global_step=3000, noise=None):
+        """One training step; `noise` (R,) injects the marcher's perturbation (default torch.rand)."""
         o, d = batch["rays_o"], batch["rays_d"]
         R = o.shape[0]
         _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
         ht = ht[:, 0].copy()
         near = (ht[:, 0] >= 0) & (ht[:, 0] < 0.01)
         ht[near, 0] = 0.01
-        noise = torch.rand(R).numpy()
+        noise = torch.rand(R).numpy() if noise is None else np.ascontiguousarray(noise, np.float32)
         rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, self.bitfield, 1, 0.5, 0.0,
                                                                              noise, 128, 1024)
         self.opt.zero_grad()
