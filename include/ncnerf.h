@@ -37,6 +37,11 @@ int ncn_packbits(const float* density_grid, int64_t n_bytes, float threshold, ui
 int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays,
                            const float* centers, const float* half_sizes, int64_t n_voxels, int max_hits,
                            int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx, void* stream);
+/* ray_aabb_intersect with render()'s near clamp fused (rendering.py:28): the first hit's t1 is set
+ * to near_distance when it lies in [0, near_distance). */
+int ncn_ray_aabb_intersect_near(const float* rays_o, const float* rays_d, int64_t n_rays, const float* centers,
+                                const float* half_sizes, int64_t n_voxels, int max_hits, float near_distance,
+                                int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx, void* stream);
 
 /* ---- training marcher: replaces vren.raymarching_train (raymarching.cu:283-332).
  * Pass 1 (walk): one walk per ray; samples go to a per-ray slab [R][max_samples] (xyz: 3 floats,
@@ -72,6 +77,21 @@ int ncn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, con
                            const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
                            int64_t n_samples, int n_rend, const float* opacity, const float* depth,
                            const float* rend, float T_threshold, float* dL_dsigmas, float* dL_draws, void* stream);
+
+/* render()'s white/zero background fused into the compositor (rendering.py:232-240, used by the
+ * train path when exp_step_factor == 0): the forward additionally writes rgb_bg = rend + bg *
+ * (1 - opacity) (R, n_rend); the backward takes dL/drgb_bg in place of dL/drend and adds the
+ * background's -bg * sum_i dL/drgb_i to dL/dopacity.  bg = 0 / rgb_bg = NULL is the plain kernel. */
+int ncn_composite_train_fw_bg(const float* sigmas, const float* raws, const float* deltas, const float* ts,
+                              const int64_t* rays_a, int64_t n_rays, int64_t n_samples, int n_rend, float T_threshold,
+                              int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws, float bg,
+                              float* rgb_bg, void* stream);
+int ncn_composite_train_bw_bg(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                              const float* dL_dws, const float* sigmas, const float* raws, const float* ws,
+                              const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
+                              int64_t n_samples, int n_rend, const float* opacity, const float* depth,
+                              const float* rend, float T_threshold, float bg, float* dL_dsigmas, float* dL_draws,
+                              void* stream);
 int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
                           int64_t* alive, int64_t n_alive, int n_samples, int n_rend, float T_threshold,
                           const int32_t* n_eff, float* opacity, float* depth, float* rend, void* stream);
@@ -131,17 +151,33 @@ int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opaci
 /* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations, one launch each over
  * 32 workgroups), cluster selection, the three cluster losses and their gradient w.r.t. the
  * normals, scaled by w_ort / w_dot / w_l1.  n_tri <= 16384.
- * out_losses[0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter; [3] = valid n;
- * [4..6] = the weighted terms; out_labels (n_tri) int32 in {0,+-1,+-2,+-3} (-9 = invalid normal);
+ * out_losses (11 floats): [0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter;
+ * [3] = valid n; [4..6] = the weighted terms; [7..9] = the weights used; [10] = total (only when
+ * photo_loss is given: photo_loss[0] + photo_loss[1] + [4] + [5] + [6], losses.py's sum over the
+ * loss dict); out_labels (n_tri) int32 in {0,+-1,+-2,+-3} (-9 = invalid normal);
  * out_centroids (K,3); dL_dnormals (3,n_tri,3) fully written: the gradient of w_ort*ort, w_dot*centr_dot and w_l1*centr_L1
  * separately, so any upstream weighting of the three terms is a 3-term combination.
- * w_dev: NULL, or 3 device floats that replace (w_ort, w_dot, w_l1) (the step-dependent weight
- *   schedule of losses.py:217 evaluated on the device, for a graph-captured step).
+ * w_dev: NULL, or 3 device floats that replace (w_ort, w_dot, w_l1).
+ * step_dev: NULL, or the device training step: the weights become the schedule of losses.py:217,
+ *   max(0, min(w, (step - sched_start) * (w / sched_grow))), evaluated on the device (graph-safe).
+ * photo_loss: NULL, or the 4 floats of ncn_photo_loss_fwd (for out_losses[10]).
  * workspace: ncn_cluster_workspace_words(K) 32-bit words of device scratch. */
 int64_t ncn_cluster_workspace_words(int K);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
-                     float w_ort, float w_dot, float w_l1, const float* w_dev, float* out_losses, int32_t* out_labels,
-                     float* out_centroids, float* dL_dnormals, float* workspace, void* stream);
+                     float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,
+                     float sched_start, float sched_grow, const float* photo_loss, float* out_losses,
+                     int32_t* out_labels, float* out_centroids, float* dL_dnormals, float* workspace, void* stream);
+/* Backward of the whole NeRFMTLoss in the reference configuration (photometric + opacity +
+ * normal-clustering terms, `all_images_triang_patch` 8x8 patches: n_rays a multiple of 64, the
+ * triangles of losses.py:307-313 in patch order, dL_dnormals the (3, 49*n_rays/64, 3) output of
+ * ncn_cluster_loss).  One thread per ray: dL_drgb (R,3) and dL_dopacity (R) of the photometric
+ * terms, and dL_ddepth (R) GATHERED from the ray's triangle roles (written, not accumulated: no
+ * zero-fill, no atomics).  up_total: NULL or the device gradient of `total`; up_terms: NULL or 5
+ * device floats (gradients of the rgb, opacity, ort, centr_dot, centr_L1 outputs), added to it. */
+int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
+                      const float* photo_loss, const float* rays_o, const float* rays_d, const float* depth,
+                      const float* dL_dnormals, const float* up_total, const float* up_terms, float* dL_drgb,
+                      float* dL_dopacity, float* dL_ddepth, void* stream);
 
 /* ---- optimizer (train_nerf.py:262-291, 954-955): global-norm clip + Adam over a flat buffer. ---- */
 /* step_inc: NULL, or a device int incremented once (the optimizer step counter of a captured step) */

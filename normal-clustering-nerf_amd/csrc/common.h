@@ -149,6 +149,14 @@ __device__ __forceinline__ void wave_sum_multi(float (&v)[K]) {
     }
 }
 
+// A zero the compiler cannot see through: indexing loop-invariant LDS data with it keeps the
+// loads inside the loop instead of hoisting them into (scarce) registers.
+__device__ __forceinline__ int opaque_zero() {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return z;
+}
+
 // Raw buffer resources (T8): a descriptor sized to one segment makes the hardware bounds check
 // return 0 for loads past it and drop stores past it, so row bodies carry no masks or branches.
 // Build them from wave-uniform values only (scalar loads / kernargs).

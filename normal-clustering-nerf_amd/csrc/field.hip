@@ -37,6 +37,13 @@ __device__ __forceinline__ half4_t relu_h4(float4_t v) {
     return h;
 }
 __device__ __forceinline__ float4_t zero4() { return float4_t{0.f, 0.f, 0.f, 0.f}; }
+// ReLU backward on a gradient tile: keep v where the saved fp16 activation is > 0, as fp16
+__device__ __forceinline__ half4_t relu_mask_h4(float4_t v, half4_t x) {
+    half4_t h;
+#pragma unroll
+    for (int i = 0; i < 4; i++) h[i] = x[i] > (_Float16)0.0f ? (_Float16)v[i] : (_Float16)0.0f;
+    return h;
+}
 
 // ---- packed weight fragment table (units: fragments of 64 lanes x 4 halves = 512 B) ----
 // forward (A = W, rows = out, K = in)
@@ -174,19 +181,15 @@ struct FwdState {
     half4_t x4[4];     // relu(G1)
     half4_t x5[4];     // relu(G2)
     float4_t out;      // rgb pre-activation tile (rows 0..2 valid on g==0)
-    uint32_t m1, m3, m4;  // relu masks: bit (4t+i)
 };
 
 __device__ __forceinline__ void mlp_sigma(const half4_t* F, int lane, half4_t e0, half4_t e1, FwdState& st) {
-    st.m1 = 0;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         float4_t acc = zero4();
         acc = mfma16(frag(F, F_L1 + 2 * t, lane), e0, acc);
         acc = mfma16(frag(F, F_L1 + 2 * t + 1, lane), e1, acc);
         st.x2[t] = relu_h4(acc);
-#pragma unroll
-        for (int i = 0; i < 4; i++) st.m1 |= (acc[i] > 0.f ? 1u : 0u) << (4 * t + i);
     }
     float4_t h = zero4();
 #pragma unroll
@@ -203,16 +206,12 @@ __device__ __forceinline__ void mlp_rgb(const half4_t* F, int lane, float dnx, f
     xd[2] = (_Float16)(g == 0 ? dnz : 0.f);
     xd[3] = (_Float16)0.f;
     st.x3d = xd;
-    st.m3 = 0;
-    st.m4 = 0;
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         float4_t acc = zero4();
         acc = mfma16(frag(F, F_L3 + 2 * t, lane), st.x3h, acc);
         acc = mfma16(frag(F, F_L3 + 2 * t + 1, lane), st.x3d, acc);
         st.x4[t] = relu_h4(acc);
-#pragma unroll
-        for (int i = 0; i < 4; i++) st.m3 |= (acc[i] > 0.f ? 1u : 0u) << (4 * t + i);
     }
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -220,8 +219,6 @@ __device__ __forceinline__ void mlp_rgb(const half4_t* F, int lane, float dnx, f
 #pragma unroll
         for (int ks = 0; ks < 4; ks++) acc = mfma16(frag(F, F_L4 + 4 * t + ks, lane), st.x4[ks], acc);
         st.x5[t] = relu_h4(acc);
-#pragma unroll
-        for (int i = 0; i < 4; i++) st.m4 |= (acc[i] > 0.f ? 1u : 0u) << (4 * t + i);
     }
     float4_t o = zero4();
 #pragma unroll
@@ -261,6 +258,7 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
     const int64_t wave0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t n_waves = (int64_t)gridDim.x * 4;
     for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
+        const half4_t* Fl = F + opaque_zero();  // fragments re-read from LDS every group (not hoisted)
         const int64_t s = grp * 16 + r;
         const bool valid = s < n;
         float x = 0.f, y = 0.f, z = 0.f;
@@ -281,7 +279,7 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
             enc_cache[(grp * 2 + 1) * 64 + lane] = b1;
         }
         FwdState st;
-        mlp_sigma(F, lane, b0, b1, st);
+        mlp_sigma(Fl, lane, b0, b1, st);
         if (g == 0 && valid) sigmas[s] = __expf(st.h[0]);  // TruncExp forward = exp
         if (mode == 1) continue;
         float dx = 0.f, dy = 0.f, dz = 0.f;
@@ -290,7 +288,7 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
             const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
             dx /= nrm; dy /= nrm; dz /= nrm;
         }
-        mlp_rgb(F, lane, dx, dy, dz, st);
+        mlp_rgb(Fl, lane, dx, dy, dz, st);
         if (g == 0 && valid) {
             rgbs[3 * s] = sigmoidf_(st.out[0]);
             rgbs[3 * s + 1] = sigmoidf_(st.out[1]);
@@ -313,23 +311,38 @@ struct WGrad {
     float4_t w1[4][2], w2[4], w3[4][2], w4[4][4], w5[4];
 };
 
-__device__ __forceinline__ half4_t transpose_tile(_Float16* slot, int lane, float4_t v) {
+// Tile transpose by MFMA: a C-layout tile (lane (g,r) = [feature 4g+i][sample r]) fed as the A
+// operand of A.I (I = 16x16 identity B fragment) comes back as [sample 4g+i][feature r], i.e. with
+// the samples on K as the dW products need.  Exact (products with 1, sums of zeros), one MFMA
+// instead of an LDS round trip.
+__device__ __forceinline__ half4_t identity_frag(int lane) {
     const int g = lane >> 4, r = lane & 15;
+    half4_t I;
 #pragma unroll
-    for (int i = 0; i < 4; i++) slot[(4 * g + i) * 16 + r] = (_Float16)v[i];
-    __builtin_amdgcn_wave_barrier();
-    const half4_t out = *(const half4_t*)(slot + r * 16 + 4 * g);
-    __builtin_amdgcn_wave_barrier();
-    return out;
+    for (int j = 0; j < 4; j++) I[j] = (_Float16)((4 * g + j == r) ? 1.0f : 0.0f);
+    return I;
 }
-__device__ __forceinline__ half4_t transpose_tile_h(_Float16* slot, int lane, half4_t v) {
-    const int g = lane >> 4, r = lane & 15;
-#pragma unroll
-    for (int i = 0; i < 4; i++) slot[(4 * g + i) * 16 + r] = v[i];
-    __builtin_amdgcn_wave_barrier();
-    const half4_t out = *(const half4_t*)(slot + r * 16 + 4 * g);
-    __builtin_amdgcn_wave_barrier();
-    return out;
+__device__ __forceinline__ half4_t transpose_tile_h(half4_t I, half4_t v) { return to_h4(mfma16(v, I, zero4())); }
+__device__ __forceinline__ half4_t transpose_tile(half4_t I, float4_t v) { return transpose_tile_h(I, to_h4(v)); }
+
+// Per-group inputs of the backward (prefetched one group ahead).
+struct BwdIn {
+    half4_t e0, e1;
+    float dx, dy, dz, dsig, dr0, dr1, dr2;
+};
+__device__ __forceinline__ void bwd_load(BwdIn& in, int64_t grp, int64_t n, int lane, const half4_t* __restrict__ enc,
+                                         const float* __restrict__ dirs, const float* __restrict__ dL_dsig,
+                                         const float* __restrict__ dL_drgb) {
+    const int64_t s = grp * 16 + (lane & 15);
+    const bool valid = s < n;
+    in.e0 = enc[(grp * 2 + 0) * 64 + lane];
+    in.e1 = enc[(grp * 2 + 1) * 64 + lane];
+    in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
+    if (valid) {
+        in.dx = dirs[3 * s]; in.dy = dirs[3 * s + 1]; in.dz = dirs[3 * s + 2];
+        in.dsig = dL_dsig ? dL_dsig[s] : 0.f;
+        if (dL_drgb) { in.dr0 = dL_drgb[3 * s]; in.dr1 = dL_drgb[3 * s + 1]; in.dr2 = dL_drgb[3 * s + 2]; }
+    }
 }
 
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
@@ -338,19 +351,16 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     float* __restrict__ dE_out, float* __restrict__ slab) {
     const int64_t n_stride = n;  // dE layout [16][n_stride]
     if (n_dev) n = min<int64_t>(n, *n_dev);
-    // One LDS arena: [fragments | transpose slots] during the loop, reused as the fp32 dW
-    // reduction buffer afterwards (43 KB total -> several workgroups per CU).
-    constexpr int FRAG_BYTES = N_FRAGS * 64 * 8, SLOT_BYTES = 4 * 2 * 256 * 2;
-    static_assert(FRAG_BYTES + SLOT_BYTES >= NCN_FIELD_NW * 4, "arena too small for the dW reduction");
-    __shared__ __attribute__((aligned(16))) char arena[FRAG_BYTES + SLOT_BYTES];
+    // LDS: the weight fragments during the loop, reused as the fp32 dW reduction buffer afterwards.
+    constexpr int FRAG_BYTES = N_FRAGS * 64 * 8;
+    static_assert(FRAG_BYTES >= NCN_FIELD_NW * 4, "arena too small for the dW reduction");
+    __shared__ __attribute__((aligned(16))) char arena[FRAG_BYTES];
     half4_t* F = (half4_t*)arena;
-    _Float16* tslots = (_Float16*)(arena + FRAG_BYTES);
     float* red = (float*)arena;
     for (int i = threadIdx.x; i < N_FRAGS * 64; i += BWD_THREADS) F[i] = wpacked[i];
     __syncthreads();
     const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, wid = threadIdx.x >> 6;
-    _Float16* sA = tslots + wid * 512;
-    _Float16* sB = tslots + wid * 512 + 256;
+    const half4_t Iden = identity_frag(lane);
     WGrad acc;
 #pragma unroll
     for (int a = 0; a < 4; a++) {
@@ -363,22 +373,28 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t n_groups = (n + 15) / 16;
     const int64_t wave0 = (int64_t)blockIdx.x * 4 + wid;
     const int64_t n_waves = (int64_t)gridDim.x * 4;
+    BwdIn nxt;
+    if (wave0 < n_groups) bwd_load(nxt, wave0, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
     for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
         const int64_t s = grp * 16 + r;
         const bool valid = s < n;
-        const half4_t e0 = enc_cache[(grp * 2 + 0) * 64 + lane];
-        const half4_t e1 = enc_cache[(grp * 2 + 1) * 64 + lane];
-        float dx = 0.f, dy = 0.f, dz = 0.f, dsig = 0.f, dr0 = 0.f, dr1 = 0.f, dr2 = 0.f;
+        const half4_t* Fl = F + opaque_zero();  // fragments re-read from LDS every group (not hoisted)
+        const BwdIn cur = nxt;  // the next group's loads go out before this group's math
+        if (grp + n_waves < n_groups) bwd_load(nxt, grp + n_waves, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+        const half4_t e0 = cur.e0, e1 = cur.e1;
+        float dx = cur.dx, dy = cur.dy, dz = cur.dz;
+        const float dsig = cur.dsig, dr0 = cur.dr0, dr1 = cur.dr1, dr2 = cur.dr2;
         if (valid) {
-            dx = dirs[3 * s]; dy = dirs[3 * s + 1]; dz = dirs[3 * s + 2];
             const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
             dx /= nrm; dy /= nrm; dz /= nrm;
-            dsig = dL_dsig ? dL_dsig[s] : 0.f;
-            if (dL_drgb) { dr0 = dL_drgb[3 * s]; dr1 = dL_drgb[3 * s + 1]; dr2 = dL_drgb[3 * s + 2]; }
         }
         FwdState st;
-        mlp_sigma(F, lane, e0, e1, st);
-        mlp_rgb(F, lane, dx, dy, dz, st);
+        mlp_sigma(Fl, lane, e0, e1, st);
+        mlp_rgb(Fl, lane, dx, dy, dz, st);
+        // Backward through the five layers with each layer's weight gradient accumulated as soon as
+        // its output gradient exists (dW[out][in] += sum_s dY[out][s] X[in][s]: A = dY with the
+        // samples on K, B = X with the samples on K, both via transpose_tile), so every activation
+        // tile dies right after its last use.  ReLU masks come from the saved fp16 activations.
         // dY5: d(pre-sigmoid) = drgb * s(1-s), rows 0..2 on g==0
         float4_t dy5 = zero4();
         if (g == 0) {
@@ -388,46 +404,69 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             dy5[2] = dr2 * s2 * (1.f - s2);
         }
         const half4_t dy5h = to_h4(dy5);
-        // L5 backward -> dG2, masked -> dD4
-        float4_t dD4[4];
+        {   // dW5: dY = dy5 (1 out tile), X = x5 (4 in tiles)
+            const half4_t A = transpose_tile_h(Iden, dy5h);
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            float4_t v = mfma16(frag(F, B_L5 + t, lane), dy5h, zero4());
-#pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = ((st.m4 >> (4 * t + i)) & 1u) ? v[i] : 0.f;
-            dD4[t] = v;
+            for (int b = 0; b < 4; b++) acc.w5[b] = mfma16(A, transpose_tile_h(Iden, st.x5[b]), acc.w5[b]);
         }
+        // L5 backward -> dG2, ReLU(x5) mask -> dD4
         half4_t dD4h[4];
 #pragma unroll
-        for (int t = 0; t < 4; t++) dD4h[t] = to_h4(dD4[t]);
-        // L4 backward -> dG1 -> dD3
-        float4_t dD3[4];
+        for (int t = 0; t < 4; t++) dD4h[t] = relu_mask_h4(mfma16(frag(Fl, B_L5 + t, lane), dy5h, zero4()), st.x5[t]);
+        {   // dW4: dY = dD4 (4 out tiles), X = x4 (4 in tiles)
+            half4_t Xt[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) Xt[b] = transpose_tile_h(Iden, st.x4[b]);
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                const half4_t A = transpose_tile_h(Iden, dD4h[a]);
+#pragma unroll
+                for (int b = 0; b < 4; b++) acc.w4[a][b] = mfma16(A, Xt[b], acc.w4[a][b]);
+            }
+        }
+        // L4 backward -> dG1, ReLU(x4) mask -> dD3
+        half4_t dD3h[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) {
             float4_t v = zero4();
 #pragma unroll
-            for (int ks = 0; ks < 4; ks++) v = mfma16(frag(F, B_L4 + 4 * t + ks, lane), dD4h[ks], v);
-#pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = ((st.m3 >> (4 * t + i)) & 1u) ? v[i] : 0.f;
-            dD3[t] = v;
+            for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L4 + 4 * t + ks, lane), dD4h[ks], v);
+            dD3h[t] = relu_mask_h4(v, st.x4[t]);
         }
-        half4_t dD3h[4];
+        {   // dW3: dY = dD3 (4 out tiles), X = [d | h] : in tile 0 = d (cols 0..2), tile 1 = h (cols 3..18)
+            const half4_t Xd = transpose_tile_h(Iden, st.x3d);
+            const half4_t Xh = transpose_tile_h(Iden, st.x3h);
 #pragma unroll
-        for (int t = 0; t < 4; t++) dD3h[t] = to_h4(dD3[t]);
+            for (int a = 0; a < 4; a++) {
+                const half4_t A = transpose_tile_h(Iden, dD3h[a]);
+                acc.w3[a][0] = mfma16(A, Xd, acc.w3[a][0]);
+                acc.w3[a][1] = mfma16(A, Xh, acc.w3[a][1]);
+            }
+        }
         // L3 backward -> dh (rgb path) ; + TruncExp backward on h[0]
         float4_t dh = zero4();
 #pragma unroll
-        for (int ks = 0; ks < 4; ks++) dh = mfma16(frag(F, B_L3 + ks, lane), dD3h[ks], dh);
+        for (int ks = 0; ks < 4; ks++) dh = mfma16(frag(Fl, B_L3 + ks, lane), dD3h[ks], dh);
         if (g == 0) dh[0] += dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
         const half4_t dhh = to_h4(dh);
-        // L2 backward -> dH1 -> dD1
+        {   // dW2: dY = dh (1 out tile), X = x2 (4 in tiles)
+            const half4_t A = transpose_tile_h(Iden, dhh);
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc.w2[b] = mfma16(A, transpose_tile_h(Iden, st.x2[b]), acc.w2[b]);
+        }
+        // L2 backward -> dH1, ReLU(x2) mask -> dD1
         half4_t dD1h[4];
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            float4_t v = mfma16(frag(F, B_L2 + t, lane), dhh, zero4());
+        for (int t = 0; t < 4; t++) dD1h[t] = relu_mask_h4(mfma16(frag(Fl, B_L2 + t, lane), dhh, zero4()), st.x2[t]);
+        {   // dW1: dY = dD1 (4 out tiles), X = e (2 in tiles)
+            const half4_t X0 = transpose_tile_h(Iden, e0);
+            const half4_t X1 = transpose_tile_h(Iden, e1);
 #pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = ((st.m1 >> (4 * t + i)) & 1u) ? v[i] : 0.f;
-            dD1h[t] = to_h4(v);
+            for (int a = 0; a < 4; a++) {
+                const half4_t A = transpose_tile_h(Iden, dD1h[a]);
+                acc.w1[a][0] = mfma16(A, X0, acc.w1[a][0]);
+                acc.w1[a][1] = mfma16(A, X1, acc.w1[a][1]);
+            }
         }
         // L1 backward -> dE (tile t holds levels 8t+2g, 8t+2g+1)
         float4_t dE[2];
@@ -435,7 +474,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         for (int t = 0; t < 2; t++) {
             float4_t v = zero4();
 #pragma unroll
-            for (int ks = 0; ks < 4; ks++) v = mfma16(frag(F, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
+            for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
             dE[t] = v;
         }
         // encoding gradient -> level-major [16][n] float2 for the scatter pass
@@ -446,51 +485,6 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             o[(int64_t)(8 + 2 * g) * n_stride + s] = make_float2(dE[1][0], dE[1][1]);
             o[(int64_t)(9 + 2 * g) * n_stride + s] = make_float2(dE[1][2], dE[1][3]);
         }
-#ifndef NCN_DIAG_NO_DW
-        // ---- weight gradients: dW[out][in] += sum_s dY[out][s] X[in][s] ----
-        // A operand = dY^T rows (out, lane r) over K = samples; B operand = X over K = samples.
-        {   // L5: dY = dy5 (1 out tile), X = x5 (4 in tiles)
-            const half4_t A = transpose_tile(sA, lane, dy5);
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc.w5[b] = mfma16(A, transpose_tile_h(sB, lane, st.x5[b]), acc.w5[b]);
-        }
-        {   // L4: dY = dD4 (4 out tiles), X = x4 (4 in tiles)
-            half4_t Xt[4];
-#pragma unroll
-            for (int b = 0; b < 4; b++) Xt[b] = transpose_tile_h(sB, lane, st.x4[b]);
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const half4_t A = transpose_tile(sA, lane, dD4[a]);
-#pragma unroll
-                for (int b = 0; b < 4; b++) acc.w4[a][b] = mfma16(A, Xt[b], acc.w4[a][b]);
-            }
-        }
-        {   // L3: dY = dD3 (4 out tiles), X = [d | h] : in tile 0 = d (cols 0..2), tile 1 = h (cols 3..18)
-            const half4_t Xd = transpose_tile_h(sB, lane, st.x3d);
-            const half4_t Xh = transpose_tile_h(sB, lane, st.x3h);
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const half4_t A = transpose_tile(sA, lane, dD3[a]);
-                acc.w3[a][0] = mfma16(A, Xd, acc.w3[a][0]);
-                acc.w3[a][1] = mfma16(A, Xh, acc.w3[a][1]);
-            }
-        }
-        {   // L2: dY = dh (1 out tile), X = x2 (4 in tiles)
-            const half4_t A = transpose_tile(sA, lane, dh);
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc.w2[b] = mfma16(A, transpose_tile_h(sB, lane, st.x2[b]), acc.w2[b]);
-        }
-        {   // L1: dY = dD1 (4 out tiles), X = e (2 in tiles)
-            const half4_t X0 = transpose_tile_h(sB, lane, e0);
-            const half4_t X1 = transpose_tile_h(sB, lane, e1);
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const half4_t A = transpose_tile_h(sA, lane, dD1h[a]);
-                acc.w1[a][0] = mfma16(A, X0, acc.w1[a][0]);
-                acc.w1[a][1] = mfma16(A, X1, acc.w1[a][1]);
-            }
-        }
-#endif
     }
     // ---- workgroup reduction of the 40 tiles into LDS (C layout: row 4g+i, col r) ----
     __syncthreads();  // every wave is done with the fragments / slots: reuse the arena

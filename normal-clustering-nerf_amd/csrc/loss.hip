@@ -36,15 +36,11 @@ __global__ void normals_fwd_kernel(const float* __restrict__ o, const float* __r
     normals[3 * t + 2] = c2 / nrm;
 }
 
-// d/d depth through P_k = o + d*depth, a = P2-P1, b = P3-P1, c = a x b, n = c / max(|c|, eps)
-__global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __restrict__ d,
-                                   const float* __restrict__ depth, const int64_t* __restrict__ x1,
-                                   const int64_t* __restrict__ x2, const int64_t* __restrict__ x3, int64_t T,
-                                   const float* __restrict__ dn, const float* __restrict__ tw,
-                                   float* __restrict__ ddepth) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= T) return;
-    const int64_t i1 = x1[t], i2 = x2[t], i3 = x3[t];
+// d/d depth through P_k = o + d*depth, a = P2-P1, b = P3-P1, c = a x b, n = c / max(|c|, eps):
+// the three vertex gradients (g1, g2, g3) of triangle t for the normal gradient g.
+__device__ __forceinline__ void tri_depth_grads(const float* __restrict__ o, const float* __restrict__ d,
+                                                const float* __restrict__ depth, int64_t i1, int64_t i2, int64_t i3,
+                                                const float g[3], float& g1, float& g2, float& g3) {
     float P1[3], P2[3], P3[3];
     tri_points(o, d, depth, i1, P1);
     tri_points(o, d, depth, i2, P2);
@@ -53,12 +49,6 @@ __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __r
     const float b[3] = {P3[0] - P1[0], P3[1] - P1[1], P3[2] - P1[2]};
     const float c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
     const float len = sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-    float g[3] = {dn[3 * t], dn[3 * t + 1], dn[3 * t + 2]};
-    if (tw) {  // dn is (3, T, 3): per-term gradients combined with the upstream term weights
-        const float w0 = tw[0], w1 = tw[1], w2 = tw[2];
-#pragma unroll
-        for (int k = 0; k < 3; k++) g[k] = w0 * g[k] + w1 * dn[T * 3 + 3 * t + k] + w2 * dn[T * 6 + 3 * t + k];
-    }
     float dc[3];
     if (len > 1e-12f) {
         const float n[3] = {c[0] / len, c[1] / len, c[2] / len};
@@ -72,9 +62,32 @@ __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __r
     // c = a x b :  da = b x dc ,  db = dc x a
     const float da[3] = {b[1] * dc[2] - b[2] * dc[1], b[2] * dc[0] - b[0] * dc[2], b[0] * dc[1] - b[1] * dc[0]};
     const float db[3] = {dc[1] * a[2] - dc[2] * a[1], dc[2] * a[0] - dc[0] * a[2], dc[0] * a[1] - dc[1] * a[0]};
-    const float g2 = da[0] * d[3 * i2] + da[1] * d[3 * i2 + 1] + da[2] * d[3 * i2 + 2];
-    const float g3 = db[0] * d[3 * i3] + db[1] * d[3 * i3 + 1] + db[2] * d[3 * i3 + 2];
-    const float g1 = -((da[0] + db[0]) * d[3 * i1] + (da[1] + db[1]) * d[3 * i1 + 1] + (da[2] + db[2]) * d[3 * i1 + 2]);
+    g2 = da[0] * d[3 * i2] + da[1] * d[3 * i2 + 1] + da[2] * d[3 * i2 + 2];
+    g3 = db[0] * d[3 * i3] + db[1] * d[3 * i3 + 1] + db[2] * d[3 * i3 + 2];
+    g1 = -((da[0] + db[0]) * d[3 * i1] + (da[1] + db[1]) * d[3 * i1 + 1] + (da[2] + db[2]) * d[3 * i1 + 2]);
+}
+// normal gradient of triangle t: dn (T,3), or with term weights tw the (3,T,3) per-term stack
+__device__ __forceinline__ void tri_normal_grad(const float* __restrict__ dn, const float* tw, int64_t T, int64_t t,
+                                                float g[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) g[k] = dn[3 * t + k];
+    if (tw) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) g[k] = tw[0] * g[k] + tw[1] * dn[T * 3 + 3 * t + k] + tw[2] * dn[T * 6 + 3 * t + k];
+    }
+}
+
+__global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __restrict__ d,
+                                   const float* __restrict__ depth, const int64_t* __restrict__ x1,
+                                   const int64_t* __restrict__ x2, const int64_t* __restrict__ x3, int64_t T,
+                                   const float* __restrict__ dn, const float* __restrict__ tw,
+                                   float* __restrict__ ddepth) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= T) return;
+    const int64_t i1 = x1[t], i2 = x2[t], i3 = x3[t];
+    float g[3], g1, g2, g3;
+    tri_normal_grad(dn, tw, T, t, g);
+    tri_depth_grads(o, d, depth, i1, i2, i3, g, g1, g2, g3);
     atomicAdd(ddepth + i1, g1);
     atomicAdd(ddepth + i2, g2);
     atomicAdd(ddepth + i3, g3);
@@ -125,6 +138,63 @@ __global__ void photo_loss_bwd_kernel(const float* __restrict__ rgb, const float
     for (int c = 0; c < 3; c++) drgb[3 * i + c] = ga == 0.f ? 0.f : ga * sa * (rgb[3 * i + c] - gt[3 * i + c]);
     const float o = op[i] + 1e-10f;
     dop[i] = gb == 0.f ? 0.f : gb * w_op * (-(logf(o) + 1.f)) / (float)R;  // filtered term: no NaN leaks
+}
+
+// ---- fused backward of NeRFMTLoss for the reference configuration (losses.py:349-362 + 420-478,
+// `all_images_triang_patch` 8x8 patches, base.py:53-58 / losses.py:307-313): one thread per ray
+// writes dL/drgb and dL/dopacity of the photometric terms and GATHERS dL/ddepth from the (at most
+// three) patch triangles the ray is a vertex of, so no zero-fill and no atomics:
+//   local (i,j) is x1 of triangle (i,j) [i,j >= 1], x2 of (i+1,j) [i <= 6, j >= 1], x3 of (i,j+1)
+//   [i >= 1, j <= 6]; triangle (i,j) of patch p is index p*49 + 7(i-1) + (j-1).
+// Upstream gradients: up_total (the `total` output) + up_terms[5] (rgb, opacity, ort, centr_dot,
+// centr_L1 outputs), either may be NULL (= 0).
+__global__ void nerf_loss_bwd_kernel(const float* __restrict__ rgb, const float* __restrict__ gt,
+                                     const float* __restrict__ op, int64_t R, float w_op,
+                                     const float* __restrict__ photo, const float* __restrict__ o,
+                                     const float* __restrict__ d, const float* __restrict__ depth,
+                                     const float* __restrict__ dn, const float* __restrict__ up_total,
+                                     const float* __restrict__ up_terms, float* __restrict__ drgb,
+                                     float* __restrict__ dop, float* __restrict__ ddepth) {
+    const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (ray >= R) return;
+    const float ut = up_total ? *up_total : 0.f;
+    float u[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) u[q] = ut + (up_terms ? up_terms[q] : 0.f);
+    // photometric (photo_loss_bwd_kernel)
+    const float ga = u[0] * photo[2], gb = u[1] * photo[3];
+    const float sa = 2.f / (float)(3 * R);
+#pragma unroll
+    for (int c = 0; c < 3; c++) drgb[3 * ray + c] = ga == 0.f ? 0.f : ga * sa * (rgb[3 * ray + c] - gt[3 * ray + c]);
+    const float oo = op[ray] + 1e-10f;
+    dop[ray] = gb == 0.f ? 0.f : gb * w_op * (-(logf(oo) + 1.f)) / (float)R;
+    // normals -> depth, gathered over this ray's triangle roles
+    const int64_t T = (R / 64) * 49;
+    const float tw[3] = {u[2], u[3], u[4]};
+    const int64_t p = ray >> 6;
+    const int loc = (int)(ray & 63), i = loc >> 3, j = loc & 7;
+    const int64_t b = p * 64;
+    float acc = 0.f;
+    float g[3], g1, g2, g3;
+    if (i >= 1 && j >= 1) {  // x1 of (i, j)
+        const int64_t t = p * 49 + 7 * (i - 1) + (j - 1);
+        tri_normal_grad(dn, tw, T, t, g);
+        tri_depth_grads(o, d, depth, ray, b + 8 * (i - 1) + j, b + 8 * i + (j - 1), g, g1, g2, g3);
+        acc += g1;
+    }
+    if (i <= 6 && j >= 1) {  // x2 of (i+1, j)
+        const int64_t t = p * 49 + 7 * i + (j - 1);
+        tri_normal_grad(dn, tw, T, t, g);
+        tri_depth_grads(o, d, depth, b + 8 * (i + 1) + j, ray, b + 8 * (i + 1) + (j - 1), g, g1, g2, g3);
+        acc += g2;
+    }
+    if (i >= 1 && j <= 6) {  // x3 of (i, j+1)
+        const int64_t t = p * 49 + 7 * (i - 1) + j;
+        tri_normal_grad(dn, tw, T, t, g);
+        tri_depth_grads(o, d, depth, b + 8 * i + (j + 1), b + 8 * (i - 1) + (j + 1), ray, g, g1, g2, g3);
+        acc += g3;
+    }
+    ddepth[ray] = acc;
 }
 
 // ---- clustering ----
@@ -567,10 +637,17 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_sums_kernel(const float* _
 template <int K>
 __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
     const float* __restrict__ normals, int n_tri, int niter, float w_ort, float w_dot, float w_l1,
-    const float* __restrict__ w_dev, const float* __restrict__ wsb, float* __restrict__ out_losses,
+    const float* __restrict__ w_dev, const int64_t* __restrict__ step_dev, float sched_start, float sched_grow,
+    const float* __restrict__ photo, const float* __restrict__ wsb, float* __restrict__ out_losses,
     int32_t* __restrict__ out_labels, float* __restrict__ out_centroids, float* __restrict__ dn) {
     const KmWs ws = km_ws((float*)wsb, K);
     if (w_dev) { w_ort = w_dev[0]; w_dot = w_dev[1]; w_l1 = w_dev[2]; }
+    if (step_dev) {  // losses.py:217: max(0, min(w, (step - start) * (w / grow)))
+        const float ds = (float)(*step_dev) - sched_start;
+        w_ort = fmaxf(0.f, fminf(w_ort, ds * (w_ort / sched_grow)));
+        w_dot = fmaxf(0.f, fminf(w_dot, ds * (w_dot / sched_grow)));
+        w_l1 = fmaxf(0.f, fminf(w_l1, ds * (w_l1 / sched_grow)));
+    }
     __shared__ ClStats S;
     __shared__ float st3[15];
     __shared__ float G[3][3][3];  // G[term][cluster][xyz]
@@ -637,6 +714,16 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
         if (blockIdx.x == 0) {
             out_losses[0] = ort; out_losses[1] = cdot; out_losses[2] = cl1; out_losses[3] = (float)nv;
             out_losses[4] = w_ort * ort; out_losses[5] = w_dot * cdot; out_losses[6] = w_l1 * cl1;
+            out_losses[7] = w_ort; out_losses[8] = w_dot; out_losses[9] = w_l1;
+            if (photo) {  // `total` in the order of losses.py's sum over the loss dict
+                float tot = 0.f;
+                tot += photo[0];
+                tot += photo[1];
+                tot += out_losses[4];
+                tot += out_losses[5];
+                tot += out_losses[6];
+                out_losses[10] = tot;
+            }
         }
     }
     __syncthreads();
@@ -665,7 +752,8 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
 
 template <int K>
 static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort,
-                           float w_dot, float w_l1, const float* w_dev, float* out_losses, int32_t* out_labels, float* out_centroids,
+                           float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev, float sched_start,
+                           float sched_grow, const float* photo, float* out_losses, int32_t* out_labels, float* out_centroids,
                            float* dn, float* ws, hipStream_t s) {
     hipLaunchKernelGGL(cluster_prep_kernel, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, seed, K, ws);
     for (int it = 0; it <= niter; it++)
@@ -674,7 +762,8 @@ static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t 
     hipLaunchKernelGGL(cluster_select_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, niter, t_sim, ws);
     hipLaunchKernelGGL(cluster_sums_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, ws);
     hipLaunchKernelGGL(cluster_grad_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, w_ort,
-                       w_dot, w_l1, w_dev, ws, out_losses, out_labels, out_centroids, dn);
+                       w_dot, w_l1, w_dev, step_dev, sched_start, sched_grow, photo, ws, out_losses, out_labels,
+                       out_centroids, dn);
 }
 
 }  // namespace ncn
@@ -721,8 +810,23 @@ int ncn_normals_bwd(const float* rays_o, const float* rays_d, const float* depth
     return 0;
 }
 
+int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
+                      const float* photo_loss, const float* rays_o, const float* rays_d, const float* depth,
+                      const float* dL_dnormals, const float* up_total, const float* up_terms, float* dL_drgb,
+                      float* dL_dopacity, float* dL_ddepth, void* stream) {
+    NCN_REQUIRE(n_rays % 64 == 0, hipErrorInvalidValue, "ncn_nerf_loss_bwd: n_rays=%lld is not whole 8x8 patches",
+                (long long)n_rays);
+    if (n_rays <= 0) return 0;
+    hipLaunchKernelGGL(nerf_loss_bwd_kernel, dim3(cdiv(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rgb, rgb_gt,
+                       opacity, n_rays, w_opacity, photo_loss, rays_o, rays_d, depth, dL_dnormals, up_total, up_terms,
+                       dL_drgb, dL_dopacity, dL_ddepth);
+    NCN_LAUNCH_CHECK("ncn_nerf_loss_bwd");
+    return 0;
+}
+
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
-                     float w_ort, float w_dot, float w_l1, const float* w_dev, float* out_losses,
+                     float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,
+                     float sched_start, float sched_grow, const float* photo_loss, float* out_losses,
                      int32_t* out_labels, float* out_centroids, float* dL_dnormals, float* workspace,
                      void* stream) {
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
@@ -730,10 +834,12 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint
     NCN_REQUIRE(niter >= 0, hipErrorInvalidValue, "ncn_cluster_loss: niter < 0");
     hipStream_t s = (hipStream_t)stream;
     if (K == 20)
-        launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, out_losses, out_labels,
+        launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
+                           sched_grow, photo_loss, out_losses, out_labels,
                            out_centroids, dL_dnormals, workspace, s);
     else if (K == 10)
-        launch_cluster<10>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, out_losses, out_labels,
+        launch_cluster<10>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
+                           sched_grow, photo_loss, out_losses, out_labels,
                            out_centroids, dL_dnormals, workspace, s);
     else
         NCN_REQUIRE(false, hipErrorInvalidValue, "ncn_cluster_loss: K must be 10 or 20 (got %d)", K);

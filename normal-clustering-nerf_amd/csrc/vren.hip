@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void ray_aabb_kernel(const float* __restrict__
                                                        const float* __restrict__ centers,
                                                        const float* __restrict__ half_sizes, int64_t V, int max_hits,
                                                        int32_t* __restrict__ hit_cnt, float* __restrict__ hits_t,
-                                                       int64_t* __restrict__ hits_idx) {
+                                                       int64_t* __restrict__ hits_idx, float near_distance) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= R) return;
     float o[3] = {rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2]};
@@ -348,6 +348,8 @@ __global__ __launch_bounds__(256) void ray_aabb_kernel(const float* __restrict__
         }
     }
     hit_cnt[r] = cnt;
+    // render()'s near clamp of the first hit (rendering.py:28), fused: t1 in [0, near) -> near
+    if (h1[0] >= 0.0f && h1[0] < near_distance) h1[0] = near_distance;
     for (int k = 0; k < max_hits; k++) {
         hits_t[(r * max_hits + k) * 2] = h1[k];
         hits_t[(r * max_hits + k) * 2 + 1] = h2[k];
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(256) void composite_fw_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
-    float* __restrict__ rend, float* __restrict__ ws) {
+    float* __restrict__ rend, float* __restrict__ ws, float bg, float* __restrict__ rgb_bg) {
     const int lane = threadIdx.x & 63;
     const RaySeg g = load_ray_seg(rays_a, R);
     const int N = g.N;
@@ -457,6 +459,10 @@ __global__ __launch_bounds__(256) void composite_fw_kernel(
         depth[g.ray] = acc[1];
 #pragma unroll
         for (int i = 0; i < C; i++) rend[g.ray * C + i] = acc[2 + i];
+        if (rgb_bg) {  // render()'s background, rendering.py:232-240: rgb = rend + bg * (1 - opacity)
+#pragma unroll
+            for (int i = 0; i < C; i++) rgb_bg[g.ray * C + i] = acc[2 + i] + bg * (1 - acc[0]);
+        }
         total_samples[g.ray] = total;
     }
 }
@@ -473,7 +479,7 @@ __global__ __launch_bounds__(256) void composite_bw_kernel(
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
     const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
-    float* __restrict__ dL_draws) {
+    float* __restrict__ dL_draws, float bg) {
     constexpr int ROWS = 2;
     const int lane = threadIdx.x & 63;
     const RaySeg g = load_ray_seg(rays_a, R);
@@ -488,7 +494,14 @@ __global__ __launch_bounds__(256) void composite_bw_kernel(
         dR[i] = dL_drend ? dL_drend[ray * C + i] : 0.f;
         RE[i] = rend[ray * C + i];
     }
-    const float gO = dO * (1 - O);
+    // with the background folded in (rgb = rend + bg * (1 - O)): dL/drend = dL/drgb and the opacity
+    // picks up -bg * sum_i dL/drgb_i (the reference's autograd through rendering.py:236)
+    float dOe = dO;
+    if (bg != 0.f) {
+#pragma unroll
+        for (int i = 0; i < C; i++) dOe -= bg * dR[i];
+    }
+    const float gO = dOe * (1 - O);
     const uint32_t nb = (uint32_t)N * 4u;
     const auto r_s = buf_rsrc(sigmas + g.start, nb), r_d = buf_rsrc(deltas + g.start, nb);
     const auto r_t = buf_rsrc(ts + g.start, nb), r_r = buf_rsrc(raws + g.start * C, nb * C);
@@ -659,9 +672,9 @@ int ncn_packbits(const float* density_grid, int64_t n_bytes, float threshold, ui
     return 0;
 }
 
-int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays, const float* centers,
-                           const float* half_sizes, int64_t n_voxels, int max_hits, int32_t* hit_cnt, float* hits_t,
-                           int64_t* hits_voxel_idx, void* stream) {
+int ncn_ray_aabb_intersect_near(const float* rays_o, const float* rays_d, int64_t n_rays, const float* centers,
+                                const float* half_sizes, int64_t n_voxels, int max_hits, float near_distance,
+                                int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx, void* stream) {
     if (n_rays <= 0) return 0;
     NCN_REQUIRE(max_hits >= 1 && max_hits <= 16, hipErrorInvalidValue,
                 "ncn_ray_aabb_intersect: max_hits must be in [1,16] (got %d)", max_hits);
@@ -669,15 +682,23 @@ int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_r
     hipStream_t s = (hipStream_t)stream;
     if (max_hits == 1)
         hipLaunchKernelGGL(ray_aabb_kernel<1>, g, b, 0, s, rays_o, rays_d, n_rays, centers, half_sizes, n_voxels,
-                           max_hits, hit_cnt, hits_t, hits_voxel_idx);
+                           max_hits, hit_cnt, hits_t, hits_voxel_idx, near_distance);
     else if (max_hits <= 4)
         hipLaunchKernelGGL(ray_aabb_kernel<4>, g, b, 0, s, rays_o, rays_d, n_rays, centers, half_sizes, n_voxels,
-                           max_hits, hit_cnt, hits_t, hits_voxel_idx);
+                           max_hits, hit_cnt, hits_t, hits_voxel_idx, near_distance);
     else
         hipLaunchKernelGGL(ray_aabb_kernel<16>, g, b, 0, s, rays_o, rays_d, n_rays, centers, half_sizes, n_voxels,
-                           max_hits, hit_cnt, hits_t, hits_voxel_idx);
+                           max_hits, hit_cnt, hits_t, hits_voxel_idx, near_distance);
     NCN_LAUNCH_CHECK("ncn_ray_aabb_intersect");
     return 0;
+}
+
+int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays, const float* centers,
+                           const float* half_sizes, int64_t n_voxels, int max_hits, int32_t* hit_cnt, float* hits_t,
+                           int64_t* hits_voxel_idx, void* stream) {
+    // near 0: no hit's t1 is in [0, 0), i.e. the plain reference kernel
+    return ncn_ray_aabb_intersect_near(rays_o, rays_d, n_rays, centers, half_sizes, n_voxels, max_hits, 0.0f, hit_cnt,
+                                       hits_t, hits_voxel_idx, stream);
 }
 
 int ncn_march_train_walk(const float* rays_o, const float* rays_d, const float* hits_t, const float* noise,
@@ -746,15 +767,38 @@ int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
                  return (int)hipErrorInvalidValue;                                             \
     }
 
+int ncn_composite_train_fw_bg(const float* sigmas, const float* raws, const float* deltas, const float* ts,
+                              const int64_t* rays_a, int64_t n_rays, int64_t n_samples, int n_rend, float T_threshold,
+                              int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws, float bg,
+                              float* rgb_bg, void* stream) {
+    if (n_rays <= 0) return 0;
+    (void)n_samples;
+    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, sigmas, raws,
+                   deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rend, ws, bg, rgb_bg);
+    NCN_LAUNCH_CHECK("ncn_composite_train_fw");
+    return 0;
+}
+
 int ncn_composite_train_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
                            const int64_t* rays_a, int64_t n_rays, int64_t n_samples, int n_rend, float T_threshold,
                            int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws,
                            void* stream) {
+    return ncn_composite_train_fw_bg(sigmas, raws, deltas, ts, rays_a, n_rays, n_samples, n_rend, T_threshold,
+                                     total_samples, opacity, depth, rend, ws, 0.f, nullptr, stream);
+}
+
+int ncn_composite_train_bw_bg(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                              const float* dL_dws, const float* sigmas, const float* raws, const float* ws,
+                              const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
+                              int64_t n_samples, int n_rend, const float* opacity, const float* depth,
+                              const float* rend, float T_threshold, float bg, float* dL_dsigmas, float* dL_draws,
+                              void* stream) {
     if (n_rays <= 0) return 0;
     (void)n_samples;
-    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, sigmas, raws,
-                   deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rend, ws);
-    NCN_LAUNCH_CHECK("ncn_composite_train_fw");
+    NCN_DISPATCH_C(n_rend, composite_bw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
+                   dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
+                   T_threshold, dL_dsigmas, dL_draws, bg);
+    NCN_LAUNCH_CHECK("ncn_composite_train_bw");
     return 0;
 }
 
@@ -763,13 +807,9 @@ int ncn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, con
                            const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
                            int64_t n_samples, int n_rend, const float* opacity, const float* depth, const float* rend,
                            float T_threshold, float* dL_dsigmas, float* dL_draws, void* stream) {
-    if (n_rays <= 0) return 0;
-    (void)n_samples;
-    NCN_DISPATCH_C(n_rend, composite_bw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
-                   dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
-                   T_threshold, dL_dsigmas, dL_draws);
-    NCN_LAUNCH_CHECK("ncn_composite_train_bw");
-    return 0;
+    return ncn_composite_train_bw_bg(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a,
+                                     n_rays, n_samples, n_rend, opacity, depth, rend, T_threshold, 0.f, dL_dsigmas,
+                                     dL_draws, stream);
 }
 
 int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,

@@ -24,12 +24,15 @@ SIGNATURES = {
     "ncn_morton3D_invert": [P, I64, P, P],
     "ncn_packbits": [P, I64, F32, P, P],
     "ncn_ray_aabb_intersect": [P, P, I64, P, P, I64, I32, P, P, P, P],
+    "ncn_ray_aabb_intersect_near": [P, P, I64, P, P, I64, I32, F32, P, P, P, P],
     "ncn_march_train_walk": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, P, P, P, P, P],
     "ncn_march_train_scan": [P, I64, P, P, P],
     "ncn_march_train_pack": [P, P, I64, I32, P, P, P, P, P, P, P, P],
     "ncn_march_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
     "ncn_composite_train_fw": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, P],
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
+    "ncn_composite_train_fw_bg": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, F32, P, P],
+    "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, P],
     "ncn_field_fwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P],
@@ -42,7 +45,8 @@ SIGNATURES = {
     "ncn_photo_loss_fwd": [P, P, P, I64, F32, P, P],
     "ncn_photo_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P],
     "ncn_cluster_workspace_words": [I32],
-    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, P, P, P, P, P],
+    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, F32, F32, P, P, P, P, P, P, P],
+    "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
 }

@@ -87,6 +87,33 @@ class VolumeRenderer(torch.autograd.Function):
         return dL_dsigmas, dL_draws, None, None, None, None
 
 
+class VolumeRendererBg(torch.autograd.Function):
+    """VolumeRenderer followed by render()'s background blend (rendering.py:232-240) as one node:
+    -> (total_samples, opacity, depth, rgb = rend + bg * (1 - opacity), ws).  Same kernels with the
+    blend in the forward's epilogue and its opacity gradient in the backward (no torch glue)."""
+
+    @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg):
+        sigmas = sigmas.contiguous(); raws = raws.contiguous()
+        total_samples, opacity, depth, rend, ws, rgb = vren.composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a,
+                                                                                       T_threshold, bg=bg)
+        ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
+        ctx.T_threshold, ctx.bg = T_threshold, bg
+        ctx.set_materialize_grads(False)
+        return total_samples.sum(), opacity, depth, rgb, ws
+
+    @staticmethod
+    @custom_bwd(device_type="cuda")
+    def backward(ctx, dL_dtotal_samples, dL_dopacity, dL_ddepth, dL_drgb, dL_dws):
+        sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws = ctx.saved_tensors
+        c = lambda t: None if t is None else t.contiguous().float()
+        dL_dsigmas, dL_draws = vren.composite_train_multi_bw(c(dL_dopacity), c(dL_ddepth), c(dL_drgb), c(dL_dws),
+                                                             sigmas, raws, ws, deltas, ts, rays_a, opacity, depth,
+                                                             rend, ctx.T_threshold, bg=ctx.bg)
+        return dL_dsigmas, dL_draws, None, None, None, None, None
+
+
 class TruncExp(torch.autograd.Function):
     """custom_functions.py:162-173 (the field kernel fuses this; kept for API parity)."""
 

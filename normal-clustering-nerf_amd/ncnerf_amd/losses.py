@@ -23,6 +23,8 @@ from torch import nn
 from . import _lib
 from ._lib import F32, I32, I64, U32, call, check_input, ptr, stream
 
+N_OUT = 11  # ncn_cluster_loss out_losses
+
 
 class _Normals(torch.autograd.Function):
     """hypersim_src/utils.py:504-541: n = normalize(cross(P2-P1, P3-P1)), P = rays_o + rays_d*depth."""
@@ -65,14 +67,15 @@ class _ClusterLoss(torch.autograd.Function):
     def forward(ctx, normals, K, niter, seed, t_sim, w):
         T = normals.shape[0]
         dev = normals.device
-        out = torch.empty(7, dtype=torch.float32, device=dev)
+        out = torch.empty(N_OUT, dtype=torch.float32, device=dev)
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
         hw, w_dev = _split_weights(w)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
-             F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
+             F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(None), F32(0.0), F32(1.0), ptr(None), ptr(out), ptr(labels),
+             ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(dn)
         terms = out[4:7].clone()
         ctx.mark_non_differentiable(labels, cents, out)
@@ -118,14 +121,15 @@ class _NormalsClusterLoss(torch.autograd.Function):
         normals = torch.empty(T, 3, dtype=torch.float32, device=dev)
         call("ncn_normals_fwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals),
              stream())
-        out = torch.empty(7, dtype=torch.float32, device=dev)
+        out = torch.empty(N_OUT, dtype=torch.float32, device=dev)
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
         hw, w_dev = _split_weights(w)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
-             F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(out), ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
+             F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(None), F32(0.0), F32(1.0), ptr(None), ptr(out), ptr(labels),
+             ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(rays_o, rays_d, depth, x1, x2, x3, dn)
         terms = out[4:7].clone()
         ctx.mark_non_differentiable(normals, labels, cents, out)
@@ -189,6 +193,73 @@ def photo_losses(rgb, rgb_gt, opacity, w_opacity):
     return _PhotoLoss.apply(f(rgb), f(rgb_gt), f(opacity), float(w_opacity))
 
 
+class _NeRFLossFused(torch.autograd.Function):
+    """NeRFMTLoss of the reference configuration (losses.py:169-587 with rgb + opacity +
+    normal-clustering terms, `all_images_triang_patch` 8x8 patches) as ONE autograd node:
+    forward = photometric reduction + normals + the clustering pipeline, whose last kernel also
+    evaluates the weight schedule from the device step and the total; backward = ONE kernel
+    (ncn_nerf_loss_bwd) writing dL/drgb, dL/dopacity and dL/ddepth (gathered per ray).
+    Outputs: total, rgb, opacity, ort, centr_dot, centr_L1 (all differentiable, 0-d), then the
+    non-differentiable labels, centroids and raw statistics."""
+
+    @staticmethod
+    def forward(ctx, rgb, opacity, depth, rays_o, rays_d, rgb_gt, x1, x2, x3, w_op, K, niter, seed, t_sim, w,
+                step_dev, sched):
+        R = rgb.shape[0]
+        T = x1.shape[0]
+        dev = rgb.device
+        photo = torch.empty(4, dtype=torch.float32, device=dev)
+        call("ncn_photo_loss_fwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(w_op), ptr(photo), stream())
+        normals = torch.empty(T, 3, dtype=torch.float32, device=dev)
+        call("ncn_normals_fwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals),
+             stream())
+        out = torch.empty(N_OUT, dtype=torch.float32, device=dev)
+        labels = torch.empty(T, dtype=torch.int32, device=dev)
+        cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
+        dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]),
+             F32(w[1]), F32(w[2]), ptr(None), ptr(step_dev), F32(sched[0]), F32(sched[1]), ptr(photo), ptr(out),
+             ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
+        ctx.save_for_backward(rgb, opacity, depth, rays_o, rays_d, rgb_gt, photo, dn)
+        ctx.w_op = w_op
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(labels, cents, out)
+        return out[10], photo[0], photo[1], out[4], out[5], out[6], labels, cents, out
+
+    @staticmethod
+    def backward(ctx, g_total, g_rgb, g_op, g_ort, g_cdot, g_cl1, *_unused):
+        rgb, opacity, depth, rays_o, rays_d, rgb_gt, photo, dn = ctx.saved_tensors
+        dev = rgb.device
+        terms = (g_rgb, g_op, g_ort, g_cdot, g_cl1)
+        up_terms = None
+        if any(g is not None for g in terms):  # a single term back-propagated on its own (rare)
+            z = torch.zeros((), device=dev)
+            up_terms = torch.stack([z if g is None else g.float().reshape(()) for g in terms]).contiguous()
+        up_total = None if g_total is None else g_total.float().contiguous()
+        R = rgb.shape[0]
+        drgb, dop, ddepth = torch.empty_like(rgb), torch.empty_like(opacity), torch.empty_like(depth)
+        call("ncn_nerf_loss_bwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(ctx.w_op), ptr(photo),
+             ptr(rays_o), ptr(rays_d), ptr(depth), ptr(dn), ptr(up_total), ptr(up_terms), ptr(drgb), ptr(dop),
+             ptr(ddepth), stream())
+        return (drgb, dop, ddepth) + (None,) * 14
+
+
+_STD_PATCH = np.arange(64).reshape(8, 8)
+_STD_OFFSETS = (_STD_PATCH[1:, 1:].reshape(-1), _STD_PATCH[:-1, 1:].reshape(-1), _STD_PATCH[1:, :-1].reshape(-1))
+
+
+def _standard_patch_offsets(patch_area, off):
+    """True if the patch triangles are the reference's 8x8 ones (base.py:53-58), host arrays only."""
+    if int(patch_area) != 64:
+        return False
+    for k, ref in zip(("x1", "x2", "x3"), _STD_OFFSETS):
+        o = off[k]
+        if isinstance(o, torch.Tensor) or not np.array_equal(np.asarray(o).reshape(-1), ref):
+            return False
+    return True
+
+
 def _offsets_key(o):
     """Cache key of a host patch-offset array; None for tensors (indexed on the device, never read)."""
     if isinstance(o, torch.Tensor):
@@ -247,21 +318,52 @@ class NeRFMTLoss(nn.Module):
             return torch.tensor(0.0, device=dev)
         return torch.where(torch.isfinite(loss), loss, torch.zeros_like(loss))
 
+    def _fused(self, pred_w_gt, target_gt, pred_unsup, kwargs):
+        """The reference configuration in one autograd node (_NeRFLossFused)."""
+        f = lambda t: t.float().contiguous()
+        step = kwargs["global_step"]
+        base = (self.norm_D_C_ort_dot_w, self.norm_D_C_centr_dot_w, self.norm_D_C_centr_L1_w)
+        if isinstance(step, torch.Tensor):  # schedule evaluated on the device (graph-captured step)
+            step_dev, w = step.to(torch.int64).reshape(()), base
+            if not step_dev.is_contiguous():
+                step_dev = step_dev.contiguous()
+        else:
+            if self.can_sched_end != -1 and step > self.can_sched_end:
+                w = (0.0, 0.0, 0.0)
+            else:
+                w = tuple(self.w_sched(x, step) for x in base)
+            step_dev = None
+        x = pred_unsup["x123_idx"]
+        for t, n in ((pred_w_gt["rgb"], "rgb"), (pred_unsup["depth"], "depth")):
+            if not t.is_cuda:
+                raise RuntimeError(f"{n} must be a CUDA tensor")
+        total, l_rgb, l_op, ort, cdot, cl1, labels, cents, raw = _NeRFLossFused.apply(
+            f(pred_w_gt["rgb"]), f(pred_unsup["opacity"]), f(pred_unsup["depth"]), f(pred_unsup["rays_o"]),
+            f(pred_unsup["rays_d"]), f(target_gt["rgb"]), x["x1"], x["x2"], x["x3"], float(self.opacity_w), 20, 20,
+            self.kmeans_seed, 1.0 - self.norm_CAN_tres, w, step_dev, (float(self.can_sched_start), float(self._grow)))
+        self.last_cluster = (labels, cents, raw)
+        return {"rgb": l_rgb, "opacity": l_op, "norm_D_C_ort_dot": ort, "norm_D_C_centr_dot": cdot,
+                "norm_D_C_centr_L1": cl1, "total": total}
+
     def forward(self, pred_raw, target_raw, **kwargs):
         pred_w_gt, target_gt, pred_unsup = {}, {}, {}
         gt_l = target_raw["rgb"].shape[0]
         for k in ("rgb", "depth", "normals", "normals_depth"):
             if k in target_raw:
                 target_gt[k] = target_raw[k]
-        pred_w_gt["rgb"] = pred_raw["rgb"][:gt_l]
-        pred_w_gt["depth"] = pred_raw["depth"][:gt_l]
-        pred_w_gt["rays_o"] = pred_raw["rays_o"][:gt_l]
-        pred_w_gt["rays_d"] = pred_raw["rays_d"][:gt_l]
+        # slices that cover the whole tensor are skipped: an autograd slice node would cost a
+        # zero-fill + copy in the backward for nothing
+        head = lambda t: t if t.shape[0] == gt_l else t[:gt_l]
+        pred_w_gt["rgb"] = head(pred_raw["rgb"])
+        pred_w_gt["depth"] = head(pred_raw["depth"])
+        pred_w_gt["rays_o"] = head(pred_raw["rays_o"])
+        pred_w_gt["rays_d"] = head(pred_raw["rays_d"])
         unsup_start = gt_l if self.random_tr_poses else 0
+        tail = lambda t: t if unsup_start == 0 else t[unsup_start:]
         pred_unsup["opacity"] = pred_raw["opacity"]
-        pred_unsup["depth"] = pred_raw["depth"][unsup_start:]
-        pred_unsup["rays_o"] = pred_raw["rays_o"][unsup_start:]
-        pred_unsup["rays_d"] = pred_raw["rays_d"][unsup_start:]
+        pred_unsup["depth"] = tail(pred_raw["depth"])
+        pred_unsup["rays_o"] = tail(pred_raw["rays_o"])
+        pred_unsup["rays_d"] = tail(pred_raw["rays_d"])
         dev = pred_raw["rgb"].device
 
         def get_triang_idx(seq_len):
@@ -292,6 +394,12 @@ class NeRFMTLoss(nn.Module):
             pred_w_gt["x123_idx"] = get_patch_triang_idx(n_w_gt, target_raw["patch_area"], off)
             pred_unsup["x123_idx"] = get_patch_triang_idx(n_unsup, target_raw["patch_area"], off)
         clustering = self.norm_D_C_ort_dot_w > 0 or self.norm_D_C_centr_dot_w > 0 or self.norm_D_C_centr_L1_w > 0
+        if (clustering and self.pred_norm_depth and unsup_start == 0 and self.opacity_w > 0
+                and self.ray_sampling_strategy in ("all_images_triang_patch", "same_image_triang_patch")
+                and self.depth_w == 0 and self.norm_DEpth_L1_w == 0 and self.norm_DEpth_dot_w == 0
+                and self.reg_depth_w == 0 and n_w_gt == pred_unsup["opacity"].shape[0] and n_w_gt % 64 == 0
+                and n_w_gt > 0 and _standard_patch_offsets(target_raw["patch_area"], off)):
+            return self._fused(pred_w_gt, target_gt, pred_unsup, kwargs)
         fuse_normals = (clustering and self.pred_norm_depth and unsup_start == 0 and self.norm_DEpth_L1_w == 0
                         and self.norm_DEpth_dot_w == 0)
         if self.pred_norm_depth and not fuse_normals:

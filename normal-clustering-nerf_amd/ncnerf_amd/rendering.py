@@ -13,7 +13,7 @@ read of the counter), which is what lets Trainer capture the whole step in one H
 import torch
 from einops import rearrange
 
-from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer
+from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer, VolumeRendererBg
 from . import vren
 
 
@@ -23,9 +23,9 @@ def render(model, rays_o, rays_d, **kwargs):
     near_distance = kwargs["near_distance"]
     rays_o = rays_o.contiguous()
     rays_d = rays_d.contiguous()
-    _, hits_t, _ = RayAABBIntersector.apply(rays_o, rays_d, model.center, model.half_size, 1)
-    t0 = hits_t[:, 0, 0]  # in-place masked fill on the view: no nonzero() host sync
-    t0.masked_fill_((t0 >= 0) & (t0 < near_distance), near_distance)
+    # RayAABBIntersector (no gradient) + the near clamp of rendering.py:28 in one kernel
+    _, hits_t, _ = vren.ray_aabb_intersect(rays_o.float(), rays_d.float(), model.center, model.half_size, 1,
+                                           near_distance=near_distance)
     render_func = render_rays_test if kwargs.get("test_time", False) else render_rays_train
     results = render_func(model, rays_o, rays_d, hits_t, **kwargs)
     for k, v in results.items():
@@ -141,10 +141,13 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
         raws = torch.cat((raws, output["norms"]), dim=-1)
     if model.pred_sem:
         raws = torch.cat((raws, output["sems"]), dim=-1)
-    (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = VolumeRenderer.apply(
-        sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4))
+    fuse_bg = exp_step_factor == 0 and raws.shape[1] == 3  # white background, rgb only
+    renderer = VolumeRendererBg if fuse_bg else VolumeRenderer
+    extra = (1.0,) if fuse_bg else ()
+    (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = renderer.apply(
+        sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4), *extra)
     i = 3
-    results["rgb"] = rend[..., :i]
+    results["rgb"] = rend if rend.shape[-1] == i else rend[..., :i]  # no slice node for rgb-only
     if model.pred_norm:
         results["norm_nn"] = rend[..., i:i + 3]
         if kwargs.get("pred_norm_nn_norm", False):
@@ -156,8 +159,9 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     results["rays_o"] = rays_d  # rendering.py:227 (quirk q1)
     results["rays_a"] = rays_a
     results["depth_std"] = torch.ones_like(results["depth"], requires_grad=False)
-    if exp_step_factor == 0:  # white: rgb + 1 * (1 - opacity), the multiply by 1 is exact
-        results["rgb"] = results["rgb"] + (1 - results["opacity"])[:, None]
+    if exp_step_factor == 0:  # white: rgb + 1 * (1 - opacity), fused into the compositor when rgb-only
+        if not fuse_bg:
+            results["rgb"] = results["rgb"] + (1 - results["opacity"])[:, None]
         return results
     if kwargs.get("random_bg", False):
         rgb_bg = torch.rand(3, device=rays_o.device)

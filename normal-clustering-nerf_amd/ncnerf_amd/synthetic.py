@@ -179,8 +179,13 @@ class SyntheticScene:
                 "x1_offsets_local": self.x1_off, "x2_offsets_local": self.x2_off, "x3_offsets_local": self.x3_off}
 
     def torch_batch(self, n_rays, seed, device, gt="surface"):
+        """batch() with the per-ray arrays on `device`; the patch offsets stay host arrays (constant
+        metadata of the sampling strategy, as the reference's base.py:53-58 keeps them)."""
         b = self.batch(n_rays, seed, gt)
         out = {}
         for k, v in b.items():
-            out[k] = torch.from_numpy(np.ascontiguousarray(v)).to(device) if isinstance(v, np.ndarray) else v
+            if isinstance(v, np.ndarray) and not k.endswith("_offsets_local"):
+                out[k] = torch.from_numpy(np.ascontiguousarray(v)).to(device)
+            else:
+                out[k] = v
         return out

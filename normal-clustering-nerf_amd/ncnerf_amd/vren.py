@@ -24,8 +24,9 @@ I32 = _lib.I32
 F32 = _lib.F32
 
 
-def ray_aabb_intersect(rays_o, rays_d, centers, half_sizes, max_hits):
-    """intersection.cu:59-100 -> [hit_cnt i32 (R), hits_t f32 (R,M,2), hits_voxel_idx i64 (R,M)]"""
+def ray_aabb_intersect(rays_o, rays_d, centers, half_sizes, max_hits, near_distance=None):
+    """intersection.cu:59-100 -> [hit_cnt i32 (R), hits_t f32 (R,M,2), hits_voxel_idx i64 (R,M)]
+    Extension: near_distance applies render()'s clamp of the first hit (rendering.py:28) in-kernel."""
     for t, n in ((rays_o, "rays_o"), (rays_d, "rays_d"), (centers, "centers"), (half_sizes, "half_sizes")):
         check_input(t, n)
         check_dtype(t, torch.float32, n)
@@ -34,8 +35,12 @@ def ray_aabb_intersect(rays_o, rays_d, centers, half_sizes, max_hits):
     hit_cnt = torch.empty(R, dtype=torch.int32, device=dev)
     hits_t = torch.empty(R, max_hits, 2, dtype=torch.float32, device=dev)
     hits_idx = torch.empty(R, max_hits, dtype=torch.int64, device=dev)
-    call("ncn_ray_aabb_intersect", ptr(rays_o), ptr(rays_d), I64(R), ptr(centers), ptr(half_sizes), I64(V),
-         I32(max_hits), ptr(hit_cnt), ptr(hits_t), ptr(hits_idx), stream())
+    if near_distance is None:
+        call("ncn_ray_aabb_intersect", ptr(rays_o), ptr(rays_d), I64(R), ptr(centers), ptr(half_sizes), I64(V),
+             I32(max_hits), ptr(hit_cnt), ptr(hits_t), ptr(hits_idx), stream())
+    else:
+        call("ncn_ray_aabb_intersect_near", ptr(rays_o), ptr(rays_d), I64(R), ptr(centers), ptr(half_sizes), I64(V),
+             I32(max_hits), F32(float(near_distance)), ptr(hit_cnt), ptr(hits_t), ptr(hits_idx), stream())
     return [hit_cnt, hits_t, hits_idx]
 
 
@@ -123,8 +128,9 @@ def raymarching_test(rays_o, rays_d, hits_t, alive_indices, density_bitfield, ca
     return [xyzs, dirs, deltas, ts, n_eff]
 
 
-def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold):
-    """volumerendering.cu:140-176 -> [total_samples i64 (R), opacity (R), depth (R), rend (R,C), ws (S)]"""
+def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold, bg=None):
+    """volumerendering.cu:140-176 -> [total_samples i64 (R), opacity (R), depth (R), rend (R,C), ws (S)]
+    Extension: bg (float) also returns rgb_bg = rend + bg * (1 - opacity) as a sixth output."""
     for t, n in ((sigmas, "sigmas"), (raws, "raws"), (deltas, "deltas"), (ts, "ts"), (rays_a, "rays_a")):
         check_input(t, n)
     R, S, C = rays_a.shape[0], sigmas.shape[0], raws.shape[1]
@@ -134,15 +140,22 @@ def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold):
     depth = torch.empty(R, dtype=torch.float32, device=dev)
     rend = torch.empty(R, C, dtype=torch.float32, device=dev)
     ws = torch.empty(S, dtype=torch.float32, device=dev)
-    call("ncn_composite_train_fw", ptr(sigmas), ptr(raws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S), I32(C),
-         F32(float(T_threshold)), ptr(total), ptr(opacity), ptr(depth), ptr(rend), ptr(ws), stream())
-    return [total, opacity, depth, rend, ws]
+    if bg is None:
+        call("ncn_composite_train_fw", ptr(sigmas), ptr(raws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S),
+             I32(C), F32(float(T_threshold)), ptr(total), ptr(opacity), ptr(depth), ptr(rend), ptr(ws), stream())
+        return [total, opacity, depth, rend, ws]
+    rgb_bg = torch.empty(R, C, dtype=torch.float32, device=dev)
+    call("ncn_composite_train_fw_bg", ptr(sigmas), ptr(raws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S),
+         I32(C), F32(float(T_threshold)), ptr(total), ptr(opacity), ptr(depth), ptr(rend), ptr(ws), F32(float(bg)),
+         ptr(rgb_bg), stream())
+    return [total, opacity, depth, rend, ws, rgb_bg]
 
 
 def composite_train_multi_bw(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a,
-                             opacity, depth, rend, T_threshold):
+                             opacity, depth, rend, T_threshold, bg=None):
     """volumerendering.cu:367-418 -> [dL_dsigmas (S), dL_draws (S,C)].
-    Gradient arguments may also be None (treated as zeros: the kernel then skips those terms)."""
+    Gradient arguments may also be None (treated as zeros: the kernel then skips those terms).
+    Extension: with bg, dL_drend is the gradient of rgb_bg (composite_train_multi_fw(bg=...))."""
     for t, n in ((sigmas, "sigmas"), (raws, "raws"), (ws, "ws"), (deltas, "deltas"), (ts, "ts"),
                  (rays_a, "rays_a"), (opacity, "opacity"), (depth, "depth"), (rend, "rend")):
         check_input(t, n)
@@ -153,9 +166,14 @@ def composite_train_multi_bw(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, r
     R, S, C = rays_a.shape[0], sigmas.shape[0], raws.shape[1]
     dsig = torch.empty(S, dtype=torch.float32, device=sigmas.device)
     draws = torch.empty(S, C, dtype=torch.float32, device=sigmas.device)
-    call("ncn_composite_train_bw", ptr(dL_dopacity), ptr(dL_ddepth), ptr(dL_drend), ptr(dL_dws), ptr(sigmas),
-         ptr(raws), ptr(ws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S), I32(C), ptr(opacity), ptr(depth),
-         ptr(rend), F32(float(T_threshold)), ptr(dsig), ptr(draws), stream())
+    if bg is None:
+        call("ncn_composite_train_bw", ptr(dL_dopacity), ptr(dL_ddepth), ptr(dL_drend), ptr(dL_dws), ptr(sigmas),
+             ptr(raws), ptr(ws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S), I32(C), ptr(opacity), ptr(depth),
+             ptr(rend), F32(float(T_threshold)), ptr(dsig), ptr(draws), stream())
+    else:
+        call("ncn_composite_train_bw_bg", ptr(dL_dopacity), ptr(dL_ddepth), ptr(dL_drend), ptr(dL_dws), ptr(sigmas),
+             ptr(raws), ptr(ws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S), I32(C), ptr(opacity), ptr(depth),
+             ptr(rend), F32(float(T_threshold)), F32(float(bg)), ptr(dsig), ptr(draws), stream())
     return [dsig, draws]
 
 

@@ -2,9 +2,10 @@
 against the eager path on identical inputs.
 
 Tolerances: static vs dynamic render bit-exact (same kernels, the field stops at the device count);
-graph vs eager training: per-step loss within 1e-4 relative and final parameters within 1e-3
-relative L2 over 4 Adam steps (the table-gradient scatter and the loss reductions use float
-atomics, so the two runs are equal up to summation order)."""
+graph vs eager training: per-step loss within 1e-4 relative; final parameters within
+max(1e-3, 4 x the eager-vs-eager run-to-run difference) relative L2 over 4 Adam steps, MLP weights
+within 1e-3 (the table-gradient flush and the loss reductions use float atomics, so two runs are
+equal up to summation order)."""
 import numpy as np
 import pytest
 import torch
@@ -44,6 +45,9 @@ def test_static_shapes_render_matches_dynamic(dev):
 
 
 def test_graph_step_matches_eager(dev):
+    """Two eager runs give the run-to-run floor (float atomics in the table-gradient flush and the
+    dW reduction sum in arrival order; Adam's m/sqrt(v) turns a sign flip of a near-zero gradient
+    into a full lr step), the graph run must stay within a small multiple of it."""
     scene = SyntheticScene()
     batches = []
     for k in range(4):
@@ -51,7 +55,7 @@ def test_graph_step_matches_eager(dev):
         b["march_noise"] = torch.rand(4096, device=dev, generator=torch.Generator(device=dev).manual_seed(k))
         batches.append(b)
     losses, params = [], []
-    for use_graph in (False, True):
+    for use_graph in (False, False, True):
         m = _model(dev, scene)
         tr = Trainer(m, update_grid=False, use_graph=use_graph)
         ls = []
@@ -61,6 +65,11 @@ def test_graph_step_matches_eager(dev):
         torch.cuda.synchronize()
         losses.append(np.array(ls))
         params.append(m.flat_params().detach().clone())
-    np.testing.assert_allclose(losses[1], losses[0], rtol=1e-4)
-    rel = (params[1] - params[0]).norm() / params[0].norm()
-    assert float(rel) < 1e-3, float(rel)
+    np.testing.assert_allclose(losses[2], losses[0], rtol=1e-4)
+    floor = float((params[1] - params[0]).norm() / params[0].norm())
+    rel = float((params[2] - params[0]).norm() / params[0].norm())
+    assert rel < max(1e-3, 4 * floor), (rel, floor)
+    # the MLP weights (dense, large gradients) agree tightly
+    n_t = _model(dev, scene)._n_table
+    rel_w = float((params[2][n_t:] - params[0][n_t:]).norm() / params[0][n_t:].norm())
+    assert rel_w < 1e-3, rel_w

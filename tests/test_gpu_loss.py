@@ -138,3 +138,39 @@ def test_photo_losses(dev, R, bad):
         assert float(l_rgb) == 0.0 and float(a.grad.abs().sum()) == 0.0
     torch.testing.assert_close(l_op, e2.detach(), rtol=1e-5, atol=0)
     torch.testing.assert_close(b.grad, b2.grad, rtol=1e-5, atol=1e-12)
+
+
+def test_fused_nerf_loss_matches_unfused(dev):
+    """NeRFMTLoss in the reference configuration through the one-node path (_NeRFLossFused: photo +
+    normals + clustering forward, ONE backward kernel gathering dL/ddepth per ray) against the
+    multi-node path (taken when the patch offsets are device tensors).  Both with the device step
+    (graph path) and a host step.  Tolerance: losses rel 1e-6, gradients rel-L2 1e-5 (the
+    depth gradient is gathered per ray instead of accumulated with atomics)."""
+    from ncnerf_amd.synthetic import SyntheticScene
+    from ncnerf_amd.trainer import HYPERSIM_HPARAMS
+    R = 8192
+    d, depth, _ = _depth_batch(dev, R, 5)
+    rng = np.random.default_rng(6)
+    rgb = torch.from_numpy(rng.random((R, 3), dtype=np.float32)).to(dev)
+    op = torch.from_numpy(rng.random(R, dtype=np.float32)).to(dev)
+    gt = torch.from_numpy(rng.random((R, 3), dtype=np.float32)).to(dev)
+    sc = SyntheticScene()
+    host_off = dict(x1_offsets_local=sc.x1_off, x2_offsets_local=sc.x2_off, x3_offsets_local=sc.x3_off)
+    dev_off = {k: torch.from_numpy(v).to(dev) for k, v in host_off.items()}
+    for step in (1800, torch.tensor(1800, device=dev)):
+        out = []
+        for off in (dev_off, host_off):
+            loss = L.NeRFMTLoss(HYPERSIM_HPARAMS)
+            a, b, c = (t.clone().requires_grad_(True) for t in (rgb, op, depth))
+            pred = dict(rgb=a, opacity=b, depth=c, rays_o=d, rays_d=d)
+            ld = loss(pred, dict(rgb=gt, patch_area=64, **off), global_step=step)
+            ld["total"].backward()
+            out.append(({k: float(v) for k, v in ld.items()}, a.grad, b.grad, c.grad))
+        (l0, *g0), (l1, *g1) = out
+        assert set(l0) == set(l1)
+        for k in l0:
+            np.testing.assert_allclose(l1[k], l0[k], rtol=1e-6, atol=1e-9, err_msg=k)
+        assert l1["norm_D_C_ort_dot"] > 0
+        for x, y in zip(g0, g1):
+            rel = float((y - x).norm() / x.norm().clamp_min(1e-30))
+            assert rel < 1e-5, rel

@@ -219,3 +219,44 @@ def test_check_input_errors(dev):
     y = torch.zeros(3, 4, dtype=torch.int32, device=dev).t()
     with pytest.raises(RuntimeError, match="must be contiguous"):
         vren.morton3D(y)
+
+
+def test_ray_aabb_near_clamp_fused(dev):
+    """ncn_ray_aabb_intersect_near == intersect + render()'s masked clamp of hits_t[:,0,0] (bit-exact)."""
+    rng = np.random.default_rng(7)
+    o, d = _edge_rays(rng, 4096)
+    c, h = np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32)
+    T = lambda a: torch.from_numpy(a).to(dev)
+    for near in (0.01, 0.3):
+        a = vren.ray_aabb_intersect(T(o), T(d), T(c), T(h), 1, near_distance=near)
+        b = vren.ray_aabb_intersect(T(o), T(d), T(c), T(h), 1)
+        t0 = b[1][:, 0, 0]
+        t0.masked_fill_((t0 >= 0) & (t0 < near), near)
+        assert (t0 == near).any()
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
+def test_composite_background_fused(dev, scene):
+    """VolumeRendererBg (background blend inside the compositor) == VolumeRenderer + the torch
+    blend of rendering.py:232-240: forward bit-exact, gradients within fp32 rounding (the opacity
+    term -bg*sum(dL/drgb) is added inside the kernel instead of by autograd)."""
+    from ncnerf_amd.custom_functions import VolumeRenderer, VolumeRendererBg
+    rays_a, deltas, ts, sig, raws = _composite_inputs(scene, 2048, 11, 20.0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    rng = np.random.default_rng(3)
+    R = rays_a.shape[0]
+    g_rgb, g_op, g_d = (T(rng.normal(size=s).astype(np.float32)) for s in ((R, 3), (R,), (R,)))
+    res = []
+    for fused in (False, True):
+        s_, r_ = T(sig).requires_grad_(True), T(raws).requires_grad_(True)
+        if fused:
+            _, op, dp, rgb, _ = VolumeRendererBg.apply(s_, r_, T(deltas), T(ts), T(rays_a), 1e-4, 1.0)
+        else:
+            _, op, dp, rend, _ = VolumeRenderer.apply(s_, r_, T(deltas), T(ts), T(rays_a), 1e-4)
+            rgb = rend + (1 - op)[:, None]
+        ((rgb * g_rgb).sum() + (op * g_op).sum() + (dp * g_d).sum()).backward()
+        res.append((rgb.detach(), op.detach(), s_.grad, r_.grad))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][2:], res[1][2:]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
