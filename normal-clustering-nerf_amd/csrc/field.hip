@@ -298,13 +298,14 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Backward.  Per 16-sample group: recompute the MLP forward from the cached encoding, back-
-// propagate through the five layers (transposed products with the W^T fragments), scatter the
-// encoding gradient of this lane's four levels into the fp32 table gradient with no-return f32
-// atomics, and accumulate dW = sum_s dY_s X_s^T over the wave's groups in 40 register tiles.
-// The dW MFMAs need samples on K: each C-layout tile is transposed through a wave-private
-// 512-byte LDS slot (4 x ds_write_b16, 1 x ds_read_b64).  At the end the four waves reduce their
-// tiles into LDS and the workgroup writes one fp32 slab row (reduced in a fixed order later).
+// Backward, MLP pass.  Per 16-sample group (inputs prefetched one group ahead): recompute the MLP
+// forward from the cached encoding, back-propagate through the five layers (transposed products
+// with the W^T fragments, re-read from LDS every group), write the encoding gradient level-major
+// for the scatter pass, and accumulate dW = sum_s dY_s X_s^T over the wave's groups in 40
+// register tiles, each layer's right after its output gradient exists.  The dW MFMAs need the
+// samples on K: a C-layout tile is transposed by one MFMA with the identity (transpose_tile).
+// At the end the four waves reduce their tiles into LDS and the workgroup writes one fp32 slab
+// row (reduced in a fixed order later).
 constexpr int BWD_THREADS = 256;
 
 struct WGrad {
@@ -545,19 +546,19 @@ __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb, floa
 // Hash-grid gradients are extremely local: the rays of a patch re-touch the same few entries per
 // level hundreds of times, so a workgroup owns one span of consecutive samples
 // (~1/4 patch) and, level by level, aggregates every contribution in an LDS hash table before
-// anything reaches memory (4096 direct-mapped slots: 16 KB keys + 64 KB int64 sums):
+// anything reaches memory (6144 slots, 4-way set associative: 24 KB keys + 96 KB int64 sums):
 //  1. consecutive samples (lanes) in the same base cell are merged first with DPP run sums inside
 //     each 16-lane row (all 8 corners shared);
-//  2. run heads look up their 8 corners (one ds_read round trip, ds_cmpst_b32 to claim an empty
-//     slot) and add with ds_add_u64 into 64-bit FIXED-POINT sums: on gfx950 an LDS f32 atomic
+//  2. run heads look up their 8 corners (one ds_read_b128 of the set per corner, ds_cmpst_b32 to
+//     claim an empty way) and add with ds_add_u64 into 64-bit FIXED-POINT sums: on gfx950 an LDS f32 atomic
 //     costs ~3 cycles per active lane (193 cycles per wave-instruction, tools/lds_atomic_bench),
 //     an LDS u64 atomic add ~13 cycles per wave-instruction.  The fixed point is exact integer
 //     arithmetic (order-independent, reproducible): per (workgroup, level) the scale is 2^k with
 //     k = 46 - e, max|dE| < 2^e, so a value within 2^23 of the level's maximum converts exactly
 //     and the LDS sum (< 2^15 contributions) cannot overflow;
-//  3. at the end of a level (or when a quarter of the slots are taken) the table is flushed: two
+//  3. at the end of a level (or when half of the slots are taken) the table is flushed: two
 //     lanes per slot, each converts its sum back to f32 and issues one f32 global atomic.
-// A contribution whose slot holds another entry (collision) goes straight to a global atomic, as
+// A contribution whose set is full of other entries goes straight to a global atomic, as
 // does a whole level whose gradient is not finite (NaN/Inf propagate as in the f32 path).
 #ifdef NCN_DIAG_PHASES
 __device__ unsigned long long ncn_sc_phase[8];
@@ -568,14 +569,20 @@ __device__ unsigned long long ncn_sc_phase[8];
 #define SC_ACC(i, a, b)
 #endif
 constexpr int SC_THREADS = 1024;
-constexpr int SC_LOG2_TS = 12;
-constexpr int SC_TS = 1 << SC_LOG2_TS;
+#ifndef SC_SETS
+#define SC_SETS 1536
+#endif
+#ifndef SC_FLUSH_FRAC
+#define SC_FLUSH_FRAC 2
+#endif
+constexpr int SC_WAYS = 4;                  // 4-way set associative: one ds_read_b128 per lookup
+constexpr int SC_TS = SC_SETS * SC_WAYS;    // 6144 slots: 24 KB keys + 96 KB sums + 12 KB claim list
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
 #ifndef SC_MERGE_LEVELS
 #define SC_MERGE_LEVELS 16
 #endif
 
-__device__ __forceinline__ uint32_t sc_pair(uint32_t e) { return (e * 0x9E3779B1u) >> (33 - SC_LOG2_TS); }
+__device__ __forceinline__ uint32_t sc_set(uint32_t e) { return __umulhi(e * 0x9E3779B1u, (uint32_t)SC_SETS); }
 
 // round(v * 2^k) as int64 for |v * 2^k| < 2^46 without f64: split at 2^23 into two exact int32s
 __device__ __forceinline__ long long sc_fix(float v, int k) {
@@ -626,7 +633,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    float xyz_min, float xyz_extent,
                                                                    const float2* __restrict__ dE,
                                                                    float* __restrict__ grad) {
-    __shared__ uint32_t keys[SC_TS];
+    __shared__ __attribute__((aligned(16))) uint32_t keys[SC_TS];
     __shared__ long long valx[SC_TS], valy[SC_TS];
     __shared__ uint16_t used[SC_TS];  // slots claimed since the last flush, in claim order
     __shared__ int fill;              // == number of entries in `used`
@@ -704,7 +711,11 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     for (int it = 0; it < total; it++) {
         SC_T(t0);
         const int l = it / nchunk, ch = it - l * nchunk;
+#ifdef NCN_DIAG_SC_LEVELS_MASK
+        const float m = ((NCN_DIAG_SC_LEVELS_MASK >> l) & 1) ? lmax[l] : 0.f;
+#else
         const float m = lmax[l];
+#endif
         if (m == 0.f) {  // uniform: nothing at this level; keep the pipeline moving
             if (it + 1 < total) load(it + 1, nx, ny, nz, ng);
             continue;
@@ -783,17 +794,19 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         }
         SC_T(t1);
         if (head && !direct) {
-            // 2-way set-associative lookup: both keys of the aligned slot pair in one ds_read_b64
-            uint2 kk[8];
+            uint4 kk[8];
 #pragma unroll
-            for (int c = 0; c < 8; c++) kk[c] = *(const uint2*)&keys[2 * sc_pair(e[c])];
+            for (int c = 0; c < 8; c++) kk[c] = *(const uint4*)&keys[SC_WAYS * sc_set(e[c])];
             int claim[8];
 #pragma unroll
             for (int c = 0; c < 8; c++) {
-                const int p0 = 2 * sc_pair(e[c]);
-                slot[c] = kk[c].x == e[c] ? p0 : (kk[c].y == e[c] ? p0 + 1 : -1);
-                // claim the first slot of the pair seen empty
-                claim[c] = slot[c] >= 0 ? -1 : (kk[c].x == SC_EMPTY ? p0 : (kk[c].y == SC_EMPTY ? p0 + 1 : -1));
+                const int p0 = SC_WAYS * sc_set(e[c]);
+                const uint32_t k0 = kk[c].x, k1 = kk[c].y, k2 = kk[c].z, k3 = kk[c].w;
+                slot[c] = k0 == e[c] ? p0 : k1 == e[c] ? p0 + 1 : k2 == e[c] ? p0 + 2 : k3 == e[c] ? p0 + 3 : -1;
+                // claim the first way of the set seen empty
+                claim[c] = slot[c] >= 0 ? -1
+                         : k0 == SC_EMPTY ? p0 : k1 == SC_EMPTY ? p0 + 1 : k2 == SC_EMPTY ? p0 + 2
+                         : k3 == SC_EMPTY ? p0 + 3 : -1;
             }
             uint32_t got[8];
 #pragma unroll
@@ -837,7 +850,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         }
         __syncthreads();
         SC_T(t3);
-        if (ch == nchunk - 1 || fill > SC_TS / 4) sc_flush(keys, valx, valy, used, &fill, grad, off, k);
+        if (ch == nchunk - 1 || fill > SC_TS / SC_FLUSH_FRAC) sc_flush(keys, valx, valy, used, &fill, grad, off, k);
         SC_T(t4);
         SC_ACC(0, t0, t1);
         SC_ACC(1, t1, t2);
