@@ -148,9 +148,9 @@ int ncn_photo_loss_fwd(const float* rgb, const float* rgb_gt, const float* opaci
                        float* loss, void* stream);
 int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
                        const float* loss, const float* upstream, float* dL_drgb, float* dL_dopacity, void* stream);
-/* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations, one launch each over
- * 32 workgroups), cluster selection, the three cluster losses and their gradient w.r.t. the
- * normals, scaled by w_ort / w_dot / w_l1.  n_tri <= 16384.
+/* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations), cluster selection,
+ * the three cluster losses and their gradient w.r.t. the normals, scaled by w_ort / w_dot / w_l1,
+ * in ONE launch of 32 co-resident workgroups (grid barriers between the phases).  n_tri <= 16384.
  * out_losses (11 floats): [0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter;
  * [3] = valid n; [4..6] = the weighted terms; [7..9] = the weights used; [10] = total (only when
  * photo_loss is given: photo_loss[0] + photo_loss[1] + [4] + [5] + [6], losses.py's sum over the
@@ -161,7 +161,9 @@ int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opaci
  * step_dev: NULL, or the device training step: the weights become the schedule of losses.py:217,
  *   max(0, min(w, (step - sched_start) * (w / sched_grow))), evaluated on the device (graph-safe).
  * photo_loss: NULL, or the 4 floats of ncn_photo_loss_fwd (for out_losses[10]).
- * workspace: ncn_cluster_workspace_words(K) 32-bit words of device scratch. */
+ * workspace: ncn_cluster_workspace_words(K) 32-bit words of device scratch, ZERO-initialised once
+ *   before its first use and reused across calls (every call leaves its barrier words at zero);
+ *   one workspace per stream (two concurrent calls must not share one). */
 int64_t ncn_cluster_workspace_words(int K);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,

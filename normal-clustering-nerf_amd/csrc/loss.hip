@@ -211,8 +211,8 @@ __global__ void nerf_loss_bwd_kernel(const float* __restrict__ rgb, const float*
 //                    labels (-9 invalid) and the zero gradient of every unselected/invalid point
 // Every workgroup reduces the same partials in the same fixed order, so all of them hold
 // bit-identical centroids/statistics and the result is run-to-run deterministic.
-constexpr int CL_THREADS = 1024;     // prep kernel
 constexpr int CL_MAX_TRI = 16384;
+constexpr int NCN_MAX_NQ = 80;       // K * 4 at K = 20
 constexpr int KM_THREADS = 256;      // multi-workgroup kernels
 constexpr int KM_BLOCKS = 32;
 constexpr int KM_CHUNK_MAX = CL_MAX_TRI / KM_BLOCKS;
@@ -241,31 +241,74 @@ __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, fl
     return best;
 }
 
-// Workspace layout (32-bit words)
+// Workspace layout (32-bit words): cross-workgroup partial sums (double-buffered for the Lloyd
+// iterations) and the grid-barrier words.  The barrier words must be zero before the first call
+// and are left zero by every call (the last workgroup to leave resets them).
 struct KmWs {
-    int* map;        // [CL_MAX_TRI] compacted valid -> original index
-    int* nv;         // [4]
-    float* cent;     // [2][K][3]
-    float* part;     // [2][KM_BLOCKS][K][4]
-    int* asg;        // [CL_MAX_TRI] final assignment (compacted order)
-    int* lab;        // [CL_MAX_TRI] selected label +-1..3 / 0 (compacted order)
-    float* p2;       // [KM_BLOCKS][12] flipped member sums per selected cluster
-    float* p3;       // [KM_BLOCKS][16] x.c, |x-c|_1, sign(x-c) sums per selected cluster
+    long long* part;  // [2][KM_BLOCKS][K][4] fixed-point (x, y, z, count) per cluster
+    long long* p2;    // [KM_BLOCKS][12] flipped member sums + counts per selected cluster
+    long long* p3;    // [KM_BLOCKS][16] x.c, |x-c|_1, sign(x-c) sums per selected cluster
+    unsigned* sync;   // [0] barrier arrivals, [1] departures, [2] error flag (stuck barrier)
 };
 __host__ __device__ inline KmWs km_ws(float* base, int K) {
     KmWs w;
-    w.map = (int*)base;
-    w.nv = (int*)base + CL_MAX_TRI;
-    w.cent = base + CL_MAX_TRI + 4;
-    w.part = w.cent + 2 * K * 3;
-    w.asg = (int*)(w.part + 2 * KM_BLOCKS * K * 4);
-    w.lab = w.asg + CL_MAX_TRI;
-    w.p2 = (float*)(w.lab + CL_MAX_TRI);
+    w.part = (long long*)base;
+    w.p2 = w.part + 2 * KM_BLOCKS * K * 4;
     w.p3 = w.p2 + KM_BLOCKS * 12;
+    w.sync = (unsigned*)(w.p3 + KM_BLOCKS * 16);
     return w;
 }
-__host__ __device__ inline int64_t km_ws_words(int K) {
-    return CL_MAX_TRI + 4 + 2 * K * 3 + 2 * KM_BLOCKS * K * 4 + 2 * CL_MAX_TRI + KM_BLOCKS * 28;
+__host__ __device__ inline int64_t km_ws_words(int K) { return 2 * (2 * KM_BLOCKS * K * 4 + KM_BLOCKS * 28) + 4; }
+
+// Every sum of the pipeline is exact: values (all |v| <= 8) are added as 64-bit fixed point
+// v * 2^40 (LDS u64 atomics inside a workgroup, then int64 partials across workgroups), so the
+// result is independent of order and partition, and is rounded to f32 once.
+constexpr double KM_FX = 1099511627776.0;  // 2^40
+__device__ __forceinline__ unsigned long long km_fix(float v) {
+    return (unsigned long long)__double2ll_rn((double)v * KM_FX);
+}
+__device__ __forceinline__ float km_unfix(long long q) { return (float)((double)q * (1.0 / KM_FX)); }
+
+// Cross-workgroup data moves with agent-scope (sc1) loads and stores only (MI355X_MICROARCH.md,
+// inter-workgroup visibility, hand-off row 1): each storing wave waits for its stores, the
+// workgroup meets at a barrier, ONE lane adds to the arrival counter; the poller's workgroup meets
+// again before any sc1 load of the published bytes.
+__device__ __forceinline__ long long ld_c(const long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_c(long long* p, long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Grid barrier number `phase` (1, 2, ...) over the KM_BLOCKS co-resident workgroups.  The spin is
+// bounded: a barrier that does not complete within ~2^22 polls sets the error word and lets the
+// workgroup run on (wrong numbers, reported by ncn_cluster_loss's caller check), never a hang.
+__device__ __forceinline__ void km_grid_sync(unsigned* sync, unsigned phase) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = phase * (unsigned)KM_BLOCKS;
+        unsigned spins = 0;
+        while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins == (1u << 22)) {
+                __hip_atomic_store(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+// Every workgroup calls this once, last: the final departure resets the barrier words.
+__device__ __forceinline__ void km_grid_exit(unsigned* sync) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned d = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == KM_BLOCKS - 1) {  // everyone has passed every barrier: nobody polls any more
+            __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // This workgroup's contiguous chunk of the compacted points.
@@ -275,44 +318,26 @@ __device__ __forceinline__ void km_chunk(int nv, int& m0, int& len) {
     len = max(0, min(nv, m0 + chunk) - m0);
 }
 
-// Fixed-order segmented sum of NQ values over the chunk held in LDS: thread (q, seg) sums
-// val(q, j) over its range of j, then NQ threads add the segments in order.  No serial wave
-// reductions, deterministic.  Ends with a barrier; result in out[NQ] (LDS).
-template <int NQ, class V>
-__device__ __forceinline__ void chunk_sum(int len, float* segbuf /* [KM_THREADS] */, float* out, V val) {
-    constexpr int SEGS = KM_THREADS / NQ;
-    const int tid = threadIdx.x, q = tid % NQ, seg = tid / NQ;
-    if (seg < SEGS) {
-        const int lo = (seg * len) / SEGS, hi = ((seg + 1) * len) / SEGS;
-        float acc = 0.f;
-#pragma unroll 4
-        for (int j = lo; j < hi; j++) acc += val(q, j);
-        segbuf[seg * NQ + q] = acc;
-    }
-    __syncthreads();
-    if (tid < NQ) {
-        float a = 0.f;
+// Exact sum of KM_BLOCKS int64 partial rows published by other workgroups (all loads issued
+// before the first add: one round trip), as f32.
+__device__ __forceinline__ float sum_rows(const long long* __restrict__ p, int row, int off) {
+    long long v[KM_BLOCKS];
 #pragma unroll
-        for (int sg = 0; sg < SEGS; sg++) a += segbuf[sg * NQ + tid];
-        out[tid] = a;
-    }
-    __syncthreads();
+    for (int b = 0; b < KM_BLOCKS; b++) v[b] = ld_c(p + b * row + off);
+    long long a = 0;
+#pragma unroll
+    for (int b = 0; b < KM_BLOCKS; b++) a += v[b];
+    return km_unfix(a);
 }
-
-// Sum of KM_BLOCKS partial rows (stride `row`) of `nq` values, fixed order, into out (LDS).
-__device__ __forceinline__ void sum_partials(const float* __restrict__ p, int row, int nq, float* out) {
-    if (threadIdx.x < nq) {
-        float a = 0.f;
-#pragma unroll 8
-        for (int b = 0; b < KM_BLOCKS; b++) a += p[b * row + threadIdx.x];
-        out[threadIdx.x] = a;
-    }
+__device__ __forceinline__ void sum_partials(const long long* __restrict__ p, int row, int nq, float* out) {
+    if (threadIdx.x < nq) out[threadIdx.x] = sum_rows(p, row, threadIdx.x);
 }
 
 // Centroid update from the per-workgroup partials (called by ALL threads of a workgroup): K*4
 // threads sum one (cluster, component) each in fixed workgroup order, K threads form the means, a
 // rare empty cluster is split from the largest one (faiss: +-1/1024 on alternating coordinates)
-// by thread 0, and K threads L2-normalise (spherical k-means).
+// by thread 0, and K threads L2-normalise (spherical k-means).  C holds C_{i-1} on entry (kept
+// for an empty cluster) and C_i on return.
 template <int K>
 struct KmUpdLds {
     float sums[K * 4];
@@ -322,8 +347,7 @@ struct KmUpdLds {
 };
 
 template <int K>
-__device__ void km_update(const float* __restrict__ part, const float* __restrict__ Cprev, float (*C)[3],
-                          KmUpdLds<K>& L) {
+__device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmUpdLds<K>& L) {
     sum_partials(part, K * 4, K * 4, L.sums);
     if (threadIdx.x == 0) L.any_empty = 0;
     __syncthreads();
@@ -332,7 +356,7 @@ __device__ void km_update(const float* __restrict__ part, const float* __restric
         const float n = L.sums[4 * k + 3];
         L.cnt[k] = n;
 #pragma unroll
-        for (int q = 0; q < 3; q++) L.nc[k][q] = n > 0.f ? L.sums[4 * k + q] / n : Cprev[3 * k + q];
+        for (int q = 0; q < 3; q++) L.nc[k][q] = n > 0.f ? L.sums[4 * k + q] / n : C[k][q];
         if (n == 0.f) L.any_empty = 1;
     }
     __syncthreads();
@@ -362,105 +386,6 @@ __device__ void km_update(const float* __restrict__ part, const float* __restric
         for (int q = 0; q < 3; q++) C[k][q] = L.nc[k][q] / nr;
     }
     __syncthreads();
-}
-
-// prep: ordered compaction of the valid normals with one independent load round per thread
-// (thread t owns points t, t+1024, ...), ballot/popcount ranks and a 256-entry block scan.
-__global__ __launch_bounds__(CL_THREADS) void cluster_prep_kernel(const float* __restrict__ normals, int n_tri,
-                                                                  uint32_t seed, int K, float* __restrict__ wsb) {
-    constexpr int R_MAX = CL_MAX_TRI / CL_THREADS;  // 16
-    constexpr int NW = CL_THREADS / 64;             // 16
-    const KmWs ws = km_ws(wsb, K);
-    __shared__ int wcnt[R_MAX * NW];
-    __shared__ int woff[R_MAX * NW];
-    __shared__ int total;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int R = (n_tri + CL_THREADS - 1) / CL_THREADS;
-    uint32_t flags = 0;
-#pragma unroll
-    for (int r = 0; r < R_MAX; r++) {
-        const int i = r * CL_THREADS + tid;
-        if (r < R && i < n_tri && valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]))
-            flags |= 1u << r;
-    }
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int rank[R_MAX];
-#pragma unroll
-    for (int r = 0; r < R_MAX; r++) {
-        const uint64_t b = __ballot((flags >> r) & 1u);
-        rank[r] = __popcll(b & lt);
-        if (lane == 0) wcnt[r * NW + wid] = r < R ? __popcll(b) : 0;
-    }
-    __syncthreads();
-    if (wid == 0) {  // exclusive scan of the R_MAX*NW = 256 counts in (tile, wave) order: 4 per lane
-        int v[4], s = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e++) { v[e] = wcnt[4 * lane + e]; s += v[e]; }
-        const int incl = wave_incl_sum_i(s, lane);
-        int run = incl - s;
-#pragma unroll
-        for (int e = 0; e < 4; e++) { woff[4 * lane + e] = run; run += v[e]; }
-        if (lane == 63) total = incl;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < R_MAX; r++)
-        if ((flags >> r) & 1u) ws.map[woff[r * NW + wid] + rank[r]] = r * CL_THREADS + tid;
-    const int tot = total;
-    if (tid == 0) ws.nv[0] = tot;
-    __threadfence_block();
-    __syncthreads();
-    // init: one seeded pick per stratum (oracle/losses_ref.py:kmeans_init_indices)
-    if (tid < K && tot >= K) {
-        const int lo = (int)(((int64_t)tid * tot) / K), hi = (int)(((int64_t)(tid + 1) * tot) / K);
-        const int span = max(hi - lo, 1);
-        const uint32_t h = mix32(seed * 0x9E3779B1u + (uint32_t)tid * 0x85EBCA77u + 1u);
-        const int i = ws.map[lo + (int)(h % (uint32_t)span)];
-        for (int q = 0; q < 3; q++) ws.cent[3 * tid + q] = normals[3 * i + q];  // buffer 0 = "C_0"
-    }
-}
-
-// One Lloyd iteration (it < niter) or the final search (it == niter, keeps the assignment).
-template <int K>
-__global__ __launch_bounds__(KM_THREADS) void kmeans_iter_kernel(const float* __restrict__ normals, int it,
-                                                                 int final_pass, float* __restrict__ wsb) {
-    constexpr int NQ = K * 4;
-    const KmWs ws = km_ws(wsb, K);
-    __shared__ float C[K][3];
-    __shared__ float pv[4][KM_CHUNK_MAX];  // x, y, z, 1
-    __shared__ int pa[KM_CHUNK_MAX];
-    __shared__ float segbuf[KM_THREADS];
-    __shared__ float outp[NQ];
-    __shared__ KmUpdLds<K> upd;
-    const int nv = ws.nv[0];
-    if (nv < K) return;
-    const int tid = threadIdx.x;
-    int m0, len;
-    km_chunk(nv, m0, len);
-    // independent of the centroids: fetch this chunk's normals while the update runs
-    for (int j = tid; j < len; j += KM_THREADS) {
-        const int i = ws.map[m0 + j];
-        pv[0][j] = normals[3 * i];
-        pv[1][j] = normals[3 * i + 1];
-        pv[2][j] = normals[3 * i + 2];
-        pv[3][j] = 1.f;
-    }
-    // centroid buffer (i & 1) holds C_i; C_0 is the prep kernel's init (buffer 0)
-    if (it == 0) {
-        if (tid < K * 3) (&C[0][0])[tid] = ws.cent[tid];
-        __syncthreads();
-    } else {
-        km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, ws.cent + ((it - 1) & 1) * K * 3, C, upd);
-        if (blockIdx.x == 0 && tid < K * 3) ws.cent[(it & 1) * K * 3 + tid] = (&C[0][0])[tid];
-    }
-    for (int j = tid; j < len; j += KM_THREADS) {
-        const int a = nearest<K>(C, pv[0][j], pv[1][j], pv[2][j]);
-        pa[j] = a;
-        if (final_pass) ws.asg[m0 + j] = a;
-    }
-    __syncthreads();
-    chunk_sum<NQ>(len, segbuf, outp, [&](int q, int j) { return pa[j] == (q >> 2) ? pv[q & 3][j] : 0.f; });
-    if (tid < NQ) ws.part[(it & 1) * KM_BLOCKS * NQ + blockIdx.x * NQ + tid] = outp[tid];
 }
 
 // Cluster selection of losses.py:75-166 from the final centroids and sizes -> label_map[K]
@@ -495,40 +420,43 @@ __device__ void select_clusters(const float (*C)[3], const float* cnt, float t_s
         L.cargmin[j] = mi;
     }
     __syncthreads();
-    if (tid == 0) {
-        int c2 = 0;
-        for (int j = 1; j < K; j++)
-            if (L.cmin[j] < L.cmin[c2]) c2 = j;
-        const int c3 = L.cargmin[c2];
-        for (int k = 0; k < K; k++) label_map[k] = 0;
+    if (tid < 64) {  // one wave: c2 = first argmin of cmin (lanes < K), its c3, then per-cluster labels
+        const float mv = tid < K ? L.cmin[tid] : INFINITY;
+        float best = mv;
+        int bi = tid < K ? tid : K;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // (value, index) min, ties -> lowest index
+            const float ov = __shfl_xor(best, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov < best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+        }
+        const int c2 = bi, c3 = L.cargmin[c2];
         const int cs[3] = {c1, c2, c3};
-        for (int q = 0; q < 3; q++)
-            for (int k = 0; k < K; k++)
-                if (L.sim[cs[q]][k] > t_sim) label_map[k] = q + 1;
-        for (int q = 0; q < 3; q++) {  // opposites (losses.py:58-72, 139-163)
-            int co = 0;
-            for (int k = 1; k < K; k++)
-                if (L.sim[cs[q]][k] < L.sim[cs[q]][co]) co = k;
-            if (-1.0f * L.sim[cs[q]][co] > t_sim)
-                for (int k = 0; k < K; k++)
-                    if (L.sim[co][k] > t_sim) label_map[k] = -(q + 1);
+        // opposite of each main cluster: first argmin of sim[cs[q]][*]
+        int co[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            float b2 = tid < K ? L.sim[cs[q]][tid] : INFINITY;
+            int i2 = tid < K ? tid : K;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const float ov = __shfl_xor(b2, o, 64);
+                const int oi = __shfl_xor(i2, o, 64);
+                if (ov < b2 || (ov == b2 && oi < i2)) { b2 = ov; i2 = oi; }
+            }
+            co[q] = i2;
+        }
+        if (tid < K) {  // the sequential overwrite order of losses.py: main clusters, then opposites
+            const int k = tid;
+            int lab = 0;
+            for (int q = 0; q < 3; q++)
+                if (L.sim[cs[q]][k] > t_sim) lab = q + 1;
+            for (int q = 0; q < 3; q++)
+                if (-1.0f * L.sim[cs[q]][co[q]] > t_sim && L.sim[co[q]][k] > t_sim) lab = -(q + 1);
+            label_map[k] = lab;
         }
     }
     __syncthreads();
-}
-
-// Chunk of selected members in LDS: pk = cluster 0..2 (-1 unselected), pv = flip-signed normal.
-__device__ __forceinline__ void load_members(const KmWs& ws, const float* __restrict__ normals, int m0, int len,
-                                             float (*pv)[KM_CHUNK_MAX], int* pk) {
-    for (int j = threadIdx.x; j < len; j += KM_THREADS) {
-        const int lb = ws.lab[m0 + j];
-        const int i = ws.map[m0 + j];
-        const float sg = lb < 0 ? -1.f : 1.f;
-        pk[j] = (lb < 0 ? -lb : lb) - 1;
-        pv[0][j] = sg * normals[3 * i];
-        pv[1][j] = sg * normals[3 * i + 1];
-        pv[2][j] = sg * normals[3 * i + 2];
-    }
 }
 
 // Per selected cluster: count, mean m, |m| and c = m/|m| from the p2 partials; ok = no empty cluster
@@ -557,90 +485,231 @@ __device__ void cluster_stats(const KmWs& ws, ClStats& S) {
 }
 
 template <int K>
-__global__ __launch_bounds__(KM_THREADS) void cluster_select_kernel(const float* __restrict__ normals, int niter,
-                                                                    float t_sim, float* __restrict__ wsb) {
-    const KmWs ws = km_ws(wsb, K);
-    __shared__ float C[K][3];
-    __shared__ float cnt[K + 4];
-    __shared__ int label_map[K];
-    __shared__ SelLds<K> sel;
-    __shared__ float pv[3][KM_CHUNK_MAX];
-    __shared__ int pk[KM_CHUNK_MAX];
-    __shared__ float segbuf[KM_THREADS];
-    __shared__ float outp[12];
-    const int nv = ws.nv[0];
-    if (nv < K) return;
-    const int tid = threadIdx.x;
-    int m0, len;
-    km_chunk(nv, m0, len);
-    for (int j = tid; j < len; j += KM_THREADS) {
-        const int i = ws.map[m0 + j];
-        pk[j] = ws.asg[m0 + j];
-        pv[0][j] = normals[3 * i];
-        pv[1][j] = normals[3 * i + 1];
-        pv[2][j] = normals[3 * i + 2];
-    }
-    if (tid < K * 3) (&C[0][0])[tid] = ws.cent[(niter & 1) * K * 3 + tid];
-    if (tid < K) {  // final cluster sizes = count column of the final-search partials
-        const float* p = ws.part + (niter & 1) * KM_BLOCKS * K * 4;
-        float a = 0.f;
-        for (int b = 0; b < KM_BLOCKS; b++) a += p[b * K * 4 + 4 * tid + 3];
-        cnt[tid] = a;
-    }
-    __syncthreads();
-    select_clusters<K>(C, cnt, t_sim, sel, label_map);
-    for (int j = tid; j < len; j += KM_THREADS) {
-        const int lb = label_map[pk[j]];
-        ws.lab[m0 + j] = lb;
-        const float sg = lb < 0 ? -1.f : 1.f;
-        pk[j] = (lb < 0 ? -lb : lb) - 1;
-        pv[0][j] *= sg;
-        pv[1][j] *= sg;
-        pv[2][j] *= sg;
-    }
-    __syncthreads();
-    chunk_sum<12>(len, segbuf, outp, [&](int q, int j) {
-        const int c = q >> 2, comp = q & 3;
-        return pk[j] != c ? 0.f : (comp < 3 ? pv[comp][j] : 1.f);
-    });
-    if (tid < 12) ws.p2[blockIdx.x * 12 + tid] = outp[tid];
-}
+struct ClusterLds {
+    float pv[3][KM_CHUNK_MAX];  // this workgroup's chunk of the compacted normals (flip-signed after select)
+    int pidx[KM_CHUNK_MAX];     // their original index
+    int pk[KM_CHUNK_MAX];       // k-means assignment, then selected cluster 0..2 (-1 unselected)
+    int plab[KM_CHUNK_MAX];     // selected label +-1..3 / 0
+    unsigned long long acc[NCN_MAX_NQ];  // this workgroup's fixed-point sums of the phase
+    float C[K][3];
+    float cnt[K];
+    int label_map[K];
+    int wcnt[CL_MAX_TRI / KM_THREADS][KM_THREADS / 64];
+    int woff[CL_MAX_TRI / KM_THREADS][KM_THREADS / 64];
+    int pick[K];
+    int picki[K];
+    int total;
+    KmUpdLds<K> upd;
+    SelLds<K> sel;
+    ClStats S;
+    float st3[15];
+    float G[3][3][3];  // G[term][cluster][xyz]
+};
 
+// The whole clustering pipeline in ONE launch of KM_BLOCKS co-resident workgroups, the phases
+// separated by grid barriers instead of kernel boundaries (23 of them at niter = 20):
+//   compaction  (no barrier: every workgroup ranks all normals itself and keeps its chunk in LDS)
+//               validity filter + ordered compaction (losses.py:427-430) and the seeded init picks
+//   niter + 1 Lloyd rounds: C_i = update(partials_{i-1}, C_{i-1}) (i > 0), assign every point to
+//               argmax <x, C_i>, per-workgroup partial sums (x, y, z, count) per cluster; the last
+//               round (i = niter) is faiss's final search and keeps the assignment
+//   select      cluster selection (losses.py:75-166) -> label per point, flipped partial sums
+//   sums        per-cluster partials of x.c, |x-c|_1, sign(x-c)
+//   grad        the three cluster losses and their analytic gradient per point (losses.py:469-478),
+//               labels (-9 invalid), the weight schedule of losses.py:217 and the loss total
+// Every workgroup reduces the same partials in the same fixed order, so all of them hold
+// bit-identical centroids/statistics and the result is run-to-run deterministic.
+#ifdef NCN_DIAG_CL_TIMES
+__device__ unsigned long long ncn_cl_times[64];
+#define CL_STAMP(i) \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (i) < 64) ncn_cl_times[(i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define CL_STAMP(i)
+#endif
 template <int K>
-__global__ __launch_bounds__(KM_THREADS) void cluster_sums_kernel(const float* __restrict__ normals,
-                                                                  float* __restrict__ wsb) {
-    const KmWs ws = km_ws(wsb, K);
-    __shared__ ClStats S;
-    __shared__ float pv[3][KM_CHUNK_MAX];
-    __shared__ int pk[KM_CHUNK_MAX];
-    __shared__ float segbuf[KM_THREADS];
-    __shared__ float outp[15];
-    const int nv = ws.nv[0];
-    if (nv < K) return;
-    int m0, len;
-    km_chunk(nv, m0, len);
-    load_members(ws, normals, m0, len, pv, pk);
-    cluster_stats(ws, S);
-    if (!S.ok) return;
-    chunk_sum<15>(len, segbuf, outp, [&](int q, int j) {
-        const int c = q / 5, comp = q % 5;
-        if (pk[j] != c) return 0.f;
-        const float x0 = pv[0][j], x1 = pv[1][j], x2 = pv[2][j];
-        if (comp == 0) return x0 * S.cc[c][0] + x1 * S.cc[c][1] + x2 * S.cc[c][2];
-        if (comp == 1) return fabsf(x0 - S.cc[c][0]) + fabsf(x1 - S.cc[c][1]) + fabsf(x2 - S.cc[c][2]);
-        const float u = pv[comp - 2][j] - S.cc[c][comp - 2];
-        return u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
-    });
-    if (threadIdx.x < 15) ws.p3[blockIdx.x * 16 + threadIdx.x] = outp[threadIdx.x];
-}
-
-template <int K>
-__global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
-    const float* __restrict__ normals, int n_tri, int niter, float w_ort, float w_dot, float w_l1,
-    const float* __restrict__ w_dev, const int64_t* __restrict__ step_dev, float sched_start, float sched_grow,
-    const float* __restrict__ photo, const float* __restrict__ wsb, float* __restrict__ out_losses,
+__global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
+    const float* __restrict__ normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort, float w_dot,
+    float w_l1, const float* __restrict__ w_dev, const int64_t* __restrict__ step_dev, float sched_start,
+    float sched_grow, const float* __restrict__ photo, float* __restrict__ wsb, float* __restrict__ out_losses,
     int32_t* __restrict__ out_labels, float* __restrict__ out_centroids, float* __restrict__ dn) {
-    const KmWs ws = km_ws((float*)wsb, K);
+    constexpr int NW = KM_THREADS / 64;
+    __shared__ ClusterLds<K> L;
+    const KmWs ws = km_ws(wsb, K);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t T3 = (int64_t)n_tri * 3;
+    CL_STAMP(0);
+    // ---- compaction: ranks of the valid normals in index order, this workgroup's chunk to LDS ----
+    const int R = (n_tri + KM_THREADS - 1) / KM_THREADS;  // <= 64 rounds
+    uint64_t flags = 0;
+    for (int r0 = 0; r0 < R; r0 += 16) {  // 16 rounds of loads in flight before their ballots
+        float a[16][3];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const int i = (r0 + u) * KM_THREADS + tid;
+            const bool in = r0 + u < R && i < n_tri;
+#pragma unroll
+            for (int q = 0; q < 3; q++) a[u][q] = in ? normals[3 * i + q] : 0.f;  // zero = invalid
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            if (r0 + u >= R) break;  // uniform
+            const bool v = valid_normal(a[u][0], a[u][1], a[u][2]);
+            flags |= (uint64_t)v << (r0 + u);
+            const uint64_t b = __ballot(v);
+            if (lane == 0) L.wcnt[r0 + u][wid] = __popcll(b);
+        }
+    }
+    __syncthreads();
+    if (wid == 0) {  // exclusive scan of the R*NW counts in (round, wave) order: 4 per lane
+        int v[4], sacc = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int q = 4 * lane + e;
+            v[e] = q < R * NW ? (&L.wcnt[0][0])[q] : 0;
+            sacc += v[e];
+        }
+        const int incl = wave_incl_sum_i(sacc, lane);
+        int run = incl - sacc;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int q = 4 * lane + e;
+            if (q < R * NW) (&L.woff[0][0])[q] = run;
+            run += v[e];
+        }
+        if (lane == 63) L.total = incl;
+    }
+    __syncthreads();
+    const int nv = L.total;
+    const bool clustered = nv >= K;
+    int m0, len;
+    km_chunk(nv, m0, len);
+    if (tid < K && clustered) {  // init: one seeded pick per stratum (oracle/losses_ref.py:kmeans_init_indices)
+        const int lo = (int)(((int64_t)tid * nv) / K), hi = (int)(((int64_t)(tid + 1) * nv) / K);
+        const int span = max(hi - lo, 1);
+        const uint32_t h = mix32(seed * 0x9E3779B1u + (uint32_t)tid * 0x85EBCA77u + 1u);
+        L.pick[tid] = lo + (int)(h % (uint32_t)span);
+    }
+    __syncthreads();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int picks[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) picks[k] = clustered ? __builtin_amdgcn_readfirstlane(L.pick[k]) : -1;
+    CL_STAMP(56);
+    for (int r = 0; r < R; r++) {
+        // uniform skip of the rounds that hold neither a rank of this chunk, nor an init pick, nor
+        // invalid normals this workgroup labels
+        const int rlo = L.woff[r][0], rhi = r + 1 < R ? L.woff[r + 1][0] : nv;
+        int kbeg = K, kend = K;  // the (sorted) picks inside [rlo, rhi): k in [kbeg, kend)
+#pragma unroll
+        for (int k = K - 1; k >= 0; k--) {
+            if (picks[k] >= rlo) kbeg = k;
+            if (picks[k] >= rhi) kend = k;
+        }
+        if (!(rlo < m0 + len && rhi > m0) && r % KM_BLOCKS != (int)blockIdx.x && kbeg == kend) continue;
+        const bool v = (flags >> r) & 1u;
+        const int rank = L.woff[r][wid] + __popcll(__ballot(v) & lt);
+        if (v) {
+            const int i = r * KM_THREADS + tid;
+            if (rank >= m0 && rank < m0 + len) L.pidx[rank - m0] = i;
+            for (int k = kbeg; k < kend; k++)  // usually none or one
+                if (picks[k] == rank) L.picki[k] = i;
+        } else if (r * KM_THREADS + tid < n_tri && r % KM_BLOCKS == (int)blockIdx.x) {  // invalid: label -9, zero grad
+            const int i = r * KM_THREADS + tid;
+            out_labels[i] = -9;
+#pragma unroll
+            for (int q = 0; q < 3; q++) dn[3 * i + q] = dn[T3 + 3 * i + q] = dn[2 * T3 + 3 * i + q] = 0.f;
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < len; j += KM_THREADS) {  // this chunk's normals and the init centroids
+        const int i = L.pidx[j];
+#pragma unroll
+        for (int q = 0; q < 3; q++) L.pv[q][j] = normals[3 * i + q];
+    }
+    if (clustered && tid < 3 * K) L.C[tid / 3][tid % 3] = normals[3 * L.picki[tid / 3] + tid % 3];
+    __syncthreads();
+    CL_STAMP(1);
+    unsigned phase = 0;
+    if (clustered) {
+        // ---- Lloyd rounds ----
+        constexpr int NQ = K * 4;
+        for (int it = 0; it <= niter; it++) {
+            if (it > 0) km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd);
+            CL_STAMP(2 + 2 * it);
+            // assignment + per-cluster (x, y, z, count) sums of the chunk (fixed point, LDS u64 atomics)
+            if (tid < NQ) L.acc[tid] = 0ull;
+            __syncthreads();
+            for (int j = tid; j < len; j += KM_THREADS) {
+                const float x = L.pv[0][j], y = L.pv[1][j], z = L.pv[2][j];
+                const int a = nearest<K>(L.C, x, y, z);
+                L.pk[j] = a;
+                atomicAdd(&L.acc[4 * a], km_fix(x));
+                atomicAdd(&L.acc[4 * a + 1], km_fix(y));
+                atomicAdd(&L.acc[4 * a + 2], km_fix(z));
+                atomicAdd(&L.acc[4 * a + 3], (unsigned long long)KM_FX);
+            }
+            __syncthreads();
+            if (tid < NQ) st_c(ws.part + (it & 1) * KM_BLOCKS * NQ + blockIdx.x * NQ + tid, (long long)L.acc[tid]);
+            CL_STAMP(3 + 2 * it);
+            km_grid_sync(ws.sync, ++phase);
+        }
+        // ---- select: final cluster sizes = count column of the final-search partials ----
+        if (tid < K) L.cnt[tid] = sum_rows(ws.part + (niter & 1) * KM_BLOCKS * NQ, NQ, 4 * tid + 3);
+        __syncthreads();
+        CL_STAMP(57);
+        select_clusters<K>(L.C, L.cnt, t_sim, L.sel, L.label_map);
+        CL_STAMP(58);
+        for (int j = tid; j < len; j += KM_THREADS) {
+            const int lb = L.label_map[L.pk[j]];
+            L.plab[j] = lb;
+            const float sg = lb < 0 ? -1.f : 1.f;
+            L.pk[j] = (lb < 0 ? -lb : lb) - 1;
+            L.pv[0][j] *= sg;
+            L.pv[1][j] *= sg;
+            L.pv[2][j] *= sg;
+        }
+        if (tid < 12) L.acc[tid] = 0ull;
+        __syncthreads();
+        for (int j = tid; j < len; j += KM_THREADS) {
+            const int c = L.pk[j];
+            if (c < 0) continue;
+#pragma unroll
+            for (int q = 0; q < 3; q++) atomicAdd(&L.acc[4 * c + q], km_fix(L.pv[q][j]));
+            atomicAdd(&L.acc[4 * c + 3], (unsigned long long)KM_FX);
+        }
+        __syncthreads();
+        if (tid < 12) st_c(ws.p2 + blockIdx.x * 12 + tid, (long long)L.acc[tid]);
+        km_grid_sync(ws.sync, ++phase);
+        // ---- sums ----
+        CL_STAMP(59);
+        cluster_stats(ws, L.S);
+        CL_STAMP(61);
+        if (L.S.ok) {
+            if (tid < 15) L.acc[tid] = 0ull;
+            __syncthreads();
+            for (int j = tid; j < len; j += KM_THREADS) {
+                const int c = L.pk[j];
+                if (c < 0) continue;
+                const float x0 = L.pv[0][j], x1 = L.pv[1][j], x2 = L.pv[2][j];
+                const float* cc = L.S.cc[c];
+                atomicAdd(&L.acc[5 * c], km_fix(x0 * cc[0] + x1 * cc[1] + x2 * cc[2]));
+                atomicAdd(&L.acc[5 * c + 1], km_fix(fabsf(x0 - cc[0]) + fabsf(x1 - cc[1]) + fabsf(x2 - cc[2])));
+#pragma unroll
+                for (int q = 0; q < 3; q++) {
+                    const float u = L.pv[q][j] - cc[q];
+                    atomicAdd(&L.acc[5 * c + 2 + q], km_fix(u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f)));
+                }
+            }
+            __syncthreads();
+            if (tid < 15) st_c(ws.p3 + blockIdx.x * 16 + tid, (long long)L.acc[tid]);
+        }
+        km_grid_sync(ws.sync, ++phase);  // uniform: S.ok is the same in every workgroup
+        CL_STAMP(62);
+        if (L.S.ok) sum_partials(ws.p3, 16, 15, L.st3);
+        __syncthreads();
+        CL_STAMP(63);
+    }
+    // ---- grad ----
     if (w_dev) { w_ort = w_dev[0]; w_dot = w_dev[1]; w_l1 = w_dev[2]; }
     if (step_dev) {  // losses.py:217: max(0, min(w, (step - start) * (w / grow)))
         const float ds = (float)(*step_dev) - sched_start;
@@ -648,44 +717,19 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
         w_dot = fmaxf(0.f, fminf(w_dot, ds * (w_dot / sched_grow)));
         w_l1 = fmaxf(0.f, fminf(w_l1, ds * (w_l1 / sched_grow)));
     }
-    __shared__ ClStats S;
-    __shared__ float st3[15];
-    __shared__ float G[3][3][3];  // G[term][cluster][xyz]
-    __shared__ float pv[3][KM_CHUNK_MAX];
-    __shared__ int pk[KM_CHUNK_MAX];
-    const int tid = threadIdx.x;
-    const int nv = ws.nv[0];
-    const int64_t T3 = (int64_t)n_tri * 3;
-    // invalid normals (not in the compaction): label -9, zero gradient
-    for (int i = blockIdx.x * KM_THREADS + tid; i < n_tri; i += KM_BLOCKS * KM_THREADS) {
-        if (!valid_normal(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2])) {
-            out_labels[i] = -9;
-#pragma unroll
-            for (int q = 0; q < 3; q++) dn[3 * i + q] = dn[T3 + 3 * i + q] = dn[2 * T3 + 3 * i + q] = 0.f;
-        }
-    }
-    int m0, len;
-    km_chunk(nv, m0, len);
-    const bool clustered = nv >= K;
-    if (clustered) {
-        load_members(ws, normals, m0, len, pv, pk);
-        cluster_stats(ws, S);
-        if (S.ok) sum_partials(ws.p3, 16, 15, st3);
-        __syncthreads();
-    }
-    const bool ok = clustered && S.ok;
-    if (blockIdx.x == 0 && tid < K * 3) out_centroids[tid] = clustered ? ws.cent[(niter & 1) * K * 3 + tid] : 0.f;
+    const bool ok = clustered && L.S.ok;
+    if (blockIdx.x == 0 && tid < K * 3) out_centroids[tid] = clustered ? (&L.C[0][0])[tid] : 0.f;
     if (tid == 0) {
         float ort = 0.f, cdot = 0.f, cl1 = 0.f;
         if (ok) {
-            const float(*cc)[3] = S.cc;
+            const float(*cc)[3] = L.S.cc;
             const float d12 = cc[0][0] * cc[1][0] + cc[0][1] * cc[1][1] + cc[0][2] * cc[1][2];
             const float d13 = cc[0][0] * cc[2][0] + cc[0][1] * cc[2][1] + cc[0][2] * cc[2][2];
             const float d23 = cc[1][0] * cc[2][0] + cc[1][1] * cc[2][1] + cc[1][2] * cc[2][2];
             ort = (fabsf(d12) + fabsf(d13) + fabsf(d23)) / 3.0f;
             for (int c = 0; c < 3; c++) {
-                cdot += 1.0f - st3[5 * c] / S.cnt[c];
-                cl1 += st3[5 * c + 1] / S.cnt[c];
+                cdot += 1.0f - L.st3[5 * c] / L.S.cnt[c];
+                cl1 += L.st3[5 * c + 1] / L.S.cnt[c];
             }
             cdot /= 3.0f;
             cl1 /= 3.0f;
@@ -698,17 +742,17 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
                                      (s12 * cc[0][q] + s23 * cc[2][q]) / 3.0f,
                                      (s13 * cc[0][q] + s23 * cc[1][q]) / 3.0f};
                 for (int c = 0; c < 3; c++) {
-                    G[0][c][q] = w_ort * go[c];
-                    G[1][c][q] = (w_dot / 3.0f) * (-S.cm[c][q]);
-                    G[2][c][q] = (w_l1 / 3.0f) * (-st3[5 * c + 2 + q] / S.cnt[c]);
+                    L.G[0][c][q] = w_ort * go[c];
+                    L.G[1][c][q] = (w_dot / 3.0f) * (-L.S.cm[c][q]);
+                    L.G[2][c][q] = (w_l1 / 3.0f) * (-L.st3[5 * c + 2 + q] / L.S.cnt[c]);
                 }
             }
             // project through c = m/|m| : dL/dm = (G - c (c.G)) / |m|, then dm/dx = 1/N
             for (int tm = 0; tm < 3; tm++)
                 for (int c = 0; c < 3; c++) {
-                    const float cg = cc[c][0] * G[tm][c][0] + cc[c][1] * G[tm][c][1] + cc[c][2] * G[tm][c][2];
+                    const float cg = cc[c][0] * L.G[tm][c][0] + cc[c][1] * L.G[tm][c][1] + cc[c][2] * L.G[tm][c][2];
                     for (int q = 0; q < 3; q++)
-                        G[tm][c][q] = (G[tm][c][q] - cc[c][q] * cg) / (fmaxf(S.cmn[c], 1e-12f) * S.cnt[c]);
+                        L.G[tm][c][q] = (L.G[tm][c][q] - cc[c][q] * cg) / (fmaxf(L.S.cmn[c], 1e-12f) * L.S.cnt[c]);
                 }
         }
         if (blockIdx.x == 0) {
@@ -729,10 +773,10 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
     __syncthreads();
     // per-normal label and gradient (direct terms + through the centroid), times the flip sign
     for (int j = tid; j < len; j += KM_THREADS) {
-        const int i = ws.map[m0 + j];
-        const int lb = clustered ? ws.lab[m0 + j] : 0;
+        const int i = L.pidx[j];
+        const int lb = clustered ? L.plab[j] : 0;
         out_labels[i] = lb;
-        const int c = clustered ? pk[j] : -1;
+        const int c = clustered ? L.pk[j] : -1;
         if (!ok || c < 0) {
 #pragma unroll
             for (int q = 0; q < 3; q++) dn[3 * i + q] = dn[T3 + 3 * i + q] = dn[2 * T3 + 3 * i + q] = 0.f;
@@ -741,28 +785,24 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_grad_kernel(
         const float sg = lb < 0 ? -1.f : 1.f;
 #pragma unroll
         for (int q = 0; q < 3; q++) {
-            const float u = pv[q][j] - S.cc[c][q];
+            const float u = L.pv[q][j] - L.S.cc[c][q];
             const float su = u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
-            dn[3 * i + q] = sg * G[0][c][q];
-            dn[T3 + 3 * i + q] = sg * ((w_dot / 3.0f) * (-S.cc[c][q] / S.cnt[c]) + G[1][c][q]);
-            dn[2 * T3 + 3 * i + q] = sg * ((w_l1 / 3.0f) * (su / S.cnt[c]) + G[2][c][q]);
+            dn[3 * i + q] = sg * L.G[0][c][q];
+            dn[T3 + 3 * i + q] = sg * ((w_dot / 3.0f) * (-L.S.cc[c][q] / L.S.cnt[c]) + L.G[1][c][q]);
+            dn[2 * T3 + 3 * i + q] = sg * ((w_l1 / 3.0f) * (su / L.S.cnt[c]) + L.G[2][c][q]);
         }
     }
+    CL_STAMP(60);
+    if (clustered) km_grid_exit(ws.sync);
 }
 
 template <int K>
 static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort,
                            float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev, float sched_start,
-                           float sched_grow, const float* photo, float* out_losses, int32_t* out_labels, float* out_centroids,
-                           float* dn, float* ws, hipStream_t s) {
-    hipLaunchKernelGGL(cluster_prep_kernel, dim3(1), dim3(CL_THREADS), 0, s, normals, n_tri, seed, K, ws);
-    for (int it = 0; it <= niter; it++)
-        hipLaunchKernelGGL(kmeans_iter_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, it,
-                           (int)(it == niter), ws);
-    hipLaunchKernelGGL(cluster_select_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, niter, t_sim, ws);
-    hipLaunchKernelGGL(cluster_sums_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, ws);
-    hipLaunchKernelGGL(cluster_grad_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, w_ort,
-                       w_dot, w_l1, w_dev, step_dev, sched_start, sched_grow, photo, ws, out_losses, out_labels,
+                           float sched_grow, const float* photo, float* out_losses, int32_t* out_labels,
+                           float* out_centroids, float* dn, float* ws, hipStream_t s) {
+    hipLaunchKernelGGL(cluster_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, seed, t_sim,
+                       w_ort, w_dot, w_l1, w_dev, step_dev, sched_start, sched_grow, photo, ws, out_losses, out_labels,
                        out_centroids, dn);
 }
 
@@ -823,6 +863,12 @@ int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacit
     NCN_LAUNCH_CHECK("ncn_nerf_loss_bwd");
     return 0;
 }
+
+#ifdef NCN_DIAG_CL_TIMES
+int ncn_diag_cl_times(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_cl_times), sizeof(unsigned long long) * 64);
+}
+#endif
 
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,

@@ -24,6 +24,19 @@ from . import _lib
 from ._lib import F32, I32, I64, U32, call, check_input, ptr, stream
 
 N_OUT = 11  # ncn_cluster_loss out_losses
+_WS = {}
+
+
+def _cluster_workspace(dev, K):
+    """The clustering workspace of (device, K): zeroed once, reused by every call (ncn_cluster_loss
+    leaves its grid-barrier words at zero).  Created on the first (eager) call, so a captured step
+    reuses it.  Calls on one device are stream-ordered in this package (one training stream)."""
+    key = (str(dev), K)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
+        _WS[key] = ws
+    return ws
 
 
 class _Normals(torch.autograd.Function):
@@ -71,7 +84,7 @@ class _ClusterLoss(torch.autograd.Function):
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
-        ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
+        ws = _cluster_workspace(dev, K)
         hw, w_dev = _split_weights(w)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
              F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(None), F32(0.0), F32(1.0), ptr(None), ptr(out), ptr(labels),
@@ -125,7 +138,7 @@ class _NormalsClusterLoss(torch.autograd.Function):
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
-        ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
+        ws = _cluster_workspace(dev, K)
         hw, w_dev = _split_weights(w)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
              F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(None), F32(0.0), F32(1.0), ptr(None), ptr(out), ptr(labels),
@@ -217,7 +230,7 @@ class _NeRFLossFused(torch.autograd.Function):
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
-        ws = torch.empty(int(_lib.lib().ncn_cluster_workspace_words(I32(K))), dtype=torch.float32, device=dev)
+        ws = _cluster_workspace(dev, K)
         call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]),
              F32(w[1]), F32(w[2]), ptr(None), ptr(step_dev), F32(sched[0]), F32(sched[1]), ptr(photo), ptr(out),
              ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
