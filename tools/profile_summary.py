@@ -1,0 +1,46 @@
+"""Summarise tools/profile_round.sh output (gpurun_out/prof_round) into profiles/<round>/:
+kernel_stats.csv (rocprofv3 --stats of the bench), composite_fw_traffic.json (per-dispatch median
+of FETCH_SIZE x2 + WRITE_SIZE for the composite forward; the x2 is the gfx950 FETCH_SIZE correction
+of MI355X_MICROARCH.md's HBM section)."""
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "gpurun_out", "prof_round")
+
+
+def counter_values(counter, kernel_sub):
+    files = glob.glob(os.path.join(SRC, counter, "**", "*counter_collection.csv"), recursive=True)
+    vals = {}
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if kernel_sub in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                key = (f, row["Dispatch_Id"])
+                vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main(rnd):
+    dst = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    k = "composite_fw_kernel"
+    fetch, write = counter_values("FETCH_SIZE", k), counter_values("WRITE_SIZE", k)
+    fm, wm = statistics.median(fetch), statistics.median(write)
+    out = {"kernel": k, "traffic_bytes_per_launch": int(round((2 * fm + wm) * 1024)),
+           "FETCH_SIZE_kb_median": fm, "WRITE_SIZE_kb_median": wm, "dispatches": len(fetch),
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over `bench.py --steps 5` "
+                     "(graph replays + eager pass + roofline launches), per-dispatch median; gfx950 correction: "
+                     "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM), WRITE_SIZE as read; Infinity-Cache hits included"}
+    json.dump(out, open(os.path.join(dst, "composite_fw_traffic.json"), "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "round1")
