@@ -109,6 +109,52 @@ __device__ __forceinline__ float wave_incl_prod_dpp_fused(float v) {
     return v;
 }
 
+// K independent inclusive product scans at once (rows of the same ray): one asm with the K
+// registers' DPP steps interleaved, so for K >= 4 the VALU-write -> DPP-read wait states are filled
+// by the other rows' steps instead of s_nops (K == 2 keeps one s_nop 0 per step).
+#define NCN_DPPM(R, CTRL) "v_mul_f32_dpp %" #R ", %" #R ", %" #R " " CTRL "\n\t"
+#define NCN_S1 "row_shr:1 row_mask:0xf bank_mask:0xf"
+#define NCN_S2 "row_shr:2 row_mask:0xf bank_mask:0xf"
+#define NCN_S4 "row_shr:4 row_mask:0xf bank_mask:0xf"
+#define NCN_S8 "row_shr:8 row_mask:0xf bank_mask:0xf"
+#define NCN_S15 "row_bcast:15 row_mask:0xa bank_mask:0xf"
+#define NCN_S31 "row_bcast:31 row_mask:0xc bank_mask:0xf"
+#define NCN_STEP2(C) NCN_DPPM(0, C) NCN_DPPM(1, C) "s_nop 0\n\t"
+#define NCN_STEP4(C) NCN_DPPM(0, C) NCN_DPPM(1, C) NCN_DPPM(2, C) NCN_DPPM(3, C)
+#define NCN_STEP8(C) NCN_STEP4(C) NCN_DPPM(4, C) NCN_DPPM(5, C) NCN_DPPM(6, C) NCN_DPPM(7, C)
+template <int K>
+__device__ __forceinline__ void wave_incl_prod_multi(float (&v)[K]) {
+    if constexpr (K == 1) {
+        v[0] = wave_incl_prod_dpp_fused(v[0]);
+    } else if constexpr (K == 2) {
+        asm volatile("s_nop 1\n\t" NCN_STEP2(NCN_S1) NCN_STEP2(NCN_S2) NCN_STEP2(NCN_S4) NCN_STEP2(NCN_S8)
+                         NCN_STEP2(NCN_S15) NCN_STEP2(NCN_S31) "s_nop 1"
+                     : "+v"(v[0]), "+v"(v[1]));
+    } else if constexpr (K == 4) {
+        asm volatile("s_nop 1\n\t" NCN_STEP4(NCN_S1) NCN_STEP4(NCN_S2) NCN_STEP4(NCN_S4) NCN_STEP4(NCN_S8)
+                         NCN_STEP4(NCN_S15) NCN_STEP4(NCN_S31) "s_nop 1"
+                     : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+    } else {
+        static_assert(K == 8, "K in {1,2,4,8}");
+        asm volatile("s_nop 1\n\t" NCN_STEP8(NCN_S1) NCN_STEP8(NCN_S2) NCN_STEP8(NCN_S4) NCN_STEP8(NCN_S8)
+                         NCN_STEP8(NCN_S15) NCN_STEP8(NCN_S31) "s_nop 1"
+                     : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                       "+v"(v[7]));
+    }
+}
+
+// Four independent inclusive sum scans at once (v_add_f32_dpp, same no-bound_ctrl identity trick:
+// a lane without a DPP source keeps its value, i.e. + 0); the 4-way interleave fills the wait states.
+__device__ __forceinline__ void wave_incl_sum4(float& a, float& b, float& c, float& d) {
+#define NCN_DPPA(R, CTRL) "v_add_f32_dpp %" #R ", %" #R ", %" #R " " CTRL "\n\t"
+#define NCN_ASTEP4(C) NCN_DPPA(0, C) NCN_DPPA(1, C) NCN_DPPA(2, C) NCN_DPPA(3, C)
+    asm volatile("s_nop 1\n\t" NCN_ASTEP4(NCN_S1) NCN_ASTEP4(NCN_S2) NCN_ASTEP4(NCN_S4) NCN_ASTEP4(NCN_S8)
+                     NCN_ASTEP4(NCN_S15) NCN_ASTEP4(NCN_S31) "s_nop 1"
+                 : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+#undef NCN_ASTEP4
+#undef NCN_DPPA
+}
+
 // Wave totals of K values at once (CDNA4 permlane swaps): v_permlane32_swap pairs values so the
 // lower half-wave carries one and the upper half the other, v_permlane16_swap halves again, then
 // one 16-lane row total per register (row_ror 8/4/2/1).  ~3K+6 instructions instead of K full

@@ -161,6 +161,241 @@ __global__ __launch_bounds__(64) void march_train_walk_kernel(
     counts[r] = n;
 }
 
+// ---------------------------------------------------------------------------------------------
+// raymarching_train pass 1, wave-parallel form (exp_step_factor == 0, i.e. constant dt; the
+// reference's configs at scale 0.5).  Both branches of the reference walk advance t along the same
+// chain c_{k+1} = fl(c_k + dt): an occupied probe emits and does `t += dt`, an empty one does
+// `do t += dt; while (t < t_target)` (raymarching.cu:221-233).  So the walk visits a subsequence of
+// that chain: after an occupied position k comes k+1, after an empty one the first j > k with
+// c_j >= t_target(k).  One wave takes one ray, 64*P chain positions per iteration (lane l holds
+// positions l + 64 j): the chain values come in closed form (march_chain), every position is
+// probed at once (one bitfield gather per lane instead of one serial walk step), and a short
+// scalar loop over ballot masks resolves which positions the walk visits.  Emitted samples are
+// compacted (mbcnt) into the slab row.  Bit-identical to the serial walk: same fmaf positions,
+// same probe, same target expression, same chain values.
+
+// Chain values in closed form.  Inside one binade [2^e, 2^(e+1)) with ulp u, c + dt rounds to
+// c + u*round(dt/u) when dt/u is not a tie, i.e. a constant step in the bit pattern; with a tie
+// (dt/u = m + 1/2, possible in at most one binade) round-to-even makes every result even, so the
+// step is constant from the second step on.  The two first steps are real float adds (r1, r) and
+// the rest of the binade is bits(v) + r1 + (k-1) r, valid while the exponent field is unchanged
+// (then the exact sum is below 2^(e+1), so the in-binade rounding applies); the step that leaves
+// the binade is again a real float add.  Fills c[j] = c_{lane + 64 j} for the window starting at
+// cb (index 0) and returns c_{64P}.  A chain that stops advancing (dt < u/2: the reference would
+// spin forever) is frozen and the caller's window cap ends the ray.
+template <int P>
+__device__ __forceinline__ float march_chain(float cb, float dt, int lane, float (&c)[P]) {
+    constexpr int L = 64 * P;
+#pragma unroll
+    for (int j = 0; j < P; j++) c[j] = cb;
+    int j0 = 0;
+    float v = cb;
+    for (;;) {
+        const uint32_t bv = __float_as_uint(v);
+        const float v1 = v + dt;
+        const uint32_t b1 = __float_as_uint(v1);
+        uint32_t r1 = b1 - bv, r = 0;
+        int K;
+        float vn;
+        if ((bv >> 23) != (b1 >> 23) || bv == 0u) {
+            K = 0;
+            vn = v1;
+        } else {
+            const float v2 = v1 + dt;
+            const uint32_t b2 = __float_as_uint(v2);
+            if ((b2 >> 23) != (b1 >> 23)) {
+                K = 1;
+                vn = v2;
+            } else {
+                r = b2 - b1;
+                if (r == 0u) {  // frozen chain (reference: endless loop)
+#pragma unroll
+                    for (int j = 0; j < P; j++)
+                        if (lane + 64 * j > j0) c[j] = v;
+                    return v;
+                }
+                const uint32_t room = (bv | 0x7FFFFFu) - bv - r1;  // bits left in the binade after step 1
+                // steps in the binade: room / r + 1 (the division only when the binade ends in the window)
+                K = (uint64_t)room >= (uint64_t)(L - 1) * r ? L : (int)(room / r + 1u);
+                vn = __uint_as_float(bv + r1 + (uint32_t)(K - 1) * r) + dt;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < P; j++) {
+            const int i = lane + 64 * j;
+            if (i > j0 && i <= j0 + K) c[j] = __uint_as_float(bv + r1 + (uint32_t)(i - j0 - 1) * r);
+        }
+        if (j0 + K >= L) return __uint_as_float(bv + r1 + (uint32_t)(L - j0 - 1) * r);
+        const int J = j0 + K + 1;
+        if (J == L) return vn;
+#pragma unroll
+        for (int j = 0; j < P; j++)
+            if (lane + 64 * j == J) c[j] = vn;
+        j0 = J;
+        v = vn;
+    }
+}
+
+// c[] as seen from lane `idx` (idx in [0, 63])
+__device__ __forceinline__ float lane_f(float v, int idx) { return __int_as_float(__builtin_amdgcn_ds_bpermute(idx << 2, __float_as_int(v))); }
+__device__ __forceinline__ int lane_i(int v, int idx) { return __builtin_amdgcn_ds_bpermute(idx << 2, v); }
+
+// First lane j > lane whose chain value reaches T (64 if none): the position an empty probe's skip
+// lands on (do t += dt while t < T).  The chain steps are dt up to rounding (< ulp/2 each), so
+// lane + ceil((T - c)/dt) is within one of the answer; one check either side fixes it, and a wave
+// whose estimate still fails (only for steps far off dt) falls back to a binary search.
+__device__ __forceinline__ int march_skip_lane(float c, float T, float dt, int lane) {
+    const float q = ceilf((T - c) / dt);
+    int j = lane + (int)fminf(fmaxf(q, 1.0f), 65.0f);
+    if (j > 64) j = 64;
+    const float cm = lane_f(c, min(j - 1, 63));  // c at j - 1 (>= lane)
+    const float cj = lane_f(c, min(j, 63));
+    if (j - 1 > lane && cm >= T) j -= 1;
+    else if (j < 64 && cj < T) j += 1;
+    const float cm2 = lane_f(c, min(j - 1, 63));
+    const float cj2 = lane_f(c, min(j, 63));
+    const bool ok = (j - 1 == lane || cm2 < T) && (j == 64 || cj2 >= T);
+    if (__ballot(!ok)) {  // binary search: last position p >= lane with c_p < T, answer p + 1
+        int p = lane;
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) {
+            const int qn = p + st;
+            const float cq = lane_f(c, min(qn, 63));
+            if (qn <= 63 && cq < T) p = qn;
+        }
+        j = p + 1;
+    }
+    return j;
+}
+
+// Positions the walk visits in this sub-window, starting at lane s (uniform), given every lane's
+// successor nxt (> lane; 64 = beyond): binary lifting over nxt (jump tables of 1, 2, 4 .. 32 steps),
+// then every lane walks the largest jumps from s that do not pass it and checks where it lands.
+__device__ __forceinline__ uint64_t march_visited(int nxt, int s, int lane) {
+    int J[6];
+    J[0] = nxt;
+#pragma unroll
+    for (int i = 1; i < 6; i++) {
+        const int v = lane_i(J[i - 1], min(J[i - 1], 63));
+        J[i] = J[i - 1] >= 64 ? 64 : v;
+    }
+    int cur = s;
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        const int v = lane_i(J[i], min(cur, 63));
+        const int cand = cur >= 64 ? 64 : v;
+        if (cand <= lane) cur = cand;
+    }
+    return __ballot(cur == lane && lane >= s);
+}
+
+template <bool ONE_CASCADE, int P>
+__global__ __launch_bounds__(256) void march_train_wave_kernel(
+    const float* __restrict__ rays_o, const float* __restrict__ rays_d, const float* __restrict__ hits_t,
+    const float* __restrict__ noise, int64_t R, const uint8_t* __restrict__ bitfield, int cascades, float scale,
+    int G, int max_samples, int32_t* __restrict__ counts, float* __restrict__ slab_xyz,
+    float* __restrict__ slab_t, float* __restrict__ slab_dt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (r >= R) return;
+    const MarchConst m = make_march_const(cascades, scale, 0.0f, G, max_samples, scale);
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t1 = hits_t[2 * r];
+    const float t2 = hits_t[2 * r + 1];
+    const float dt = calc_dt(m, 0.0f);  // esf == 0: clamp(0, dt_min, dt_max) for every t >= 0
+    int n = 0;
+    if (t1 >= 0) {  // :195-198; a miss (t1 = -1) never enters the loop (:204)
+        t1 = fmaf(dt, noise[r], t1);
+        float* sx = slab_xyz + r * (int64_t)max_samples * 3;
+        float* st = slab_t + r * (int64_t)max_samples;
+        float* sd = slab_dt + r * (int64_t)max_samples;
+        float cb = t1;
+        bool pend = false, done = false;
+        float ptgt = 0.f;
+        int s = 0;  // next visited lane of the current sub-window (when !pend)
+        for (int it = 0; it < (1 << 16) && !done; it++) {
+            float c[P];
+            const float cnext = march_chain<P>(cb, dt, lane, c);
+            float X[P], Y[P], Z[P], tgt[P];
+            bool occ[P];
+#pragma unroll
+            for (int j = 0; j < P; j++) {
+                X[j] = fmaf(c[j], dx, ox);
+                Y[j] = fmaf(c[j], dy, oy);
+                Z[j] = fmaf(c[j], dz, oz);
+                int nx, ny, nz;
+                float mip_bound;
+                uint32_t cbi = 0xFFFFFFFFu, cbv = 0;
+                occ[j] = probe<ONE_CASCADE>(m, bitfield, X[j], Y[j], Z[j], dt, nx, ny, nz, mip_bound, cbi, cbv);
+                // skip_voxel's target (raymarching.cu:224-229) for an empty probe at this position
+                const float tx =
+                    fmaf(fmaf(0.5f, signf_(dx), (float)nx + 0.5f) * m.gsi * 2 - 1, mip_bound, -X[j]) * dxi;
+                const float ty =
+                    fmaf(fmaf(0.5f, signf_(dy), (float)ny + 0.5f) * m.gsi * 2 - 1, mip_bound, -Y[j]) * dyi;
+                const float tz =
+                    fmaf(fmaf(0.5f, signf_(dz), (float)nz + 0.5f) * m.gsi * 2 - 1, mip_bound, -Z[j]) * dzi;
+                tgt[j] = c[j] + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+            }
+#pragma unroll
+            for (int j = 0; j < P; j++) {
+                if (done) break;
+                const uint64_t lt_m = __ballot(c[j] < t2);  // loop condition t < t2 (:204)
+                const uint64_t occ_m = __ballot(occ[j]);
+                if (pend) {
+                    const uint64_t mm = __ballot(c[j] >= ptgt);
+                    if (!mm) continue;  // the skip runs past this sub-window
+                    s = __builtin_ctzll(mm);
+                    pend = false;
+                }
+                // successor of every position if the walk visits it (64 = beyond this sub-window)
+                // (march_skip_lane reads other lanes: evaluated by the whole wave, then selected)
+                const int skip = march_skip_lane(c[j], tgt[j], dt, lane);
+                const int nxt = !(c[j] < t2) ? 64 : (occ[j] ? lane + 1 : skip);  // 64: the walk ends here
+                const uint64_t vis = march_visited(nxt, s, lane);
+                const uint64_t term = vis & ~lt_m;
+                uint64_t emit = vis & occ_m & lt_m;
+                const int room = max_samples - n;
+                if (__popcll(emit) >= room) {  // the room-th sample ends the walk (:204 n < max_samples)
+                    uint64_t e2 = emit;
+                    for (int q = 1; q < room; q++) e2 &= e2 - 1;
+                    const int last = __builtin_ctzll(e2);
+                    emit &= (last == 63) ? ~0ull : ((2ull << last) - 1);
+                    done = true;
+                }
+                if (term) {
+                    emit &= (1ull << __builtin_ctzll(term)) - 1;
+                    done = true;
+                }
+                if (emit) {
+                    if ((emit >> lane) & 1) {
+                        const int k = n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(emit >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)emit, 0));
+                        sx[3 * k] = X[j];
+                        sx[3 * k + 1] = Y[j];
+                        sx[3 * k + 2] = Z[j];
+                        st[k] = c[j];
+                        sd[k] = dt;
+                    }
+                    n += __popcll(emit);
+                }
+                if (!done) {  // carry: after the last visited position
+                    const int lastv = 63 - __builtin_clzll(vis);
+                    if ((occ_m >> lastv) & 1) {
+                        s = 0;  // emitted at lane lastv (== 63): the next position is lane 0 of the next sub-window
+                    } else {
+                        pend = true;  // an empty position whose skip target lies past this sub-window
+                        ptgt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tgt[j]), lastv));
+                    }
+                }
+            }
+            cb = cnext;
+        }
+    }
+    if (lane == 0) counts[r] = n;
+}
+
 // raymarching_train pass 2: exclusive scan of the counts in ray order (one workgroup; replaces the
 // atomicAdd start offsets of raymarching.cu:237-241) -> rays_a, counter = {S, R}.
 __global__ __launch_bounds__(1024) void march_train_scan_kernel(const int32_t* __restrict__ counts, int64_t R,
@@ -367,7 +602,6 @@ __global__ __launch_bounds__(256) void ray_aabb_kernel(const float* __restrict__
 // transmittance carries to the next row.  Every per-sample array is addressed through a buffer
 // descriptor sized to the ray's segment (buf_rsrc): lanes past N read 0 (so a = 0, 1 - a = 1 and
 // w = 0 fall out without masks) and their stores are dropped.  Per-ray values are scalar loads.
-constexpr int CF_ROWS = 4;
 
 // The ray handled by this wave and its segment.  The wave index is clamped instead of returning
 // early so the kernarg, rays_a and array-pointer loads issue as one scalar batch; `live` guards
@@ -388,6 +622,114 @@ __device__ __forceinline__ RaySeg load_ray_seg(const int64_t* __restrict__ rays_
     return s;
 }
 
+// One block of a ray's rows (forward).  sigma/delta of every row of the block are loaded up front
+// (the transmittance needs only them), t/raw of rows 0-3 with them; the ROWS product scans run
+// interleaved in one asm (wave_incl_prod_multi) and only the carries chain through readlane; t/raw
+// of rows 4-7 (ROWS == 8) are fetched after rows 0-3 are accumulated (keeps the kernel at 8
+// waves/SIMD).  GUARD: rows past N are skipped (uniform branches).  Returns true when the ray
+// stopped in this block (quirk q6: the stopping sample is composited, not counted); the rest of the
+// segment then gets ws = 0 (volumerendering.cu:133 breaks, ws stays 0).
+template <int C, int ROWS, bool GUARD>
+__device__ __forceinline__ bool composite_fw_block(const __amdgpu_buffer_rsrc_t& r_s,
+                                                   const __amdgpu_buffer_rsrc_t& r_d,
+                                                   const __amdgpu_buffer_rsrc_t& r_t,
+                                                   const __amdgpu_buffer_rsrc_t& r_r,
+                                                   const __amdgpu_buffer_rsrc_t& r_w, int base, int N, float T_thr,
+                                                   int lane, float& Tc, float (&acc)[2 + C], int& total) {
+    constexpr int RT = ROWS < 4 ? ROWS : 4;
+    float sg[ROWS], dl[ROWS], tt[RT], rr[RT][C];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        const uint32_t k = (uint32_t)(base + r * 64 + lane);
+        if (!GUARD || r == 0 || base + r * 64 < N) {
+            sg[r] = buf_load(r_s, k * 4u);
+            dl[r] = buf_load(r_d, k * 4u);
+            if (r < RT) {
+                tt[r] = buf_load(r_t, k * 4u);
+#pragma unroll
+                for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+            }
+        } else {
+            sg[r] = dl[r] = 0.f;
+            if (r < RT) {
+                tt[r] = 0.f;
+#pragma unroll
+                for (int i = 0; i < C; i++) rr[r][i] = 0.f;
+            }
+        }
+    }
+    float a[ROWS], om[ROWS], p[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        a[r] = 1.0f - __expf(-sg[r] * dl[r]);
+        om[r] = p[r] = 1.0f - a[r];
+    }
+    wave_incl_prod_multi<ROWS>(p);
+    // transmittance in front of (Tb) and after (Ta) each sample; lanes past N carry the last Ta
+    float Tb[ROWS];
+    uint64_t stopm[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        Tb[r] = Tc * wave_shr1_dpp(p[r], 1.0f);
+        const float Ta = Tb[r] * om[r];
+        stopm[r] = __ballot(Ta <= T_thr);
+        Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
+    }
+    int srow = ROWS, slane = 64;  // first sample whose Ta <= T_thr (T is non-increasing)
+#pragma unroll
+    for (int r = ROWS - 1; r >= 0; r--)
+        if (stopm[r]) {
+            srow = r;
+            slane = __builtin_ctzll(stopm[r]);
+        }
+    float w[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        w[r] = (r < srow || (r == srow && lane <= slane)) ? a[r] * Tb[r] : 0.f;
+        if (!GUARD || r == 0 || base + r * 64 < N) buf_store(r_w, (uint32_t)(base + r * 64 + lane) * 4u, w[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < RT; r++) {
+        acc[0] += w[r];
+        acc[1] = fmaf(w[r], tt[r], acc[1]);
+#pragma unroll
+        for (int i = 0; i < C; i++) acc[2 + i] = fmaf(w[r], rr[r][i], acc[2 + i]);
+    }
+    if constexpr (ROWS > 4) {
+        if (base + 4 * 64 < N && srow >= 4) {
+            float t2[ROWS - 4], r2[ROWS - 4][C];
+#pragma unroll
+            for (int r = 4; r < ROWS; r++) {
+                const uint32_t k = (uint32_t)(base + r * 64 + lane);
+                if (base + r * 64 < N) {
+                    t2[r - 4] = buf_load(r_t, k * 4u);
+#pragma unroll
+                    for (int i = 0; i < C; i++) r2[r - 4][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+                } else {
+                    t2[r - 4] = 0.f;
+#pragma unroll
+                    for (int i = 0; i < C; i++) r2[r - 4][i] = 0.f;
+                }
+            }
+#pragma unroll
+            for (int r = 4; r < ROWS; r++) {
+                acc[0] += w[r];
+                acc[1] = fmaf(w[r], t2[r - 4], acc[1]);
+#pragma unroll
+                for (int i = 0; i < C; i++) acc[2 + i] = fmaf(w[r], r2[r - 4][i], acc[2 + i]);
+            }
+        }
+    }
+    if (srow < ROWS) {
+        total = base + srow * 64 + slane;
+        for (int k = base + ROWS * 64 + lane; k < N; k += 64) buf_store(r_w, (uint32_t)k * 4u, 0.f);
+        return true;
+    }
+    return false;
+}
+
+// Forward (volumerendering.cu:97-176): a ray with N <= 256 samples is one block of 1, 2 or 4 rows
+// (every row non-empty: no guards), a longer one runs in guarded blocks of 8 rows.
 template <int C>
 __global__ __launch_bounds__(256) void composite_fw_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
@@ -406,52 +748,15 @@ __global__ __launch_bounds__(256) void composite_fw_kernel(
 #pragma unroll
     for (int i = 0; i < 2 + C; i++) acc[i] = 0.f;
     int total = N;
-    // base == 0 runs once even for N == 0 (all loads read 0): the loads then need only the
-    // segment, so the compiler issues them right behind the scalar batch
-    for (int base = 0; base == 0 || base < N; base += 64 * CF_ROWS) {
-        float sg[CF_ROWS], dl[CF_ROWS], tt[CF_ROWS], rr[CF_ROWS][C];
-#pragma unroll
-        for (int r = 0; r < CF_ROWS; r++) {
-            const uint32_t k = (uint32_t)(base + r * 64 + lane);
-            if (r == 0 || base + r * 64 < N) {  // uniform
-                sg[r] = buf_load(r_s, k * 4u);
-                dl[r] = buf_load(r_d, k * 4u);
-                tt[r] = buf_load(r_t, k * 4u);
-#pragma unroll
-                for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
-            } else {
-                sg[r] = dl[r] = tt[r] = 0.f;
-#pragma unroll
-                for (int i = 0; i < C; i++) rr[r][i] = 0.f;
-            }
-        }
-        bool stopped = false;
-#pragma unroll
-        for (int r = 0; r < CF_ROWS; r++) {
-            const int kb = base + r * 64;
-            if (kb >= N) break;  // uniform
-            const float a = 1.0f - __expf(-sg[r] * dl[r]);
-            const float om = 1.0f - a;
-            const float Tb = Tc * wave_shr1_dpp(wave_incl_prod_dpp_fused(om), 1.0f);  // in front of the sample
-            const float Ta = Tb * om;                                                  // ... and after it
-            // lanes past N carry Ta of the last sample, so they can only match after a real one
-            const uint64_t stopm = __ballot(Ta <= T_thr);
-            const int stop_lane = stopm ? __builtin_ctzll(stopm) : 64;
-            const float w = lane <= stop_lane ? a * Tb : 0.f;
-            buf_store(r_w, (uint32_t)(kb + lane) * 4u, w);
-            acc[0] += w;
-            acc[1] = fmaf(w, tt[r], acc[1]);
-#pragma unroll
-            for (int i = 0; i < C; i++) acc[2 + i] = fmaf(w, rr[r][i], acc[2 + i]);
-            if (stopm) {  // rest of the segment: ws = 0 (volumerendering.cu:133 breaks, ws stays 0)
-                total = kb + stop_lane;
-                for (int k = kb + 64 + lane; k < N; k += 64) buf_store(r_w, (uint32_t)k * 4u, 0.f);
-                stopped = true;
-                break;
-            }
-            Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
-        }
-        if (stopped) break;
+    if (N <= 64) {  // N == 0 included: every load reads 0, every store is dropped
+        composite_fw_block<C, 1, false>(r_s, r_d, r_t, r_r, r_w, 0, N, T_thr, lane, Tc, acc, total);
+    } else if (N <= 128) {
+        composite_fw_block<C, 2, false>(r_s, r_d, r_t, r_r, r_w, 0, N, T_thr, lane, Tc, acc, total);
+    } else if (N <= 256) {
+        composite_fw_block<C, 4, false>(r_s, r_d, r_t, r_r, r_w, 0, N, T_thr, lane, Tc, acc, total);
+    } else {
+        for (int base = 0; base < N; base += 8 * 64)
+            if (composite_fw_block<C, 8, true>(r_s, r_d, r_t, r_r, r_w, base, N, T_thr, lane, Tc, acc, total)) break;
     }
     wave_sum_multi<2 + C>(acc);
     if (g.live && lane == 0) {
@@ -467,22 +772,113 @@ __global__ __launch_bounds__(256) void composite_fw_kernel(
     }
 }
 
-// volumerendering.cu:297-364.  T is the post-update transmittance (quirk q10); d/r are inclusive
-// prefix sums of w*t and w*raw; (sum - pre[s]) is the suffix of dL_dws*ws over the WHOLE marched
-// segment (:331-335).  Evaluation order of dL_dsigmas follows :349-359.  Same row structure as the
-// forward; the prefix sums are DPP scans carried across rows.  A NULL upstream gradient skips its
-// term (the reference's are zero tensors: dL_dws is always zero in training, quirk q5).
-template <int C>
-__global__ __launch_bounds__(256) void composite_bw_kernel(
+// Backward, one block of a ray's rows (volumerendering.cu:297-364).  T is the post-update
+// transmittance (quirk q10); d/r are inclusive prefix sums of w*t and w*raw; (sum - pre[s]) is the
+// suffix of dL_dws*ws over the WHOLE marched segment (:331-335).  Evaluation order of dL_dsigmas
+// follows :349-359.  All of the block's loads are issued up front; the product scans run
+// interleaved, the prefix sums of (w*t, w*raw_0..2) as one 4-way DPP scan per row; carries chain
+// through readlane.  DWS: a non-NULL dL_dws (the reference's is a zero tensor in training, q5).
+template <int C, int ROWS, bool GUARD, bool DWS>
+__device__ __forceinline__ bool composite_bw_block(
+    const __amdgpu_buffer_rsrc_t& r_s, const __amdgpu_buffer_rsrc_t& r_d, const __amdgpu_buffer_rsrc_t& r_t,
+    const __amdgpu_buffer_rsrc_t& r_r, const __amdgpu_buffer_rsrc_t& r_dw, const __amdgpu_buffer_rsrc_t& r_ws,
+    const __amdgpu_buffer_rsrc_t& r_gs, const __amdgpu_buffer_rsrc_t& r_gr, int base, int N, float T_thr,
+    int lane, float gO, float dD, float D, float tot, const float (&dR)[C], const float (&RE)[C], float& Tc,
+    float& cd, float& cpw, float (&cr)[C]) {
+    float sg[ROWS], dl[ROWS], tt[ROWS], rr[ROWS][C], dws[ROWS], pw[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        const uint32_t k = (uint32_t)(base + r * 64 + lane);
+        if (!GUARD || r == 0 || base + r * 64 < N) {
+            sg[r] = buf_load(r_s, k * 4u);
+            dl[r] = buf_load(r_d, k * 4u);
+            tt[r] = buf_load(r_t, k * 4u);
+#pragma unroll
+            for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+            dws[r] = DWS ? buf_load(r_dw, k * 4u) : 0.f;
+            pw[r] = DWS ? dws[r] * buf_load(r_ws, k * 4u) : 0.f;
+        } else {
+            sg[r] = dl[r] = tt[r] = dws[r] = pw[r] = 0.f;
+#pragma unroll
+            for (int i = 0; i < C; i++) rr[r][i] = 0.f;
+        }
+    }
+    float a[ROWS], om[ROWS], p[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        a[r] = 1.0f - __expf(-sg[r] * dl[r]);
+        om[r] = p[r] = 1.0f - a[r];
+    }
+    wave_incl_prod_multi<ROWS>(p);
+    float Tb[ROWS], Ta[ROWS];
+    uint64_t stopm[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        Tb[r] = Tc * wave_shr1_dpp(p[r], 1.0f);
+        Ta[r] = Tb[r] * om[r];
+        stopm[r] = __ballot(Ta[r] <= T_thr);
+        Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta[r]), 63));
+    }
+    int srow = ROWS, slane = 64;
+#pragma unroll
+    for (int r = ROWS - 1; r >= 0; r--)
+        if (stopm[r]) {
+            srow = r;
+            slane = __builtin_ctzll(stopm[r]);
+        }
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        const bool inc = r < srow || (r == srow && lane <= slane);
+        const float w = inc ? a[r] * Tb[r] : 0.f;
+        // inclusive prefixes (this row + carry) of w*t, w*raw_i, dL_dws*ws
+        float run_d = w * tt[r], run_r[C];
+#pragma unroll
+        for (int i = 0; i < C; i++) run_r[i] = w * rr[r][i];
+        if constexpr (C == 3) {
+            wave_incl_sum4(run_d, run_r[0], run_r[1], run_r[2]);
+        } else {
+            run_d = wave_incl_sum_dpp(run_d);
+#pragma unroll
+            for (int i = 0; i < C; i++) run_r[i] = wave_incl_sum_dpp(run_r[i]);
+        }
+        run_d += cd;
+#pragma unroll
+        for (int i = 0; i < C; i++) run_r[i] += cr[i];
+        const float run_pw = DWS ? cpw + wave_incl_sum_dpp(pw[r]) : 0.f;
+        float gs = gO + dD * (tt[r] * Ta[r] - (D - run_d)) + Ta[r] * dws[r] - (tot - run_pw);
+        const bool live_row = !GUARD || r == 0 || base + r * 64 < N;
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            gs += dR[i] * (rr[r][i] * Ta[r] - (RE[i] - run_r[i]));
+            if (live_row) buf_store(r_gr, (uint32_t)(base + r * 64 + lane) * (4u * C) + 4u * i, dR[i] * w);
+        }
+        if (live_row) buf_store(r_gs, (uint32_t)(base + r * 64 + lane) * 4u, inc ? gs * dl[r] : 0.f);
+        cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_d), 63));
+        if (DWS) cpw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_pw), 63));
+#pragma unroll
+        for (int i = 0; i < C; i++) cr[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_r[i]), 63));
+    }
+    if (srow < ROWS) {  // rest of the segment: zero gradients
+        for (int k = base + ROWS * 64 + lane; k < N; k += 64) {
+            buf_store(r_gs, (uint32_t)k * 4u, 0.f);
+#pragma unroll
+            for (int i = 0; i < C; i++) buf_store(r_gr, (uint32_t)k * (4u * C) + 4u * i, 0.f);
+        }
+        return true;
+    }
+    return false;
+}
+
+// Backward (volumerendering.cu:297-418): same block structure as the forward (1/2/4-row blocks for
+// N <= 256, guarded 4-row blocks beyond).  A NULL upstream gradient skips its term.
+template <int C, bool DWS>
+__device__ __forceinline__ void composite_bw_ray(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
-    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
-    const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
-    const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
-    float* __restrict__ dL_draws, float bg) {
-    constexpr int ROWS = 2;
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts, const RaySeg& g,
+    const float* __restrict__ opacity, const float* __restrict__ depth, const float* __restrict__ rend,
+    float T_thr, float* __restrict__ dL_dsigmas, float* __restrict__ dL_draws, float bg) {
     const int lane = threadIdx.x & 63;
-    const RaySeg g = load_ray_seg(rays_a, R);
     const int N = g.N;
     const int64_t ray = g.ray;
     const float dO = dL_dopacity ? dL_dopacity[ray] : 0.f;
@@ -506,79 +902,55 @@ __global__ __launch_bounds__(256) void composite_bw_kernel(
     const auto r_s = buf_rsrc(sigmas + g.start, nb), r_d = buf_rsrc(deltas + g.start, nb);
     const auto r_t = buf_rsrc(ts + g.start, nb), r_r = buf_rsrc(raws + g.start * C, nb * C);
     const auto r_gs = buf_rsrc(dL_dsigmas + g.start, nb), r_gr = buf_rsrc(dL_draws + g.start * C, nb * C);
-    const bool has_dws = dL_dws != nullptr;
-    const auto r_dw = buf_rsrc(has_dws ? dL_dws + g.start : dL_dsigmas, has_dws ? nb : 0u);
-    const auto r_ws = buf_rsrc(has_dws ? ws + g.start : dL_dsigmas, has_dws ? nb : 0u);
+    const auto r_dw = buf_rsrc(DWS ? dL_dws + g.start : dL_dsigmas, DWS ? nb : 0u);
+    const auto r_ws = buf_rsrc(DWS ? ws + g.start : dL_dsigmas, DWS ? nb : 0u);
     float tot = 0.f;  // sum of dL_dws * ws over the whole segment
-    if (has_dws) {
+    if (DWS) {
         for (int k = lane; k < N; k += 64) tot = fmaf(buf_load(r_dw, k * 4u), buf_load(r_ws, k * 4u), tot);
         tot = wave_sum_dpp(tot);
     }
     float Tc = 1.0f, cd = 0.f, cpw = 0.f, cr[C];
 #pragma unroll
     for (int i = 0; i < C; i++) cr[i] = 0.f;
-    for (int base = 0; base == 0 || base < N; base += 64 * ROWS) {
-        float sg[ROWS], dl[ROWS], tt[ROWS], rr[ROWS][C], dws[ROWS], pw[ROWS];
-#pragma unroll
-        for (int r = 0; r < ROWS; r++) {
-            const uint32_t k = (uint32_t)(base + r * 64 + lane);
-            if (r == 0 || base + r * 64 < N) {
-                sg[r] = buf_load(r_s, k * 4u);
-                dl[r] = buf_load(r_d, k * 4u);
-                tt[r] = buf_load(r_t, k * 4u);
-#pragma unroll
-                for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
-                dws[r] = has_dws ? buf_load(r_dw, k * 4u) : 0.f;
-                pw[r] = has_dws ? dws[r] * buf_load(r_ws, k * 4u) : 0.f;
-            } else {
-                sg[r] = dl[r] = tt[r] = dws[r] = pw[r] = 0.f;
-#pragma unroll
-                for (int i = 0; i < C; i++) rr[r][i] = 0.f;
-            }
-        }
-        bool stopped = false;
-#pragma unroll
-        for (int r = 0; r < ROWS; r++) {
-            const int kb = base + r * 64;
-            if (kb >= N) break;
-            const float a = 1.0f - __expf(-sg[r] * dl[r]);
-            const float om = 1.0f - a;
-            const float Tb = Tc * wave_shr1_dpp(wave_incl_prod_dpp_fused(om), 1.0f);
-            const float Ta = Tb * om;
-            const uint64_t stopm = __ballot(Ta <= T_thr);
-            const int stop_lane = stopm ? __builtin_ctzll(stopm) : 64;
-            const bool inc = lane <= stop_lane;
-            const float w = inc ? a * Tb : 0.f;
-            // inclusive prefixes (this row + carry) of w*t, w*raw_i, dL_dws*ws
-            const float run_d = cd + wave_incl_sum_dpp(w * tt[r]);
-            const float run_pw = cpw + wave_incl_sum_dpp(pw[r]);
-            float run_r[C];
-#pragma unroll
-            for (int i = 0; i < C; i++) run_r[i] = cr[i] + wave_incl_sum_dpp(w * rr[r][i]);
-            float gs = gO + dD * (tt[r] * Ta - (D - run_d)) + Ta * dws[r] - (tot - run_pw);
-#pragma unroll
-            for (int i = 0; i < C; i++) {
-                gs += dR[i] * (rr[r][i] * Ta - (RE[i] - run_r[i]));
-                buf_store(r_gr, (uint32_t)(kb + lane) * (4u * C) + 4u * i, dR[i] * w);
-            }
-            buf_store(r_gs, (uint32_t)(kb + lane) * 4u, inc ? gs * dl[r] : 0.f);
-            if (stopm) {
-                for (int k = kb + 64 + lane; k < N; k += 64) {
-                    buf_store(r_gs, (uint32_t)k * 4u, 0.f);
-#pragma unroll
-                    for (int i = 0; i < C; i++) buf_store(r_gr, (uint32_t)k * (4u * C) + 4u * i, 0.f);
-                }
-                stopped = true;
-                break;
-            }
-            Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
-            cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_d), 63));
-            cpw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_pw), 63));
-#pragma unroll
-            for (int i = 0; i < C; i++) cr[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_r[i]), 63));
-        }
-        if (stopped) break;
+#define NCN_BW_BLOCK(ROWS, GUARD, BASE)                                                                    \
+    composite_bw_block<C, ROWS, GUARD, DWS>(r_s, r_d, r_t, r_r, r_dw, r_ws, r_gs, r_gr, BASE, N, T_thr, lane, gO, \
+                                            dD, D, tot, dR, RE, Tc, cd, cpw, cr)
+    if (N <= 64) {
+        NCN_BW_BLOCK(1, false, 0);
+    } else if (N <= 128) {
+        NCN_BW_BLOCK(2, false, 0);
+    } else if (N <= 256) {
+        NCN_BW_BLOCK(4, false, 0);
+    } else {
+        for (int base = 0; base < N; base += 4 * 64)
+            if (NCN_BW_BLOCK(4, true, base)) break;
     }
+#undef NCN_BW_BLOCK
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void composite_bw_kernel_nodws(
+    const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
+    const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
+    const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
+    const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
+    float* __restrict__ dL_draws, float bg) {
+    const RaySeg g = load_ray_seg(rays_a, R);
+    composite_bw_ray<C, false>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, g, opacity,
+                               depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+}
+template <int C>
+__global__ __launch_bounds__(256) void composite_bw_kernel_dws(
+    const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
+    const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
+    const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
+    const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
+    float* __restrict__ dL_draws, float bg) {
+    const RaySeg g = load_ray_seg(rays_a, R);
+    composite_bw_ray<C, true>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, g, opacity,
+                              depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
 }
 
 // composite_test_multi_fw (volumerendering.cu:504-550): lane per alive ray, serial (test path).
@@ -708,6 +1080,19 @@ int ncn_march_train_walk(const float* rays_o, const float* rays_d, const float* 
     if (n_rays <= 0) return 0;
     NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && grid_size <= 1024 && max_samples >= 1, hipErrorInvalidValue,
                 "ncn_march_train_walk: bad cascades/grid_size/max_samples");
+    if (exp_step_factor == 0.0f) {  // constant dt: the wave-parallel walk
+        dim3 g(cdiv(n_rays, 4)), b(256);
+        if (cascades == 1)
+            hipLaunchKernelGGL((march_train_wave_kernel<true, 2>), g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t,
+                               noise, n_rays, bitfield, cascades, scale, grid_size, max_samples, counts, slab_xyz,
+                               slab_t, slab_dt);
+        else
+            hipLaunchKernelGGL((march_train_wave_kernel<false, 2>), g, b, 0, (hipStream_t)stream, rays_o, rays_d,
+                               hits_t, noise, n_rays, bitfield, cascades, scale, grid_size, max_samples, counts,
+                               slab_xyz, slab_t, slab_dt);
+        NCN_LAUNCH_CHECK("ncn_march_train_walk");
+        return 0;
+    }
     dim3 g(cdiv(n_rays, 64)), b(64);
     if (cascades == 1)
         hipLaunchKernelGGL(march_train_walk_kernel<true>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, noise,
@@ -795,9 +1180,15 @@ int ncn_composite_train_bw_bg(const float* dL_dopacity, const float* dL_ddepth, 
                               void* stream) {
     if (n_rays <= 0) return 0;
     (void)n_samples;
-    NCN_DISPATCH_C(n_rend, composite_bw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
+    if (dL_dws) {
+        NCN_DISPATCH_C(n_rend, composite_bw_kernel_dws, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
                    dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
                    T_threshold, dL_dsigmas, dL_draws, bg);
+    } else {
+        NCN_DISPATCH_C(n_rend, composite_bw_kernel_nodws, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
+                   dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
+                   T_threshold, dL_dsigmas, dL_draws, bg);
+    }
     NCN_LAUNCH_CHECK("ncn_composite_train_bw");
     return 0;
 }

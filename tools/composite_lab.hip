@@ -421,3 +421,38 @@ extern "C" int lab_composite_fw(int variant, const float* sigmas, const float* r
 #undef ARGS
     return (int)hipGetLastError();
 }
+
+// Speed-of-light reference (not a compositor): the same algorithmic bytes as the forward, streamed
+// flat with 16-B loads and no per-ray structure: read sigmas/deltas/ts/raws (24 B/sample) and
+// rays_a, write ws (4 B/sample) and the per-ray outputs.
+namespace lab {
+__global__ __launch_bounds__(256) void flat_stream(const float4* __restrict__ sg, const float4* __restrict__ dl,
+                                                   const float4* __restrict__ tt, const float4* __restrict__ rw,
+                                                   int64_t S4, const int64_t* __restrict__ rays_a, int64_t R,
+                                                   float* __restrict__ opacity, float* __restrict__ depth,
+                                                   float* __restrict__ rend, int64_t* __restrict__ total,
+                                                   float4* __restrict__ ws) {
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = n; i < S4; i += stride) {
+        const float4 a = sg[i], b = dl[i], c = tt[i], r0 = rw[3 * i], r1 = rw[3 * i + 1], r2 = rw[3 * i + 2];
+        ws[i] = make_float4(a.x * b.x + c.x + r0.x + r1.x + r2.x, a.y * b.y + c.y + r0.y + r1.y + r2.y,
+                            a.z * b.z + c.z + r0.z + r1.z + r2.z, a.w * b.w + c.w + r0.w + r1.w + r2.w);
+    }
+    for (int64_t r = n; r < R; r += stride) {
+        const int64_t q = rays_a[3 * r + 2];
+        opacity[r] = (float)q; depth[r] = 0.f;
+        rend[3 * r] = rend[3 * r + 1] = rend[3 * r + 2] = 0.f;
+        total[r] = q;
+    }
+}
+}  // namespace lab
+
+extern "C" int lab_flat_stream(int blocks, const float* sigmas, const float* raws, const float* deltas,
+                               const float* ts, const int64_t* rays_a, int64_t R, int64_t S, int64_t* total,
+                               float* opacity, float* depth, float* rend, float* ws, void* stream) {
+    hipLaunchKernelGGL(lab::flat_stream, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float4*)sigmas,
+                       (const float4*)deltas, (const float4*)ts, (const float4*)raws, S / 4, rays_a, R, opacity,
+                       depth, rend, total, (float4*)ws);
+    return (int)hipGetLastError();
+}

@@ -98,3 +98,32 @@ for v in variants:
         errs = [(a.double() - b_.double()).abs().max().item() for a, b_ in zip(ref, o_)]
         line += "  maxdiff " + " ".join(f"{e:.2g}" for e in errs)
     print(line, flush=True)
+
+lab.lab_flat_stream.restype = ctypes.c_int
+for blocks in (256, 512, 1024, 2048, 4096, max(1, S // 1024)):
+    o_ = outs()
+
+    def fs(o2, blocks=blocks):
+        return lab.lab_flat_stream(ctypes.c_int(blocks), ptr(sig), ptr(rgb), ptr(deltas), ptr(ts), ptr(rays_a),
+                                   I64(R), I64(S), *[ptr(t) for t in o2], stream())
+    us = timeit(fs, o_)
+    fb = 28.0 * (S // 4 * 4) + 52.0 * R
+    print(f"{'flat%d' % blocks:12s} {us:7.2f} us  {fb / us / 1e3:7.1f} GB/s (flat-stream floor)", flush=True)
+
+# attribution of the product kernel's time (tools/composite_lab2.hip)
+lab2 = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "lab2.so"))
+lab2.lab2_cfw.restype = ctypes.c_int
+names = {0: "prod", 1: "no-ws", 2: "one-round", 3: "fake-seg", 4: "rows8", 5: "rows2", 6: "no-ws+1round",
+         7: "no-ws+fake", 8: "nows+fake+1row", 9: "rows8 no-ws", 10: "blocks"}
+for v in range(11):
+    o_ = outs()
+
+    def f2(o2, v=v):
+        return lab2.lab2_cfw(ctypes.c_int(v), ptr(sig), ptr(rgb), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S),
+                             F32(1e-4), *[ptr(t) for t in o2], stream())
+    us = timeit(f2, o_)
+    line = f"{'L2-' + names[v]:18s} {us:7.2f} us  {byts / us / 1e3:7.1f} GB/s"
+    if v in (0, 4, 5, 10):
+        errs = [(a.double() - b_.double()).abs().max().item() for a, b_ in zip(ref, o_)]
+        line += "  maxdiff " + " ".join(f"{e:.2g}" for e in errs)
+    print(line, flush=True)
