@@ -203,6 +203,14 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
+// Workgroup barrier that orders LDS only: waits for the wave's own LDS operations (lgkmcnt) but
+// not for its outstanding global loads/stores/atomics (vmcnt), which __syncthreads() also drains.
+// For phases that exchange data through LDS while fire-and-forget global stores / atomics or
+// prefetch loads are in flight.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Raw buffer resources (T8): a descriptor sized to one segment makes the hardware bounds check
 // return 0 for loads past it and drop stores past it, so row bodies carry no masks or branches.
 // Build them from wave-uniform values only (scalar loads / kernargs).

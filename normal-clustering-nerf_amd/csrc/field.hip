@@ -298,35 +298,41 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Backward, MLP pass.  Per 16-sample group (inputs prefetched one group ahead): recompute the MLP
-// forward from the cached encoding, back-propagate through the five layers (transposed products
-// with the W^T fragments, re-read from LDS every group), write the encoding gradient level-major
-// for the scatter pass, and accumulate dW = sum_s dY_s X_s^T over the wave's groups in 40
-// register tiles, each layer's right after its output gradient exists.  The dW MFMAs need the
-// samples on K: a C-layout tile is transposed by one MFMA with the identity (transpose_tile).
-// At the end the four waves reduce their tiles into LDS and the workgroup writes one fp32 slab
-// row (reduced in a fixed order later).
-constexpr int BWD_THREADS = 256;
+// Backward, MLP pass.  A workgroup of 8 waves (one per CU: 2 waves per SIMD) takes 8 groups of 16
+// samples per step.  Phase 1, every wave on its own group (inputs prefetched one step ahead):
+// recompute the MLP forward from the cached encoding, back-propagate through the five layers
+// (transposed products with the W^T fragments from LDS), write the encoding gradient level-major
+// for the scatter pass, and put the 30 operand fragments of the weight gradient (dY and X tiles
+// of every layer, transposed so that the samples are on K) into an LDS exchange area.  Phase 2,
+// after a barrier: wave w owns 5 of the 40 dW tiles and accumulates them over the step's 8
+// groups straight from the exchange area.  So no wave holds all of dW (the old one-wave-per-SIMD
+// layout kept 160 accumulator registers per wave), the two waves of a SIMD overlap their MFMA
+// chains, and every tile is written once per workgroup into its slab row at the end.
+constexpr int BWD_WAVES = 8;
+constexpr int BWD_THREADS = 64 * BWD_WAVES;
+// exchange fragments per group: dW operands, A = dY^T, B = X^T (16x16 fp16 MFMA fragments)
+constexpr int XA5 = 0, XB5 = 1, XA4 = 5, XB4 = 9, XA3 = 13, XB3D = 17, XB3H = 18, XA2 = 19, XB2 = 20, XA1 = 24,
+              XB1 = 28, N_XFRAG = 30;
 
-struct WGrad {
-    float4_t w1[4][2], w2[4], w3[4][2], w4[4][4], w5[4];
-};
-
-// Tile transpose by MFMA: a C-layout tile (lane (g,r) = [feature 4g+i][sample r]) fed as the A
-// operand of A.I (I = 16x16 identity B fragment) comes back as [sample 4g+i][feature r], i.e. with
-// the samples on K as the dW products need.  Exact (products with 1, sums of zeros), one MFMA
-// instead of an LDS round trip.
-__device__ __forceinline__ half4_t identity_frag(int lane) {
+// dW operands through LDS images: a C-layout tile (lane (g,r) holds [feature 4g+i][sample r]) is
+// stored as a [sample][feature] image (16 rows of 32 B; lane (g,r) writes 8 B at row r, chunk g,
+// chunks XOR-swizzled by row>>2 against write bank conflicts) and read back with the gfx950
+// transposed read ds_read_b64_tr_b16: lane 4q+p of group g addresses row 4g+q, chunk p, and lane
+// (g,i) receives column i of rows 4g..4g+3, i.e. [feature i][samples 4g..4g+3] — the A/B fragment
+// of a product that sums over the samples.  (EXEC must be all ones at the read.)
+typedef short short4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void x_put(_Float16* tile, int lane, half4_t v) {
     const int g = lane >> 4, r = lane & 15;
-    half4_t I;
-#pragma unroll
-    for (int j = 0; j < 4; j++) I[j] = (_Float16)((4 * g + j == r) ? 1.0f : 0.0f);
-    return I;
+    *(half4_t*)(tile + r * 16 + 4 * (g ^ (r >> 2))) = v;
 }
-__device__ __forceinline__ half4_t transpose_tile_h(half4_t I, half4_t v) { return to_h4(mfma16(v, I, zero4())); }
-__device__ __forceinline__ half4_t transpose_tile(half4_t I, float4_t v) { return transpose_tile_h(I, to_h4(v)); }
+__device__ __forceinline__ half4_t x_get(const _Float16* tile, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) short4_t*)(tile + (4 * g + q) * 16 + 4 * (p ^ g)));
+    return __builtin_bit_cast(half4_t, v);
+}
 
-// Per-group inputs of the backward (prefetched one group ahead).
+// Per-group inputs of the backward (prefetched one step ahead).
 struct BwdIn {
     half4_t e0, e1;
     float dx, dy, dz, dsig, dr0, dr1, dr2;
@@ -346,187 +352,191 @@ __device__ __forceinline__ void bwd_load(BwdIn& in, int64_t grp, int64_t n, int 
     }
 }
 
+// Phase 1 for one group: forward recompute, backward through the layers, dE out, dW operands out.
+__device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const BwdIn& cur,
+                                          int64_t grp, int64_t n, int64_t n_stride, int lane,
+                                          float* __restrict__ dE_out) {
+    const int g = lane >> 4, r = lane & 15;
+    const int64_t s = grp * 16 + r;
+    const bool valid = s < n;
+    float dx = cur.dx, dy = cur.dy, dz = cur.dz;
+    if (valid) {
+        const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
+        dx /= nrm; dy /= nrm; dz /= nrm;
+    }
+    FwdState st;
+    mlp_sigma(Fl, lane, cur.e0, cur.e1, st);
+    mlp_rgb(Fl, lane, dx, dy, dz, st);
+    // dY5: d(pre-sigmoid) = drgb * s(1-s), rows 0..2 on g==0
+    float4_t dy5 = zero4();
+    if (g == 0) {
+        const float s0 = sigmoidf_(st.out[0]), s1 = sigmoidf_(st.out[1]), s2 = sigmoidf_(st.out[2]);
+        dy5[0] = cur.dr0 * s0 * (1.f - s0);
+        dy5[1] = cur.dr1 * s1 * (1.f - s1);
+        dy5[2] = cur.dr2 * s2 * (1.f - s2);
+    }
+    const half4_t dy5h = to_h4(dy5);
+    x_put(Xw + XA5 * 256, lane, dy5h);
+#pragma unroll
+    for (int b = 0; b < 4; b++) x_put(Xw + (XB5 + b) * 256, lane, st.x5[b]);
+    // L5 backward -> dG2, ReLU(x5) mask -> dD4
+    half4_t dD4h[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) dD4h[t] = relu_mask_h4(mfma16(frag(Fl, B_L5 + t, lane), dy5h, zero4()), st.x5[t]);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        x_put(Xw + (XA4 + t) * 256, lane, dD4h[t]);
+        x_put(Xw + (XB4 + t) * 256, lane, st.x4[t]);
+    }
+    // L4 backward -> dG1, ReLU(x4) mask -> dD3
+    half4_t dD3h[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        float4_t v = zero4();
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L4 + 4 * t + ks, lane), dD4h[ks], v);
+        dD3h[t] = relu_mask_h4(v, st.x4[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++) x_put(Xw + (XA3 + t) * 256, lane, dD3h[t]);
+    x_put(Xw + XB3D * 256, lane, st.x3d);
+    x_put(Xw + XB3H * 256, lane, st.x3h);
+    // L3 backward -> dh (rgb path) ; + TruncExp backward on h[0]
+    float4_t dh = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) dh = mfma16(frag(Fl, B_L3 + ks, lane), dD3h[ks], dh);
+    if (g == 0) dh[0] += cur.dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
+    const half4_t dhh = to_h4(dh);
+    x_put(Xw + XA2 * 256, lane, dhh);
+#pragma unroll
+    for (int b = 0; b < 4; b++) x_put(Xw + (XB2 + b) * 256, lane, st.x2[b]);
+    // L2 backward -> dH1, ReLU(x2) mask -> dD1
+    half4_t dD1h[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) dD1h[t] = relu_mask_h4(mfma16(frag(Fl, B_L2 + t, lane), dhh, zero4()), st.x2[t]);
+#pragma unroll
+    for (int t = 0; t < 4; t++) x_put(Xw + (XA1 + t) * 256, lane, dD1h[t]);
+    x_put(Xw + XB1 * 256, lane, cur.e0);
+    x_put(Xw + (XB1 + 1) * 256, lane, cur.e1);
+    // L1 backward -> dE (tile t holds levels 8t+2g, 8t+2g+1)
+    float4_t dE[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        float4_t v = zero4();
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
+        dE[t] = v;
+    }
+    if (valid) {  // encoding gradient -> level-major [16][n] float2 for the scatter pass
+        float2* o = (float2*)dE_out;
+        o[(int64_t)(2 * g) * n_stride + s] = make_float2(dE[0][0], dE[0][1]);
+        o[(int64_t)(2 * g + 1) * n_stride + s] = make_float2(dE[0][2], dE[0][3]);
+        o[(int64_t)(8 + 2 * g) * n_stride + s] = make_float2(dE[1][0], dE[1][1]);
+        o[(int64_t)(9 + 2 * g) * n_stride + s] = make_float2(dE[1][2], dE[1][3]);
+    }
+}
+
+// Phase 2: the dW tiles owned by wave `wid`, accumulated over the exchange fragments of `ng`
+// groups.  Ownership (5 tiles each): waves 0-3: W4 row-block a = wid (4 tiles) + W5 column block
+// wid; waves 4-5: W3 row-blocks 2(wid-4), +1 (d and h tiles) + W2 block wid-4; waves 6-7: W1
+// row-blocks 2(wid-6), +1 (two K tiles) + W2 block wid-4.
+__device__ __forceinline__ void bwd_dw(const _Float16* X, int ng, int wid, int lane, float4_t (&acc)[5]) {
+    for (int q = 0; q < ng; q++) {
+        const _Float16* Xq = X + q * N_XFRAG * 256;
+        if (wid < 4) {
+            const half4_t A4 = x_get(Xq + (XA4 + wid) * 256, lane);
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[b] = mfma16(A4, x_get(Xq + (XB4 + b) * 256, lane), acc[b]);
+            acc[4] = mfma16(x_get(Xq + XA5 * 256, lane), x_get(Xq + (XB5 + wid) * 256, lane), acc[4]);
+        } else if (wid < 6) {
+            const half4_t Bd = x_get(Xq + XB3D * 256, lane), Bh = x_get(Xq + XB3H * 256, lane);
+#pragma unroll
+            for (int aa = 0; aa < 2; aa++) {
+                const half4_t A3 = x_get(Xq + (XA3 + 2 * (wid - 4) + aa) * 256, lane);
+                acc[2 * aa] = mfma16(A3, Bd, acc[2 * aa]);
+                acc[2 * aa + 1] = mfma16(A3, Bh, acc[2 * aa + 1]);
+            }
+            acc[4] = mfma16(x_get(Xq + XA2 * 256, lane), x_get(Xq + (XB2 + wid - 4) * 256, lane), acc[4]);
+        } else {
+            const half4_t B0 = x_get(Xq + XB1 * 256, lane), B1 = x_get(Xq + (XB1 + 1) * 256, lane);
+#pragma unroll
+            for (int aa = 0; aa < 2; aa++) {
+                const half4_t A1 = x_get(Xq + (XA1 + 2 * (wid - 6) + aa) * 256, lane);
+                acc[2 * aa] = mfma16(A1, B0, acc[2 * aa]);
+                acc[2 * aa + 1] = mfma16(A1, B1, acc[2 * aa + 1]);
+            }
+            acc[4] = mfma16(x_get(Xq + XA2 * 256, lane), x_get(Xq + (XB2 + wid - 4) * 256, lane), acc[4]);
+        }
+    }
+}
+
+// The owned tiles (C layout: lane (g,r) = rows 4g+i, column r) into the workgroup's slab row.
+__device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, int lane, const float4_t (&acc)[5]) {
+    const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int row = 4 * g + i;
+        if (wid < 4) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) out[W4_OFF + (16 * wid + row) * 64 + 16 * b + r] = acc[b][i];
+            if (row < 3) out[W5_OFF + row * 64 + 16 * wid + r] = acc[4][i];
+        } else if (wid < 6) {
+#pragma unroll
+            for (int aa = 0; aa < 2; aa++) {
+                const int orow = 16 * (2 * (wid - 4) + aa) + row;
+                if (r < 3) out[W3_OFF + orow * 19 + r] = acc[2 * aa][i];
+                out[W3_OFF + orow * 19 + 3 + r] = acc[2 * aa + 1][i];
+            }
+            out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
+        } else {
+#pragma unroll
+            for (int aa = 0; aa < 2; aa++) {
+                const int orow = 16 * (2 * (wid - 6) + aa) + row;
+                out[W1_OFF + orow * 32 + r] = acc[2 * aa][i];
+                out[W1_OFF + orow * 32 + 16 + r] = acc[2 * aa + 1][i];
+            }
+            out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
+        }
+    }
+}
+
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const half4_t* __restrict__ wpacked,
     const half4_t* __restrict__ enc_cache, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
     float* __restrict__ dE_out, float* __restrict__ slab) {
     const int64_t n_stride = n;  // dE layout [16][n_stride]
     if (n_dev) n = min<int64_t>(n, *n_dev);
-    // LDS: the weight fragments during the loop, reused as the fp32 dW reduction buffer afterwards.
-    constexpr int FRAG_BYTES = N_FRAGS * 64 * 8;
-    static_assert(FRAG_BYTES >= NCN_FIELD_NW * 4, "arena too small for the dW reduction");
-    __shared__ __attribute__((aligned(16))) char arena[FRAG_BYTES];
-    half4_t* F = (half4_t*)arena;
-    float* red = (float*)arena;
+    __shared__ half4_t F[N_FRAGS * 64];                    // 38.9 KB weight fragments
+    __shared__ __attribute__((aligned(16))) _Float16 X[BWD_WAVES * N_XFRAG * 256];  // 120 KB dW operand images
     for (int i = threadIdx.x; i < N_FRAGS * 64; i += BWD_THREADS) F[i] = wpacked[i];
     __syncthreads();
-    const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15, wid = threadIdx.x >> 6;
-    const half4_t Iden = identity_frag(lane);
-    WGrad acc;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float4_t acc[5];
 #pragma unroll
-    for (int a = 0; a < 4; a++) {
-        acc.w2[a] = zero4(); acc.w5[a] = zero4();
-#pragma unroll
-        for (int b = 0; b < 2; b++) { acc.w1[a][b] = zero4(); acc.w3[a][b] = zero4(); }
-#pragma unroll
-        for (int b = 0; b < 4; b++) acc.w4[a][b] = zero4();
-    }
+    for (int t = 0; t < 5; t++) acc[t] = zero4();
     const int64_t n_groups = (n + 15) / 16;
-    const int64_t wave0 = (int64_t)blockIdx.x * 4 + wid;
-    const int64_t n_waves = (int64_t)gridDim.x * 4;
+    const int64_t stride = (int64_t)gridDim.x * BWD_WAVES;
+    int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
     BwdIn nxt;
-    if (wave0 < n_groups) bwd_load(nxt, wave0, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
-    for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
-        const int64_t s = grp * 16 + r;
-        const bool valid = s < n;
-        const half4_t* Fl = F + opaque_zero();  // fragments re-read from LDS every group (not hoisted)
-        const BwdIn cur = nxt;  // the next group's loads go out before this group's math
-        if (grp + n_waves < n_groups) bwd_load(nxt, grp + n_waves, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
-        const half4_t e0 = cur.e0, e1 = cur.e1;
-        float dx = cur.dx, dy = cur.dy, dz = cur.dz;
-        const float dsig = cur.dsig, dr0 = cur.dr0, dr1 = cur.dr1, dr2 = cur.dr2;
-        if (valid) {
-            const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
-            dx /= nrm; dy /= nrm; dz /= nrm;
-        }
-        FwdState st;
-        mlp_sigma(Fl, lane, e0, e1, st);
-        mlp_rgb(Fl, lane, dx, dy, dz, st);
-        // Backward through the five layers with each layer's weight gradient accumulated as soon as
-        // its output gradient exists (dW[out][in] += sum_s dY[out][s] X[in][s]: A = dY with the
-        // samples on K, B = X with the samples on K, both via transpose_tile), so every activation
-        // tile dies right after its last use.  ReLU masks come from the saved fp16 activations.
-        // dY5: d(pre-sigmoid) = drgb * s(1-s), rows 0..2 on g==0
-        float4_t dy5 = zero4();
-        if (g == 0) {
-            const float s0 = sigmoidf_(st.out[0]), s1 = sigmoidf_(st.out[1]), s2 = sigmoidf_(st.out[2]);
-            dy5[0] = dr0 * s0 * (1.f - s0);
-            dy5[1] = dr1 * s1 * (1.f - s1);
-            dy5[2] = dr2 * s2 * (1.f - s2);
-        }
-        const half4_t dy5h = to_h4(dy5);
-        {   // dW5: dY = dy5 (1 out tile), X = x5 (4 in tiles)
-            const half4_t A = transpose_tile_h(Iden, dy5h);
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc.w5[b] = mfma16(A, transpose_tile_h(Iden, st.x5[b]), acc.w5[b]);
-        }
-        // L5 backward -> dG2, ReLU(x5) mask -> dD4
-        half4_t dD4h[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) dD4h[t] = relu_mask_h4(mfma16(frag(Fl, B_L5 + t, lane), dy5h, zero4()), st.x5[t]);
-        {   // dW4: dY = dD4 (4 out tiles), X = x4 (4 in tiles)
-            half4_t Xt[4];
-#pragma unroll
-            for (int b = 0; b < 4; b++) Xt[b] = transpose_tile_h(Iden, st.x4[b]);
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const half4_t A = transpose_tile_h(Iden, dD4h[a]);
-#pragma unroll
-                for (int b = 0; b < 4; b++) acc.w4[a][b] = mfma16(A, Xt[b], acc.w4[a][b]);
-            }
-        }
-        // L4 backward -> dG1, ReLU(x4) mask -> dD3
-        half4_t dD3h[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            float4_t v = zero4();
-#pragma unroll
-            for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L4 + 4 * t + ks, lane), dD4h[ks], v);
-            dD3h[t] = relu_mask_h4(v, st.x4[t]);
-        }
-        {   // dW3: dY = dD3 (4 out tiles), X = [d | h] : in tile 0 = d (cols 0..2), tile 1 = h (cols 3..18)
-            const half4_t Xd = transpose_tile_h(Iden, st.x3d);
-            const half4_t Xh = transpose_tile_h(Iden, st.x3h);
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const half4_t A = transpose_tile_h(Iden, dD3h[a]);
-                acc.w3[a][0] = mfma16(A, Xd, acc.w3[a][0]);
-                acc.w3[a][1] = mfma16(A, Xh, acc.w3[a][1]);
-            }
-        }
-        // L3 backward -> dh (rgb path) ; + TruncExp backward on h[0]
-        float4_t dh = zero4();
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++) dh = mfma16(frag(Fl, B_L3 + ks, lane), dD3h[ks], dh);
-        if (g == 0) dh[0] += dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
-        const half4_t dhh = to_h4(dh);
-        {   // dW2: dY = dh (1 out tile), X = x2 (4 in tiles)
-            const half4_t A = transpose_tile_h(Iden, dhh);
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc.w2[b] = mfma16(A, transpose_tile_h(Iden, st.x2[b]), acc.w2[b]);
-        }
-        // L2 backward -> dH1, ReLU(x2) mask -> dD1
-        half4_t dD1h[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) dD1h[t] = relu_mask_h4(mfma16(frag(Fl, B_L2 + t, lane), dhh, zero4()), st.x2[t]);
-        {   // dW1: dY = dD1 (4 out tiles), X = e (2 in tiles)
-            const half4_t X0 = transpose_tile_h(Iden, e0);
-            const half4_t X1 = transpose_tile_h(Iden, e1);
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const half4_t A = transpose_tile_h(Iden, dD1h[a]);
-                acc.w1[a][0] = mfma16(A, X0, acc.w1[a][0]);
-                acc.w1[a][1] = mfma16(A, X1, acc.w1[a][1]);
-            }
-        }
-        // L1 backward -> dE (tile t holds levels 8t+2g, 8t+2g+1)
-        float4_t dE[2];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            float4_t v = zero4();
-#pragma unroll
-            for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
-            dE[t] = v;
-        }
-        // encoding gradient -> level-major [16][n] float2 for the scatter pass
-        if (valid) {
-            float2* o = (float2*)dE_out;
-            o[(int64_t)(2 * g) * n_stride + s] = make_float2(dE[0][0], dE[0][1]);
-            o[(int64_t)(2 * g + 1) * n_stride + s] = make_float2(dE[0][2], dE[0][3]);
-            o[(int64_t)(8 + 2 * g) * n_stride + s] = make_float2(dE[1][0], dE[1][1]);
-            o[(int64_t)(9 + 2 * g) * n_stride + s] = make_float2(dE[1][2], dE[1][3]);
-        }
+    if (base + wid < n_groups) bwd_load(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+    for (; base < n_groups; base += stride) {
+        const int64_t grp = base + wid;
+        const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
+        const BwdIn cur = nxt;
+        if (grp + stride < n_groups) bwd_load(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+#ifndef NCN_DIAG_BWD_NO_P1
+        if (grp < n_groups)
+            bwd_group(F + opaque_zero(), X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out);
+#else
+        if (cur.dsig == 1234.5f) dE_out[grp] = 0.f;
+#endif
+        lds_barrier();  // (the dE stores and the next step's loads stay in flight)
+#ifndef NCN_DIAG_BWD_NO_DW
+        bwd_dw(X, ng, wid, lane, acc);
+#endif
+        lds_barrier();
     }
-    // ---- workgroup reduction of the 40 tiles into LDS (C layout: row 4g+i, col r) ----
-    __syncthreads();  // every wave is done with the fragments / slots: reuse the arena
-    for (int i = threadIdx.x; i < NCN_FIELD_NW; i += BWD_THREADS) red[i] = 0.f;
-    __syncthreads();
-    // W1 [64][32]
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) atomicAdd(&red[W1_OFF + (16 * a + 4 * g + i) * 32 + 16 * b + r], acc.w1[a][b][i]);
-    // W2 [16][64]
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) atomicAdd(&red[W2_OFF + (4 * g + i) * 64 + 16 * b + r], acc.w2[b][i]);
-    // W3 [64][19]: in tile 0 -> cols 0..2 (d), in tile 1 -> cols 3..18 (h)
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            if (r < 3) atomicAdd(&red[W3_OFF + (16 * a + 4 * g + i) * 19 + r], acc.w3[a][0][i]);
-            atomicAdd(&red[W3_OFF + (16 * a + 4 * g + i) * 19 + 3 + r], acc.w3[a][1][i]);
-        }
-    // W4 [64][64]
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) atomicAdd(&red[W4_OFF + (16 * a + 4 * g + i) * 64 + 16 * b + r], acc.w4[a][b][i]);
-    // W5 [3][64]
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (4 * g + i < 3) atomicAdd(&red[W5_OFF + (4 * g + i) * 64 + 16 * b + r], acc.w5[b][i]);
-    __syncthreads();
-    float* out = slab + (int64_t)blockIdx.x * NCN_FIELD_NW;
-    for (int i = threadIdx.x; i < NCN_FIELD_NW; i += BWD_THREADS) out[i] = red[i];
+    bwd_store_dw(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc);
 }
 
 // Sum of the per-workgroup dW slabs: blockIdx.y takes a chunk of slabs (coalesced 1 KB rows),
@@ -543,89 +553,368 @@ __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb, floa
 
 // ---------------------------------------------------------------------------------------------
 // Scatter of the encoding gradient into the fp32 table gradient (tcnn kernel_grid_backward).
-// Hash-grid gradients are extremely local: the rays of a patch re-touch the same few entries per
-// level hundreds of times, so a workgroup owns one span of consecutive samples
-// (~1/4 patch) and, level by level, aggregates every contribution in an LDS hash table before
-// anything reaches memory (6144 slots, 4-way set associative: 24 KB keys + 96 KB int64 sums):
-//  1. consecutive samples (lanes) in the same base cell are merged first with DPP run sums inside
-//     each 16-lane row (all 8 corners shared);
-//  2. run heads look up their 8 corners (one ds_read_b128 of the set per corner, ds_cmpst_b32 to
-//     claim an empty way) and add with ds_add_u64 into 64-bit FIXED-POINT sums: on gfx950 an LDS f32 atomic
-//     costs ~3 cycles per active lane (193 cycles per wave-instruction, tools/lds_atomic_bench),
-//     an LDS u64 atomic add ~13 cycles per wave-instruction.  The fixed point is exact integer
-//     arithmetic (order-independent, reproducible): per (workgroup, level) the scale is 2^k with
-//     k = 46 - e, max|dE| < 2^e, so a value within 2^23 of the level's maximum converts exactly
-//     and the LDS sum (< 2^15 contributions) cannot overflow;
-//  3. at the end of a level (or when half of the slots are taken) the table is flushed: two
-//     lanes per slot, each converts its sum back to f32 and issues one f32 global atomic.
-// A contribution whose set is full of other entries goes straight to a global atomic, as
-// does a whole level whose gradient is not finite (NaN/Inf propagate as in the f32 path).
-#ifdef NCN_DIAG_PHASES
-__device__ unsigned long long ncn_sc_phase[8];
-#define SC_T(v) const unsigned long long v = __builtin_readcyclecounter()
-#define SC_ACC(i, a, b) ph[i] += (b) - (a)
-#else
-#define SC_T(v)
-#define SC_ACC(i, a, b)
-#endif
+// Hash-grid gradients are extremely local: the samples of one ray stay in the same cell of a
+// coarse level for tens of steps, and the rays of a patch re-touch the same entries (per
+// 2-8K-sample span the contributions per distinct entry are ~460 at level 0 and still ~6 at
+// level 15).  So the work is organised around runs and a per-workgroup LDS table:
+//  * a unit of work is (span of consecutive samples, level); the span is 8192 samples on levels
+//    0-9, 4096 on 10-11, 2048 on 12-15 (1024 lanes x 8/4/2 samples), so that a unit's distinct
+//    entries fit the table;
+//  * phase A, lane-sequential: every lane walks its 8/4/2 consecutive samples and sums the eight
+//    corner contributions of consecutive samples in the same cell in registers (a run); a cell
+//    change (or the lane's last sample) emits a run record (cell, 16 sums) into the wave's LDS
+//    staging area (ballot + mbcnt compaction, 64 records);
+//  * phase B, when the staging area is full: one record per lane, its 8 corners looked up in a
+//    4-way set-associative LDS table (one ds_read_b128 per set, ds_cmpst to claim a way) and
+//    added with ds_add_u64 as 64-bit FIXED-POINT sums (exact integer arithmetic: order-independent
+//    and reproducible; an LDS f32 atomic costs ~3 cycles per active lane on gfx950, a u64 add
+//    ~13 per wave-instruction).  Per unit the scale is 2^k with k = 46 - e, max|dE| < 2^e: a
+//    record sums at most 8 samples and an entry gets at most 8192 contributions, so the sums
+//    stay below 2^62.  A corner whose set is full goes straight to a global f32 atomic;
+//  * at the end of the unit the claimed slots (the `used` list) are flushed with one f32 global
+//    atomic per non-zero sum and reset.  A unit whose gradient is not finite adds every record
+//    straight to global memory (NaN/Inf propagate as in the f32 path).
 constexpr int SC_THREADS = 1024;
-#ifndef SC_SETS
-#define SC_SETS 1536
-#endif
-#ifndef SC_FLUSH_FRAC
-#define SC_FLUSH_FRAC 2
-#endif
-constexpr int SC_WAYS = 4;                  // 4-way set associative: one ds_read_b128 per lookup
-constexpr int SC_TS = SC_SETS * SC_WAYS;    // 6144 slots: 24 KB keys + 96 KB sums + 12 KB claim list
+constexpr int SC_WAVES = SC_THREADS / 64;
+constexpr int SC_WAYS = 4;                 // 4-way set associative: one ds_read_b128 per lookup
+constexpr int SC_REC = 64;                 // staged run records per wave (80 B each: 80 KB)
+// Two LDS layouts over one arena: run levels 768 sets (3072 slots, 66 KB) + the record staging
+// (80 KB); direct levels 1536 sets (6144 slots, 132 KB) and no staging.
+constexpr int SC_SETS_RUN = 768, SC_SETS_DIR = 1536;
+constexpr int sc_layout_bytes(int sets, bool staging) {
+    return sets * SC_WAYS * (4 + 8 + 8 + 2) + (staging ? SC_WAVES * SC_REC * 80 : 0);
+}
+constexpr int SC_ARENA = sc_layout_bytes(SC_SETS_RUN, true) > sc_layout_bytes(SC_SETS_DIR, false)
+                             ? sc_layout_bytes(SC_SETS_RUN, true) : sc_layout_bytes(SC_SETS_DIR, false);
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
-#ifndef SC_MERGE_LEVELS
-#define SC_MERGE_LEVELS 16
-#endif
 
-__device__ __forceinline__ uint32_t sc_set(uint32_t e) { return __umulhi(e * 0x9E3779B1u, (uint32_t)SC_SETS); }
+__device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
 
-// round(v * 2^k) as int64 for |v * 2^k| < 2^46 without f64: split at 2^23 into two exact int32s
+// round(v * 2^k) as int64 (|v * 2^k| < 2^51): v * 2^k is exact in f64, adding 1.5 * 2^52 rounds it
+// to an integer in the low mantissa bits (round-to-nearest-even), and the bit pattern minus that of
+// 1.5 * 2^52 is the two's-complement integer.  Three f64/int ops instead of an f32 hi/lo split.
 __device__ __forceinline__ long long sc_fix(float v, int k) {
-    const float x = ldexpf(v, k - 23);   // |x| < 2^23
-    const float hi = truncf(x);          // exact
-    const float lo = ldexpf(x - hi, 23); // exact fraction, |lo| < 2^23
-    return ((long long)(int)hi << 23) + (long long)(int)rintf(lo);
+    const double magic = 6755399441055744.0;  // 1.5 * 2^52
+    const double y = fma((double)v, __longlong_as_double((long long)(1023 + k) << 52), magic);
+    return __double_as_longlong(y) - __double_as_longlong(magic);
 }
 
-// Flush: only the slots claimed since the last flush (the `used` list), two lanes per slot (x and
-// y of one entry are adjacent floats: 8-B pieces per atomic instruction), one f32 global atomic per
-// non-zero sum; then exactly those slots are reset.  Cost proportional to the entries, not the table.
-__device__ __forceinline__ void sc_flush(uint32_t* keys, long long* valx, long long* valy,
-                                         const uint16_t* used, int* fill, float* __restrict__ grad, uint32_t off,
-                                         int k) {
-    const int nf = *fill;
+// samples per lane (log2) and span of a unit on level l
+// levels 0-9: 8 samples per lane with run records (unit = 8192 samples); levels 10-15 (cells
+// shorter than ~2 steps, runs rarely longer than one sample): 2 samples per lane, each added
+// directly (unit = 2048 samples)
+constexpr int SC_RUN_LEVELS = 10;
+#ifndef SC_C_RUN
+#define SC_C_RUN 6  // samples per lane on the run levels (unit = 1024 * SC_C_RUN samples)
+#endif
+
+struct ScRec {
+    uint32_t k0, k1, pad0, pad1;  // cell: k0 = px | py << 16, k1 = pz
+    float v[16];                  // corner c: (x, y) sums at 2c, 2c+1
+};
+
+// The current layout's arrays inside the arena (uniform pointers) and the per-workgroup scalars.
+struct ScShared {
+    uint32_t* keys;
+    long long *valx, *valy;
+    uint16_t* used;  // slots claimed since the last flush, in claim order
+    ScRec* rec;      // [SC_WAVES][SC_REC] (run layout only)
+    uint32_t sets;
+    int slots;
+    float* wmax;
+    int* fill;
+};
+__device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fill, bool run) {
+    ScShared sh;
+    sh.sets = run ? SC_SETS_RUN : SC_SETS_DIR;
+    sh.slots = (int)sh.sets * SC_WAYS;
+    sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used, records (16-B aligned)
+    sh.valy = sh.valx + sh.slots;
+    sh.keys = (uint32_t*)(sh.valy + sh.slots);
+    sh.used = (uint16_t*)(sh.keys + sh.slots);
+    sh.rec = (ScRec*)(sh.used + sh.slots);
+    sh.wmax = wmax;
+    sh.fill = fill;
+    return sh;
+}
+
+// Level geometry of the unit, uniform.
+struct ScLevel {
+    float scale;
+    uint32_t res, params, off;
+    bool dense, direct;
+    int k;
+};
+
+__device__ __forceinline__ void sc_corner_entries(const ScLevel& L, uint32_t px, uint32_t py, uint32_t pz,
+                                                  uint32_t (&e)[8]) {
+    if (L.dense) {
+        const uint32_t b0 = px + L.res * py + L.res * L.res * pz;
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            e[c] = b0 + (c & 1) + ((c >> 1) & 1) * L.res + ((c >> 2) & 1) * L.res * L.res;
+            e[c] = e[c] < L.params ? e[c] : e[c] % L.params;  // as grid_index (boundary corner)
+        }
+    } else {  // params is 2^19 on every hashed level
+        const uint32_t hy0 = py * 2654435761u, hy1 = (py + 1) * 2654435761u;
+        const uint32_t hz0 = pz * 805459861u, hz1 = (pz + 1) * 805459861u;
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            e[c] = ((px + (c & 1)) ^ ((c & 2) ? hy1 : hy0) ^ ((c & 4) ? hz1 : hz0)) & (L.params - 1);
+    }
+}
+
+// Phase B core: one contribution set per lane (cell px,py,pz; v = the 8 corners' (x, y) sums).
+// Called by the whole wave; lanes with all-zero v add nothing.
+__device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint32_t py, uint32_t pz,
+                                       const float (&v)[16], const ScLevel& L, float* __restrict__ grad) {
+    uint32_t e[8];
+    sc_corner_entries(L, px, py, pz, e);
+    if (L.direct) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            if (v[2 * c] != 0.f || v[2 * c + 1] != 0.f) {
+                atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
+                atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
+            }
+        }
+        return;
+    }
+    uint32_t newmask = 0;
+    int slot[8];
+#pragma unroll 2
+    for (int c = 0; c < 8; c++) {
+        slot[c] = -1;
+        if (v[2 * c] == 0.f && v[2 * c + 1] == 0.f) continue;
+        const int p0 = SC_WAYS * sc_set(e[c], sh.sets);
+        const uint4 kk = *(const uint4*)&sh.keys[p0];
+        int sl = kk.x == e[c] ? p0 : kk.y == e[c] ? p0 + 1 : kk.z == e[c] ? p0 + 2 : kk.w == e[c] ? p0 + 3 : -1;
+        if (sl < 0) {  // claim the first way of the set seen empty
+            const int cl = kk.x == SC_EMPTY ? p0 : kk.y == SC_EMPTY ? p0 + 1 : kk.z == SC_EMPTY ? p0 + 2
+                         : kk.w == SC_EMPTY ? p0 + 3 : -1;
+            if (cl >= 0) {
+                const uint32_t got = atomicCAS(&sh.keys[cl], SC_EMPTY, e[c]);
+                if (got == SC_EMPTY) { sl = cl; newmask |= 1u << c; }
+                else if (got == e[c]) sl = cl;
+            }
+        }
+        slot[c] = sl;
+        if (sl >= 0) {
+#if defined(NCN_DIAG_SC_PACKED)
+            atomicAdd((unsigned long long*)&sh.valx[sl], (unsigned long long)(sc_fix(v[2 * c], L.k - 20) + (sc_fix(v[2 * c + 1], L.k - 20) << 32)));
+#elif !defined(NCN_DIAG_SC_NO_LDSADD)
+            atomicAdd((unsigned long long*)&sh.valx[sl], (unsigned long long)sc_fix(v[2 * c], L.k));
+            atomicAdd((unsigned long long*)&sh.valy[sl], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
+#endif
+        } else {  // set full of other entries
+#ifndef NCN_DIAG_SC_NO_FALLBACK
+            atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
+            atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
+#endif
+        }
+    }
+    // append the claimed slots to `used`: one LDS atomic per wave
+    const int mine = __builtin_popcount(newmask);
+    const float incl = wave_incl_sum_dpp((float)mine);
+    const int wtot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
+    if (wtot) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(sh.fill, wtot);
+        base = __builtin_amdgcn_readfirstlane(base);
+        int pos = base + (int)incl - mine;
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            if (newmask & (1u << c)) sh.used[pos++] = (uint16_t)slot[c];
+    }
+}
+
+// Phase B of the staged records 0..cnt-1 of this wave (one per lane).
+__device__ __forceinline__ void sc_phase_b(ScShared& sh, int wid, int lane, int cnt, const ScLevel& L,
+                                           float* __restrict__ grad) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's record writes are visible
+    const bool act = lane < cnt;
+    const ScRec& R = sh.rec[wid * SC_REC + (act ? lane : 0)];
+    const uint32_t k0 = R.k0, k1 = R.k1;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = act ? R.v[i] : 0.f;
+    sc_add(sh, lane, k0 & 0xFFFFu, k0 >> 16, k1, v, L, grad);
+}
+
+// Stage the records of the lanes with `em` (cell px,py,pz and the 16 sums); a full staging area
+// is processed first.  Called by the whole wave.
+__device__ __forceinline__ void sc_emit(ScShared& sh, int wid, int lane, int& staged, bool em, uint32_t px,
+                                        uint32_t py, uint32_t pz, const float (&acc)[16], const ScLevel& L,
+                                        float* __restrict__ grad) {
+    const uint64_t m = __ballot(em);
+    const int cnt = __popcll(m);
+    if (cnt == 0) return;
+    if (staged + cnt > SC_REC) {
+        sc_phase_b(sh, wid, lane, staged, L, grad);
+        staged = 0;
+    }
+    if (em) {
+        const int pos = staged + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        ScRec& R = sh.rec[wid * SC_REC + pos];
+        *(uint4*)&R.k0 = make_uint4(px | (py << 16), pz, 0u, 0u);
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) *(float4*)&R.v[i] = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
+    }
+    staged += cnt;
+}
+
+// Sample position in [0,1]^3 as the forward computes it ((x - min) / extent; a power-of-two
+// extent — 1.0 at the configs' scale 0.5 — multiplies by its exact reciprocal instead).
+struct ScNorm {
+    float mn, ext, inv;
+    bool pow2;
+    __device__ __forceinline__ float operator()(float v) const { return pow2 ? (v - mn) * inv : (v - mn) / ext; }
+};
+
+__device__ __forceinline__ void sc_corner_sums(const LevelPos& p, float2 g, float (&v)[16]) {
+    // corner weights in the forward's association ((wx * wy) * wz)
+    const float wx[2] = {1.0f - p.fx, p.fx}, wy[2] = {1.0f - p.fy, p.fy}, wz[2] = {1.0f - p.fz, p.fz};
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+        v[2 * c] = fmaf(w, g.x, v[2 * c]);
+        v[2 * c + 1] = fmaf(w, g.y, v[2 * c + 1]);
+    }
+}
+
+// A lane's C consecutive samples (normalised positions and dE of the unit's level), loaded at the
+// start of the unit in one batch; samples past the end carry dE = 0.
+template <int C>
+struct ScChunk {
+    float x[C], y[C], z[C];
+    float2 g[C];
+};
+template <int C>
+__device__ __forceinline__ float sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
+                                               const float2* __restrict__ dEl, const ScNorm& nrm) {
+    float m = 0.f;  // max |dE| (INFINITY if not finite)
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        const int64_t s = sb + i;
+        const bool in = s < s1;
+        const int64_t sc = in ? s : sb;  // (sb < s1 whenever any sample is in range)
+        ch.g[i] = in ? dEl[sc] : make_float2(0.f, 0.f);
+        ch.x[i] = in ? nrm(xyzs[3 * sc]) : 0.f;
+        ch.y[i] = in ? nrm(xyzs[3 * sc + 1]) : 0.f;
+        ch.z[i] = in ? nrm(xyzs[3 * sc + 2]) : 0.f;
+        const float a = fmaxf(fabsf(ch.g[i].x), fabsf(ch.g[i].y));
+        m = (isfinite(ch.g[i].x) && isfinite(ch.g[i].y)) ? fmaxf(m, a) : INFINITY;
+    }
+    return m;
+}
+
+// Phase A over the lane's chunk; step C emits the last run.  The loop is not unrolled (one emit
+// site: phase B is inlined once); the chunk is walked as a shift register instead of indexed.
+template <int C>
+__device__ __forceinline__ void sc_phase_a(ScShared& sh, int wid, int lane, ScChunk<C>& ch, const ScLevel& L,
+                                           float* __restrict__ grad, int& staged) {
+    bool have = false;
+    uint32_t cx = 0, cy = 0, cz = 0;
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0.f;
+#pragma unroll 1
+    for (int i = 0; i <= C; i++) {
+        const float2 g = ch.g[0];
+        const bool valid = g.x != 0.f || g.y != 0.f;
+        const LevelPos p = level_pos(L.scale, ch.x[0], ch.y[0], ch.z[0]);
+#pragma unroll
+        for (int j = 0; j + 1 < C; j++) {
+            ch.g[j] = ch.g[j + 1]; ch.x[j] = ch.x[j + 1]; ch.y[j] = ch.y[j + 1]; ch.z[j] = ch.z[j + 1];
+        }
+        ch.g[C - 1] = make_float2(0.f, 0.f);
+        const bool change = have && (i == C || (valid && (p.px != cx || p.py != cy || p.pz != cz)));
+        sc_emit(sh, wid, lane, staged, change, cx, cy, cz, acc, L, grad);
+        const bool start = valid && (change || !have);
+        cx = start ? p.px : cx;
+        cy = start ? p.py : cy;
+        cz = start ? p.pz : cz;
+        have = have || valid;
+#pragma unroll
+        for (int j = 0; j < 16; j++) acc[j] = start ? 0.f : acc[j];
+        sc_corner_sums(p, g, acc);  // g == 0 on an invalid step: adds nothing
+    }
+}
+
+// Direct form (fine levels): every sample's 8 corners go to the table as they are.
+template <int C>
+__device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
+                                          float* __restrict__ grad) {
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        const LevelPos p = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = 0.f;
+        sc_corner_sums(p, ch.g[i], v);
+        sc_add(sh, lane, p.px, p.py, p.pz, v, L, grad);
+    }
+}
+
+// One unit: load the chunk, the unit's fixed-point scale (block max), phase A/B or direct, flush.
+template <int C, bool RUNS>
+__device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
+                                        const float* __restrict__ xyzs, const float2* __restrict__ dEl,
+                                        const ScNorm& nrm, const LevelTable& Lt, float* __restrict__ grad) {
+    ScChunk<C> ch;
+    float m = sc_load_chunk<C>(ch, s0 + (int64_t)threadIdx.x * C, s1, xyzs, dEl, nrm);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) sh.wmax[wid] = m;
+    lds_barrier();
+    m = 0.f;
+#pragma unroll
+    for (int w = 0; w < SC_WAVES; w++) m = fmaxf(m, sh.wmax[w]);
+#ifdef NCN_DIAG_SC_LEVELS_MASK
+    if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
+#endif
+    if (m == 0.f) {  // uniform: nothing to add on this unit
+        lds_barrier();  // (wmax is rewritten by the next unit)
+        return;
+    }
+    ScLevel L;
+    L.scale = Lt.scale[l];
+    L.res = Lt.res[l];
+    L.params = Lt.params[l];
+    L.off = Lt.offset[l];
+    L.dense = (uint64_t)L.res * L.res * L.res <= L.params;  // tcnn: stride stays <= params
+    L.direct = !isfinite(m);
+    int e2 = 0;
+    (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
+    L.k = 46 - e2;
+    if (RUNS) {
+        int staged = 0;
+        sc_phase_a<C>(sh, wid, lane, ch, L, grad, staged);
+        if (staged) sc_phase_b(sh, wid, lane, staged, L, grad);
+    } else {
+        sc_direct<C>(sh, lane, ch, L, grad);
+    }
+    lds_barrier();
+    // flush: the claimed slots, two lanes per slot (x and y of one entry are adjacent floats)
+    const int nf = *sh.fill;
     for (int i = threadIdx.x; i < 2 * nf; i += SC_THREADS) {
-        const int slot = used[i >> 1];
-        const uint32_t key = keys[slot];
-        const long long q = (i & 1) ? valy[slot] : valx[slot];
-#ifdef NCN_DIAG_SC_NO_GATOMIC
-        if (q == 12345) grad[2 * (size_t)(off + key) + (i & 1)] = 1.f;
-#else
-        if (q != 0) atomicAdd(grad + 2 * (size_t)(off + key) + (i & 1), (float)ldexp((double)q, -k));
+        const int slot = sh.used[i >> 1];
+        const uint32_t key = sh.keys[slot];
+        const long long q = (i & 1) ? sh.valy[slot] : sh.valx[slot];
+#ifndef NCN_DIAG_SC_NO_FLUSH
+        if (q != 0) atomicAdd(grad + 2 * (size_t)(L.off + key) + (i & 1), (float)ldexp((double)q, -L.k));
 #endif
     }
-    __syncthreads();  // every lane has read its slots
+    lds_barrier();  // every lane has read its slots
     for (int i = threadIdx.x; i < nf; i += SC_THREADS) {
-        const int slot = used[i];
-        keys[slot] = SC_EMPTY;
-        valx[slot] = 0;
-        valy[slot] = 0;
+        const int slot = sh.used[i];
+        sh.keys[slot] = SC_EMPTY;
+        sh.valx[slot] = 0;
+        sh.valy[slot] = 0;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) *fill = 0;
-    __syncthreads();
-}
-
-__device__ __forceinline__ int64_t scatter_span_of(int64_t n) {
-    // ~one span per CU: n/256 samples, at least 1024, a multiple of 64; at most 2^16 so that the
-    // fixed-point sums keep their headroom (each sample adds at most once to an entry)
-    int64_t sp = min<int64_t>(65536, max<int64_t>(1024, (n + 255) / 256));
-    return (sp + 63) / 64 * 64;
+    if (threadIdx.x == 0) *sh.fill = 0;
+    lds_barrier();
 }
 
 __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
@@ -633,240 +922,54 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    float xyz_min, float xyz_extent,
                                                                    const float2* __restrict__ dE,
                                                                    float* __restrict__ grad) {
-    __shared__ __attribute__((aligned(16))) uint32_t keys[SC_TS];
-    __shared__ long long valx[SC_TS], valy[SC_TS];
-    __shared__ uint16_t used[SC_TS];  // slots claimed since the last flush, in claim order
-    __shared__ int fill;              // == number of entries in `used`
-    __shared__ float wmax[SC_THREADS / 64][16];
-    __shared__ float lmax[16];
-    for (int i = threadIdx.x; i < SC_TS; i += SC_THREADS) {
-        keys[i] = SC_EMPTY;
-        valx[i] = 0;
-        valy[i] = 0;
-    }
-    if (threadIdx.x == 0) fill = 0;
-    const int lane = threadIdx.x & 63, r = lane & 15, wid = threadIdx.x >> 6;
+    __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
+    __shared__ float wmax[SC_WAVES];
+    __shared__ int fill;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
-    const int64_t span = scatter_span_of(n), nspans = (n + span - 1) / span;
-    for (int64_t sp = blockIdx.x; sp < nspans; sp += gridDim.x) {
-    const int64_t s0 = sp * span, s1 = min(n, s0 + span);
-    // fixed-point scale per level: max |dE| over the span, all 16 levels in one load round
-    {
-        float m[16];
-#pragma unroll
-        for (int l = 0; l < 16; l++) m[l] = 0.f;
-        for (int64_t s = s0 + threadIdx.x; s < s1; s += SC_THREADS) {
-#pragma unroll
-            for (int l = 0; l < 16; l++) {
-                const float2 g = dE[(int64_t)l * n_stride + s];
-                const float a = fmaxf(fabsf(g.x), fabsf(g.y));
-                m[l] = (isfinite(g.x) && isfinite(g.y)) ? fmaxf(m[l], a) : INFINITY;
+    ScNorm nrm;
+    nrm.mn = xyz_min;
+    nrm.ext = xyz_extent;
+    nrm.inv = 1.0f / xyz_extent;
+    nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
+    // units, level-major: run levels in spans of 8192 samples (8 per lane), direct levels in spans
+    // of 2048 (2 per lane)
+    constexpr int C_RUN = SC_C_RUN, C_DIR = 2;
+    const int64_t ur = (n + SC_THREADS * C_RUN - 1) / (SC_THREADS * C_RUN);
+    const int64_t ud = (n + SC_THREADS * C_DIR - 1) / (SC_THREADS * C_DIR);
+    const int64_t n_units = SC_RUN_LEVELS * ur + (16 - SC_RUN_LEVELS) * ud;
+    // (grid-stride: a workgroup takes its run units first, then its direct ones: one layout switch)
+    int layout = -1;
+    ScShared sh;
+    for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+        const int run = u < SC_RUN_LEVELS * ur;
+        if (run != layout) {  // (re)initialise the table of the new layout
+            lds_barrier();
+            sh = sc_layout(arena, wmax, &fill, run);
+            for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) {
+                sh.keys[i] = SC_EMPTY;
+                sh.valx[i] = 0;
+                sh.valy[i] = 0;
             }
+            if (threadIdx.x == 0) fill = 0;
+            lds_barrier();
+            layout = run;
         }
-#pragma unroll
-        for (int l = 0; l < 16; l++) {
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) m[l] = fmaxf(m[l], __shfl_xor(m[l], o, 64));
-        }
-        if (lane < 16) {
-            float v = m[0];
-#pragma unroll
-            for (int l = 1; l < 16; l++) v = lane == l ? m[l] : v;
-            wmax[wid][lane] = v;
-        }
-        __syncthreads();
-        if (threadIdx.x < 16) {
-            float v = 0.f;
-            for (int w = 0; w < SC_THREADS / 64; w++) v = fmaxf(v, wmax[w][threadIdx.x]);
-            lmax[threadIdx.x] = v;
-        }
-        __syncthreads();
-    }
-    // the span is cut into nchunk EQUAL chunks (<= SC_THREADS samples each) so that no chunk
-    // leaves most waves idle at its barrier
-    const int nchunk = (int)((s1 - s0 + SC_THREADS - 1) / SC_THREADS);
-    const int64_t len = s1 - s0;
-    const int total = 16 * max(nchunk, 0);
-    // software pipeline over (level, chunk): the next item's loads are in flight while this one
-    // is aggregated
-    auto load = [&](int it, float& x, float& y, float& z, float2& g) {
-        const int l = it / nchunk, ch = it - l * nchunk;
-        const int64_t c0 = s0 + len * ch / nchunk, c1 = s0 + len * (ch + 1) / nchunk;
-        const int64_t s = c0 + threadIdx.x;
-        x = y = z = 0.f;
-        g = make_float2(0.f, 0.f);
-        if (s < c1) {
-            x = xyzs[3 * s];
-            y = xyzs[3 * s + 1];
-            z = xyzs[3 * s + 2];
-            g = dE[(int64_t)l * n_stride + s];
-        }
-    };
-    float nx, ny, nz;
-    float2 ng;
-    if (total > 0) load(0, nx, ny, nz, ng);
-#ifdef NCN_DIAG_PHASES
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    for (int it = 0; it < total; it++) {
-        SC_T(t0);
-        const int l = it / nchunk, ch = it - l * nchunk;
-#ifdef NCN_DIAG_SC_LEVELS_MASK
-        const float m = ((NCN_DIAG_SC_LEVELS_MASK >> l) & 1) ? lmax[l] : 0.f;
-#else
-        const float m = lmax[l];
-#endif
-        if (m == 0.f) {  // uniform: nothing at this level; keep the pipeline moving
-            if (it + 1 < total) load(it + 1, nx, ny, nz, ng);
-            continue;
-        }
-        const float scale = Lt.scale[l];
-        const uint32_t res = Lt.res[l], params = Lt.params[l], off = Lt.offset[l];
-        const bool dense = (uint64_t)res * res * res <= params;  // tcnn: stride stays <= params
-        const bool direct = !isfinite(m);
-        int e2 = 0;
-        (void)frexpf(direct ? 1.f : m, &e2);  // m < 2^e2
-        const int k = 46 - e2;
-        const int64_t c1 = s0 + len * (ch + 1) / nchunk;
-        const int64_t s = s0 + len * ch / nchunk + threadIdx.x;
-        const float x = (nx - xyz_min) / xyz_extent, y = (ny - xyz_min) / xyz_extent, z = (nz - xyz_min) / xyz_extent;
-        const float2 gv = ng;
-        if (it + 1 < total) load(it + 1, nx, ny, nz, ng);
-        const bool valid = s < c1 && ((gv.x != 0.f) || (gv.y != 0.f));
-        const LevelPos p = level_pos(scale, x, y, z);
-        // corner weights in the forward's association ((wx * wy) * wz) and entry indices without
-        // per-corner grid_index branches: dense = base + dx + dy*res + dz*res^2, hashed =
-        // ((x+dx) ^ (y+dy)*P1 ^ (z+dz)*P2) & (params-1) (params is 2^19 on every hashed level)
-        const float wx[2] = {1.0f - p.fx, p.fx}, wy[2] = {1.0f - p.fy, p.fy}, wz[2] = {1.0f - p.fz, p.fz};
-        uint32_t e[8];
-        if (dense) {
-            const uint32_t b0 = p.px + res * p.py + res * res * p.pz;
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                e[c] = b0 + (c & 1) + ((c >> 1) & 1) * res + ((c >> 2) & 1) * res * res;
-                e[c] = e[c] < params ? e[c] : e[c] % params;  // as grid_index (boundary corner)
-            }
+        if (run) {
+            const int l = (int)(u / ur);
+            const int64_t s0 = (u - l * ur) * (SC_THREADS * C_RUN), s1 = min(n, s0 + SC_THREADS * C_RUN);
+            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * n_stride, nrm, Lt, grad);
         } else {
-            const uint32_t hy0 = p.py * 2654435761u, hy1 = (p.py + 1) * 2654435761u;
-            const uint32_t hz0 = p.pz * 805459861u, hz1 = (p.pz + 1) * 805459861u;
-#pragma unroll
-            for (int c = 0; c < 8; c++)
-                e[c] = ((p.px + (c & 1)) ^ ((c & 2) ? hy1 : hy0) ^ ((c & 4) ? hz1 : hz0)) & (params - 1);
+            const int64_t v = u - SC_RUN_LEVELS * ur;
+            const int l = SC_RUN_LEVELS + (int)(v / ud);
+            const int64_t s0 = (v - (l - SC_RUN_LEVELS) * ud) * (SC_THREADS * C_DIR), s1 = min(n, s0 + SC_THREADS * C_DIR);
+            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * n_stride, nrm, Lt, grad);
         }
-        // runs of lanes in the same base cell, merged with DPP suffix sums inside each 16-lane row
-        // (an inactive lane gets a key nobody else has).  Coarse levels only: from level
-        // SC_MERGE_LEVELS on most lanes head their own run and the merge would cost more VALU
-        // than the LDS traffic it saves.
-        bool head = valid;
-        float v0[8], v1[8];
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
-            v0[c] = valid ? w * gv.x : 0.f;
-            v1[c] = valid ? w * gv.y : 0.f;
-        }
-        if (l < SC_MERGE_LEVELS) {
-            const int key = valid ? (int)(p.px + res * (p.py + res * p.pz)) : (int)(0xFFFFFFF0u - (uint32_t)r);
-            const int key_next = dppi<DPP_ROW_SL(1)>(key);
-            const int key_prev = dppi<DPP_ROW_SR(1)>(key);
-            int link[4];
-            link[0] = (r < 15) && (key_next == key);
-            link[1] = link[0] && dppi<DPP_ROW_SL(1)>(link[0]);
-            link[2] = link[1] && dppi<DPP_ROW_SL(2)>(link[1]);
-            link[3] = link[2] && dppi<DPP_ROW_SL(4)>(link[2]);
-            head = valid && (r == 0 || key_prev != key);
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                run_sum<0>(v0[c], link); run_sum<0>(v1[c], link);
-                run_sum<1>(v0[c], link); run_sum<1>(v1[c], link);
-                run_sum<2>(v0[c], link); run_sum<2>(v1[c], link);
-                run_sum<3>(v0[c], link); run_sum<3>(v1[c], link);
-            }
-        }
-        uint32_t newmask = 0;  // corners whose slot this lane claimed
-        int slot[8];
-        if (head && direct) {
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                atomicAdd(grad + 2 * (size_t)(off + e[c]), v0[c]);
-                atomicAdd(grad + 2 * (size_t)(off + e[c]) + 1, v1[c]);
-            }
-        }
-        SC_T(t1);
-        if (head && !direct) {
-            uint4 kk[8];
-#pragma unroll
-            for (int c = 0; c < 8; c++) kk[c] = *(const uint4*)&keys[SC_WAYS * sc_set(e[c])];
-            int claim[8];
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                const int p0 = SC_WAYS * sc_set(e[c]);
-                const uint32_t k0 = kk[c].x, k1 = kk[c].y, k2 = kk[c].z, k3 = kk[c].w;
-                slot[c] = k0 == e[c] ? p0 : k1 == e[c] ? p0 + 1 : k2 == e[c] ? p0 + 2 : k3 == e[c] ? p0 + 3 : -1;
-                // claim the first way of the set seen empty
-                claim[c] = slot[c] >= 0 ? -1
-                         : k0 == SC_EMPTY ? p0 : k1 == SC_EMPTY ? p0 + 1 : k2 == SC_EMPTY ? p0 + 2
-                         : k3 == SC_EMPTY ? p0 + 3 : -1;
-            }
-            uint32_t got[8];
-#pragma unroll
-            for (int c = 0; c < 8; c++) got[c] = claim[c] >= 0 ? atomicCAS(&keys[claim[c]], SC_EMPTY, e[c]) : 0u;
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                if (claim[c] >= 0) {
-                    if (got[c] == SC_EMPTY) { slot[c] = claim[c]; newmask |= 1u << c; }
-                    else if (got[c] == e[c]) slot[c] = claim[c];
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                if (slot[c] >= 0) {
-                    atomicAdd((unsigned long long*)&valx[slot[c]], (unsigned long long)sc_fix(v0[c], k));
-                    atomicAdd((unsigned long long*)&valy[slot[c]], (unsigned long long)sc_fix(v1[c], k));
-                } else {
-#ifdef NCN_DIAG_SC_NO_FALLBACK
-                    if (v0[c] == 1234.5f) grad[c] = v1[c];
-#else
-                    atomicAdd(grad + 2 * (size_t)(off + e[c]), v0[c]);
-                    atomicAdd(grad + 2 * (size_t)(off + e[c]) + 1, v1[c]);
-#endif
-                }
-            }
-        }
-        SC_T(t2);
-        {   // append the claimed slots to `used`: one LDS atomic per wave
-            const int mine = __builtin_popcount(newmask);
-            const float incl = wave_incl_sum_dpp((float)mine);
-            const int wtot = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
-            int base = 0;
-            if (wtot) {
-                if (lane == 0) base = atomicAdd(&fill, wtot);
-                base = __builtin_amdgcn_readfirstlane(base);
-                int pos = base + (int)incl - mine;
-#pragma unroll
-                for (int c = 0; c < 8; c++)
-                    if (newmask & (1u << c)) used[pos++] = (uint16_t)slot[c];
-            }
-        }
-        __syncthreads();
-        SC_T(t3);
-        if (ch == nchunk - 1 || fill > SC_TS / SC_FLUSH_FRAC) sc_flush(keys, valx, valy, used, &fill, grad, off, k);
-        SC_T(t4);
-        SC_ACC(0, t0, t1);
-        SC_ACC(1, t1, t2);
-        SC_ACC(2, t2, t3);
-        SC_ACC(3, t3, t4);
-    }
-#ifdef NCN_DIAG_PHASES
-    if (threadIdx.x == 0 && blockIdx.x == 7)
-        for (int i = 0; i < 4; i++) ncn_sc_phase[i] = ph[i];
-#endif
-    __syncthreads();  // lmax / wmax are rewritten by the next span
     }
 }
 
 static int scatter_grid(int64_t n_cap) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(256, (n_cap + 1023) / 1024));  // one per CU
+    return (int)std::max<int64_t>(1, std::min<int64_t>(256, (n_cap + 255) / 256));  // one per CU
 }
 
 static LevelTable make_table(const uint32_t* levels) {
@@ -917,8 +1020,8 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
 
 int ncn_field_bwd_blocks(int64_t n) {
     const int64_t groups = (n + 15) / 16;
-    // 2 workgroups per CU on 256 CUs; at least ~4 groups per wave
-    return (int)std::max<int64_t>(1, std::min<int64_t>(512, (groups + 15) / 16));
+    // one 8-wave workgroup per CU on 256 CUs; at least ~4 steps of 8 groups each
+    return (int)std::max<int64_t>(1, std::min<int64_t>(256, (groups + 31) / 32));
 }
 
 int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * n : 0; }
@@ -941,11 +1044,6 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
     return 0;
 }
 
-#ifdef NCN_DIAG_PHASES
-int ncn_diag_read_phases(unsigned long long* host) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_phase), 8 * sizeof(unsigned long long));
-}
-#endif
 
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream) {
     if (n_blocks <= 0) return 0;

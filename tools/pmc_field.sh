@@ -1,8 +1,8 @@
 #!/bin/bash
-# PMC passes over tools/field_probe.py, one counter group per pass
+# PMC passes over tools/field_probe.py, one counter group per pass (summarise: tools/pmc_summary.py)
 export TMPDIR=/tmp
 i=0
-for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"; do
+for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES" "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY" "TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum"; do
   i=$((i+1))
-  timeout -k 10 200 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_sc/p$i -o p -- python3 tools/field_probe.py > gpurun_out/pmc_sc_$i.log 2>&1 || exit $?
+  timeout -k 10 200 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_field/p$i -o p -- python3 tools/field_probe.py > gpurun_out/pmc_field_$i.log 2>&1 || exit $?
 done
