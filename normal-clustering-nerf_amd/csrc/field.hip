@@ -504,7 +504,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const half4_t* __restrict__ wpacked,
     const half4_t* __restrict__ enc_cache, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
     float* __restrict__ dE_out, float* __restrict__ slab) {
-    const int64_t n_stride = n;  // dE layout [16][n_stride]
+    const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     if (n_dev) n = min<int64_t>(n, *n_dev);
     __shared__ half4_t F[N_FRAGS * 64];                    // 38.9 KB weight fragments
     __shared__ __attribute__((aligned(16))) _Float16 X[BWD_WAVES * N_XFRAG * 256];  // 120 KB dW operand images
@@ -603,9 +603,11 @@ __device__ __forceinline__ long long sc_fix(float v, int k) {
 // levels 0-9: 8 samples per lane with run records (unit = 8192 samples); levels 10-15 (cells
 // shorter than ~2 steps, runs rarely longer than one sample): 2 samples per lane, each added
 // directly (unit = 2048 samples)
-constexpr int SC_RUN_LEVELS = 10;
+#ifndef SC_RUN_LEVELS
+#define SC_RUN_LEVELS 10
+#endif
 #ifndef SC_C_RUN
-#define SC_C_RUN 6  // samples per lane on the run levels (unit = 1024 * SC_C_RUN samples)
+#define SC_C_RUN 4  // samples per lane on the run levels (unit = 1024 * SC_C_RUN samples)
 #endif
 
 struct ScRec {
@@ -790,19 +792,58 @@ struct ScChunk {
     float x[C], y[C], z[C];
     float2 g[C];
 };
+// C is 2 or 4 and the lane's first sample sb a multiple of C: the chunk's xyz (12C bytes) and dE
+// (8C bytes) are 16-B (C = 4) / 8-B (C = 2) aligned pieces, loaded with dwordx4 / dwordx2 — a lane
+// reads contiguous bytes, so fewer, wider load instructions (the lane-strided pattern costs TA
+// cycles per touched cache line).  A partial last chunk falls back to per-sample loads.
 template <int C>
 __device__ __forceinline__ float sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
                                                const float2* __restrict__ dEl, const ScNorm& nrm) {
+    static_assert(C == 2 || C == 4, "chunk of 2 or 4 samples");
+    float xs[3 * C];
+    if (sb + C <= s1) {
+        if constexpr (C == 4) {
+            const float4* px = (const float4*)(xyzs + 3 * sb);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const float4 v = px[q];
+                xs[4 * q] = v.x; xs[4 * q + 1] = v.y; xs[4 * q + 2] = v.z; xs[4 * q + 3] = v.w;
+            }
+            const float4* pg = (const float4*)(dEl + sb);
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const float4 v = pg[q];
+                ch.g[2 * q] = make_float2(v.x, v.y);
+                ch.g[2 * q + 1] = make_float2(v.z, v.w);
+            }
+        } else {
+            const float2* px = (const float2*)(xyzs + 3 * sb);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const float2 v = px[q];
+                xs[2 * q] = v.x; xs[2 * q + 1] = v.y;
+            }
+            const float4 v = *(const float4*)(dEl + sb);
+            ch.g[0] = make_float2(v.x, v.y);
+            ch.g[1] = make_float2(v.z, v.w);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            const bool in = sb + i < s1;
+            const int64_t sc = in ? sb + i : 0;
+            ch.g[i] = in ? dEl[sc] : make_float2(0.f, 0.f);
+            xs[3 * i] = in ? xyzs[3 * sc] : 0.f;
+            xs[3 * i + 1] = in ? xyzs[3 * sc + 1] : 0.f;
+            xs[3 * i + 2] = in ? xyzs[3 * sc + 2] : 0.f;
+        }
+    }
     float m = 0.f;  // max |dE| (INFINITY if not finite)
 #pragma unroll
     for (int i = 0; i < C; i++) {
-        const int64_t s = sb + i;
-        const bool in = s < s1;
-        const int64_t sc = in ? s : sb;  // (sb < s1 whenever any sample is in range)
-        ch.g[i] = in ? dEl[sc] : make_float2(0.f, 0.f);
-        ch.x[i] = in ? nrm(xyzs[3 * sc]) : 0.f;
-        ch.y[i] = in ? nrm(xyzs[3 * sc + 1]) : 0.f;
-        ch.z[i] = in ? nrm(xyzs[3 * sc + 2]) : 0.f;
+        ch.x[i] = nrm(xs[3 * i]);
+        ch.y[i] = nrm(xs[3 * i + 1]);
+        ch.z[i] = nrm(xs[3 * i + 2]);
         const float a = fmaxf(fabsf(ch.g[i].x), fabsf(ch.g[i].y));
         m = (isfinite(ch.g[i].x) && isfinite(ch.g[i].y)) ? fmaxf(m, a) : INFINITY;
     }
@@ -858,10 +899,19 @@ __device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<
 }
 
 // One unit: load the chunk, the unit's fixed-point scale (block max), phase A/B or direct, flush.
+#ifdef NCN_DIAG_SC_TIMES
+__device__ unsigned long long ncn_sc_times[256][8];  // per workgroup, wave 0: cycles per phase x {run, dir}
+#define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
+#define SC_TADD(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2 + (RUNS ? 0 : 1)] += (b) - (a)
+#else
+#define SC_TNOW(v)
+#define SC_TADD(i, a, b)
+#endif
 template <int C, bool RUNS>
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const float2* __restrict__ dEl,
                                         const ScNorm& nrm, const LevelTable& Lt, float* __restrict__ grad) {
+    SC_TNOW(t0);
     ScChunk<C> ch;
     float m = sc_load_chunk<C>(ch, s0 + (int64_t)threadIdx.x * C, s1, xyzs, dEl, nrm);
 #pragma unroll
@@ -888,6 +938,7 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
     L.k = 46 - e2;
+    SC_TNOW(t1);
     if (RUNS) {
         int staged = 0;
         sc_phase_a<C>(sh, wid, lane, ch, L, grad, staged);
@@ -895,7 +946,9 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     } else {
         sc_direct<C>(sh, lane, ch, L, grad);
     }
+    SC_TNOW(t2);
     lds_barrier();
+    SC_TNOW(t3);
     // flush: the claimed slots, two lanes per slot (x and y of one entry are adjacent floats)
     const int nf = *sh.fill;
     for (int i = threadIdx.x; i < 2 * nf; i += SC_THREADS) {
@@ -915,6 +968,11 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     }
     if (threadIdx.x == 0) *sh.fill = 0;
     lds_barrier();
+    SC_TNOW(t4);
+    SC_TADD(0, t0, t1);
+    SC_TADD(1, t1, t2);
+    SC_TADD(2, t2, t3);
+    SC_TADD(3, t3, t4);
 }
 
 __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
@@ -927,6 +985,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     __shared__ int fill;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
+    const int64_t e_stride = (n_stride + 3) & ~(int64_t)3;  // dE row stride (as written by field_bwd)
     ScNorm nrm;
     nrm.mn = xyz_min;
     nrm.ext = xyz_extent;
@@ -958,12 +1017,12 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         if (run) {
             const int l = (int)(u / ur);
             const int64_t s0 = (u - l * ur) * (SC_THREADS * C_RUN), s1 = min(n, s0 + SC_THREADS * C_RUN);
-            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * n_stride, nrm, Lt, grad);
+            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, grad);
         } else {
             const int64_t v = u - SC_RUN_LEVELS * ur;
             const int l = SC_RUN_LEVELS + (int)(v / ud);
             const int64_t s0 = (v - (l - SC_RUN_LEVELS) * ud) * (SC_THREADS * C_DIR), s1 = min(n, s0 + SC_THREADS * C_DIR);
-            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * n_stride, nrm, Lt, grad);
+            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, grad);
         }
     }
 }
@@ -1024,7 +1083,7 @@ int ncn_field_bwd_blocks(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(256, (groups + 31) / 32));
 }
 
-int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * n : 0; }
+int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(int64_t)3) : 0; }
 
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
                   float xyz_min,
@@ -1032,7 +1091,8 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
                   void* stream) {
     if (n <= 0) return 0;
-    NCN_REQUIRE(((uintptr_t)dE_ws & 7) == 0, hipErrorInvalidValue, "ncn_field_bwd: dE_ws must be 8-byte aligned");
+    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
+                "ncn_field_bwd: dE_ws and xyzs must be 16-byte aligned");
     const LevelTable Lt = make_table(levels);
     hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
                        dirs, n, n_dev, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas,
@@ -1044,6 +1104,16 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
     return 0;
 }
 
+
+#ifdef NCN_DIAG_SC_TIMES
+int ncn_diag_sc_times(unsigned long long* host, int reset) {
+    if (reset) {
+        static unsigned long long zero[256][8];
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(ncn_sc_times), zero, sizeof(zero));
+    }
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_times), 256 * 8 * sizeof(unsigned long long));
+}
+#endif
 
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream) {
     if (n_blocks <= 0) return 0;

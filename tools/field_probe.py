@@ -55,7 +55,7 @@ drgb = torch.randn(n, 3, device=dev, generator=gen) * 1e-3
 gtab = torch.zeros_like(table)
 nb = main.ncn_field_bwd_blocks(I64(n))
 slab = torch.empty(nb * 19712, device=dev)
-dE_ws = torch.empty(32 * n, device=dev)
+dE_ws = torch.empty(int(main.ncn_field_bwd_dE_floats(I64(n))), device=dev)
 
 
 def bwd(lib):
@@ -98,6 +98,16 @@ for name, L in libs:
         relb = ((g1 - gref)[big].abs() / gref[big].abs()).max().item()
         print(f"   table-grad vs main: rel-L2 {rel:.3e}, max rel on entries > 1e-3 max: {relb:.3e}")
     print(f"{name:16s} fwd {timeit(fwd, L):8.1f} us   bwd {timeit(bwd, L):8.1f} us", flush=True)
+    if hasattr(L, "ncn_diag_sc_times"):
+        buf = (ctypes.c_ulonglong * (256 * 8))()
+        L.ncn_diag_sc_times(buf, 1)
+        assert bwd(L) == 0
+        torch.cuda.synchronize()
+        L.ncn_diag_sc_times(buf, 0)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8).astype(np.float64)
+        names = ["load+max", "work", "barrier", "flush"]
+        print("   scatter cycles per WG (mean over WGs), run | direct:",
+              "  ".join(f"{nm} {a[:, 2 * i].mean():.0f}|{a[:, 2 * i + 1].mean():.0f}" for i, nm in enumerate(names)))
     if hasattr(L, "ncn_diag_read_phases"):
         buf = (ctypes.c_ulonglong * 8)()
         L.ncn_diag_read_phases(buf)
