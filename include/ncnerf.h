@@ -189,6 +189,15 @@ int ncn_sumsq(const float* x, int64_t n, float* out_partial /* >= 1024 floats */
 int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
              const float* sumsq_partial, float max_norm, float lr, float beta1, float beta2, float eps,
              float weight_decay, int step, const float* lr_dev, const int* step_dev, void* stream);
+/* The whole step in two launches (sum of squares whose last workgroup forms the clip factor and
+ * step scalars, then Adam of both groups): elements [0, n_group0) use weight decay wd0 (apex group
+ * 0, the hash grid), the rest wd1.  step_dev is incremented (device step counter) and drives the
+ * bias corrections; work holds ncn_adam_step_work_floats() floats, zero before the first call (its
+ * arrival counter is left zero by every call).  Buffers 16-byte aligned. */
+int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+                  float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
+                  const float* lr_dev, int* step_dev, float* work, void* stream);
+int64_t ncn_adam_step_work_floats(void);
 
 #ifdef __cplusplus
 }

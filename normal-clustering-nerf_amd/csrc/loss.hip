@@ -213,8 +213,14 @@ __global__ void nerf_loss_bwd_kernel(const float* __restrict__ rgb, const float*
 // bit-identical centroids/statistics and the result is run-to-run deterministic.
 constexpr int CL_MAX_TRI = 16384;
 constexpr int NCN_MAX_NQ = 80;       // K * 4 at K = 20
-constexpr int KM_THREADS = 256;      // multi-workgroup kernels
-constexpr int KM_BLOCKS = 32;
+#ifndef KM_THREADS_CFG
+#define KM_THREADS_CFG 256
+#endif
+#ifndef KM_BLOCKS_CFG
+#define KM_BLOCKS_CFG 32
+#endif
+constexpr int KM_THREADS = KM_THREADS_CFG;  // threads per workgroup of the clustering kernel
+constexpr int KM_BLOCKS = KM_BLOCKS_CFG;    // co-resident workgroups (grid barriers)
 constexpr int KM_CHUNK_MAX = CL_MAX_TRI / KM_BLOCKS;
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

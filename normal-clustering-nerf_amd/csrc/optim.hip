@@ -57,17 +57,114 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
         bc1 = 1.0f - powf(b1, st);
         bc2 = 1.0f - powf(b2, st);
     }
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const float gi = g[i] * cf;
-        const float mi = b1 * m[i] + (1.f - b1) * gi;
-        const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-        m[i] = mi;
-        v[i] = vi;
+    auto upd = [&](float& pi, float gr, float& mi, float& vi) {
+        const float gi = gr * cf;
+        mi = b1 * mi + (1.f - b1) * gi;
+        vi = b2 * vi + (1.f - b2) * gi * gi;
         const float denom = sqrtf(vi / bc2) + eps;
-        p[i] = p[i] - lr * ((mi / bc1) / denom + wd * p[i]);
+        pi = pi - lr * ((mi / bc1) / denom + wd * pi);
+    };
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+    const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+    const int64_t n4 = vec ? n / 4 : 0;
+    for (int64_t i = tid; i < n4; i += nth) {  // 16-B accesses: 28 B/param at full width
+        float4 P = ((float4*)p)[i], M = ((float4*)m)[i], V = ((float4*)v)[i];
+        const float4 G = ((const float4*)g)[i];
+        upd(P.x, G.x, M.x, V.x);
+        upd(P.y, G.y, M.y, V.y);
+        upd(P.z, G.z, M.z, V.z);
+        upd(P.w, G.w, M.w, V.w);
+        ((float4*)p)[i] = P;
+        ((float4*)m)[i] = M;
+        ((float4*)v)[i] = V;
     }
+    for (int64_t i = 4 * n4 + tid; i < n; i += nth) upd(p[i], g[i], m[i], v[i]);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The optimizer step in two launches (train_nerf.py:262-285 + 955):
+//  1. adam_prep_kernel: per-workgroup sums of squares of the gradient; the LAST workgroup to finish
+//     (arrival counter) adds the partials in a fixed order and writes the step's scalars — clip
+//     factor, bias corrections of the incremented device step, lr — then resets the counter;
+//  2. adam_apply_kernel: Adam of both groups (index < n_group0: weight decay wd0, else wd1) with
+//     16-B accesses, reading the four scalars.
+// Replaces sumsq + one Adam launch per group (each of whose workgroups re-summed the partials).
+constexpr int ADAM_BLOCKS = 1024;
+__global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float max_norm,
+                                                        float b1, float b2, float lr, const float* __restrict__ lr_dev,
+                                                        int* __restrict__ step_dev, float* __restrict__ work) {
+    float* part = work;                                // [ADAM_BLOCKS]
+    unsigned* cnt = (unsigned*)(work + ADAM_BLOCKS);   // arrival counter (left zero)
+    float* sc = work + ADAM_BLOCKS + 4;                // cf, bc1, bc2, lr
+    __shared__ float red[4];
+    __shared__ bool last;
+    const int64_t n4 = n / 4;
+    const float4* g4 = (const float4*)g;
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 x = g4[i];
+        s = fmaf(x.x, x.x, s); s = fmaf(x.y, x.y, s); s = fmaf(x.z, x.z, s); s = fmaf(x.w, x.w, s);
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) s = fmaf(g[i], g[i], s);
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    // hand-off with agent-scope (sc1) accesses only (MI355X_MICROARCH.md inter-workgroup visibility):
+    // store the partial, wait for it, then one arrival add.  No __threadfence(): a device-scope
+    // release writes the L2 back, which right after the table-gradient scatter costs ~40 us.
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&part[blockIdx.x], red[0] + red[1] + red[2] + red[3], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x < 64) {
+        float t = 0.f;
+        for (int i = threadIdx.x; i < (int)gridDim.x; i += 64)
+            t += __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = wave_sum(t);
+        if (threadIdx.x == 0) {
+            const float c = max_norm / (sqrtf(t) + 1e-6f);
+            const int st = *step_dev + 1;  // device step counter
+            *step_dev = st;
+            sc[0] = max_norm > 0.f ? fminf(c, 1.0f) : 1.0f;
+            sc[1] = 1.0f - powf(b1, (float)st);
+            sc[2] = 1.0f - powf(b2, (float)st);
+            sc[3] = lr_dev ? *lr_dev : lr;
+            *cnt = 0u;
+        }
+    }
+}
+__global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                         int64_t n0, float b1, float b2, float eps, float wd0,
+                                                         float wd1, const float* __restrict__ sc) {
+    const float cf = sc[0], bc1 = sc[1], bc2 = sc[2], lr = sc[3];
+    auto upd = [&](float& pi, float gr, float& mi, float& vi, float wd) {
+        const float gi = gr * cf;
+        mi = b1 * mi + (1.f - b1) * gi;
+        vi = b2 * vi + (1.f - b2) * gi * gi;
+        const float denom = sqrtf(vi / bc2) + eps;
+        pi = pi - lr * ((mi / bc1) / denom + wd * pi);
+    };
+    const int64_t n4 = n / 4, tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+    for (int64_t i = tid; i < n4; i += nth) {
+        float4 P = ((float4*)p)[i], M = ((float4*)m)[i], V = ((float4*)v)[i];
+        const float4 G = ((const float4*)g)[i];
+        const int64_t e = 4 * i;
+        upd(P.x, G.x, M.x, V.x, e < n0 ? wd0 : wd1);
+        upd(P.y, G.y, M.y, V.y, e + 1 < n0 ? wd0 : wd1);
+        upd(P.z, G.z, M.z, V.z, e + 2 < n0 ? wd0 : wd1);
+        upd(P.w, G.w, M.w, V.w, e + 3 < n0 ? wd0 : wd1);
+        ((float4*)p)[i] = P;
+        ((float4*)m)[i] = M;
+        ((float4*)v)[i] = V;
+    }
+    for (int64_t i = 4 * n4 + tid; i < n; i += nth) upd(p[i], g[i], m[i], v[i], i < n0 ? wd0 : wd1);
+}
 }  // namespace ncn
 
 using namespace ncn;
@@ -87,12 +184,32 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
     if (n <= 0) return 0;
     NCN_REQUIRE(step >= 1 || step_dev, hipErrorInvalidValue, "ncn_adam: step must be >= 1");
     const float bc1 = 1.0f - powf(beta1, (float)std::max(step, 1)), bc2 = 1.0f - powf(beta2, (float)std::max(step, 1));
-    const int blocks = (int)std::min<int64_t>(cdiv(n, 256), 2048);
+    const int blocks = (int)std::min<int64_t>(cdiv(n, 1024), 2048);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, sumsq_partial, max_norm, lr, beta1, beta2, eps, weight_decay, bc1, bc2, lr_dev,
                        step_dev);
     NCN_LAUNCH_CHECK("ncn_adam");
     return 0;
 }
+
+int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+                  float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
+                  const float* lr_dev, int* step_dev, float* work, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
+                hipErrorInvalidValue, "ncn_adam_step: buffers must be 16-byte aligned");
+    NCN_REQUIRE(step_dev != nullptr && work != nullptr, hipErrorInvalidValue,
+                "ncn_adam_step: needs the device step counter and the work buffer");
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(ADAM_BLOCKS), dim3(256), 0, (hipStream_t)stream, grads, n, max_norm,
+                       beta1, beta2, lr, lr_dev, step_dev, work);
+    NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
+    const int blocks = (int)std::min<int64_t>(cdiv(n, 1024), 2048);
+    hipLaunchKernelGGL(adam_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
+                       exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
+    NCN_LAUNCH_CHECK("ncn_adam_step");
+    return 0;
+}
+
+int64_t ncn_adam_step_work_floats(void) { return ADAM_BLOCKS + 8; }
 
 }  // extern "C"

@@ -49,6 +49,8 @@ SIGNATURES = {
     "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
+    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F32, F32, F32, F32, P, P, P, P],
+    "ncn_adam_step_work_floats": [],
 }
 
 _lib = None
@@ -80,6 +82,7 @@ def lib():
             fn.restype = ctypes.c_int
         L.ncn_cluster_workspace_words.restype = ctypes.c_int64
         L.ncn_field_bwd_dE_floats.restype = ctypes.c_int64
+        L.ncn_adam_step_work_floats.restype = ctypes.c_int64
         L.ncn_last_error.argtypes = []
         L.ncn_last_error.restype = ctypes.c_char_p
         L.ncn_version.restype = ctypes.c_int

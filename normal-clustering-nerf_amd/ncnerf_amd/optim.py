@@ -2,13 +2,15 @@
 
 Reference: apex FusedAdam (AdamW mode, eps 1e-15) with two groups — hash-grid features (weight
 decay 0) and MLP weights (weight decay 1e-6) — (train_nerf.py:262-285), gradient clipping by global
-L2 norm 0.05 (train_nerf.py:955), CosineAnnealingLR over epochs (:286-288).  One sum-of-squares
-kernel + one Adam kernel per group; the clip factor never leaves the device.
+L2 norm 0.05 (train_nerf.py:955), CosineAnnealingLR over epochs (:286-288).  One launch per step
+(ncn_adam_step: sum of squares, grid barrier, Adam of both groups); the clip factor never leaves
+the device.
 """
 import math
 
 import torch
 
+from . import _lib
 from ._lib import F32, I32, I64, call, ptr, stream
 
 
@@ -22,6 +24,7 @@ class FlatAdam:
         self.m = torch.zeros_like(flat)
         self.v = torch.zeros_like(flat)
         self.part = torch.empty(1024, dtype=torch.float32, device=flat.device)
+        self.work = torch.zeros(int(_lib.lib().ncn_adam_step_work_floats()), dtype=torch.float32, device=flat.device)
         self.step_count = 0
         # device-side step counter and learning rate: the step kernels read them, so the optimizer
         # step can sit inside a captured HIP graph (the counter is bumped by the sum-of-squares kernel)
@@ -43,13 +46,10 @@ class FlatAdam:
         self.step_count += 1
         p = self.model.flat_params()
         g = self.model.flat_grad()
-        s = stream()
-        call("ncn_sumsq", ptr(g), I64(g.numel()), ptr(self.part), ptr(self.step_dev), s)
         b1, b2 = self.betas
-        for lo, hi, wd in ((0, self.n_table, self.wd[0]), (self.n_table, p.numel(), self.wd[1])):
-            call("ncn_adam", ptr(p[lo:hi]), ptr(g[lo:hi]), ptr(self.m[lo:hi]), ptr(self.v[lo:hi]), I64(hi - lo),
-                 ptr(self.part), F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(wd),
-                 I32(self.step_count), ptr(self.lr_dev), ptr(self.step_dev), s)
+        call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
+             F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
+             ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), stream())
 
     def state_tensors(self):
         """Every tensor the step mutates (parameters, moments, device counters)."""

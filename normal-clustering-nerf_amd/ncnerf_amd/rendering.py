@@ -8,7 +8,9 @@ output dict, including the reference quirks that downstream losses depend on:
 Removed: the dead `(rays_a[:,2]==0).any()` host sync (rendering.py:195-196).
 Extensions (not in the reference): kwargs['march_noise'] injects the marcher noise (test hook);
 kwargs['static_shapes']=True keeps every shape independent of the marched sample count (no host
-read of the counter), which is what lets Trainer capture the whole step in one HIP graph.
+read of the counter), which is what lets Trainer capture the whole step in one HIP graph;
+kwargs['premarched'] (a march_train_static() result) skips intersect + march: the pipelined step
+marches the next batch while the current one is rendered.
 """
 import torch
 from einops import rearrange
@@ -23,6 +25,8 @@ def render(model, rays_o, rays_d, **kwargs):
     near_distance = kwargs["near_distance"]
     rays_o = rays_o.contiguous()
     rays_d = rays_d.contiguous()
+    if kwargs.get("premarched") is not None and not kwargs.get("test_time", False):
+        return render_rays_train(model, rays_o, rays_d, None, **kwargs)
     # RayAABBIntersector (no gradient) + the near clamp of rendering.py:28 in one kernel
     _, hits_t, _ = vren.ray_aabb_intersect(rays_o.float(), rays_d.float(), model.center, model.half_size, 1,
                                            near_distance=near_distance)
@@ -124,11 +128,17 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     if hasattr(model, "prepare_weights"):
         model.prepare_weights()  # queue the fp16 weight packing ahead of the marcher's host read of S
     static = bool(kwargs.get("static_shapes", False))
-    rays_a, xyzs, dirs, results["deltas"], results["ts"], results["rm_samples"] = RayMarcher.apply(
-        rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
-        model.grid_size, max_samples, kwargs.get("march_noise"), static)
+    pm = kwargs.get("premarched")
+    if pm is not None:  # marched ahead (march_train_static): same tensors RayMarcher would return
+        static = True
+        rays_a, xyzs, dirs, results["deltas"], results["ts"], results["rm_samples"] = (
+            pm["rays_a"], pm["xyzs"], pm["dirs"], pm["deltas"], pm["ts"], pm["counter"][0])
+    else:
+        rays_a, xyzs, dirs, results["deltas"], results["ts"], results["rm_samples"] = RayMarcher.apply(
+            rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
+            model.grid_size, max_samples, kwargs.get("march_noise"), static)
     for k, v in list(kwargs.items()):  # rendering.py:198-200
-        if isinstance(v, torch.Tensor) and k not in ("march_noise",):
+        if isinstance(v, torch.Tensor) and k not in ("march_noise", "premarched"):
             if static:
                 raise NotImplementedError(f"per-ray tensor kwarg {k!r} on the static-shape path")
             kwargs[k] = torch.repeat_interleave(v[rays_a[:, 0]], rays_a[:, 2], 0)
@@ -158,7 +168,7 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     results["rays_d"] = rays_d
     results["rays_o"] = rays_d  # rendering.py:227 (quirk q1)
     results["rays_a"] = rays_a
-    results["depth_std"] = torch.ones_like(results["depth"], requires_grad=False)
+    results["depth_std"] = _ones(results["depth"])  # rendering.py:230 (constant: cached, no fill per call)
     if exp_step_factor == 0:  # white: rgb + 1 * (1 - opacity), fused into the compositor when rgb-only
         if not fuse_bg:
             results["rgb"] = results["rgb"] + (1 - results["opacity"])[:, None]
@@ -169,3 +179,37 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
         rgb_bg = torch.zeros(3, device=rays_o.device)
     results["rgb"] = results["rgb"] + rgb_bg * rearrange(1 - results["opacity"], "n -> n 1")
     return results
+
+
+_ONES = {}
+
+
+def _ones(like):
+    """A cached all-ones tensor shaped like `like` (read-only by convention)."""
+    key = (tuple(like.shape), like.dtype, like.device)
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones(like.shape, dtype=like.dtype, device=like.device)
+    return t
+
+
+@torch.no_grad()
+def march_train_static(model, rays_o, rays_d, out=None, **kwargs):
+    """The intersect + march part of render_rays_train on the static-shape path (rendering.py:24-28,
+    190-197) as a standalone stage: returns {'rays_a', 'xyzs', 'dirs', 'deltas', 'ts', 'counter'}
+    (capacity-sized sample arrays, device count in counter[0]) for render(..., premarched=...).
+    out: a previous result whose tensors are overwritten in place (fixed buffers for graphs)."""
+    exp_step_factor = kwargs.get("exp_step_factor", 0.0)
+    rays_o = rays_o.contiguous().float()
+    rays_d = rays_d.contiguous().float()
+    _, hits_t, _ = vren.ray_aabb_intersect(rays_o, rays_d, model.center, model.half_size, 1,
+                                           near_distance=kwargs["near_distance"])
+    noise = kwargs.get("march_noise")
+    if noise is None:
+        noise = torch.rand_like(rays_o[:, 0])  # custom_functions.py:83
+    keys = ("rays_a", "xyzs", "dirs", "deltas", "ts", "counter")
+    res = vren.raymarching_train(rays_o, rays_d, hits_t[:, 0].contiguous(), model.density_bitfield, model.cascades,
+                                 model.scale, exp_step_factor, noise.contiguous(), model.grid_size,
+                                 kwargs["max_samples"], static_capacity=True,
+                                 out=None if out is None else [out[k] for k in keys])
+    return dict(zip(keys, res))

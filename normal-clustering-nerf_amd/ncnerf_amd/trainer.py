@@ -58,7 +58,10 @@ class Trainer:
             kw["march_noise"] = batch["march_noise"]
         results = render(m, batch["rays_o"], batch["rays_d"], **kw)
         loss_d = self.loss(results, batch, global_step=step_dev)
-        loss_d["total"].backward()
+        total = loss_d["total"]
+        if getattr(self, "_one", None) is None or self._one.device != total.device:
+            self._one = torch.ones((), dtype=total.dtype, device=total.device)
+        torch.autograd.backward(total, grad_tensors=self._one)  # (no ones_like fill node per step)
         if with_opt:
             self.opt.step()
         return results, loss_d
@@ -90,9 +93,13 @@ class Trainer:
     def _graph_step(self, batch, global_step):
         if self.graph is None:
             self._capture(batch)
+        dst, src = [], []
         for k, v in batch.items():
             if k in self._static and hasattr(v, "copy_") and v is not self._static[k]:
-                self._static[k].copy_(v, non_blocking=True)
+                dst.append(self._static[k])
+                src.append(v)
+        if dst:
+            torch._foreach_copy_(dst, src, non_blocking=True)  # one launch for the whole batch
         self._step_dev.fill_(global_step)
         self.graph.replay()
         if not self._with_opt:

@@ -74,13 +74,14 @@ def packbits(density_grid, density_threshold, density_bitfield):
 
 
 def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, noise,
-                      grid_size, max_samples, static_capacity=False):
+                      grid_size, max_samples, static_capacity=False, out=None):
     """raymarching.cu:283-332 -> [rays_a i64 (R,3), xyzs (S,3), dirs (S,3), deltas (S), ts (S), counter i32 (2)].
 
     Walk -> scan -> (read S, the reference's own sync point custom_functions.py:91) -> pack.
     static_capacity=True (extension): the host never reads S; the sample arrays have the capacity
     R*max_samples, rows >= counter[0] are unspecified, and consumers take counter[0:1] as the
-    device-resident count (the graph-captured training step)."""
+    device-resident count (the graph-captured training step).  out (static_capacity only): the six
+    output tensors to write instead of allocating them (the pipelined step's fixed buffers)."""
     for t, n in ((rays_o, "rays_o"), (rays_d, "rays_d"), (hits_t, "hits_t"), (density_bitfield, "density_bitfield"),
                  (noise, "noise")):
         check_input(t, n)
@@ -92,17 +93,24 @@ def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
     slab_xyz = torch.empty(R * ms * 3, dtype=torch.float32, device=dev)
     slab_t = torch.empty(R * ms, dtype=torch.float32, device=dev)
     slab_dt = torch.empty(R * ms, dtype=torch.float32, device=dev)
-    rays_a = torch.empty(R, 3, dtype=torch.int64, device=dev)
-    counter = torch.empty(2, dtype=torch.int32, device=dev)
+    if out is not None and not static_capacity:
+        raise ValueError("out= needs static_capacity=True")
+    rays_a = out[0] if out is not None else torch.empty(R, 3, dtype=torch.int64, device=dev)
+    counter = out[5] if out is not None else torch.empty(2, dtype=torch.int32, device=dev)
     call("ncn_march_train_walk", ptr(rays_o), ptr(rays_d), ptr(hits_t), ptr(noise), I64(R), ptr(density_bitfield),
          I32(int(cascades)), F32(float(scale)), F32(float(exp_step_factor)), I32(int(grid_size)), I32(ms),
          ptr(counts), ptr(slab_xyz), ptr(slab_t), ptr(slab_dt), s)
     call("ncn_march_train_scan", ptr(counts), I64(R), ptr(rays_a), ptr(counter), s)
     S = R * ms if static_capacity else int(counter[0].item())
-    xyzs = torch.empty(S, 3, dtype=torch.float32, device=dev)
-    dirs = torch.empty(S, 3, dtype=torch.float32, device=dev)
-    deltas = torch.empty(S, dtype=torch.float32, device=dev)
-    ts = torch.empty(S, dtype=torch.float32, device=dev)
+    if out is not None:
+        xyzs, dirs, deltas, ts = out[1:5]
+        if xyzs.shape[0] != S or dirs.shape[0] != S or deltas.shape[0] != S or ts.shape[0] != S:
+            raise RuntimeError("raymarching_train: out= buffers must hold R*max_samples samples")
+    else:
+        xyzs = torch.empty(S, 3, dtype=torch.float32, device=dev)
+        dirs = torch.empty(S, 3, dtype=torch.float32, device=dev)
+        deltas = torch.empty(S, dtype=torch.float32, device=dev)
+        ts = torch.empty(S, dtype=torch.float32, device=dev)
     call("ncn_march_train_pack", ptr(rays_d), ptr(rays_a), I64(R), I32(ms), ptr(slab_xyz), ptr(slab_t),
          ptr(slab_dt), ptr(xyzs), ptr(dirs), ptr(deltas), ptr(ts), s)
     return [rays_a, xyzs, dirs, deltas, ts, counter]

@@ -2,10 +2,10 @@
 against the eager path on identical inputs.
 
 Tolerances: static vs dynamic render bit-exact (same kernels, the field stops at the device count);
-graph vs eager training: per-step loss within 1e-4 relative; final parameters within
-max(1e-3, 4 x the eager-vs-eager run-to-run difference) relative L2 over 4 Adam steps, MLP weights
-within 1e-3 (the table-gradient flush and the loss reductions use float atomics, so two runs are
-equal up to summation order)."""
+graph vs eager training: per-step loss within 1e-4 relative; over 4 Adam steps at most 1e-5 of
+the hash-table entries moved by more than 1e-4 and under 0.1% by more than 1e-6 between any two
+runs (the table-gradient flush uses float atomics: two runs are equal up to summation order, and
+Adam with eps 1e-15 turns a near-zero gradient's sign into a full lr step); MLP weights within 1e-3."""
 import numpy as np
 import pytest
 import torch
@@ -66,10 +66,15 @@ def test_graph_step_matches_eager(dev):
         losses.append(np.array(ls))
         params.append(m.flat_params().detach().clone())
     np.testing.assert_allclose(losses[2], losses[0], rtol=1e-4)
-    floor = float((params[1] - params[0]).norm() / params[0].norm())
-    rel = float((params[2] - params[0]).norm() / params[0].norm())
-    assert rel < max(1e-3, 4 * floor), (rel, floor)
-    # the MLP weights (dense, large gradients) agree tightly
+    # hash-table entries: the float-atomic summation order differs run to run, and Adam (eps 1e-15)
+    # turns the sign of a near-zero gradient into a full +-lr step, so a handful of the 11.4M
+    # entries may move by ~lr between ANY two runs (eager or graph); everything else agrees
     n_t = _model(dev, scene)._n_table
+    for other in (1, 2):
+        d = (params[other][:n_t] - params[0][:n_t]).abs()
+        big = int((d > 1e-4).sum())
+        assert big <= 1e-5 * n_t, (other, big)
+        assert float((d > 1e-6).float().mean()) < 1e-3, other
+    # the MLP weights (dense, large gradients) agree tightly
     rel_w = float((params[2][n_t:] - params[0][n_t:]).norm() / params[0][n_t:].norm())
     assert rel_w < 1e-3, rel_w

@@ -10,7 +10,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from ncnerf_amd import _lib  # noqa: E402
 
-so = os.path.join(ROOT, "tools", "_build", "lib_ncn_diag_cl_times.so")
+so = os.environ.get("NCN_CL_PROBE_SO", os.path.join(ROOT, "tools", "_build", "lib_ncn_diag_cl_times.so"))
 _lib.LIB_PATH = so
 L = _lib.lib()
 from ncnerf_amd import losses as Lo  # noqa: E402
