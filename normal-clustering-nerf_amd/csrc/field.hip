@@ -125,28 +125,41 @@ __device__ __forceinline__ LevelPos level_pos(float scale, float x, float y, flo
     return p;
 }
 
-// trilinear interpolation of one level (tcnn kernel_grid: corner bit d -> +1 along dim d)
+// trilinear interpolation of one level (tcnn kernel_grid: corner bit d -> +1 along dim d).  Entry
+// indices without per-corner grid_index branches: a dense level (res^3 <= params: tcnn's stride
+// never exceeds params) is base + dx + dy*res + dz*res^2 (mod params only at the boundary corner
+// res^3 == params can't reach: kept as in grid_index), a hashed one ((x+dx) ^ (y+dy)*P1 ^
+// (z+dz)*P2) & (params-1) with the four products formed once (params is 2^19 on every hashed
+// level).  Corner weights in the association ((wx * wy) * wz) of the reference loop.
 __device__ __forceinline__ float2 encode_level(const float2* __restrict__ tab, const LevelTable& L, int l, float x,
                                                float y, float z) {
     const LevelPos p = level_pos(L.scale[l], x, y, z);
     const uint32_t params = L.params[l], res = L.res[l], off = L.offset[l];
-    float2 v[8];
-    float w[8];
+    uint32_t e[8];
+    if ((uint64_t)res * res * res <= params) {
+        const uint32_t b0 = p.px + res * p.py + res * res * p.pz;
 #pragma unroll
-    for (int c = 0; c < 8; c++) {
-        const uint32_t cx = p.px + (c & 1), cy = p.py + ((c >> 1) & 1), cz = p.pz + ((c >> 2) & 1);
-        v[c] = tab[off + grid_index(params, res, cx, cy, cz)];
-        float wt = 1.0f;
-        wt *= (c & 1) ? p.fx : 1.0f - p.fx;
-        wt *= (c & 2) ? p.fy : 1.0f - p.fy;
-        wt *= (c & 4) ? p.fz : 1.0f - p.fz;
-        w[c] = wt;
+        for (int c = 0; c < 8; c++) {
+            const uint32_t i = b0 + (c & 1) + ((c >> 1) & 1) * res + ((c >> 2) & 1) * res * res;
+            e[c] = i < params ? i : i % params;
+        }
+    } else {
+        const uint32_t hy0 = p.py * 2654435761u, hy1 = (p.py + 1) * 2654435761u;
+        const uint32_t hz0 = p.pz * 805459861u, hz1 = (p.pz + 1) * 805459861u;
+        const uint32_t mask = params - 1;
+#pragma unroll
+        for (int c = 0; c < 8; c++) e[c] = ((p.px + (c & 1)) ^ ((c & 2) ? hy1 : hy0) ^ ((c & 4) ? hz1 : hz0)) & mask;
     }
+    float2 v[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = tab[off + e[c]];
+    const float wx[2] = {1.0f - p.fx, p.fx}, wy[2] = {1.0f - p.fy, p.fy}, wz[2] = {1.0f - p.fz, p.fz};
     float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-        acc.x = fmaf(w[c], v[c].x, acc.x);
-        acc.y = fmaf(w[c], v[c].y, acc.y);
+        const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+        acc.x = fmaf(w, v[c].x, acc.x);
+        acc.y = fmaf(w, v[c].y, acc.y);
     }
     return acc;
 }
