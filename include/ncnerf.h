@@ -127,6 +127,7 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
                   const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
+                  float* level_max /* 16 * ncn_field_bwd_blocks(n) floats of workspace (per-level max |dE|) */,
                   void* stream);
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream);
 

@@ -366,9 +366,12 @@ __device__ __forceinline__ void bwd_load(BwdIn& in, int64_t grp, int64_t n, int 
 }
 
 // Phase 1 for one group: forward recompute, backward through the layers, dE out, dW operands out.
+__device__ __forceinline__ float lmax_upd(float m, float a, float b) {  // non-finite -> INF
+    return (isfinite(a) && isfinite(b)) ? fmaxf(m, fmaxf(fabsf(a), fabsf(b))) : INFINITY;
+}
 __device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const BwdIn& cur,
                                           int64_t grp, int64_t n, int64_t n_stride, int lane,
-                                          float* __restrict__ dE_out) {
+                                          float* __restrict__ dE_out, float (&lm)[4]) {
     const int g = lane >> 4, r = lane & 15;
     const int64_t s = grp * 16 + r;
     const bool valid = s < n;
@@ -440,6 +443,11 @@ __device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const
         for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
         dE[t] = v;
     }
+    // per-level max |dE| of this lane's levels (2g, 2g+1, 8+2g, 9+2g): the scatter's fixed-point scale
+    lm[0] = lmax_upd(lm[0], dE[0][0], dE[0][1]);
+    lm[1] = lmax_upd(lm[1], dE[0][2], dE[0][3]);
+    lm[2] = lmax_upd(lm[2], dE[1][0], dE[1][1]);
+    lm[3] = lmax_upd(lm[3], dE[1][2], dE[1][3]);
     if (valid) {  // encoding gradient -> level-major [16][n] float2 for the scatter pass
         float2* o = (float2*)dE_out;
         o[(int64_t)(2 * g) * n_stride + s] = make_float2(dE[0][0], dE[0][1]);
@@ -516,7 +524,7 @@ __device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, i
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const half4_t* __restrict__ wpacked,
     const half4_t* __restrict__ enc_cache, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
-    float* __restrict__ dE_out, float* __restrict__ slab) {
+    float* __restrict__ dE_out, float* __restrict__ slab, float* __restrict__ level_max) {
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     if (n_dev) n = min<int64_t>(n, *n_dev);
     __shared__ half4_t F[N_FRAGS * 64];                    // 38.9 KB weight fragments
@@ -527,6 +535,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     float4_t acc[5];
 #pragma unroll
     for (int t = 0; t < 5; t++) acc[t] = zero4();
+    float lm[4] = {0.f, 0.f, 0.f, 0.f};
     const int64_t n_groups = (n + 15) / 16;
     const int64_t stride = (int64_t)gridDim.x * BWD_WAVES;
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
@@ -539,7 +548,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         if (grp + stride < n_groups) bwd_load(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
 #ifndef NCN_DIAG_BWD_NO_P1
         if (grp < n_groups)
-            bwd_group(F + opaque_zero(), X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out);
+            bwd_group(F + opaque_zero(), X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm);
 #else
         if (cur.dsig == 1234.5f) dE_out[grp] = 0.f;
 #endif
@@ -550,6 +559,33 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         lds_barrier();
     }
     bwd_store_dw(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc);
+    // level maxima: the 16 lanes of a row (same g) share their 4 levels; the row leaders of the 8
+    // waves meet in LDS and the workgroup writes its row of level_max [blocks][16] (no atomics: the
+    // scatter reduces the rows)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float m = lm[i];
+        m = fmaxf(m, dppf<0x128>(m));  // row_ror 8
+        m = fmaxf(m, dppf<0x124>(m));
+        m = fmaxf(m, dppf<0x122>(m));
+        m = fmaxf(m, dppf<0x121>(m));
+        lm[i] = m;
+    }
+    __shared__ float lmw[BWD_WAVES][16];
+    if ((lane & 15) == 0) {
+        const int g = lane >> 4;
+        lmw[wid][2 * g] = lm[0];
+        lmw[wid][2 * g + 1] = lm[1];
+        lmw[wid][8 + 2 * g] = lm[2];
+        lmw[wid][9 + 2 * g] = lm[3];
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        float m = 0.f;
+#pragma unroll
+        for (int w = 0; w < BWD_WAVES; w++) m = fmaxf(m, lmw[w][threadIdx.x]);
+        level_max[blockIdx.x * 16 + threadIdx.x] = m;
+    }
 }
 
 // Sum of the per-workgroup dW slabs: blockIdx.y takes a chunk of slabs (coalesced 1 KB rows),
@@ -600,6 +636,7 @@ constexpr int sc_layout_bytes(int sets, bool staging) {
 constexpr int SC_ARENA = sc_layout_bytes(SC_SETS_RUN, true) > sc_layout_bytes(SC_SETS_DIR, false)
                              ? sc_layout_bytes(SC_SETS_RUN, true) : sc_layout_bytes(SC_SETS_DIR, false);
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
+constexpr int SC_TS_NONE = -2;  // slot[] of an inactive lane
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
 
@@ -695,37 +732,44 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
         }
         return;
     }
+    // per corner: one ds_read_b128 of the set; a hit adds, a miss claims the first empty way with
+    // ds_cmpst (a uniform branch skips the claim step when no lane of the wave misses: the common
+    // case on coarse levels); a full set falls back to a global atomic.  Lanes with no
+    // contribution (v == 0: beyond the span / zero dE) take part with nothing to add.
+    const bool act = (v[0] != 0.f) | (v[1] != 0.f) | (v[2] != 0.f) | (v[3] != 0.f) | (v[4] != 0.f) | (v[5] != 0.f) |
+                     (v[6] != 0.f) | (v[7] != 0.f) | (v[8] != 0.f) | (v[9] != 0.f) | (v[10] != 0.f) |
+                     (v[11] != 0.f) | (v[12] != 0.f) | (v[13] != 0.f) | (v[14] != 0.f) | (v[15] != 0.f);
     uint32_t newmask = 0;
     int slot[8];
 #pragma unroll 2
     for (int c = 0; c < 8; c++) {
-        slot[c] = -1;
-        if (v[2 * c] == 0.f && v[2 * c + 1] == 0.f) continue;
         const int p0 = SC_WAYS * sc_set(e[c], sh.sets);
         const uint4 kk = *(const uint4*)&sh.keys[p0];
         int sl = kk.x == e[c] ? p0 : kk.y == e[c] ? p0 + 1 : kk.z == e[c] ? p0 + 2 : kk.w == e[c] ? p0 + 3 : -1;
-        if (sl < 0) {  // claim the first way of the set seen empty
-            const int cl = kk.x == SC_EMPTY ? p0 : kk.y == SC_EMPTY ? p0 + 1 : kk.z == SC_EMPTY ? p0 + 2
-                         : kk.w == SC_EMPTY ? p0 + 3 : -1;
+        const int cl = (!act || sl >= 0) ? -1
+                     : kk.x == SC_EMPTY ? p0 : kk.y == SC_EMPTY ? p0 + 1 : kk.z == SC_EMPTY ? p0 + 2
+                     : kk.w == SC_EMPTY ? p0 + 3 : -1;
+        if (__ballot(cl >= 0)) {  // uniform
             if (cl >= 0) {
                 const uint32_t got = atomicCAS(&sh.keys[cl], SC_EMPTY, e[c]);
                 if (got == SC_EMPTY) { sl = cl; newmask |= 1u << c; }
                 else if (got == e[c]) sl = cl;
             }
         }
-        slot[c] = sl;
-        if (sl >= 0) {
-#if defined(NCN_DIAG_SC_PACKED)
-            atomicAdd((unsigned long long*)&sh.valx[sl], (unsigned long long)(sc_fix(v[2 * c], L.k - 20) + (sc_fix(v[2 * c + 1], L.k - 20) << 32)));
-#elif !defined(NCN_DIAG_SC_NO_LDSADD)
+        slot[c] = act ? sl : SC_TS_NONE;
+        if (act && sl >= 0) {
+#ifndef NCN_DIAG_SC_NO_LDSADD
             atomicAdd((unsigned long long*)&sh.valx[sl], (unsigned long long)sc_fix(v[2 * c], L.k));
             atomicAdd((unsigned long long*)&sh.valy[sl], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
 #endif
-        } else {  // set full of other entries
+        }
+        if (__ballot(act && sl < 0)) {  // uniform: some lane's set is full of other entries
+            if (act && sl < 0) {
 #ifndef NCN_DIAG_SC_NO_FALLBACK
-            atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
-            atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
+                atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
+                atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
 #endif
+            }
         }
     }
     // append the claimed slots to `used`: one LDS atomic per wave
@@ -810,7 +854,7 @@ struct ScChunk {
 // reads contiguous bytes, so fewer, wider load instructions (the lane-strided pattern costs TA
 // cycles per touched cache line).  A partial last chunk falls back to per-sample loads.
 template <int C>
-__device__ __forceinline__ float sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
+__device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
                                                const float2* __restrict__ dEl, const ScNorm& nrm) {
     static_assert(C == 2 || C == 4, "chunk of 2 or 4 samples");
     float xs[3 * C];
@@ -851,16 +895,12 @@ __device__ __forceinline__ float sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64
             xs[3 * i + 2] = in ? xyzs[3 * sc + 2] : 0.f;
         }
     }
-    float m = 0.f;  // max |dE| (INFINITY if not finite)
 #pragma unroll
     for (int i = 0; i < C; i++) {
         ch.x[i] = nrm(xs[3 * i]);
         ch.y[i] = nrm(xs[3 * i + 1]);
         ch.z[i] = nrm(xs[3 * i + 2]);
-        const float a = fmaxf(fabsf(ch.g[i].x), fabsf(ch.g[i].y));
-        m = (isfinite(ch.g[i].x) && isfinite(ch.g[i].y)) ? fmaxf(m, a) : INFINITY;
     }
-    return m;
 }
 
 // Phase A over the lane's chunk; step C emits the last run.  The loop is not unrolled (one emit
@@ -911,7 +951,8 @@ __device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<
     }
 }
 
-// One unit: load the chunk, the unit's fixed-point scale (block max), phase A/B or direct, flush.
+// One unit: load the chunk, phase A/B or direct, flush.  The fixed-point scale is per level, from
+// the max |dE| the MLP pass recorded (level_max): no per-unit reduction or barrier.
 #ifdef NCN_DIAG_SC_TIMES
 __device__ unsigned long long ncn_sc_times[256][8];  // per workgroup, wave 0: cycles per phase x {run, dir}
 #define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -923,24 +964,14 @@ __device__ unsigned long long ncn_sc_times[256][8];  // per workgroup, wave 0: c
 template <int C, bool RUNS>
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const float2* __restrict__ dEl,
-                                        const ScNorm& nrm, const LevelTable& Lt, float* __restrict__ grad) {
+                                        const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad) {
     SC_TNOW(t0);
-    ScChunk<C> ch;
-    float m = sc_load_chunk<C>(ch, s0 + (int64_t)threadIdx.x * C, s1, xyzs, dEl, nrm);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if (lane == 0) sh.wmax[wid] = m;
-    lds_barrier();
-    m = 0.f;
-#pragma unroll
-    for (int w = 0; w < SC_WAVES; w++) m = fmaxf(m, sh.wmax[w]);
 #ifdef NCN_DIAG_SC_LEVELS_MASK
     if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
 #endif
-    if (m == 0.f) {  // uniform: nothing to add on this unit
-        lds_barrier();  // (wmax is rewritten by the next unit)
-        return;
-    }
+    if (m == 0.f) return;  // uniform: nothing to add on this level
+    ScChunk<C> ch;
+    sc_load_chunk<C>(ch, s0 + (int64_t)threadIdx.x * C, s1, xyzs, dEl, nrm);
     ScLevel L;
     L.scale = Lt.scale[l];
     L.res = Lt.res[l];
@@ -992,10 +1023,18 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
                                                                    const float2* __restrict__ dE,
-                                                                   float* __restrict__ grad) {
+                                                                   float* __restrict__ grad,
+                                                                   const float* __restrict__ level_max, int lm_rows) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
     __shared__ float wmax[SC_WAVES];
     __shared__ int fill;
+    // per-level max |dE| over the MLP pass's workgroup rows (the fixed-point scale of each level);
+    // visible to every thread at the first layout barrier
+    __shared__ float lmax_s[16];
+    if (threadIdx.x < 16) lmax_s[threadIdx.x] = 0.f;
+    __syncthreads();
+    for (int i = threadIdx.x; i < lm_rows * 16; i += SC_THREADS)  // one load per thread, LDS max
+        atomicMax((unsigned*)&lmax_s[i & 15], __float_as_uint(level_max[i]));  // (non-negative floats)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
     const int64_t e_stride = (n_stride + 3) & ~(int64_t)3;  // dE row stride (as written by field_bwd)
@@ -1030,12 +1069,12 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         if (run) {
             const int l = (int)(u / ur);
             const int64_t s0 = (u - l * ur) * (SC_THREADS * C_RUN), s1 = min(n, s0 + SC_THREADS * C_RUN);
-            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, grad);
+            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, lmax_s[l], grad);
         } else {
             const int64_t v = u - SC_RUN_LEVELS * ur;
             const int l = SC_RUN_LEVELS + (int)(v / ud);
             const int64_t s0 = (v - (l - SC_RUN_LEVELS) * ud) * (SC_THREADS * C_DIR), s1 = min(n, s0 + SC_THREADS * C_DIR);
-            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, grad);
+            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, lmax_s[l], grad);
         }
     }
 }
@@ -1102,17 +1141,19 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
                   const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
-                  void* stream) {
+                  float* level_max, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
                 "ncn_field_bwd: dE_ws and xyzs must be 16-byte aligned");
+    NCN_REQUIRE(level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd: level_max workspace required");
     const LevelTable Lt = make_table(levels);
     hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
                        dirs, n, n_dev, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas,
-                       dL_drgbs, dE_ws, slab);
+                       dL_drgbs, dE_ws, slab, level_max);
     NCN_LAUNCH_CHECK("ncn_field_bwd");
     hipLaunchKernelGGL(field_scatter_kernel, dim3(scatter_grid(n)), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n,
-                       n_dev, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, grad_table);
+                       n_dev, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max,
+                       ncn_field_bwd_blocks(n));
     NCN_LAUNCH_CHECK("ncn_field_bwd (scatter)");
     return 0;
 }

@@ -38,7 +38,7 @@ SIGNATURES = {
     "ncn_field_fwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
     "ncn_field_bwd_dE_floats": [I64],
-    "ncn_field_bwd": [P, P, I64, P, P, F32, F32, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd": [P, P, I64, P, P, F32, F32, P, P, P, P, P, P, P, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],

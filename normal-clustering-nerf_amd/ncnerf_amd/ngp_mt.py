@@ -108,12 +108,20 @@ class _FieldFunction(torch.autograd.Function):
         dsig, drgb = c(dL_dsigmas), c(dL_drgbs)
         call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
              F32(model._xyz_extent),
-             ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), ptr(dE_ws), stream())
+             ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()),
+             stream())
         call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
         return None, None, None, None, None, None, None, None
 
 
 class NGPMT(nn.Module):
+    def _level_max(self):
+        """ncn_field_bwd's per-level max |dE| workspace: 16 floats per MLP-pass workgroup (<= 256)."""
+        dev = self._flat.device
+        if getattr(self, "_lmax", None) is None or self._lmax.device != dev:
+            self._lmax = torch.empty(16 * 256, dtype=torch.float32, device=dev)
+        return self._lmax
+
     def __init__(self, scale, grid_size, rgb_act="Sigmoid", pred_sem=False, pred_norm=False, seed=1337, **kwargs):
         super().__init__()
         if rgb_act != "Sigmoid":

@@ -56,12 +56,13 @@ gtab = torch.zeros_like(table)
 nb = main.ncn_field_bwd_blocks(I64(n))
 slab = torch.empty(nb * 19712, device=dev)
 dE_ws = torch.empty(int(main.ncn_field_bwd_dE_floats(I64(n))), device=dev)
+lmax = torch.empty(16 * 256, device=dev)
 
 
 def bwd(lib):
     return lib.ncn_field_bwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), model._levels_ptr, F32(model._xyz_min),
                              F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(gtab), ptr(slab),
-                             ptr(dE_ws), stream())
+                             ptr(dE_ws), ptr(lmax), stream())
 
 
 def timeit(f, lib, reps=20):
