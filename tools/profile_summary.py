@@ -40,6 +40,18 @@ def main(rnd):
                      "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM), WRITE_SIZE as read; Infinity-Cache hits included"}
     json.dump(out, open(os.path.join(dst, "composite_fw_traffic.json"), "w"), indent=1)
     print(json.dumps(out))
+    # the bench's roofline launches are the last 50 composite_fw dispatches of the traced run: their
+    # rocprof average must agree with bench.py's live HIP-event figure (roofline.avg_launch_us)
+    traces = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+         for r in csv.DictReader(open(traces[0])) if k in r["Kernel_Name"]]
+    live = {"kernel": k, "roofline_launches": 50, "rocprof_avg_us": round(statistics.mean(d[-50:]), 3),
+            "rocprof_median_us": round(statistics.median(d[-50:]), 3),
+            "all_dispatches_avg_us": round(statistics.mean(d), 3), "dispatches": len(d),
+            "method": "rocprofv3 --kernel-trace of `bench.py --steps 30`; the last 50 dispatches are bench.py's "
+                      "back-to-back roofline launches"}
+    json.dump(live, open(os.path.join(dst, "composite_fw_rocprof_timing.json"), "w"), indent=1)
+    print(json.dumps(live))
 
 
 if __name__ == "__main__":
