@@ -32,6 +32,24 @@ int ncn_morton3D(const int32_t* coords, int64_t n, int32_t* out, void* stream);
 int ncn_morton3D_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream);
 int ncn_packbits(const float* density_grid, int64_t n_bytes, float threshold, uint8_t* bitfield, void* stream);
 
+/* ---- occupancy-grid refresh: replaces NGPMT.update_density_grid (ngp_mt.py:340-368) and its
+ *      sample_uniform_and_occupied_cells (ngp_mt.py:245-262) / get_all_cells (:237-243).
+ *      Per cascade c: ncn_grid_sample (cells hit: all when warmup, else each cell independently
+ *      with the marginal hit probability of M uniform + M occupied draws; the others are decayed
+ *      in place) -> ncn_field_fwd(mode 1, n_dev = n_list) over list_xyzs -> ncn_grid_apply; then
+ *      ncn_grid_packbits over all cascades (min(mean of positive cells, threshold) -> packbits,
+ *      the threshold written to *thr_out).  list_xyzs / list_idx hold n_cells entries; n_list and
+ *      thr_out are device scalars; work is ncn_grid_work_bytes() bytes, zero before the first call
+ *      (its arrival counter is left zero).  Nothing is read back on the host. ---- */
+int64_t ncn_grid_work_bytes(void);
+int ncn_grid_sample(float* density_grid_c, int64_t n_cells, int grid_size, float s_minus_half_grid, float half_grid,
+                    float threshold, int64_t M, int warmup, uint64_t seed, float decay, const float* count_grid_c,
+                    float* list_xyzs, int32_t* list_idx, int32_t* n_list, void* work, void* stream);
+int ncn_grid_apply(float* density_grid_c, const int32_t* list_idx, const float* sigmas, const int32_t* n_list,
+                   int64_t capacity, float decay, const float* count_grid_c, void* stream);
+int ncn_grid_packbits(const float* density_grid, int64_t n_total, double threshold, uint8_t* bitfield,
+                      float* thr_out, void* work, void* stream);
+
 /* ---- ray / AABB: replaces vren.ray_aabb_intersect (binding.cpp:12-24, intersection.cu:59-100).
  *      hits_t (R,max_hits,2) and hits_voxel_idx (R,max_hits) are fully written (-1 when empty). ---- */
 int ncn_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays,

@@ -89,7 +89,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 //  2. adam_apply_kernel: Adam of both groups (index < n_group0: weight decay wd0, else wd1) with
 //     16-B accesses, reading the four scalars.
 // Replaces sumsq + one Adam launch per group (each of whose workgroups re-summed the partials).
-constexpr int ADAM_BLOCKS = 1024;
+constexpr int ADAM_BLOCKS = 2048;  // max workgroups of adam_prep (partials)
+constexpr int ADAM_UNROLL = 8;
 __global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float max_norm,
                                                         float b1, float b2, float lr, const float* __restrict__ lr_dev,
                                                         int* __restrict__ step_dev, float* __restrict__ work) {
@@ -98,12 +99,17 @@ __global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict_
     float* sc = work + ADAM_BLOCKS + 4;                // cf, bc1, bc2, lr
     __shared__ float red[4];
     __shared__ bool last;
-    const int64_t n4 = n / 4;
+    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
     const float4* g4 = (const float4*)g;
     float s = 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-        const float4 x = g4[i];
-        s = fmaf(x.x, x.x, s); s = fmaf(x.y, x.y, s); s = fmaf(x.z, x.z, s); s = fmaf(x.w, x.w, s);
+    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n4; b += ADAM_UNROLL * stride) {
+        float4 x[ADAM_UNROLL];  // ADAM_UNROLL independent loads in flight per thread
+#pragma unroll
+        for (int u = 0; u < ADAM_UNROLL; u++) x[u] = b + u * stride < n4 ? g4[b + u * stride] : make_float4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < ADAM_UNROLL; u++) {
+            s = fmaf(x[u].x, x[u].x, s); s = fmaf(x[u].y, x[u].y, s); s = fmaf(x[u].z, x[u].z, s); s = fmaf(x[u].w, x[u].w, s);
+        }
     }
     if (blockIdx.x == 0)
         for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) s = fmaf(g[i], g[i], s);
@@ -121,21 +127,33 @@ __global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict_
     }
     __syncthreads();
     if (!last) return;
-    if (threadIdx.x < 64) {
-        float t = 0.f;
-        for (int i = threadIdx.x; i < (int)gridDim.x; i += 64)
-            t += __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = wave_sum(t);
-        if (threadIdx.x == 0) {
-            const float c = max_norm / (sqrtf(t) + 1e-6f);
-            const int st = *step_dev + 1;  // device step counter
-            *step_dev = st;
-            sc[0] = max_norm > 0.f ? fminf(c, 1.0f) : 1.0f;
-            sc[1] = 1.0f - powf(b1, (float)st);
-            sc[2] = 1.0f - powf(b2, (float)st);
-            sc[3] = lr_dev ? *lr_dev : lr;
-            *cnt = 0u;
+    // the gridDim.x (<= ADAM_BLOCKS) partials: every thread loads its share at once (one round
+    // trip), fixed-order sums
+    float t = 0.f;
+    {
+        float q[ADAM_BLOCKS / 256];
+#pragma unroll
+        for (int u = 0; u < ADAM_BLOCKS / 256; u++) {
+            const int i = u * 256 + threadIdx.x;
+            q[u] = i < (int)gridDim.x ? __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
         }
+#pragma unroll
+        for (int u = 0; u < ADAM_BLOCKS / 256; u++) t += q[u];
+    }
+    t = wave_sum(t);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        t = red[0] + red[1] + red[2] + red[3];
+        const float c = max_norm / (sqrtf(t) + 1e-6f);
+        const int st = *step_dev + 1;  // device step counter
+        *step_dev = st;
+        sc[0] = max_norm > 0.f ? fminf(c, 1.0f) : 1.0f;
+        sc[1] = 1.0f - powf(b1, (float)st);
+        sc[2] = 1.0f - powf(b2, (float)st);
+        sc[3] = lr_dev ? *lr_dev : lr;
+        *cnt = 0u;
     }
 }
 __global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -200,7 +218,8 @@ int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_
                 hipErrorInvalidValue, "ncn_adam_step: buffers must be 16-byte aligned");
     NCN_REQUIRE(step_dev != nullptr && work != nullptr, hipErrorInvalidValue,
                 "ncn_adam_step: needs the device step counter and the work buffer");
-    hipLaunchKernelGGL(adam_prep_kernel, dim3(ADAM_BLOCKS), dim3(256), 0, (hipStream_t)stream, grads, n, max_norm,
+    const int prep_blocks = (int)std::min<int64_t>(ADAM_BLOCKS, std::max<int64_t>(1, cdiv(n / 4, 256 * ADAM_UNROLL)));
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(256), 0, (hipStream_t)stream, grads, n, max_norm,
                        beta1, beta2, lr, lr_dev, step_dev, work);
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
     const int blocks = (int)std::min<int64_t>(cdiv(n, 1024), 2048);

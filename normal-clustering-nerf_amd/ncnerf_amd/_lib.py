@@ -17,6 +17,8 @@ I64 = ctypes.c_int64
 I32 = ctypes.c_int
 U32 = ctypes.c_uint32
 F32 = ctypes.c_float
+F64 = ctypes.c_double
+U64 = ctypes.c_uint64
 
 # name -> argtypes (stream last); every function returns int (hipError_t)
 SIGNATURES = {
@@ -51,6 +53,10 @@ SIGNATURES = {
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
     "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F32, F32, F32, F32, P, P, P, P],
     "ncn_adam_step_work_floats": [],
+    "ncn_grid_work_bytes": [],
+    "ncn_grid_sample": [P, I64, I32, F32, F32, F32, I64, I32, U64, F32, P, P, P, P, P, P],
+    "ncn_grid_apply": [P, P, P, P, I64, F32, P, P],
+    "ncn_grid_packbits": [P, I64, F64, P, P, P, P],
 }
 
 _lib = None
@@ -83,6 +89,7 @@ def lib():
         L.ncn_cluster_workspace_words.restype = ctypes.c_int64
         L.ncn_field_bwd_dE_floats.restype = ctypes.c_int64
         L.ncn_adam_step_work_floats.restype = ctypes.c_int64
+        L.ncn_grid_work_bytes.restype = ctypes.c_int64
         L.ncn_last_error.argtypes = []
         L.ncn_last_error.restype = ctypes.c_char_p
         L.ncn_version.restype = ctypes.c_int

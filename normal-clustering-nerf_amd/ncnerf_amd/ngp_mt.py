@@ -302,28 +302,60 @@ class NGPMT(nn.Module):
                 valid_mask = (count > 0) & (~too_near_to_cam.any(0))
                 self.density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
 
+    def _grid_ws(self):
+        """Device workspace of the grid refresh: hit list (positions, cell indices, densities) of one
+        cascade's capacity, the list count, the effective threshold and the reduction scratch."""
+        dev, N = self.density_grid.device, self.grid_size ** 3
+        ws = getattr(self, "_gws", None)
+        if ws is None or ws["xyzs"].device != dev or ws["idx"].numel() != N:
+            nbytes = int(_lib.lib().ncn_grid_work_bytes())
+            ws = {"xyzs": torch.empty(N, 3, device=dev), "idx": torch.empty(N, dtype=torch.int32, device=dev),
+                  "sigmas": torch.empty(N, device=dev), "scal": torch.zeros(4, dtype=torch.int32, device=dev),
+                  "work": torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=dev)}
+            self._gws = ws
+        return ws
+
     @torch.no_grad()
-    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):
-        """ngp_mt.py:340-368.  Quirk q12: with no cell > 0 the mean is NaN and packbits, comparing
-        against NaN, clears the bitfield — reproduced."""
-        density_grid_tmp = torch.zeros_like(self.density_grid)
-        if warmup:
-            cells = self.get_all_cells()
-        else:
-            cells = self.sample_uniform_and_occupied_cells(self.grid_size ** 3 // 4, density_threshold)
-        for c in range(self.cascades):
-            indices, coords = cells[c]
-            s = min(2 ** (c - 1), self.scale)
-            half_grid_size = s / self.grid_size
-            xyzs_w = (coords / (self.grid_size - 1) * 2 - 1) * (s - half_grid_size)
-            xyzs_w += (torch.rand_like(xyzs_w) * 2 - 1) * half_grid_size
-            density_grid_tmp[c, indices] = self.density(xyzs_w.contiguous())
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False, seed=None):
+        """ngp_mt.py:340-368 on the device (csrc/grid.hip): per cascade ncn_grid_sample -> density
+        pass (ncn_field_fwd mode 1 over the hit list, device count) -> ncn_grid_apply, then
+        ncn_grid_packbits.  Cells hit: all of them in warmup (get_all_cells), else each cell with the
+        marginal probability of the reference's M uniform + M occupied draws with replacement
+        (sample_uniform_and_occupied_cells, M = G^3/4) — the documented sampling deviation of
+        grid.hip.  The density grid is updated in place (the reference rebinds it to the same values).
+        Quirk q12: with no cell > 0 the mean is NaN and the bitfield is cleared — reproduced.
+        No host synchronisation; `seed` (default: drawn from torch's CPU generator) fixes the draw."""
+        G, C = self.grid_size, self.cascades
+        N = G ** 3
+        dg = self.density_grid
+        if not (dg.is_cuda and dg.is_contiguous() and dg.dtype == torch.float32 and dg.shape == (C, N)):
+            raise RuntimeError("density_grid must be a contiguous CUDA float32 (cascades, grid_size**3) tensor")
+        cnt = None
         if erode:
-            decay = torch.clamp(decay ** (1 / self.count_grid), 0.1, 0.95)
-        self.density_grid = torch.where(self.density_grid < 0, self.density_grid,
-                                        torch.maximum(self.density_grid * decay, density_grid_tmp))
-        mean_density = self.density_grid[self.density_grid > 0].mean().item()
-        vren.packbits(self.density_grid.contiguous(), min(mean_density, density_threshold), self.density_bitfield)
+            cnt = self.count_grid.float().contiguous()
+        ws = self._grid_ws()
+        n_list = ws["scal"][0:1]
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        packed = self._take_packed()
+        table = self.xyz_encoder.params
+        for c in range(C):
+            s = min(2 ** (c - 1), self.scale)
+            half_grid_size = s / G
+            dgc = dg[c]
+            cc = cnt[c] if cnt is not None else None
+            call("ncn_grid_sample", ptr(dgc), I64(N), I32(G), F32(s - half_grid_size), F32(half_grid_size),
+                 F32(density_threshold), I64(N // 4), I32(1 if warmup else 0),
+                 _lib.U64((seed + 0x9E3779B97F4A7C15 * c) % 2 ** 64), F32(decay), ptr(cc), ptr(ws["xyzs"]),
+                 ptr(ws["idx"]), ptr(n_list), ptr(ws["work"]), stream())
+            call("ncn_field_fwd", ptr(ws["xyzs"]), ptr(None), I64(N), ptr(n_list), ptr(table), self._levels_ptr,
+                 F32(self._xyz_min), F32(self._xyz_extent), ptr(packed), I32(1), ptr(ws["sigmas"]), ptr(None),
+                 ptr(None), stream())
+            call("ncn_grid_apply", ptr(dgc), ptr(ws["idx"]), ptr(ws["sigmas"]), ptr(n_list), I64(N), F32(decay),
+                 ptr(cc), stream())
+        thr_out = ws["scal"][1:2].view(torch.float32)
+        call("ncn_grid_packbits", ptr(dg), I64(C * N), _lib.F64(density_threshold), ptr(self.density_bitfield),
+             ptr(thr_out), ptr(ws["work"]), stream())
 
 
 def register_grid_buffers(model):

@@ -171,3 +171,42 @@ def composite_test_multi_fw(sigmas, raws, deltas, ts, hits_t, alive_indices, T_t
     lib().ref_composite_test_fw(_p(sg, f32p), _p(rw, f32p), _p(dl, f32p), _p(t, f32p), _p(alive_indices, i64p),
                                 I64(A), ctypes.c_int(N), ctypes.c_int(C), ctypes.c_float(T_threshold), _p(ne, i32p),
                                 _p(opacity, f32p), _p(depth, f32p), _p(rend, f32p))
+
+
+# ---- occupancy-grid refresh (ngp_mt.py:305-368), numpy restatement -------------------------------
+def grid_hit_probabilities(n_cells, M, n_occ):
+    """Marginal probability that a cell is drawn at least once by M uniform draws over n_cells
+    cells (sample_uniform_and_occupied_cells, ngp_mt.py:252-255) and by M draws over the n_occ
+    occupied cells (:256-259), both with replacement."""
+    p_u = -np.expm1(M * np.log1p(-1.0 / n_cells))
+    p_o = -np.expm1(M * np.log1p(-1.0 / n_occ)) if n_occ > 0 else 0.0
+    return float(p_u), float(p_o)
+
+
+def grid_cell_positions(cells, grid_size, s):
+    """Un-jittered world position of each cell (ngp_mt.py:318): (coords/(G-1)*2-1)*(s-half_grid), f32."""
+    coords = morton3D_invert(np.asarray(cells, np.int32)).astype(np.float32)
+    hg = s / grid_size
+    x = coords / np.float32(grid_size - 1)
+    x = x * np.float32(2) - np.float32(1)
+    return x * np.float32(s - hg), hg
+
+
+def density_grid_update(grid, cells, sigmas, decay, threshold, count_grid=None):
+    """ngp_mt.py:320-326: density_grid_tmp[cells] = sigmas; grid = where(grid < 0, grid,
+    max(grid*decay, tmp)) (decay per cell with erode: clamp(decay**(1/count), 0.1, 0.95));
+    mean of the positive cells; bitfield = packbits(grid, min(mean, threshold)).  f32 arithmetic as
+    torch; the mean in f64 (torch: f32 tree reduction).  Returns (grid, threshold_used, bitfield)."""
+    g = np.asarray(grid, np.float32)
+    tmp = np.zeros_like(g)
+    tmp.reshape(-1)[np.asarray(cells, np.int64)] = np.asarray(sigmas, np.float32)
+    d = np.float32(decay)
+    if count_grid is not None:
+        with np.errstate(divide="ignore"):
+            d = np.clip(np.float32(decay) ** (np.float32(1) / np.asarray(count_grid, np.float32)),
+                        np.float32(0.1), np.float32(0.95)).astype(np.float32)
+    new = np.where(g < 0, g, np.maximum(g * d, tmp)).astype(np.float32)
+    pos = new[new > 0]
+    mean = np.float32(pos.astype(np.float64).mean()) if pos.size else np.float32(np.nan)
+    thr = min(float(mean), threshold)
+    return new, thr, packbits(new, thr)
