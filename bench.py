@@ -118,7 +118,8 @@ def main():
     from ncnerf_amd.trainer import Trainer
 
     rank, world = distributed.init_from_env()
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    # (modulo: a 1-GPU rehearsal of the N>1 path with NCN_DIST_BACKEND=gloo puts every rank on cuda:0)
+    local_rank = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     torch.manual_seed(1234 + rank)

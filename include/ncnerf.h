@@ -210,11 +210,12 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
              float weight_decay, int step, const float* lr_dev, const int* step_dev, void* stream);
 /* The whole step in two launches (sum of squares whose last workgroup forms the clip factor and
  * step scalars, then Adam of both groups): elements [0, n_group0) use weight decay wd0 (apex group
- * 0, the hash grid), the rest wd1.  step_dev is incremented (device step counter) and drives the
+ * 0, the hash grid), the rest wd1.  The gradient used is grads * grad_scale (1/world after an
+ * all-reduce SUM: the average of DDP without a separate division pass), clipped by its L2 norm.  step_dev is incremented (device step counter) and drives the
  * bias corrections; work holds ncn_adam_step_work_floats() floats, zero before the first call (its
  * arrival counter is left zero by every call).  Buffers 16-byte aligned. */
 int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
-                  float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
+                  float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
                   const float* lr_dev, int* step_dev, float* work, void* stream);
 int64_t ncn_adam_step_work_floats(void);
 

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 // Replaces sumsq + one Adam launch per group (each of whose workgroups re-summed the partials).
 constexpr int ADAM_BLOCKS = 2048;  // max workgroups of adam_prep (partials)
 constexpr int ADAM_UNROLL = 8;
-__global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float max_norm,
+__global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float gscale, float max_norm,
                                                         float b1, float b2, float lr, const float* __restrict__ lr_dev,
                                                         int* __restrict__ step_dev, float* __restrict__ work) {
     float* part = work;                                // [ADAM_BLOCKS]
@@ -146,10 +146,10 @@ __global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict_
     __syncthreads();
     if (threadIdx.x == 0) {
         t = red[0] + red[1] + red[2] + red[3];
-        const float c = max_norm / (sqrtf(t) + 1e-6f);
+        const float c = max_norm / (sqrtf(t) * gscale + 1e-6f);  // norm of the scaled gradient
         const int st = *step_dev + 1;  // device step counter
         *step_dev = st;
-        sc[0] = max_norm > 0.f ? fminf(c, 1.0f) : 1.0f;
+        sc[0] = (max_norm > 0.f ? fminf(c, 1.0f) : 1.0f) * gscale;
         sc[1] = 1.0f - powf(b1, (float)st);
         sc[2] = 1.0f - powf(b2, (float)st);
         sc[3] = lr_dev ? *lr_dev : lr;
@@ -211,7 +211,7 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
 }
 
 int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
-                  float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
+                  float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
                   const float* lr_dev, int* step_dev, float* work, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
@@ -219,7 +219,7 @@ int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_
     NCN_REQUIRE(step_dev != nullptr && work != nullptr, hipErrorInvalidValue,
                 "ncn_adam_step: needs the device step counter and the work buffer");
     const int prep_blocks = (int)std::min<int64_t>(ADAM_BLOCKS, std::max<int64_t>(1, cdiv(n / 4, 256 * ADAM_UNROLL)));
-    hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(256), 0, (hipStream_t)stream, grads, n, max_norm,
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(256), 0, (hipStream_t)stream, grads, n, grad_scale, max_norm,
                        beta1, beta2, lr, lr_dev, step_dev, work);
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
     const int blocks = (int)std::min<int64_t>(cdiv(n, 1024), 2048);

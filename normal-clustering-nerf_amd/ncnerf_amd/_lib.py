@@ -51,7 +51,7 @@ SIGNATURES = {
     "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
-    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F32, F32, F32, F32, P, P, P, P],
+    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F32, F32, F32, F32, F32, P, P, P, P],
     "ncn_adam_step_work_floats": [],
     "ncn_grid_work_bytes": [],
     "ncn_grid_sample": [P, I64, I32, F32, F32, F32, I64, I32, U64, F32, P, P, P, P, P, P],

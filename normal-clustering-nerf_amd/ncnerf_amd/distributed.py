@@ -17,8 +17,8 @@ def init_from_env(backend=None):
     if "WORLD_SIZE" not in os.environ or int(os.environ["WORLD_SIZE"]) <= 1:
         return 0, 1
     if not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # NCN_DIST_BACKEND=gloo: rehearse the N>1 path with several ranks on one GPU
+            backend = os.environ.get("NCN_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         dist.init_process_group(backend=backend)
     return dist.get_rank(), dist.get_world_size()
 
@@ -27,11 +27,17 @@ def is_distributed():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
-def allreduce_grads(flat_grad):
-    """Average the flat gradient over ranks (single bucket: the buffer is contiguous)."""
+def allreduce_grads(flat_grad, average=True):
+    """Sum the flat gradient over ranks (single bucket: the buffer is contiguous).  Returns the scale
+    that turns the sum into DDP's average (1/world): with average=False the caller folds it into the
+    optimizer (FlatAdam.step(grad_scale)) instead of a separate division pass over the buffer."""
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
-        flat_grad.div_(dist.get_world_size())
+        if average:
+            flat_grad.div_(dist.get_world_size())
+            return 1.0
+        return 1.0 / dist.get_world_size()
+    return 1.0
 
 
 def broadcast_occupancy(model, src=0):

@@ -42,13 +42,14 @@ class FlatAdam:
             self.lr = 0.5 * self.base_lr * (1 + math.cos(math.pi * epoch / self.num_epochs))
             self.lr_dev.fill_(self.lr)
 
-    def step(self):
+    def step(self, grad_scale=1.0):
+        """grad_scale: the gradient used is flat_grad * grad_scale (1/world after an all-reduce SUM)."""
         self.step_count += 1
         p = self.model.flat_params()
         g = self.model.flat_grad()
         b1, b2 = self.betas
         call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
-             F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
+             F32(grad_scale), F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
              ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), stream())
 
     def state_tensors(self):

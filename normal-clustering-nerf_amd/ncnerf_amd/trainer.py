@@ -103,8 +103,7 @@ class Trainer:
         self._step_dev.fill_(global_step)
         self.graph.replay()
         if not self._with_opt:
-            distributed.allreduce_grads(self.model.flat_grad())
-            self.opt.step()
+            self.opt.step(grad_scale=distributed.allreduce_grads(self.model.flat_grad(), average=False))
         else:
             self.opt.step_count += 1
         return self._out
@@ -121,6 +120,5 @@ class Trainer:
         results = render(m, batch["rays_o"], batch["rays_d"], **kw)
         loss_d = self.loss(results, batch, global_step=global_step)
         loss_d["total"].backward()
-        distributed.allreduce_grads(m.flat_grad())
-        self.opt.step()
+        self.opt.step(grad_scale=distributed.allreduce_grads(m.flat_grad(), average=False))
         return results, loss_d

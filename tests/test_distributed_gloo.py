@@ -29,6 +29,9 @@ def _worker(rank, world, port, q):
     assert (r, w) == (rank, world)
     g = torch.arange(10, dtype=torch.float32) * (rank + 1)
     distributed.allreduce_grads(g)
+    g2 = torch.ones(4) * (rank + 1)
+    scale = distributed.allreduce_grads(g2, average=False)  # sum; the 1/world goes to the optimizer
+    assert scale == 0.5 and g2.tolist() == [3.0] * 4
     m = _Model(rank)
     distributed.broadcast_occupancy(m)
     lo, hi = distributed.shard_patches(1024, rank, world)
