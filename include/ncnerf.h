@@ -76,6 +76,22 @@ int ncn_march_train_pack(const float* rays_d, const int64_t* rays_a, int64_t n_r
                          const float* slab_xyz, const float* slab_t, const float* slab_dt,
                          float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
 
+/* raymarching_train for the training step in two launches (constant dt, exp_step_factor == 0):
+ * render()'s single-AABB intersection + near clamp (intersection.cu:5-56, rendering.py:24-28), the
+ * jitter (custom_functions.py:83; `noise` (R) or, when NULL, a counter-based uniform of (seed,
+ * *rng_counter, ray): graph replays draw fresh noise through the device counter) and the walk; then
+ * the placement (every workgroup adds the sample counts of the rays before it) and the packing:
+ * writes rays_a, the packed xyzs/dirs/deltas/ts (capacity R*max_samples rows, first counter[0]
+ * valid) and counter = {S, R}.  Slabs as ncn_march_train_walk; work =
+ * ncn_march_train_fused_work_bytes(R) bytes of scratch.  R <= 16384. */
+int64_t ncn_march_train_fused_work_bytes(int64_t n_rays);
+int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_rays, float cx, float cy, float cz,
+                          float hx, float hy, float hz, float near_distance, const float* noise, uint64_t seed,
+                          const int64_t* rng_counter, const uint8_t* bitfield, int cascades, float scale,
+                          int grid_size, int max_samples, float* slab_xyz, float* slab_t, float* slab_dt, void* work,
+                          int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
+                          void* stream);
+
 /* ---- test-time marcher: replaces vren.raymarching_test (raymarching.cu:407-454).
  * Outputs (A,N_samples[,3]) are fully written (zeros past n_eff).  Mutates hits_t[r][0]. ---- */
 int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive, int64_t n_alive,

@@ -289,28 +289,17 @@ __device__ __forceinline__ uint64_t march_visited(int nxt, int s, int lane) {
     return __ballot(cur == lane && lane >= s);
 }
 
+// The wave-parallel walk of one ray (raymarching.cu:195-279 with constant dt): samples to the
+// ray's slab row (sx/st/sd), returns their count (wave-uniform).
 template <bool ONE_CASCADE, int P>
-__global__ __launch_bounds__(256) void march_train_wave_kernel(
-    const float* __restrict__ rays_o, const float* __restrict__ rays_d, const float* __restrict__ hits_t,
-    const float* __restrict__ noise, int64_t R, const uint8_t* __restrict__ bitfield, int cascades, float scale,
-    int G, int max_samples, int32_t* __restrict__ counts, float* __restrict__ slab_xyz,
-    float* __restrict__ slab_t, float* __restrict__ slab_dt) {
-    const int lane = threadIdx.x & 63;
-    const int64_t r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    if (r >= R) return;
-    const MarchConst m = make_march_const(cascades, scale, 0.0f, G, max_samples, scale);
-    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
-    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+__device__ __forceinline__ int march_walk_wave(const MarchConst& m, const uint8_t* __restrict__ bitfield, float ox,
+                                               float oy, float oz, float dx, float dy, float dz, float t1, float t2,
+                                               float noise_r, float dt, int lane, float* __restrict__ sx,
+                                               float* __restrict__ st, float* __restrict__ sd) {
     const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
-    float t1 = hits_t[2 * r];
-    const float t2 = hits_t[2 * r + 1];
-    const float dt = calc_dt(m, 0.0f);  // esf == 0: clamp(0, dt_min, dt_max) for every t >= 0
     int n = 0;
     if (t1 >= 0) {  // :195-198; a miss (t1 = -1) never enters the loop (:204)
-        t1 = fmaf(dt, noise[r], t1);
-        float* sx = slab_xyz + r * (int64_t)max_samples * 3;
-        float* st = slab_t + r * (int64_t)max_samples;
-        float* sd = slab_dt + r * (int64_t)max_samples;
+        t1 = fmaf(dt, noise_r, t1);
         float cb = t1;
         bool pend = false, done = false;
         float ptgt = 0.f;
@@ -356,8 +345,8 @@ __global__ __launch_bounds__(256) void march_train_wave_kernel(
                 const uint64_t vis = march_visited(nxt, s, lane);
                 const uint64_t term = vis & ~lt_m;
                 uint64_t emit = vis & occ_m & lt_m;
-                const int room = max_samples - n;
-                if (__popcll(emit) >= room) {  // the room-th sample ends the walk (:204 n < max_samples)
+                const int room = m.max_samples - n;
+                if (__popcll(emit) >= room) {  // the room-th sample ends the walk (:204 n < m.max_samples)
                     uint64_t e2 = emit;
                     for (int q = 1; q < room; q++) e2 &= e2 - 1;
                     const int last = __builtin_ctzll(e2);
@@ -393,6 +382,24 @@ __global__ __launch_bounds__(256) void march_train_wave_kernel(
             cb = cnext;
         }
     }
+    return n;
+}
+
+template <bool ONE_CASCADE, int P>
+__global__ __launch_bounds__(256) void march_train_wave_kernel(
+    const float* __restrict__ rays_o, const float* __restrict__ rays_d, const float* __restrict__ hits_t,
+    const float* __restrict__ noise, int64_t R, const uint8_t* __restrict__ bitfield, int cascades, float scale,
+    int G, int max_samples, int32_t* __restrict__ counts, float* __restrict__ slab_xyz,
+    float* __restrict__ slab_t, float* __restrict__ slab_dt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (r >= R) return;
+    const MarchConst m = make_march_const(cascades, scale, 0.0f, G, max_samples, scale);
+    const float t1 = hits_t[2 * r];
+    const int n = march_walk_wave<ONE_CASCADE, P>(
+        m, bitfield, rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2], rays_d[3 * r], rays_d[3 * r + 1],
+        rays_d[3 * r + 2], t1, hits_t[2 * r + 1], t1 >= 0 ? noise[r] : 0.f, calc_dt(m, 0.0f), lane,
+        slab_xyz + r * (int64_t)max_samples * 3, slab_t + r * (int64_t)max_samples, slab_dt + r * (int64_t)max_samples);
     if (lane == 0) counts[r] = n;
 }
 
@@ -471,6 +478,130 @@ __global__ __launch_bounds__(256) void march_train_pack_kernel(
         dirs[3 * start + k] = d3[k % 3];
     }
     for (int k = lane; k < cnt; k += 64) {
+        ts[start + k] = st[k];
+        deltas[start + k] = sd[k];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// raymarching_train for the training step in TWO launches (constant dt), replacing ray_aabb +
+// rand + walk + scan + pack:
+//  1. march_train_walk2: per ray (one wave) the single-AABB intersection with render()'s near
+//     clamp (intersection.cu:5-56 at max_hits 1, rendering.py:28; bit-identical to
+//     ray_aabb_kernel<1>), the jitter (custom_functions.py:83: torch.rand_like; here `noise` or, when
+//     NULL, a counter-based uniform of (seed, *rng_ctr, ray)), the walk into the ray's slab row;
+//     counts per ray and the sum of each workgroup's 4 rays;
+//  2. march_train_place: every workgroup sums the sums of the workgroups before it (all loads in
+//     one round trip, no inter-workgroup waiting), places its 4 rays (rays_a) and copies their slab
+//     rows into the packed outputs; the last workgroup writes counter = {S, R}.
+// (A single-pass decoupled look-back version was slower: the look-back of late workgroups walks
+// back through many not-yet-prefixed predecessors, one memory round trip per 64 of them.)
+__device__ __forceinline__ float march_uniform(uint64_t seed, uint64_t ctr, uint32_t r) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr * 0x100000001B3ull + r + 1u);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+constexpr int PLACE_MAX_WG = 256 * 16;  // workgroup sums one place workgroup can add in one round trip
+
+template <bool ONE_CASCADE, int P>
+__global__ __launch_bounds__(256) void march_train_walk2_kernel(
+    const float* __restrict__ rays_o, const float* __restrict__ rays_d, int64_t R, float cx, float cy, float cz,
+    float hx, float hy, float hz, float near_distance, const float* __restrict__ noise, uint64_t seed,
+    const int64_t* __restrict__ rng_ctr, const uint8_t* __restrict__ bitfield, int cascades, float scale, int G,
+    int max_samples, float* __restrict__ slab_xyz, float* __restrict__ slab_t, float* __restrict__ slab_dt,
+    int32_t* __restrict__ counts, int32_t* __restrict__ wg_sum) {
+    __shared__ int cnt_s[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wv));
+    const bool live = r0 < R;
+    const int64_t r = live ? r0 : R - 1;
+    const MarchConst m = make_march_const(cascades, scale, 0.0f, G, max_samples, scale);
+    const float o[3] = {rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2]};
+    const float d[3] = {rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2]};
+    const float c3[3] = {cx, cy, cz}, h3[3] = {hx, hy, hz};
+    float a1[3], a2[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float inv = 1.0f / d[k];
+        const float tmin = (c3[k] - h3[k] - o[k]) * inv;
+        const float tmax = (c3[k] + h3[k] - o[k]) * inv;
+        a1[k] = fminf(tmin, tmax);
+        a2[k] = fmaxf(tmin, tmax);
+    }
+    float t1 = fmaxf(fmaxf(a1[0], a1[1]), a1[2]);
+    float t2 = fminf(fminf(a2[0], a2[1]), a2[2]);
+    if (t1 > t2) { t1 = -1.0f; t2 = -1.0f; }
+    if (t2 > 0) t1 = fmaxf(t1, 0.0f);
+    else { t1 = -1.0f; t2 = -1.0f; }
+    if (t1 >= 0.0f && t1 < near_distance) t1 = near_distance;
+    float nz = 0.f;
+    if (t1 >= 0) nz = noise ? noise[r] : march_uniform(seed, rng_ctr ? (uint64_t)*rng_ctr : 0ull, (uint32_t)r);
+    int n = 0;
+    if (live)
+        n = march_walk_wave<ONE_CASCADE, P>(m, bitfield, o[0], o[1], o[2], d[0], d[1], d[2], t1, t2, nz,
+                                            calc_dt(m, 0.0f), lane, slab_xyz + r * (int64_t)max_samples * 3,
+                                            slab_t + r * (int64_t)max_samples, slab_dt + r * (int64_t)max_samples);
+    if (lane == 0) {
+        cnt_s[wv] = n;
+        if (live) counts[r] = n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) wg_sum[blockIdx.x] = cnt_s[0] + cnt_s[1] + cnt_s[2] + cnt_s[3];
+}
+
+__global__ __launch_bounds__(256) void march_train_place_kernel(
+    const float* __restrict__ rays_d, int64_t R, int max_samples, const int32_t* __restrict__ counts,
+    const int32_t* __restrict__ wg_sum, const float* __restrict__ slab_xyz, const float* __restrict__ slab_t,
+    const float* __restrict__ slab_dt, int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
+    float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts, int32_t* __restrict__ counter) {
+    __shared__ int red[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    // exclusive prefix over the workgroup sums [0, b): 16 loads per thread, all in flight
+    int v[PLACE_MAX_WG / 256];
+#pragma unroll
+    for (int u = 0; u < PLACE_MAX_WG / 256; u++) {
+        const int i = u * 256 + threadIdx.x;
+        v[u] = i < b ? wg_sum[i] : 0;
+    }
+    const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(b * 4 + wv));
+    const bool live = r0 < R;
+    const int64_t r = live ? r0 : R - 1;
+    const int n = live ? counts[r] : 0;
+    int acc = 0;
+#pragma unroll
+    for (int u = 0; u < PLACE_MAX_WG / 256; u++) acc += v[u];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) red[wv] = acc;
+    __syncthreads();
+    int start = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    if (lane == 0) red[wv] = n;
+    __syncthreads();
+    for (int w = 0; w < wv; w++) start += red[w];
+    if (b == (int)gridDim.x - 1 && threadIdx.x == 0) {
+        counter[0] = start + red[0] + red[1] + red[2] + red[3];  // (thread 0: start = the workgroup's prefix)
+        counter[1] = (int32_t)R;
+    }
+    if (!live) return;
+    if (lane == 0) {
+        rays_a[3 * r] = r;
+        rays_a[3 * r + 1] = start;
+        rays_a[3 * r + 2] = n;
+    }
+    const float d3[3] = {rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2]};
+    const float* sx = slab_xyz + r * (int64_t)max_samples * 3;
+    const float* st = slab_t + r * (int64_t)max_samples;
+    const float* sd = slab_dt + r * (int64_t)max_samples;
+    for (int k = lane; k < 3 * n; k += 64) {
+        xyzs[3 * (int64_t)start + k] = sx[k];
+        dirs[3 * (int64_t)start + k] = d3[k % 3];
+    }
+    for (int k = lane; k < n; k += 64) {
         ts[start + k] = st[k];
         deltas[start + k] = sd[k];
     }
@@ -1103,6 +1234,39 @@ int ncn_march_train_walk(const float* rays_o, const float* rays_d, const float* 
                            noise, n_rays, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, counts,
                            slab_xyz, slab_t, slab_dt);
     NCN_LAUNCH_CHECK("ncn_march_train_walk");
+    return 0;
+}
+
+int64_t ncn_march_train_fused_work_bytes(int64_t n_rays) { return (n_rays + cdiv(n_rays, 4)) * 4; }
+
+int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_rays, float cx, float cy, float cz,
+                          float hx, float hy, float hz, float near_distance, const float* noise, uint64_t seed,
+                          const int64_t* rng_counter, const uint8_t* bitfield, int cascades, float scale,
+                          int grid_size, int max_samples, float* slab_xyz, float* slab_t, float* slab_dt, void* work,
+                          int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
+                          void* stream) {
+    if (n_rays <= 0) return 0;
+    NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && grid_size <= 1024 && max_samples >= 1 && work != nullptr,
+                hipErrorInvalidValue, "ncn_march_train_fused: bad cascades/grid_size/max_samples/work");
+    const int64_t nwg = cdiv(n_rays, 4);
+    NCN_REQUIRE(nwg <= PLACE_MAX_WG && n_rays * (int64_t)max_samples < (1ll << 31), hipErrorInvalidValue,
+                "ncn_march_train_fused: n_rays must be <= %d (and n_rays * max_samples < 2^31)", 4 * PLACE_MAX_WG);
+    int32_t* counts = (int32_t*)work;
+    int32_t* wg_sum = counts + n_rays;
+    hipStream_t s = (hipStream_t)stream;
+    dim3 g(nwg), b(256);
+#define NCN_WALK2_ARGS                                                                                         \
+    rays_o, rays_d, n_rays, cx, cy, cz, hx, hy, hz, near_distance, noise, seed, rng_counter, bitfield, cascades, \
+        scale, grid_size, max_samples, slab_xyz, slab_t, slab_dt, counts, wg_sum
+    if (cascades == 1)
+        hipLaunchKernelGGL((march_train_walk2_kernel<true, 2>), g, b, 0, s, NCN_WALK2_ARGS);
+    else
+        hipLaunchKernelGGL((march_train_walk2_kernel<false, 2>), g, b, 0, s, NCN_WALK2_ARGS);
+#undef NCN_WALK2_ARGS
+    NCN_LAUNCH_CHECK("ncn_march_train_fused(walk)");
+    hipLaunchKernelGGL(march_train_place_kernel, g, b, 0, s, rays_d, n_rays, max_samples, counts, wg_sum, slab_xyz,
+                       slab_t, slab_dt, rays_a, xyzs, dirs, deltas, ts, counter);
+    NCN_LAUNCH_CHECK("ncn_march_train_fused(place)");
     return 0;
 }
 

@@ -29,6 +29,9 @@ SIGNATURES = {
     "ncn_ray_aabb_intersect_near": [P, P, I64, P, P, I64, I32, F32, P, P, P, P],
     "ncn_march_train_walk": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, P, P, P, P, P],
     "ncn_march_train_scan": [P, I64, P, P, P],
+    "ncn_march_train_fused_work_bytes": [I64],
+    "ncn_march_train_fused": [P, P, I64, F32, F32, F32, F32, F32, F32, F32, P, U64, P, P, I32, F32, I32, I32, P, P, P,
+                              P, P, P, P, P, P, P, P],
     "ncn_march_train_pack": [P, P, I64, I32, P, P, P, P, P, P, P, P],
     "ncn_march_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
     "ncn_composite_train_fw": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, P],
@@ -90,6 +93,7 @@ def lib():
         L.ncn_field_bwd_dE_floats.restype = ctypes.c_int64
         L.ncn_adam_step_work_floats.restype = ctypes.c_int64
         L.ncn_grid_work_bytes.restype = ctypes.c_int64
+        L.ncn_march_train_fused_work_bytes.restype = ctypes.c_int64
         L.ncn_last_error.argtypes = []
         L.ncn_last_error.restype = ctypes.c_char_p
         L.ncn_version.restype = ctypes.c_int

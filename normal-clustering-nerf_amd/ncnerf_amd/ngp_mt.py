@@ -134,6 +134,8 @@ class NGPMT(nn.Module):
         self.register_buffer("xyz_min", -torch.ones(1, 3) * scale)
         self.register_buffer("xyz_max", torch.ones(1, 3) * scale)
         self.register_buffer("half_size", (self.xyz_max - self.xyz_min) / 2)
+        # the scene box as host floats for the one-launch marcher (no device read per step)
+        self._aabb = (tuple(float(v) for v in self.center[0]), tuple(float(v) for v in self.half_size[0]))
         self.cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)  # ngp_mt.py:34
         self.grid_size = grid_size
         self.register_buffer("density_bitfield", torch.zeros(self.cascades * grid_size ** 3 // 8, dtype=torch.uint8))

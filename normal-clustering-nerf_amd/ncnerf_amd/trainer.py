@@ -35,6 +35,7 @@ class Trainer:
                                   test_time=False, random_bg=False, anneal_strategy="none", anneal_steps=0)
         self.use_graph = use_graph
         self.graph = None
+        self._rng_seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # marcher jitter stream (CPU generator)
 
     def _maybe_update_grid(self, global_step):
         m = self.model
@@ -56,6 +57,8 @@ class Trainer:
         kw = dict(self.render_kwargs, global_step=0, static_shapes=True)
         if "march_noise" in batch:
             kw["march_noise"] = batch["march_noise"]
+        else:  # jitter drawn on the device from the step counter: no torch RNG node in the graph
+            kw["march_rng"] = (self._rng_seed, step_dev)
         results = render(m, batch["rays_o"], batch["rays_d"], **kw)
         loss_d = self.loss(results, batch, global_step=step_dev)
         total = loss_d["total"]

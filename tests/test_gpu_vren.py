@@ -93,6 +93,59 @@ def test_raymarching_train_bitexact(dev, scene, n, edge, ms):
         assert 20 < S / n < 1024, f"unexpected samples/ray {S / n}"
 
 
+def _march_uniform_np(seed, ctr, n):
+    """numpy restatement of march_uniform (csrc/vren.hip): splitmix64 of (seed, counter, ray)."""
+    M = (1 << 64) - 1
+    out = np.empty(n, np.float32)
+    for r in range(n):
+        z = (seed + 0x9E3779B97F4A7C15 * ((ctr * 0x100000001B3 + r + 1) & M)) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        out[r] = np.float32((z >> 40) * (1.0 / 16777216.0))
+    return out
+
+
+class _Box:
+    """The attributes march_train_fused reads from the model."""
+    def __init__(self, bitfield):
+        self._aabb = ((0.0, 0.0, 0.0), (0.5, 0.5, 0.5))
+        self.density_bitfield, self.cascades, self.scale, self.grid_size = bitfield, 1, 0.5, 128
+
+
+@pytest.mark.parametrize("n,edge,ms", [(8192, False, 1024), (2048, True, 1024), (777, False, 64), (1, False, 1024),
+                                       (3, True, 1024)])
+def test_fused_marcher_bitexact(dev, scene, n, edge, ms):
+    """ncn_march_train_fused (intersect + near clamp + jitter + walk, then placement + pack: two
+    launches) == the oracle's ray_aabb_intersect + near clamp + raymarching_train, bit for bit; the
+    device RNG path == the oracle fed the same uniforms; repeated launches give identical results."""
+    from ncnerf_amd.rendering import march_train_fused
+    o, d, ht, noise = _march_inputs(scene, n, 11 + n, dev, edge)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    box = _Box(T(scene.bitfield))
+    names = ("rays_a", "xyzs", "dirs", "deltas", "ts", "counter")
+    ref = vren_ref.raymarching_train(o, d, ht, scene.bitfield, 1, 0.5, 0.0, noise, 128, ms)
+    S = int(ref[5][0])
+    for rep in range(3):
+        out = march_train_fused(box, T(o), T(d), 0.01, ms, noise=T(noise))
+        torch.cuda.synchronize()
+        for name, r in zip(names, ref):
+            a = out[name].cpu().numpy()
+            if name in ("xyzs", "dirs", "deltas", "ts"):
+                a = a[:S]
+            assert np.array_equal(a, r), f"rep {rep} {name}: {np.argwhere(a != r)[:5]}"
+    # device RNG: (seed, counter) -> the same uniforms as the numpy restatement
+    seed, step = 1234567891234, 42
+    out = march_train_fused(box, T(o), T(d), 0.01, ms, rng=(seed, torch.tensor(step, device=dev)))
+    ref = vren_ref.raymarching_train(o, d, ht, scene.bitfield, 1, 0.5, 0.0, _march_uniform_np(seed, step, n), 128, ms)
+    S = int(ref[5][0])
+    for name, r in zip(names, ref):
+        a = out[name].cpu().numpy()
+        if name in ("xyzs", "dirs", "deltas", "ts"):
+            a = a[:S]
+        assert np.array_equal(a, r), f"rng {name}"
+
+
 def test_raymarching_train_exp_step_and_cascades(dev, scene):
     """exp_step_factor > 0 and cascades > 1 (scale 1.0 -> C=2) take the general mip path."""
     rng = np.random.default_rng(3)
