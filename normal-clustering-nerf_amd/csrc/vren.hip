@@ -571,6 +571,20 @@ __global__ __launch_bounds__(256) void march_train_place_kernel(
     const bool live = r0 < R;
     const int64_t r = live ? r0 : R - 1;
     const int n = live ? counts[r] : 0;
+    // the first 256 samples of the ray's slab row are fetched while the prefix is formed
+    const float d3[3] = {rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2]};
+    const float* sx = slab_xyz + r * (int64_t)max_samples * 3;
+    const float* st = slab_t + r * (int64_t)max_samples;
+    const float* sd = slab_dt + r * (int64_t)max_samples;
+    constexpr int PF = 4;  // rows of 64 prefetched (xyz: 3 floats per sample -> 3*PF loads)
+    float px[3 * PF], pt[PF], pd[PF];
+#pragma unroll
+    for (int q = 0; q < 3 * PF; q++) px[q] = q * 64 + lane < 3 * n ? sx[q * 64 + lane] : 0.f;
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+        pt[q] = q * 64 + lane < n ? st[q * 64 + lane] : 0.f;
+        pd[q] = q * 64 + lane < n ? sd[q * 64 + lane] : 0.f;
+    }
     int acc = 0;
 #pragma unroll
     for (int u = 0; u < PLACE_MAX_WG / 256; u++) acc += v[u];
@@ -593,15 +607,29 @@ __global__ __launch_bounds__(256) void march_train_place_kernel(
         rays_a[3 * r + 1] = start;
         rays_a[3 * r + 2] = n;
     }
-    const float d3[3] = {rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2]};
-    const float* sx = slab_xyz + r * (int64_t)max_samples * 3;
-    const float* st = slab_t + r * (int64_t)max_samples;
-    const float* sd = slab_dt + r * (int64_t)max_samples;
-    for (int k = lane; k < 3 * n; k += 64) {
-        xyzs[3 * (int64_t)start + k] = sx[k];
-        dirs[3 * (int64_t)start + k] = d3[k % 3];
+    float* ox = xyzs + 3 * (int64_t)start;
+    float* od = dirs + 3 * (int64_t)start;
+#pragma unroll
+    for (int q = 0; q < 3 * PF; q++) {
+        const int k = q * 64 + lane;
+        if (k < 3 * n) {
+            ox[k] = px[q];
+            od[k] = d3[k % 3];
+        }
     }
-    for (int k = lane; k < n; k += 64) {
+#pragma unroll
+    for (int q = 0; q < PF; q++) {
+        const int k = q * 64 + lane;
+        if (k < n) {
+            ts[start + k] = pt[q];
+            deltas[start + k] = pd[q];
+        }
+    }
+    for (int k = 3 * PF * 64 + lane; k < 3 * n; k += 64) {
+        ox[k] = sx[k];
+        od[k] = d3[k % 3];
+    }
+    for (int k = PF * 64 + lane; k < n; k += 64) {
         ts[start + k] = st[k];
         deltas[start + k] = sd[k];
     }
