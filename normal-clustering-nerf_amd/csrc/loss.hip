@@ -254,7 +254,7 @@ struct KmWs {
     long long* part;  // [2][KM_BLOCKS][K][4] fixed-point (x, y, z, count) per cluster
     long long* p2;    // [KM_BLOCKS][12] flipped member sums + counts per selected cluster
     long long* p3;    // [KM_BLOCKS][16] x.c, |x-c|_1, sign(x-c) sums per selected cluster
-    unsigned* sync;   // [0] barrier arrivals, [1] departures, [2] error flag (stuck barrier)
+    unsigned* sync;   // [0] barrier arrivals, [1] departures, [2] error flag (stuck barrier), [3] launch sequence
 };
 __host__ __device__ inline KmWs km_ws(float* base, int K) {
     KmWs w;
@@ -274,6 +274,9 @@ __device__ __forceinline__ unsigned long long km_fix(float v) {
     return (unsigned long long)__double2ll_rn((double)v * KM_FX);
 }
 __device__ __forceinline__ float km_unfix(long long q) { return (float)((double)q * (1.0 / KM_FX)); }
+__device__ __forceinline__ unsigned long long km_fixl(float v) {  // Lloyd partials: 2^32 (tagged words)
+    return (unsigned long long)__double2ll_rn((double)v * 4294967296.0);
+}
 
 // Cross-workgroup data moves with agent-scope (sc1) loads and stores only (MI355X_MICROARCH.md,
 // inter-workgroup visibility, hand-off row 1): each storing wave waits for its stores, the
@@ -313,6 +316,7 @@ __device__ __forceinline__ void km_grid_exit(unsigned* sync) {
         if (d == KM_BLOCKS - 1) {  // everyone has passed every barrier: nobody polls any more
             __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&sync[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // launch sequence (tags)
         }
     }
 }
@@ -339,6 +343,43 @@ __device__ __forceinline__ void sum_partials(const long long* __restrict__ p, in
     if (threadIdx.x < nq) out[threadIdx.x] = sum_rows(p, row, threadIdx.x);
 }
 
+// Lloyd-round partials are published as TAGGED words instead of behind a grid barrier: each
+// int64 word = tag << 42 | (fixed-point value mod 2^42), value = sum * 2^32 (a workgroup's sum of
+// at most KM_CHUNK_MAX unit components: |value| < 2^41).  tag = (launch sequence + 1) << 5 | round,
+// so a reader polls the words themselves until all KM_BLOCKS rows carry the round's tag: one
+// store and (usually) one load round trip per round instead of store + arrive + poll + load.
+// The rows are double-buffered by round parity: a workgroup writes round it+2 only after it read
+// round it+1 from every workgroup, each of which published it+1 only after reading round it.
+constexpr double KM_FXL = 4294967296.0;  // 2^32
+constexpr unsigned long long KM_VMASK = (1ull << 42) - 1;
+__device__ __forceinline__ long long km_tagged(unsigned tag, long long v) {
+    return (long long)(((unsigned long long)tag << 42) | ((unsigned long long)v & KM_VMASK));
+}
+__device__ __forceinline__ unsigned km_round_tag(unsigned seq, int it) { return (((seq + 1u) & 0x1FFFFu) << 5) | (unsigned)it; }
+// Exact sum of the KM_BLOCKS tagged words p[b * row + off] once every one carries `tag` (bounded
+// poll: a row that never arrives sets the error word, as km_grid_sync does).
+__device__ __forceinline__ float sum_rows_tagged(const long long* __restrict__ p, int row, int off, unsigned tag,
+                                                 unsigned* sync) {
+    long long v[KM_BLOCKS];
+    for (unsigned spins = 0;; spins++) {
+#pragma unroll
+        for (int b = 0; b < KM_BLOCKS; b++) v[b] = ld_c(p + b * row + off);
+        bool ready = true;
+#pragma unroll
+        for (int b = 0; b < KM_BLOCKS; b++) ready &= ((unsigned long long)v[b] >> 42) == tag;
+        if (ready) break;
+        if (spins == (1u << 20)) {
+            __hip_atomic_store(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    long long a = 0;
+#pragma unroll
+    for (int b = 0; b < KM_BLOCKS; b++) a += (long long)((unsigned long long)v[b] << 22) >> 22;  // sign-extend 42 bits
+    return (float)((double)a * (1.0 / KM_FXL));
+}
+
 // Centroid update from the per-workgroup partials (called by ALL threads of a workgroup): K*4
 // threads sum one (cluster, component) each in fixed workgroup order, K threads form the means, a
 // rare empty cluster is split from the largest one (faiss: +-1/1024 on alternating coordinates)
@@ -353,8 +394,9 @@ struct KmUpdLds {
 };
 
 template <int K>
-__device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmUpdLds<K>& L) {
-    sum_partials(part, K * 4, K * 4, L.sums);
+__device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmUpdLds<K>& L, unsigned tag,
+                          unsigned* sync) {
+    if (threadIdx.x < K * 4) L.sums[threadIdx.x] = sum_rows_tagged(part, K * 4, threadIdx.x, tag, sync);
     if (threadIdx.x == 0) L.any_empty = 0;
     __syncthreads();
     if (threadIdx.x < K) {
@@ -636,11 +678,13 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     __syncthreads();
     CL_STAMP(1);
     unsigned phase = 0;
+    const unsigned seq = __hip_atomic_load(&ws.sync[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (clustered) {
-        // ---- Lloyd rounds ----
+        // ---- Lloyd rounds (tagged partials, no grid barrier) ----
         constexpr int NQ = K * 4;
         for (int it = 0; it <= niter; it++) {
-            if (it > 0) km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd);
+            if (it > 0)
+                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, km_round_tag(seq, it - 1), ws.sync);
             CL_STAMP(2 + 2 * it);
             // assignment + per-cluster (x, y, z, count) sums of the chunk (fixed point, LDS u64 atomics)
             if (tid < NQ) L.acc[tid] = 0ull;
@@ -649,18 +693,21 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
                 const float x = L.pv[0][j], y = L.pv[1][j], z = L.pv[2][j];
                 const int a = nearest<K>(L.C, x, y, z);
                 L.pk[j] = a;
-                atomicAdd(&L.acc[4 * a], km_fix(x));
-                atomicAdd(&L.acc[4 * a + 1], km_fix(y));
-                atomicAdd(&L.acc[4 * a + 2], km_fix(z));
-                atomicAdd(&L.acc[4 * a + 3], (unsigned long long)KM_FX);
+                atomicAdd(&L.acc[4 * a], km_fixl(x));
+                atomicAdd(&L.acc[4 * a + 1], km_fixl(y));
+                atomicAdd(&L.acc[4 * a + 2], km_fixl(z));
+                atomicAdd(&L.acc[4 * a + 3], (unsigned long long)KM_FXL);
             }
             __syncthreads();
-            if (tid < NQ) st_c(ws.part + (it & 1) * KM_BLOCKS * NQ + blockIdx.x * NQ + tid, (long long)L.acc[tid]);
+            if (tid < NQ)
+                st_c(ws.part + (it & 1) * KM_BLOCKS * NQ + blockIdx.x * NQ + tid,
+                     km_tagged(km_round_tag(seq, it), (long long)L.acc[tid]));
             CL_STAMP(3 + 2 * it);
-            km_grid_sync(ws.sync, ++phase);
         }
         // ---- select: final cluster sizes = count column of the final-search partials ----
-        if (tid < K) L.cnt[tid] = sum_rows(ws.part + (niter & 1) * KM_BLOCKS * NQ, NQ, 4 * tid + 3);
+        if (tid < K)
+            L.cnt[tid] = sum_rows_tagged(ws.part + (niter & 1) * KM_BLOCKS * NQ, NQ, 4 * tid + 3, km_round_tag(seq, niter),
+                                         ws.sync);
         __syncthreads();
         CL_STAMP(57);
         select_clusters<K>(L.C, L.cnt, t_sim, L.sel, L.label_map);
@@ -883,7 +930,7 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint
                      void* stream) {
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
                 "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
-    NCN_REQUIRE(niter >= 0, hipErrorInvalidValue, "ncn_cluster_loss: niter < 0");
+    NCN_REQUIRE(niter >= 0 && niter <= 31, hipErrorInvalidValue, "ncn_cluster_loss: niter must be in [0, 31]");
     hipStream_t s = (hipStream_t)stream;
     if (K == 20)
         launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
