@@ -207,12 +207,13 @@ def _fused_march_ok(model, kw, n_rays):
 
 
 @torch.no_grad()
-def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=None, rng=None):
+def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=None, rng=None, out=None):
     """ncn_march_train_fused: RayAABBIntersector + near clamp (rendering.py:24-28) + RayMarcher
     (custom_functions.py:79-100) in two launches -> {'rays_a', 'xyzs', 'dirs', 'deltas', 'ts', 'counter'}
     with capacity-sized sample arrays (device count counter[0]).  noise: (R,) jitter, else
     rng = (seed, int64 device counter) draws it on the device (graph replays advance the counter),
-    else torch.rand_like as the reference (custom_functions.py:83)."""
+    else torch.rand_like as the reference (custom_functions.py:83).  out: a previous result (or
+    march_buffers()) whose tensors are overwritten in place; its '_slab' scratch is reused."""
     from ._lib import F32, I32, I64, U64, call, check_input, lib, ptr, stream
     rays_o = rays_o.contiguous().float()
     rays_d = rays_d.contiguous().float()
@@ -220,7 +221,8 @@ def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=N
     check_input(rays_d, "rays_d")
     R, dev, ms = rays_o.shape[0], rays_o.device, int(max_samples)
     cap = R * ms
-    ws = torch.empty((int(lib().ncn_march_train_fused_work_bytes(I64(R))) + 3) // 4, dtype=torch.int32, device=dev)
+    if out is None:
+        out = march_buffers(R, ms, dev)
     seed, ctr = 0, None
     if noise is not None:
         noise = noise.contiguous().float()
@@ -229,10 +231,9 @@ def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=N
         seed, ctr = rng
     else:
         noise = torch.rand_like(rays_o[:, 0])  # custom_functions.py:83
-    f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
-    slab_xyz, slab_t, slab_dt = f(cap * 3), f(cap), f(cap)
-    out = {"rays_a": torch.empty(R, 3, dtype=torch.int64, device=dev), "xyzs": f(cap, 3), "dirs": f(cap, 3),
-           "deltas": f(cap), "ts": f(cap), "counter": torch.empty(2, dtype=torch.int32, device=dev)}
+    if out["xyzs"].shape[0] != cap or out["rays_a"].shape[0] != R:
+        raise RuntimeError("march_train_fused: out= buffers are sized for another batch")
+    slab_xyz, slab_t, slab_dt, ws = out["_slab"]
     c, h = model._aabb
     call("ncn_march_train_fused", ptr(rays_o), ptr(rays_d), I64(R), F32(c[0]), F32(c[1]), F32(c[2]), F32(h[0]),
          F32(h[1]), F32(h[2]), F32(near_distance), ptr(noise), U64(int(seed) % 2 ** 64), ptr(ctr),
@@ -240,6 +241,28 @@ def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=N
          I32(ms), ptr(slab_xyz), ptr(slab_t), ptr(slab_dt), ptr(ws), ptr(out["rays_a"]), ptr(out["xyzs"]),
          ptr(out["dirs"]), ptr(out["deltas"]), ptr(out["ts"]), ptr(out["counter"]), stream())
     return out
+
+
+def march_buffers(R, max_samples, device, share_scratch=None):
+    """Output + scratch buffers of march_train_fused for R rays (capacity R*max_samples samples);
+    share_scratch: another march_buffers() whose scratch (slabs, work) is reused (never concurrently)."""
+    from ._lib import I64, lib
+    cap = R * int(max_samples)
+    f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=device)
+    if share_scratch is not None:
+        scratch = share_scratch["_slab"]
+    else:
+        ws = torch.empty((int(lib().ncn_march_train_fused_work_bytes(I64(R))) + 3) // 4, dtype=torch.int32,
+                         device=device)
+        scratch = (f(cap * 3), f(cap), f(cap), ws)
+    return {"rays_a": torch.empty(R, 3, dtype=torch.int64, device=device), "xyzs": f(cap, 3), "dirs": f(cap, 3),
+            "deltas": f(cap), "ts": f(cap), "counter": torch.empty(2, dtype=torch.int32, device=device),
+            "_slab": scratch}
+
+
+# march_uniform(seed, ctr + 1, r) == march_uniform(seed + RNG_NEXT_STEP, ctr, r) (csrc/vren.hip): the
+# pipelined trainer draws step k+1's jitter during step k from the same device step counter
+RNG_NEXT_STEP = (0x9E3779B97F4A7C15 * 0x100000001B3) % 2 ** 64
 
 
 @torch.no_grad()
