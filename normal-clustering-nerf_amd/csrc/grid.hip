@@ -28,7 +28,7 @@ namespace ncn {
 
 constexpr int GR_BLOCKS = 256;   // workgroups of the two grid-wide reductions (one partial per thread of the last)
 constexpr int GR_UNROLL = 8;   // float4 loads in flight per thread in the reductions
-constexpr int GS_ITER = 32;      // grid_select: cells per thread (8192 per workgroup, one Morton block)
+constexpr int GS_ITER = 8;       // grid_select: cells per thread (2048 per workgroup, one Morton block)
 
 // Workspace (ncn_grid_work_bytes): per-workgroup partials, the arrival counter (left zero by every
 // call), and the per-call scalars.
@@ -49,13 +49,14 @@ __device__ __forceinline__ uint32_t gr_compact3(uint32_t x) {  // morton3D_inver
     return x;
 }
 
-// splitmix64 of (seed, cell, stream) -> uniform in [0, 1) with 24 random bits
+// 32-bit counter-based hash of (seed, cell, stream) (murmur3 finaliser over a seed-keyed mix:
+// 32-bit multiplies only) -> uniform in [0, 1) with 24 random bits
 __device__ __forceinline__ float gr_uniform(uint64_t seed, uint32_t cell, uint32_t stream) {
-    uint64_t z = seed + 0x9E3779B97F4A7C15ull * ((uint64_t)cell * 8u + stream + 1u);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+    uint32_t h = (uint32_t)seed ^ (cell * 0x9E3779B1u + stream * 0x85EBCA77u);
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    h += (uint32_t)(seed >> 32);
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
 // torch.maximum: NaN if either operand is NaN
@@ -141,8 +142,8 @@ __global__ __launch_bounds__(256) void grid_occ_kernel(const float* __restrict__
     }
 }
 
-// 2. cells (index = Morton code of the coordinates, ngp_mt.py:255/260) in blocks of 8192 per
-//    workgroup, 32 per thread.  Pass 1: hit test; cells not hit take the update with
+// 2. cells (index = Morton code of the coordinates, ngp_mt.py:255/260) in blocks of 2048 per
+//    workgroup, 8 per thread.  Pass 1: hit test; cells not hit take the update with
 //    density_grid_tmp = 0 (ngp_mt.py:323-324) right here; per (round, wave) hit counts to LDS.  One
 //    atomic per workgroup reserves its slice of the hit list; pass 2 appends the hit cells' jittered
 //    positions (ngp_mt.py:318-319) in Morton order within the block.
@@ -175,16 +176,15 @@ __global__ __launch_bounds__(256) void grid_select_kernel(float* __restrict__ gr
         if (lane == 0) cnt[k][wv] = (int)__popcll(m);
     }
     __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the 128 counts in (round, wave) order, 2 per lane
-        const int q0 = 2 * lane, q1 = 2 * lane + 1;
-        const int c0 = (&cnt[0][0])[q0], c1 = (&cnt[0][0])[q1];
-        const int incl = wave_incl_sum_i(c0 + c1, lane);
-        int total = __shfl(incl, 63, 64);
+    static_assert(GS_ITER * 4 <= 64, "one count per lane");
+    if (threadIdx.x < 64) {  // exclusive scan of the GS_ITER*4 counts in (round, wave) order, one per lane
+        const int c0 = lane < GS_ITER * 4 ? (&cnt[0][0])[lane] : 0;
+        const int incl = wave_incl_sum_i(c0, lane);
+        const int total = __shfl(incl, 63, 64);
         int base = 0;
         if (lane == 63 && total > 0) base = atomicAdd(n_list, total);
         base = __shfl(base, 63, 64);
-        (&cnt[0][0])[q0] = base + incl - c0 - c1;
-        (&cnt[0][0])[q1] = base + incl - c1;
+        if (lane < GS_ITER * 4) (&cnt[0][0])[lane] = base + incl - c0;
     }
     __syncthreads();
     if (!hits) return;
