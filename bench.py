@@ -28,7 +28,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
-TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_walk", "ncn_field_fwd",
+TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
          "ncn_field_bwd", "ncn_cluster_loss")
 
 
