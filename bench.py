@@ -48,17 +48,16 @@ def composite_fw_roofline(model, batch, dev, reps=50):
     the batch is marched and the field evaluated once, then `reps` launches of the kernel are queued
     back to back behind a GPU spin (so host launch latency is hidden) between two events on the
     launch stream.  Returns (algorithmic bytes per launch, average launch duration in us)."""
-    from ncnerf_amd import _lib, vren
+    from ncnerf_amd import _lib
     from ncnerf_amd._lib import F32, I32, I64, ptr, stream
-    from ncnerf_amd.custom_functions import RayAABBIntersector
+    from ncnerf_amd.rendering import march_train_fused
     with torch.no_grad():
         o, d = batch["rays_o"].contiguous(), batch["rays_d"].contiguous()
         R = o.shape[0]
-        _, hits_t, _ = RayAABBIntersector.apply(o, d, model.center, model.half_size, 1)
-        t0 = hits_t[:, 0, 0]
-        t0.masked_fill_((t0 >= 0) & (t0 < 0.01), 0.01)
-        rays_a, xyzs, dirs, deltas, ts, _ = vren.raymarching_train(
-            o, d, hits_t[:, 0].contiguous(), model.density_bitfield, 1, 0.5, 0.0, torch.rand(R, device=dev), 128, 1024)
+        # the training step's marcher (its rays_a row order: long rays first)
+        mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(R, device=dev))
+        S = int(mk["counter"][0].item())
+        rays_a, xyzs, dirs, deltas, ts = mk["rays_a"], mk["xyzs"][:S], mk["dirs"][:S], mk["deltas"][:S], mk["ts"][:S]
         out = model(xyzs, dirs)
         sig, rgb = out["sigmas"].contiguous(), out["rgbs"].contiguous()
         S = sig.shape[0]

@@ -82,7 +82,9 @@ int ncn_march_train_pack(const float* rays_d, const int64_t* rays_a, int64_t n_r
  * *rng_counter, ray): graph replays draw fresh noise through the device counter) and the walk; then
  * the placement (every workgroup adds the sample counts of the rays before it) and the packing:
  * writes rays_a, the packed xyzs/dirs/deltas/ts (capacity R*max_samples rows, first counter[0]
- * valid) and counter = {S, R}.  Slabs as ncn_march_train_walk; work =
+ * valid) and counter = {S, R}.  Sample segments are in ray order; rays_a ROWS put the rays with
+ * more than 256 samples first (each class in ray order), so the compositors start them first (the
+ * reference's rows are in atomicAdd order: any row order is within its contract).  Slabs as ncn_march_train_walk; work =
  * ncn_march_train_fused_work_bytes(R) bytes of scratch.  R <= 16384. */
 int64_t ncn_march_train_fused_work_bytes(int64_t n_rays);
 int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_rays, float cx, float cy, float cz,

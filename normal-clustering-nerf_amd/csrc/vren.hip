@@ -505,6 +505,12 @@ __device__ __forceinline__ float march_uniform(uint64_t seed, uint64_t ctr, uint
 }
 
 constexpr int PLACE_MAX_WG = 256 * 16;  // workgroup sums one place workgroup can add in one round trip
+// rays_a ROW order of the training step: rays with more than PLACE_LONG samples (more than one
+// round of the compositors' row blocks) take the first rows, so the compositors dispatch their
+// waves first and their extra round trip overlaps the rest of the launch.  Sample segments stay in
+// ray order.  (The reference's rows and starts are both in atomicAdd order, raymarching.cu:237-241:
+// any row order is within its contract; consumers index outputs by rays_a[:, 0].)
+constexpr int PLACE_LONG = 256;
 
 template <bool ONE_CASCADE, int P>
 __global__ __launch_bounds__(256) void march_train_walk2_kernel(
@@ -549,7 +555,12 @@ __global__ __launch_bounds__(256) void march_train_walk2_kernel(
         if (live) counts[r] = n;
     }
     __syncthreads();
-    if (threadIdx.x == 0) wg_sum[blockIdx.x] = cnt_s[0] + cnt_s[1] + cnt_s[2] + cnt_s[3];
+    if (threadIdx.x == 0) {  // sample sum | number of long rays << 26 (rays placed first by march_train_place)
+        int nl = 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) nl += cnt_s[w] > PLACE_LONG;
+        wg_sum[blockIdx.x] = (cnt_s[0] + cnt_s[1] + cnt_s[2] + cnt_s[3]) | (nl << 26);
+    }
 }
 
 __global__ __launch_bounds__(256) void march_train_place_kernel(
@@ -557,15 +568,16 @@ __global__ __launch_bounds__(256) void march_train_place_kernel(
     const int32_t* __restrict__ wg_sum, const float* __restrict__ slab_xyz, const float* __restrict__ slab_t,
     const float* __restrict__ slab_dt, int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
     float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts, int32_t* __restrict__ counter) {
-    __shared__ int red[4];
+    __shared__ int red[4], redl[4], redt[4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.x;
-    // exclusive prefix over the workgroup sums [0, b): 16 loads per thread, all in flight
+    // exclusive prefix over the workgroup sums [0, b) and the total of long rays: 16 loads per
+    // thread (every workgroup's word), all in flight
     int v[PLACE_MAX_WG / 256];
 #pragma unroll
     for (int u = 0; u < PLACE_MAX_WG / 256; u++) {
         const int i = u * 256 + threadIdx.x;
-        v[u] = i < b ? wg_sum[i] : 0;
+        v[u] = i < (int)gridDim.x ? wg_sum[i] : 0;
     }
     const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(b * 4 + wv));
     const bool live = r0 < R;
@@ -585,27 +597,47 @@ __global__ __launch_bounds__(256) void march_train_place_kernel(
         pt[q] = q * 64 + lane < n ? st[q * 64 + lane] : 0.f;
         pd[q] = q * 64 + lane < n ? sd[q * 64 + lane] : 0.f;
     }
-    int acc = 0;
+    int acc = 0, lpre = 0, ltot = 0;  // samples before this workgroup, long rays before it, in all
 #pragma unroll
-    for (int u = 0; u < PLACE_MAX_WG / 256; u++) acc += v[u];
+    for (int u = 0; u < PLACE_MAX_WG / 256; u++) {
+        const int i = u * 256 + threadIdx.x;
+        const int nl = (int)((unsigned)v[u] >> 26);
+        if (i < b) {
+            acc += v[u] & ((1 << 26) - 1);
+            lpre += nl;
+        }
+        ltot += nl;
+    }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) red[wv] = acc;
+    for (int off = 32; off >= 1; off >>= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        lpre += __shfl_xor(lpre, off, 64);
+        ltot += __shfl_xor(ltot, off, 64);
+    }
+    if (lane == 0) { red[wv] = acc; redl[wv] = lpre; redt[wv] = ltot; }
     __syncthreads();
     int start = red[0] + red[1] + red[2] + red[3];
+    const int long_before = redl[0] + redl[1] + redl[2] + redl[3];
+    const int long_total = redt[0] + redt[1] + redt[2] + redt[3];
     __syncthreads();
     if (lane == 0) red[wv] = n;
     __syncthreads();
-    for (int w = 0; w < wv; w++) start += red[w];
+    int lw = 0;  // long rays among the earlier waves of this workgroup
+    for (int w = 0; w < wv; w++) {
+        start += red[w];
+        lw += red[w] > PLACE_LONG;
+    }
+    const int64_t row = n > PLACE_LONG ? (int64_t)(long_before + lw)
+                                       : (int64_t)long_total + (4 * (int64_t)b - long_before) + (wv - lw);
     if (b == (int)gridDim.x - 1 && threadIdx.x == 0) {
         counter[0] = start + red[0] + red[1] + red[2] + red[3];  // (thread 0: start = the workgroup's prefix)
         counter[1] = (int32_t)R;
     }
     if (!live) return;
     if (lane == 0) {
-        rays_a[3 * r] = r;
-        rays_a[3 * r + 1] = start;
-        rays_a[3 * r + 2] = n;
+        rays_a[3 * row] = r;
+        rays_a[3 * row + 1] = start;
+        rays_a[3 * row + 2] = n;
     }
     float* ox = xyzs + 3 * (int64_t)start;
     float* od = dirs + 3 * (int64_t)start;
@@ -1277,7 +1309,8 @@ int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_ra
     NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && grid_size <= 1024 && max_samples >= 1 && work != nullptr,
                 hipErrorInvalidValue, "ncn_march_train_fused: bad cascades/grid_size/max_samples/work");
     const int64_t nwg = cdiv(n_rays, 4);
-    NCN_REQUIRE(nwg <= PLACE_MAX_WG && n_rays * (int64_t)max_samples < (1ll << 31), hipErrorInvalidValue,
+    NCN_REQUIRE(nwg <= PLACE_MAX_WG && n_rays * (int64_t)max_samples < (1ll << 31) && max_samples < (1 << 24),
+                hipErrorInvalidValue,
                 "ncn_march_train_fused: n_rays must be <= %d (and n_rays * max_samples < 2^31)", 4 * PLACE_MAX_WG);
     int32_t* counts = (int32_t*)work;
     int32_t* wg_sum = counts + n_rays;
