@@ -109,9 +109,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grid-update", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager (Python-launched) step instead of a HIP graph")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="pipelined graph step: march the next batch during the current one's losses (measured "
-                         "slower on this runtime: DESIGN.md)")
     args = ap.parse_args()
 
     from ncnerf_amd import _lib, distributed
@@ -137,13 +134,8 @@ def main():
     step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
     if trainer.update_grid:  # first-call costs of the refresh path stay out of the timed region
         model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
-    pipe = args.pipeline and not args.no_graph
-
-    def nxt(k):  # the pipelined step marches the following step's batch during this one
-        return batches[(k + 1) % n_batches] if pipe else None
-
     for k in range(args.warmup):
-        trainer.step(batches[k % n_batches], global_step=step0 + k, next_batch=nxt(k))
+        trainer.step(batches[k % n_batches], global_step=step0 + k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -153,8 +145,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        results, _ = trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k,
-                                  next_batch=nxt(args.warmup + k))
+        results, _ = trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k)
         counts.append((results["rm_samples"].clone(), results["vr_samples"].clone()))
     torch.cuda.synchronize()
     if world > 1:
@@ -209,7 +200,7 @@ def main():
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
-                   "step": "eager" if args.no_graph else ("hip_graph_pipelined" if pipe else "hip_graph")},
+                   "step": "eager" if args.no_graph else "hip_graph"},
         "samples_per_s": round(float(tot[0].item()) / el, 1),
         "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),

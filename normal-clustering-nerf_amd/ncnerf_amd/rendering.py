@@ -260,10 +260,6 @@ def march_buffers(R, max_samples, device, share_scratch=None):
             "_slab": scratch}
 
 
-# march_uniform(seed, ctr + 1, r) == march_uniform(seed + RNG_NEXT_STEP, ctr, r) (csrc/vren.hip): the
-# pipelined trainer draws step k+1's jitter during step k from the same device step counter
-RNG_NEXT_STEP = (0x9E3779B97F4A7C15 * 0x100000001B3) % 2 ** 64
-
 
 @torch.no_grad()
 def march_train_static(model, rays_o, rays_d, out=None, **kwargs):

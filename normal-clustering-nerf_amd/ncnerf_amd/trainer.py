@@ -9,7 +9,7 @@ import torch
 from . import distributed
 from .losses import NeRFMTLoss
 from .optim import FlatAdam
-from .rendering import RNG_NEXT_STEP, march_buffers, march_train_fused, render
+from .rendering import render
 
 HYPERSIM_HPARAMS = dict(
     scale=0.5, grid_size=128, rend_max_samples=1024, rend_near_dist=0.01, density_tresh_decay=1.0,
@@ -43,8 +43,6 @@ class Trainer:
             thr = 0.01 * self.h["rend_max_samples"] / 3 ** 0.5 * self.h["density_tresh_decay"]
             m.update_density_grid(thr, warmup=global_step < self.warmup_steps)
             distributed.broadcast_occupancy(m)
-            return True
-        return False
 
     # -- graph-captured step ---------------------------------------------------------------------
     # The whole step (zero_grad, render with static shapes, losses, backward, [optimizer]) is one
@@ -53,34 +51,15 @@ class Trainer:
     # replay costs one launch instead of ~150 Python-driven ones.  Inputs are copied into the
     # graph's static batch buffers; the occupancy-grid refresh and the RCCL all-reduce (N > 1)
     # run eagerly around it.
-    def _march_into(self, batch, step_dev, buf, next_step=False):
-        """march_train_fused of `batch` into the fixed buffers `buf` (jitter: the batch's march_noise,
-        else the device RNG at step_dev (+1 when next_step))."""
-        noise = batch.get("march_noise")
-        rng = None if noise is not None else ((self._rng_seed + (RNG_NEXT_STEP if next_step else 0)) % 2 ** 64,
-                                              step_dev)
-        march_train_fused(self.model, batch["rays_o"], batch["rays_d"], self.render_kwargs["near_distance"],
-                          self.render_kwargs["max_samples"], noise=noise, rng=rng, out=buf)
-
-    def _body(self, batch, step_dev, with_opt, pm=None, nxt=None):
-        """One step.  pm: this batch's samples, marched ahead (pipelined step); nxt = (next batch,
-        buffers): march the next batch on a side stream while this step's losses run (the clustering
-        kernel leaves most CUs idle), joined at the end of the step."""
+    def _body(self, batch, step_dev, with_opt):
         m = self.model
         self.opt.zero_grad()
         kw = dict(self.render_kwargs, global_step=0, static_shapes=True)
-        if pm is not None:
-            kw["premarched"] = pm
-        elif "march_noise" in batch:
+        if "march_noise" in batch:
             kw["march_noise"] = batch["march_noise"]
         else:  # jitter drawn on the device from the step counter: no torch RNG node in the graph
             kw["march_rng"] = (self._rng_seed, step_dev)
         results = render(m, batch["rays_o"], batch["rays_d"], **kw)
-        if nxt is not None:
-            main = torch.cuda.current_stream()
-            self._mstream.wait_stream(main)
-            with torch.cuda.stream(self._mstream):
-                self._march_into(nxt[0], step_dev, nxt[1], next_step=True)
         loss_d = self.loss(results, batch, global_step=step_dev)
         total = loss_d["total"]
         if getattr(self, "_one", None) is None or self._one.device != total.device:
@@ -88,8 +67,6 @@ class Trainer:
         torch.autograd.backward(total, grad_tensors=self._one)  # (no ones_like fill node per step)
         if with_opt:
             self.opt.step()
-        if nxt is not None:
-            torch.cuda.current_stream().wait_stream(self._mstream)
         return results, loss_d
 
     def _capture(self, batch):
@@ -134,79 +111,9 @@ class Trainer:
             self.opt.step_count += 1
         return self._out
 
-    # -- pipelined graph step -------------------------------------------------------------------
-    # step(batch, global_step, next_batch): graph `c` renders the batch from march buffers c
-    # (marched during the previous step) and marches next_batch into buffers 1-c on a side stream
-    # concurrently with its losses; the two graphs alternate.  The first step and every step
-    # after a grid refresh march their own batch eagerly first (a premarch used the old grid).
-    def _pipe_setup(self, batch, next_batch):
-        dev = batch["rays_o"].device
-        R = batch["rays_o"].shape[0]
-        ms = self.render_kwargs["max_samples"]
-        a = march_buffers(R, ms, dev)
-        self._mbuf = [a, march_buffers(R, ms, dev, share_scratch=a)]
-        self._mstream = torch.cuda.Stream(device=dev)
-        self._p_static = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in batch.items()}
-        self._p_next = {k: next_batch[k].clone() for k in ("rays_o", "rays_d", "march_noise") if k in next_batch}
-        self._p_step_dev = torch.zeros((), dtype=torch.int64, device=dev)
-        self._p_with_opt = not distributed.is_distributed()
-        self._pgraphs = [None, None]
-        self._cur, self._pm_valid = 0, False
-
-    def _pipe_capture(self, c):
-        dev = self._p_step_dev.device
-        state = self.opt.state_tensors()
-        saved = [t.clone() for t in state]  # warm-up steps must not advance training
-        saved_count = self.opt.step_count
-        args = (self._p_static, self._p_step_dev, self._p_with_opt, self._mbuf[c], (self._p_next, self._mbuf[1 - c]))
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                self._body(*args)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            out = self._body(*args)
-        for t, v in zip(state, saved):
-            t.copy_(v)
-        self.opt.step_count = saved_count
-        self._pgraphs[c] = (g, out)
-
-    def _pipe_step(self, batch, global_step, next_batch, refreshed):
-        if getattr(self, "_pgraphs", None) is None:
-            self._pipe_setup(batch, next_batch)
-        dst, src = [], []
-        for k, v in batch.items():
-            if k in self._p_static and hasattr(v, "copy_") and v is not self._p_static[k]:
-                dst.append(self._p_static[k])
-                src.append(v)
-        for k, v in self._p_next.items():
-            dst.append(v)
-            src.append(next_batch[k])
-        torch._foreach_copy_(dst, src, non_blocking=True)  # one launch for both batches
-        self._p_step_dev.fill_(global_step)
-        c = self._cur
-        if refreshed or not self._pm_valid:  # no valid premarch of this batch: march it now
-            self._march_into(self._p_static, self._p_step_dev, self._mbuf[c])
-        if self._pgraphs[c] is None:
-            self._pipe_capture(c)
-        g, out = self._pgraphs[c]
-        g.replay()
-        if not self._p_with_opt:
-            self.opt.step(grad_scale=distributed.allreduce_grads(self.model.flat_grad(), average=False))
-        else:
-            self.opt.step_count += 1
-        self._cur, self._pm_valid = 1 - c, True
-        return out
-
-    def step(self, batch, global_step, next_batch=None):
-        """One training step.  next_batch (graph mode): the batch of the following step, marched
-        during this one (the pipelined step); pass the same next_batch as the next call's batch."""
+    def step(self, batch, global_step):
         m = self.model
-        refreshed = self._maybe_update_grid(global_step)
-        if self.use_graph and next_batch is not None and self.render_kwargs.get("anneal_steps", 0) == 0:
-            return self._pipe_step(batch, global_step, next_batch, refreshed)
+        self._maybe_update_grid(global_step)
         if self.use_graph:
             return self._graph_step(batch, global_step)
         self.opt.zero_grad()

@@ -78,53 +78,3 @@ def test_graph_step_matches_eager(dev):
     # the MLP weights (dense, large gradients) agree tightly
     rel_w = float((params[2][n_t:] - params[0][n_t:]).norm() / params[0][n_t:].norm())
     assert rel_w < 1e-3, rel_w
-
-
-def test_pipelined_step_matches_graph_step(dev):
-    """Trainer.step(batch, k, next_batch) (graph c renders buffers c marched during the previous
-    step and marches the next batch on a side stream during its losses) == the plain graph step:
-    over 8 steps (a grid refresh at the first) the marched sample counts are identical and the
-    parameters within the run-to-run floor (float-atomic summation order: plain vs plain again).
-    Continuing across the next refresh (global_step % 16 == 0: the premarch is stale and the batch
-    must be re-marched), every step's sample count equals a fresh march of its batch on the grid
-    of that step (device RNG jitter of that step)."""
-    from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
-    from ncnerf_amd.rendering import march_train_fused
-    from ncnerf_amd.synthetic import SyntheticScene
-    from ncnerf_amd.trainer import Trainer
-    scene = SyntheticScene()
-    batches = [scene.torch_batch(2048, seed=100 + k, device=dev) for k in range(5)]
-    outs = []
-    for pipelined in (False, False, True):
-        torch.manual_seed(0)
-        m = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
-        with torch.no_grad():
-            m.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
-            m.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
-        tr = Trainer(m, update_grid=True, use_graph=True)
-        rm = []
-        for k in range(8):  # 3008 .. 3015: refresh at 3008 only
-            b, nb = batches[k % 5], batches[(k + 1) % 5]
-            torch.manual_seed(1000 + k)  # the refresh draws its seed from the CPU generator
-            res, _ = tr.step(b, 3008 + k, next_batch=nb if pipelined else None)
-            rm.append(int(res["rm_samples"].item()))
-        torch.cuda.synchronize()
-        outs.append((m.flat_params().clone(), rm))
-    (p0, r0), (pf, _), (p1, r1) = outs  # plain, plain again (run-to-run floor), pipelined
-    assert r0 == r1
-    n_t = m._n_table
-    floor = int(((pf[:n_t] - p0[:n_t]).abs() > 1e-4).sum())
-    d = (p1[:n_t] - p0[:n_t]).abs()
-    assert int((d > 1e-4).sum()) <= 3 * floor + 1e-5 * n_t, (int((d > 1e-4).sum()), floor)
-    floor6 = float(((pf[:n_t] - p0[:n_t]).abs() > 1e-6).float().mean())
-    assert float((d > 1e-6).float().mean()) < 3 * floor6 + 1e-3, (float((d > 1e-6).float().mean()), floor6)
-    fw = float((pf[n_t:] - p0[n_t:]).norm() / p0[n_t:].norm())
-    assert float((p1[n_t:] - p0[n_t:]).norm() / p0[n_t:].norm()) < 3 * fw + 1e-3, fw
-    # the pipelined trainer continues across the refresh at 3016
-    for k in range(8, 12):
-        step, b, nb = 3008 + k, batches[k % 5], batches[(k + 1) % 5]
-        res, _ = tr.step(b, step, next_batch=nb)
-        got = int(res["rm_samples"].item())
-        ref = march_train_fused(m, b["rays_o"], b["rays_d"], 0.01, 1024,
-                                rng=(tr._rng_seed, torch.tensor(step, device=dev)))
-        assert got == int(ref["counter"][0].item()), (step, got)
