@@ -274,8 +274,8 @@ __device__ __forceinline__ unsigned long long km_fix(float v) {
     return (unsigned long long)__double2ll_rn((double)v * KM_FX);
 }
 __device__ __forceinline__ float km_unfix(long long q) { return (float)((double)q * (1.0 / KM_FX)); }
-__device__ __forceinline__ unsigned long long km_fixl(float v) {  // Lloyd partials: 2^32 (tagged words)
-    return (unsigned long long)__double2ll_rn((double)v * 4294967296.0);
+__device__ __forceinline__ unsigned long long km_fixl(float v) {  // Lloyd partials: 2^39 (tagged words)
+    return (unsigned long long)__double2ll_rn((double)v * 549755813888.0);
 }
 
 // Cross-workgroup data moves with agent-scope (sc1) loads and stores only (MI355X_MICROARCH.md,
@@ -308,7 +308,9 @@ __device__ __forceinline__ void km_grid_sync(unsigned* sync, unsigned phase) {
     }
     __syncthreads();
 }
-// Every workgroup calls this once, last: the final departure resets the barrier words.
+// Every workgroup calls this once, last: the final departure resets the barrier words and advances
+// the launch sequence of the Lloyd tags (every launch, so a launch that did not cluster never
+// leaves the next one with the tags of an older launch's partials).
 __device__ __forceinline__ void km_grid_exit(unsigned* sync) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -344,18 +346,23 @@ __device__ __forceinline__ void sum_partials(const long long* __restrict__ p, in
 }
 
 // Lloyd-round partials are published as TAGGED words instead of behind a grid barrier: each
-// int64 word = tag << 42 | (fixed-point value mod 2^42), value = sum * 2^32 (a workgroup's sum of
-// at most KM_CHUNK_MAX unit components: |value| < 2^41).  tag = (launch sequence + 1) << 5 | round,
+// int64 word = tag << 50 | (fixed-point value mod 2^50), value = sum * 2^39 (a workgroup's sum of
+// at most KM_CHUNK_MAX = 512 unit components: |value| <= 2^48; the precision of the barrier-based
+// 2^40 sums within a factor 2).  tag = ((launch sequence + 1) mod 2^9) << 5 | round; every launch
+// writes every word of both buffers (a launch that does not cluster writes void tags), so a word
+// is never older than the previous launch and 9 sequence bits cannot alias,
 // so a reader polls the words themselves until all KM_BLOCKS rows carry the round's tag: one
 // store and (usually) one load round trip per round instead of store + arrive + poll + load.
 // The rows are double-buffered by round parity: a workgroup writes round it+2 only after it read
 // round it+1 from every workgroup, each of which published it+1 only after reading round it.
-constexpr double KM_FXL = 4294967296.0;  // 2^32
-constexpr unsigned long long KM_VMASK = (1ull << 42) - 1;
+constexpr double KM_FXL = 549755813888.0;  // 2^39
+constexpr int KM_TAG_SHIFT = 50;
+constexpr unsigned long long KM_VMASK = (1ull << KM_TAG_SHIFT) - 1;
+constexpr unsigned KM_VOID_ROUND = 31;  // round field of the void words (niter <= 30)
 __device__ __forceinline__ long long km_tagged(unsigned tag, long long v) {
-    return (long long)(((unsigned long long)tag << 42) | ((unsigned long long)v & KM_VMASK));
+    return (long long)(((unsigned long long)tag << KM_TAG_SHIFT) | ((unsigned long long)v & KM_VMASK));
 }
-__device__ __forceinline__ unsigned km_round_tag(unsigned seq, int it) { return (((seq + 1u) & 0x1FFFFu) << 5) | (unsigned)it; }
+__device__ __forceinline__ unsigned km_round_tag(unsigned seq, int it) { return (((seq + 1u) & 0x1FFu) << 5) | (unsigned)it; }
 // Exact sum of the KM_BLOCKS tagged words p[b * row + off] once every one carries `tag` (bounded
 // poll: a row that never arrives sets the error word, as km_grid_sync does).
 __device__ __forceinline__ float sum_rows_tagged(const long long* __restrict__ p, int row, int off, unsigned tag,
@@ -366,7 +373,7 @@ __device__ __forceinline__ float sum_rows_tagged(const long long* __restrict__ p
         for (int b = 0; b < KM_BLOCKS; b++) v[b] = ld_c(p + b * row + off);
         bool ready = true;
 #pragma unroll
-        for (int b = 0; b < KM_BLOCKS; b++) ready &= ((unsigned long long)v[b] >> 42) == tag;
+        for (int b = 0; b < KM_BLOCKS; b++) ready &= ((unsigned long long)v[b] >> KM_TAG_SHIFT) == tag;
         if (ready) break;
         if (spins == (1u << 20)) {
             __hip_atomic_store(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -376,7 +383,8 @@ __device__ __forceinline__ float sum_rows_tagged(const long long* __restrict__ p
     }
     long long a = 0;
 #pragma unroll
-    for (int b = 0; b < KM_BLOCKS; b++) a += (long long)((unsigned long long)v[b] << 22) >> 22;  // sign-extend 42 bits
+    for (int b = 0; b < KM_BLOCKS; b++)  // sign-extend the 50-bit values
+        a += (long long)((unsigned long long)v[b] << (64 - KM_TAG_SHIFT)) >> (64 - KM_TAG_SHIFT);
     return (float)((double)a * (1.0 / KM_FXL));
 }
 
@@ -679,6 +687,13 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     CL_STAMP(1);
     unsigned phase = 0;
     const unsigned seq = __hip_atomic_load(&ws.sync[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!clustered || niter == 0) {  // the buffers the Lloyd rounds do not write get void words
+        const long long vw = km_tagged(km_round_tag(seq, KM_VOID_ROUND), 0);
+        for (int q = tid; q < K * 4; q += KM_THREADS) {
+            if (!clustered) st_c(ws.part + blockIdx.x * K * 4 + q, vw);
+            st_c(ws.part + (KM_BLOCKS + blockIdx.x) * K * 4 + q, vw);
+        }
+    }
     if (clustered) {
         // ---- Lloyd rounds (tagged partials, no grid barrier) ----
         constexpr int NQ = K * 4;
@@ -846,7 +861,7 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
         }
     }
     CL_STAMP(60);
-    if (clustered) km_grid_exit(ws.sync);
+    km_grid_exit(ws.sync);  // every launch (clustered or not) advances the tag sequence
 }
 
 template <int K>
@@ -930,7 +945,7 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint
                      void* stream) {
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
                 "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
-    NCN_REQUIRE(niter >= 0 && niter <= 31, hipErrorInvalidValue, "ncn_cluster_loss: niter must be in [0, 31]");
+    NCN_REQUIRE(niter >= 0 && niter <= 30, hipErrorInvalidValue, "ncn_cluster_loss: niter must be in [0, 30]");
     hipStream_t s = (hipStream_t)stream;
     if (K == 20)
         launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,

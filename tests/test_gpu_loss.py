@@ -174,3 +174,17 @@ def test_fused_nerf_loss_matches_unfused(dev):
         for x, y in zip(g0, g1):
             rel = float((y - x).norm() / x.norm().clamp_min(1e-30))
             assert rel < 1e-5, rel
+
+
+def test_cluster_after_unclustered_call(dev):
+    """A launch with too few normals must not leave the next clustered launch reading an older
+    launch's Lloyd partials (the tag sequence advances on every launch)."""
+    for seed in (3, 4):
+        X = _manhattan_normals(6272, seed=seed)
+        L.cluster_losses(torch.from_numpy(X).to(dev), K=20, niter=20, seed=1234)
+        L.cluster_losses(torch.from_numpy(_manhattan_normals(12, seed=seed)).to(dev), K=20)
+    X = _manhattan_normals(6272, seed=6272)  # the data of test_cluster_loss_parity[6272-0]
+    valid = losses_ref.valid_normals_mask(torch.from_numpy(X)).numpy()
+    C, a = losses_ref.spherical_kmeans(X[valid], K=20, niter=20, seed=1234)
+    _, labels, cents, _ = L.cluster_losses(torch.from_numpy(X).to(dev), K=20, niter=20, seed=1234, t_similar=0.99)
+    np.testing.assert_allclose(cents.cpu().numpy(), C, atol=1e-5)
