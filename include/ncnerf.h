@@ -170,6 +170,11 @@ int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void*
 /* ---- normal clustering loss path: replaces _extract_normals_from_ray_batch
  *      (hypersim_src/utils.py:504-541) and the faiss + torch cluster block of NeRFMTLoss
  *      (losses.py:47-166, 420-478). ---- */
+/* ncn_photo_loss_fwd + ncn_normals_fwd in one launch (the fused loss node's independent parts). */
+int ncn_photo_normals_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays,
+                          float w_opacity, float* loss, const float* rays_o, const float* rays_d, const float* depth,
+                          const int64_t* x1, const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals,
+                          void* stream);
 int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
                     const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals, void* stream);
 /* dL_ddepth += ...; if term_weights (3 device floats) is non-NULL, dL_dnormals is the (3,n_tri,3)

@@ -17,12 +17,10 @@ __device__ __forceinline__ void tri_points(const float* __restrict__ o, const fl
     for (int k = 0; k < 3; k++) P[k] = o[3 * i + k] + d[3 * i + k] * depth[i];
 }
 
-__global__ void normals_fwd_kernel(const float* __restrict__ o, const float* __restrict__ d,
-                                   const float* __restrict__ depth, const int64_t* __restrict__ x1,
-                                   const int64_t* __restrict__ x2, const int64_t* __restrict__ x3, int64_t T,
-                                   float* __restrict__ normals) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= T) return;
+__device__ __forceinline__ void normals_fwd_one(const float* __restrict__ o, const float* __restrict__ d,
+                                                const float* __restrict__ depth, const int64_t* __restrict__ x1,
+                                                const int64_t* __restrict__ x2, const int64_t* __restrict__ x3,
+                                                int64_t t, float* __restrict__ normals) {
     float P1[3], P2[3], P3[3];
     tri_points(o, d, depth, x1[t], P1);
     tri_points(o, d, depth, x2[t], P2);
@@ -34,6 +32,15 @@ __global__ void normals_fwd_kernel(const float* __restrict__ o, const float* __r
     normals[3 * t] = c0 / nrm;
     normals[3 * t + 1] = c1 / nrm;
     normals[3 * t + 2] = c2 / nrm;
+}
+
+__global__ void normals_fwd_kernel(const float* __restrict__ o, const float* __restrict__ d,
+                                   const float* __restrict__ depth, const int64_t* __restrict__ x1,
+                                   const int64_t* __restrict__ x2, const int64_t* __restrict__ x3, int64_t T,
+                                   float* __restrict__ normals) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= T) return;
+    normals_fwd_one(o, d, depth, x1, x2, x3, t, normals);
 }
 
 // d/d depth through P_k = o + d*depth, a = P2-P1, b = P3-P1, c = a x b, n = c / max(|c|, eps):
@@ -96,10 +103,9 @@ __global__ void normals_bwd_kernel(const float* __restrict__ o, const float* __r
 // ---- photometric MSE + opacity entropy (losses.py:349-362, validity filter :246-262) ----
 // One workgroup: loss[0] = mean((rgb - gt)^2), loss[1] = w_op * mean(-o log o), o = opacity + 1e-10.
 constexpr int PH_THREADS = 1024;
-__global__ __launch_bounds__(PH_THREADS) void photo_loss_fwd_kernel(const float* __restrict__ rgb,
-                                                                    const float* __restrict__ gt,
-                                                                    const float* __restrict__ op, int64_t R,
-                                                                    float w_op, float* __restrict__ loss) {
+__device__ __forceinline__ void photo_loss_fwd_wg(const float* __restrict__ rgb, const float* __restrict__ gt,
+                                                  const float* __restrict__ op, int64_t R, float w_op,
+                                                  float* __restrict__ loss) {
     __shared__ float red[2][PH_THREADS / 64];
     float a = 0.f, b = 0.f;
     for (int64_t i = threadIdx.x; i < R; i += PH_THREADS) {
@@ -124,6 +130,29 @@ __global__ __launch_bounds__(PH_THREADS) void photo_loss_fwd_kernel(const float*
         loss[2] = isfinite(mse) ? 1.f : 0.f;
         loss[3] = isfinite(ent) ? 1.f : 0.f;
     }
+}
+
+__global__ __launch_bounds__(PH_THREADS) void photo_loss_fwd_kernel(const float* __restrict__ rgb,
+                                                                    const float* __restrict__ gt,
+                                                                    const float* __restrict__ op, int64_t R,
+                                                                    float w_op, float* __restrict__ loss) {
+    photo_loss_fwd_wg(rgb, gt, op, R, w_op, loss);
+}
+
+// The photometric/opacity reduction (workgroup 0) and the normals from depth (the other
+// workgroups, one triangle per thread) in one launch: the two independent forward parts of the
+// fused loss node.
+__global__ __launch_bounds__(PH_THREADS) void photo_normals_fwd_kernel(
+    const float* __restrict__ rgb, const float* __restrict__ gt, const float* __restrict__ op, int64_t R, float w_op,
+    float* __restrict__ loss, const float* __restrict__ o, const float* __restrict__ d,
+    const float* __restrict__ depth, const int64_t* __restrict__ x1, const int64_t* __restrict__ x2,
+    const int64_t* __restrict__ x3, int64_t T, float* __restrict__ normals) {
+    if (blockIdx.x == 0) {
+        photo_loss_fwd_wg(rgb, gt, op, R, w_op, loss);
+        return;
+    }
+    const int64_t t = (int64_t)(blockIdx.x - 1) * PH_THREADS + threadIdx.x;
+    if (t < T) normals_fwd_one(o, d, depth, x1, x2, x3, t, normals);
 }
 // grads scaled by the upstream gradient g[0..1] (device scalars) and zeroed for filtered terms
 __global__ void photo_loss_bwd_kernel(const float* __restrict__ rgb, const float* __restrict__ gt,
@@ -896,6 +925,17 @@ int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opaci
     hipLaunchKernelGGL(photo_loss_bwd_kernel, dim3(cdiv(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rgb, rgb_gt,
                        opacity, n_rays, w_opacity, loss, upstream, dL_drgb, dL_dopacity);
     NCN_LAUNCH_CHECK("ncn_photo_loss_bwd");
+    return 0;
+}
+
+int ncn_photo_normals_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays,
+                          float w_opacity, float* loss, const float* rays_o, const float* rays_d, const float* depth,
+                          const int64_t* x1, const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals,
+                          void* stream) {
+    hipLaunchKernelGGL(photo_normals_fwd_kernel, dim3(1 + cdiv(std::max<int64_t>(n_tri, 0), PH_THREADS)),
+                       dim3(PH_THREADS), 0, (hipStream_t)stream, rgb, rgb_gt, opacity, n_rays, w_opacity, loss, rays_o,
+                       rays_d, depth, x1, x2, x3, n_tri, normals);
+    NCN_LAUNCH_CHECK("ncn_photo_normals_fwd");
     return 0;
 }
 

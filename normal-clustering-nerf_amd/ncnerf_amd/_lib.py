@@ -48,6 +48,7 @@ SIGNATURES = {
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],
     "ncn_photo_loss_fwd": [P, P, P, I64, F32, P, P],
+    "ncn_photo_normals_fwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, I64, P, P],
     "ncn_photo_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P],
     "ncn_cluster_workspace_words": [I32],
     "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, F32, F32, P, P, P, P, P, P, P],

@@ -222,10 +222,9 @@ class _NeRFLossFused(torch.autograd.Function):
         T = x1.shape[0]
         dev = rgb.device
         photo = torch.empty(4, dtype=torch.float32, device=dev)
-        call("ncn_photo_loss_fwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(w_op), ptr(photo), stream())
         normals = torch.empty(T, 3, dtype=torch.float32, device=dev)
-        call("ncn_normals_fwd", ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals),
-             stream())
+        call("ncn_photo_normals_fwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(w_op), ptr(photo),
+             ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals), stream())
         out = torch.empty(N_OUT, dtype=torch.float32, device=dev)
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
