@@ -797,13 +797,17 @@ __global__ __launch_bounds__(256) void ray_aabb_kernel(const float* __restrict__
 // The ray handled by this wave and its segment.  The wave index is clamped instead of returning
 // early so the kernarg, rays_a and array-pointer loads issue as one scalar batch; `live` guards
 // the per-ray stores of the (at most 3) surplus waves of the last block.
+// Waves (rays) per workgroup of the compositors.
+#ifndef CF_WPB
+#define CF_WPB 4
+#endif
 struct RaySeg {
     int64_t ray, start;
     int N;
     bool live;
 };
 __device__ __forceinline__ RaySeg load_ray_seg(const int64_t* __restrict__ rays_a, int64_t R) {
-    const int64_t n0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int64_t n0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * CF_WPB + (threadIdx.x >> 6)));
     const int64_t n = n0 < R ? n0 : R - 1;
     RaySeg s;
     s.ray = rays_a[3 * n];
@@ -922,7 +926,7 @@ __device__ __forceinline__ bool composite_fw_block(const __amdgpu_buffer_rsrc_t&
 // Forward (volumerendering.cu:97-176): a ray with N <= 256 samples is one block of 1, 2 or 4 rows
 // (every row non-empty: no guards), a longer one runs in guarded blocks of 8 rows.
 template <int C>
-__global__ __launch_bounds__(256) void composite_fw_kernel(
+__global__ __launch_bounds__(64 * CF_WPB) void composite_fw_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
@@ -1120,7 +1124,7 @@ __device__ __forceinline__ void composite_bw_ray(
 }
 
 template <int C>
-__global__ __launch_bounds__(256) void composite_bw_kernel_nodws(
+__global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_nodws(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
@@ -1132,7 +1136,7 @@ __global__ __launch_bounds__(256) void composite_bw_kernel_nodws(
                                depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
 }
 template <int C>
-__global__ __launch_bounds__(256) void composite_bw_kernel_dws(
+__global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_dws(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
@@ -1383,7 +1387,7 @@ int ncn_composite_train_fw_bg(const float* sigmas, const float* raws, const floa
                               float* rgb_bg, void* stream) {
     if (n_rays <= 0) return 0;
     (void)n_samples;
-    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, sigmas, raws,
+    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0, (hipStream_t)stream, sigmas, raws,
                    deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rend, ws, bg, rgb_bg);
     NCN_LAUNCH_CHECK("ncn_composite_train_fw");
     return 0;
@@ -1406,11 +1410,11 @@ int ncn_composite_train_bw_bg(const float* dL_dopacity, const float* dL_ddepth, 
     if (n_rays <= 0) return 0;
     (void)n_samples;
     if (dL_dws) {
-        NCN_DISPATCH_C(n_rend, composite_bw_kernel_dws, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
+        NCN_DISPATCH_C(n_rend, composite_bw_kernel_dws, dim3(cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0, (hipStream_t)stream, dL_dopacity,
                    dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
                    T_threshold, dL_dsigmas, dL_draws, bg);
     } else {
-        NCN_DISPATCH_C(n_rend, composite_bw_kernel_nodws, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dopacity,
+        NCN_DISPATCH_C(n_rend, composite_bw_kernel_nodws, dim3(cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0, (hipStream_t)stream, dL_dopacity,
                    dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
                    T_threshold, dL_dsigmas, dL_draws, bg);
     }

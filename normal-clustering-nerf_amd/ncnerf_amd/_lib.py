@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libncnerf.so")
+LIB_PATH = os.environ.get("NCN_LIB_PATH") or os.path.join(_HERE, "libncnerf.so")  # (override: diagnostics)
 
 P = ctypes.c_void_p
 I64 = ctypes.c_int64
