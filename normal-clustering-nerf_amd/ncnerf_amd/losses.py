@@ -5,7 +5,7 @@ normals-from-depth vs GT normals L1/dot (:388-411), RegNeRF depth smoothness (:4
 normal-clustering block (:420-509) with its weight schedule (:217) and validity filter (:246-262).
 The clustering block runs on the GPU end to end: `_extract_normals_from_ray_batch`
 (hypersim_src/utils.py:504-541) is `ncn_normals_fwd/bwd`, and faiss k-means + the cluster selection
-+ the three cluster losses + their gradient are ONE workgroup kernel (`ncn_cluster_loss`), so the
++ the three cluster losses + their gradient are ONE persistent launch (`ncn_cluster_loss`), so the
 step no longer copies normals to the host (losses.py:434) or syncs on `.item()`s.
 
 The k-means is a deterministic spherical Lloyd k-means (stratified seeded init, faiss-style
