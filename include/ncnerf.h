@@ -32,6 +32,16 @@ int ncn_morton3D(const int32_t* coords, int64_t n, int32_t* out, void* stream);
 int ncn_morton3D_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream);
 int ncn_packbits(const float* density_grid, int64_t n_bytes, float threshold, uint8_t* bitfield, void* stream);
 
+/* ---- distortion loss: replaces vren.distortion_loss_fw / _bw (binding.cpp, losses.cu:47-175;
+ *      losses.py:16-44).  fw: loss (R, by ray_idx), ws/wts inclusive scans (S); bw: dL_dws (S) for
+ *      every sample of every ray (the caller zero-fills samples outside all rays, as the
+ *      reference's torch::zeros). ---- */
+int ncn_distortion_loss_fw(const float* ws, const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
+                           float* loss, float* ws_inclusive_scan, float* wts_inclusive_scan, void* stream);
+int ncn_distortion_loss_bw(const float* dL_dloss, const float* ws_inclusive_scan, const float* wts_inclusive_scan,
+                           const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                           int64_t n_rays, float* dL_dws, void* stream);
+
 /* ---- occupancy-grid refresh: replaces NGPMT.update_density_grid (ngp_mt.py:340-368) and its
  *      sample_uniform_and_occupied_cells (ngp_mt.py:245-262) / get_all_cells (:237-243).
  *      Per cascade c: ncn_grid_sample (cells hit: all when warmup, else each cell independently

@@ -57,6 +57,8 @@ SIGNATURES = {
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
     "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F32, F32, F32, F32, F32, P, P, P, P],
     "ncn_adam_step_work_floats": [],
+    "ncn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
+    "ncn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],
     "ncn_grid_work_bytes": [],
     "ncn_grid_sample": [P, I64, I32, F32, F32, F32, I64, I32, U64, F32, P, P, P, P, P, P],
     "ncn_grid_apply": [P, P, P, P, I64, F32, P, P],

@@ -11,7 +11,7 @@ step no longer copies normals to the host (losses.py:434) or syncs on `.item()`s
 The k-means is a deterministic spherical Lloyd k-means (stratified seeded init, faiss-style
 empty-cluster split); faiss itself is not available and unpinned, see DESIGN.md.
 
-Not provided (weight 0 in every reference config, hyperparameters.py:33-49): distortion, semantic,
+Not provided (weight 0 in every reference config, hyperparameters.py:33-49): semantic,
 Manhattan-NeRF and the canonical-direction terms (raise if enabled).
 """
 import einops
@@ -20,7 +20,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import _lib
+from . import _lib, vren
 from ._lib import F32, I32, I64, U32, call, check_input, ptr, stream
 
 N_OUT = 11  # ncn_cluster_loss out_losses
@@ -279,6 +279,25 @@ def _offsets_key(o):
     return bytes(memoryview(np.ascontiguousarray(o, dtype=np.int64)))
 
 
+class DistortionLoss(torch.autograd.Function):
+    """losses.py:16-44: the Mip-NeRF 360 distortion loss in DVGO-v2's O(N) form
+    (vren.distortion_loss_fw/bw -> ncn_distortion_loss_fw/bw).  ws, deltas, ts (S), rays_a (R,3)
+    -> loss (R) by ray_idx."""
+
+    @staticmethod
+    def forward(ctx, ws, deltas, ts, rays_a):
+        loss, ws_inclusive_scan, wts_inclusive_scan = vren.distortion_loss_fw(ws, deltas, ts, rays_a)
+        ctx.save_for_backward(ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dL_dloss):
+        ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a = ctx.saved_tensors
+        dL_dws = vren.distortion_loss_bw(dL_dloss.contiguous(), ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts,
+                                         rays_a)
+        return dL_dws, None, None, None
+
+
 class NeRFMTLoss(nn.Module):
     """losses.py:169-587 (hot-path subset, see module docstring)."""
 
@@ -303,7 +322,7 @@ class NeRFMTLoss(nn.Module):
         self.random_tr_poses = h.get("random_tr_poses", False)
         self.pred_norm_depth = h.get("pred_norm_depth", False)
         self.kmeans_seed = h.get("kmeans_seed", 1234)
-        for name in ("distortion_w", "sem_w", "manhattan_nerf_w", "norm_D_C_can_dot_w", "norm_D_C_can_L1_w"):
+        for name in ("sem_w", "manhattan_nerf_w", "norm_D_C_can_dot_w", "norm_D_C_can_L1_w"):
             if getattr(self, name) > 0:
                 raise NotImplementedError(f"loss term {name} is not part of the ported hot path (0 in all configs)")
         if self.norm_DEpth_L1_w > 0 or self.norm_DEpth_dot_w > 0:
@@ -406,7 +425,7 @@ class NeRFMTLoss(nn.Module):
             pred_w_gt["x123_idx"] = get_patch_triang_idx(n_w_gt, target_raw["patch_area"], off)
             pred_unsup["x123_idx"] = get_patch_triang_idx(n_unsup, target_raw["patch_area"], off)
         clustering = self.norm_D_C_ort_dot_w > 0 or self.norm_D_C_centr_dot_w > 0 or self.norm_D_C_centr_L1_w > 0
-        if (clustering and self.pred_norm_depth and unsup_start == 0 and self.opacity_w > 0
+        if (clustering and self.pred_norm_depth and unsup_start == 0 and self.opacity_w > 0 and self.distortion_w == 0
                 and self.ray_sampling_strategy in ("all_images_triang_patch", "same_image_triang_patch")
                 and self.depth_w == 0 and self.norm_DEpth_L1_w == 0 and self.norm_DEpth_dot_w == 0
                 and self.reg_depth_w == 0 and n_w_gt == pred_unsup["opacity"].shape[0] and n_w_gt % 64 == 0
@@ -432,6 +451,10 @@ class NeRFMTLoss(nn.Module):
         if self.opacity_w > 0 and "opacity" not in loss_d:
             o = pred_unsup["opacity"] + 1e-10
             loss_d["opacity"] = self._validity(self.opacity_w * (-o * torch.log(o)).mean(), dev)
+        if self.distortion_w > 0:  # losses.py:365-369 with quirk q5: ws := ts (losses.py:290)
+            ts = pred_raw["ts"].float().contiguous()
+            dist = DistortionLoss.apply(ts, pred_raw["deltas"].float().contiguous(), ts, pred_raw["rays_a"].contiguous())
+            loss_d["distortion"] = self._validity(self.distortion_w * dist.mean(), dev)
         if self.depth_w > 0:
             d_pred, d_tgt = pred_w_gt["depth"], target_gt["depth"]
             valid = d_tgt > 0

@@ -12,12 +12,12 @@ Deliberate differences (DESIGN.md "Parity contract"):
     R*max_samples rows (callers slice by counter[0], custom_functions.py:91-96, so slicing is a
     no-op), and `rays_a` is in ray order (the reference's order comes from atomicAdd).
   * dead-code entry points of the reference (ray_sphere_intersect, the rgb-only composite
-    variants) and the distortion loss (weight 0 in every config) are not provided.
+    variants) are not provided.
 """
 import torch
 
 from . import _lib
-from ._lib import call, check_dtype, check_input, ptr, stream
+from ._lib import I64, call, check_dtype, check_input, ptr, stream
 
 I64 = _lib.I64
 I32 = _lib.I32
@@ -195,3 +195,28 @@ def composite_test_multi_fw(sigmas, raws, deltas, ts, hits_t, alive_indices, T_t
     A, N, C = sigmas.shape[0], sigmas.shape[1], raws.shape[2]
     call("ncn_composite_test_fw", ptr(sigmas), ptr(raws), ptr(deltas), ptr(ts), ptr(alive_indices), I64(A), I32(N),
          I32(C), F32(float(T_threshold)), ptr(N_eff_samples), ptr(opacity), ptr(depth), ptr(rend), stream())
+
+
+def distortion_loss_fw(ws, deltas, ts, rays_a):
+    """losses.cu:69-100 -> [loss (R) by ray_idx, ws_inclusive_scan (S), wts_inclusive_scan (S)]."""
+    for t, n in ((ws, "ws"), (deltas, "deltas"), (ts, "ts"), (rays_a, "rays_a")):
+        check_input(t, n)
+    R, S = rays_a.shape[0], ws.shape[0]
+    loss = torch.zeros(R, dtype=torch.float32, device=ws.device)
+    wsi = torch.zeros(S, dtype=torch.float32, device=ws.device)
+    wtsi = torch.zeros(S, dtype=torch.float32, device=ws.device)
+    call("ncn_distortion_loss_fw", ptr(ws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), ptr(loss), ptr(wsi), ptr(wtsi),
+         stream())
+    return [loss, wsi, wtsi]
+
+
+def distortion_loss_bw(dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a):
+    """losses.cu:143-175 -> dL_dws (S)."""
+    for t, n in ((dL_dloss, "dL_dloss"), (ws_inclusive_scan, "ws_inclusive_scan"),
+                 (wts_inclusive_scan, "wts_inclusive_scan"), (ws, "ws"), (deltas, "deltas"), (ts, "ts"),
+                 (rays_a, "rays_a")):
+        check_input(t, n)
+    dws = torch.zeros(ws.shape[0], dtype=torch.float32, device=ws.device)
+    call("ncn_distortion_loss_bw", ptr(dL_dloss), ptr(ws_inclusive_scan), ptr(wts_inclusive_scan), ptr(ws),
+         ptr(deltas), ptr(ts), ptr(rays_a), I64(rays_a.shape[0]), ptr(dws), stream())
+    return dws

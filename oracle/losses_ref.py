@@ -167,3 +167,55 @@ def validity(loss):
     if loss.nelement() != 1 or torch.isnan(loss) or torch.isinf(loss):
         return torch.zeros((), dtype=loss.dtype)
     return loss
+
+
+# ---- distortion loss (losses.py:16-44, models/csrc/losses.cu) -------------------------------------
+def distortion_loss_fw(ws, deltas, ts, rays_a):
+    """losses.cu:47-100 restated per ray with sequential f32 prefix sums (thrust's order):
+    -> (loss (R) by ray_idx, ws_inclusive_scan (S), wts_inclusive_scan (S))."""
+    ws = np.asarray(ws, np.float32); deltas = np.asarray(deltas, np.float32); ts = np.asarray(ts, np.float32)
+    rays_a = np.asarray(rays_a, np.int64)
+    S = ws.shape[0]
+    wts = (ws * ts).astype(np.float32)
+    wsi, wtsi = np.zeros(S, np.float32), np.zeros(S, np.float32)
+    wse, wtse = np.zeros(S, np.float32), np.zeros(S, np.float32)
+    loss = np.zeros(rays_a.shape[0], np.float32)
+    for r, s0, n in rays_a:
+        if n == 0:
+            continue
+        sl = slice(s0, s0 + n)
+        wsi[sl] = np.cumsum(ws[sl], dtype=np.float32)
+        wtsi[sl] = np.cumsum(wts[sl], dtype=np.float32)
+        wse[sl] = wsi[sl] - ws[sl]
+        wtse[sl] = wtsi[sl] - wts[sl]
+    _loss = (np.float32(2) * (wtsi * wse - wsi * wtse) + np.float32(1.0 / 3) * ws * ws * deltas).astype(np.float32)
+    for r, s0, n in rays_a:
+        loss[r] = _loss[s0:s0 + n].sum(dtype=np.float32)
+    return loss, wsi, wtsi
+
+
+def distortion_loss_bw(dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a):
+    """losses.cu:103-140 -> dL_dws (S)."""
+    wsi, wtsi = np.asarray(ws_inclusive_scan, np.float32), np.asarray(wts_inclusive_scan, np.float32)
+    ws = np.asarray(ws, np.float32); deltas = np.asarray(deltas, np.float32); ts = np.asarray(ts, np.float32)
+    g = np.asarray(dL_dloss, np.float32)
+    out = np.zeros(ws.shape[0], np.float32)
+    for r, s0, n in np.asarray(rays_a, np.int64):
+        if n == 0:
+            continue
+        e = s0 + n - 1
+        for s in range(s0, e + 1):
+            before = np.float32(0) if s == s0 else ts[s] * wsi[s - 1] - wtsi[s - 1]
+            v = g[r] * 2 * (before + (wtsi[e] - wtsi[s] - ts[s] * (wsi[e] - wsi[s])))
+            out[s] = v + g[r] * np.float32(2.0 / 3) * ws[s] * deltas[s]
+    return out
+
+
+def distortion_loss_naive(ws, deltas, ts, rays_a):
+    """The definition the O(N) form implements (Mip-NeRF 360 / DVGO-v2), float64 torch:
+    sum_i sum_j w_i w_j |t_i - t_j| + 1/3 sum_i w_i^2 delta_i per ray (t ascending within a ray)."""
+    out = []
+    for r, s0, n in np.asarray(rays_a, np.int64):
+        w, t, d = ws[s0:s0 + n], ts[s0:s0 + n], deltas[s0:s0 + n]
+        out.append((w[:, None] * w[None, :] * (t[:, None] - t[None, :]).abs()).sum() + (w * w * d).sum() / 3)
+    return torch.stack(out)

@@ -64,7 +64,7 @@ def test_weight_schedule_matches_reference_formula():
 
 def test_loss_rejects_terms_outside_the_hot_path():
     with pytest.raises(NotImplementedError):
-        NeRFMTLoss(dict(HYPERSIM_HPARAMS, loss_distortion_w=1e-3))
+        NeRFMTLoss(dict(HYPERSIM_HPARAMS, loss_sem_w=1e-3))  # semantic head: not provided
 
 
 def test_vren_rejects_cpu_tensors():

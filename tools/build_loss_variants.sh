@@ -8,6 +8,6 @@ for v in "$@"; do
   name=${v//=/_}; name=${name//,/+}
   defs=$(echo "$v" | tr ',' '\n' | sed 's/^/-D/' | tr '\n' ' ')
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -munsafe-fp-atomics $defs \
-    $SRC/vren.hip $SRC/field.hip $SRC/loss.hip $SRC/optim.hip $SRC/grid.hip $SRC/errors.cpp -o tools/_build/lib_${name,,}.so &
+    $SRC/vren.hip $SRC/field.hip $SRC/loss.hip $SRC/optim.hip $SRC/grid.hip $SRC/distortion.hip $SRC/errors.cpp -o tools/_build/lib_${name,,}.so &
 done
 wait
