@@ -169,6 +169,7 @@ __global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, 
         pi = pi - lr * ((mi / bc1) / denom + wd * pi);
     };
     const int64_t n4 = n / 4, tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+#pragma unroll 2
     for (int64_t i = tid; i < n4; i += nth) {
         float4 P = ((float4*)p)[i], M = ((float4*)m)[i], V = ((float4*)v)[i];
         const float4 G = ((const float4*)g)[i];
@@ -222,7 +223,8 @@ int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_
     hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(256), 0, (hipStream_t)stream, grads, n, grad_scale, max_norm,
                        beta1, beta2, lr, lr_dev, step_dev, work);
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
-    const int blocks = (int)std::min<int64_t>(cdiv(n, 1024), 2048);
+    // two float4 per thread (8 loads of p/g/m/v in flight): ~n/2048 workgroups
+    const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 16384);
     hipLaunchKernelGGL(adam_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
     NCN_LAUNCH_CHECK("ncn_adam_step");
