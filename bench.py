@@ -9,12 +9,19 @@ the flat gradient] -> clip + Adam, and the occupancy-grid refresh every 16 steps
 generated on the device before the timed region.  N>1: one process per GPU (torchrun), weak
 scaling (8192 rays per rank), value = all ranks' rays / max-over-ranks time.
 
+Launch: under torchrun (WORLD_SIZE set) every process is one rank; `--gpus N` with N > 1 and no
+WORLD_SIZE spawns the N local ranks itself (child processes with RANK/LOCAL_RANK/WORLD_SIZE and a
+127.0.0.1 rendezvous, started before this process touches the GPU) and exits with the worst child
+status.  Either way the run fails unless the process group has exactly --gpus ranks.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -22,6 +29,42 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """Start n local ranks of this script (no GPU call has happened in this process) and return the
+    worst exit status.  Rank 0's stdout (the JSON line) passes through; the others' is discarded."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    return rc
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
+    _gpus = 1
+    for _i, _a in enumerate(sys.argv):
+        if _a == "--gpus" and _i + 1 < len(sys.argv):
+            _gpus = int(sys.argv[_i + 1])
+        elif _a.startswith("--gpus="):
+            _gpus = int(_a.split("=", 1)[1])
+    if _gpus > 1:
+        sys.exit(spawn_ranks(_gpus, sys.argv[1:]))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -80,24 +123,37 @@ def composite_fw_roofline(model, batch, dev, reps=50):
     return 24.0 * S_vr + 4.0 * S + 52.0 * R, us
 
 
-def cpu_baseline(n_rays=2048, budget_s=15.0, max_steps=10):
-    """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on host cores)."""
+def cpu_baseline(n_rays=2048, steps=20, warmup=3):
+    """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on the host cores),
+    timed as BASELINE.md §2 asks: median wall time of 20 steps after 3 warm-up steps.  Threads: all
+    cores this process may run on (its affinity mask), capped by OMP_NUM_THREADS when the box sets
+    it (the GPU box's CPU share); both counts are reported."""
     from oracle.train_ref import CPUTrainer
     from ncnerf_amd.synthetic import SyntheticScene
-    threads = min(16, os.cpu_count() or 1)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    threads = affinity
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(threads)
     scene = SyntheticScene()
     tr = CPUTrainer(scene.bitfield)
-    tr.step(scene.batch(n_rays, seed=999))  # warm-up
-    t0 = time.perf_counter()
-    steps = 0
-    while steps < max_steps and (time.perf_counter() - t0) < budget_s:
-        tr.step(scene.batch(n_rays, seed=steps))
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n_rays * steps / dt, 1), "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} full training steps of {n_rays} rays (config #1) on the oracle CPU path "
-                      f"(oracle/train_ref.py: C marcher/compositor + torch fp32 field/losses), {dt:.1f} s"}
+    for k in range(warmup):
+        tr.step(scene.batch(n_rays, seed=999 + k))
+    times = []
+    for k in range(steps):
+        b = scene.batch(n_rays, seed=k)
+        t0 = time.perf_counter()
+        tr.step(b)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": round(n_rays / med, 1), "unit": "rays/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+            "sample": f"median of {steps} full training steps of {n_rays} rays (config #1) after {warmup} warm-up "
+                      f"steps on the oracle CPU path (oracle/train_ref.py: C marcher/compositor + torch fp32 "
+                      f"field/losses), {med * 1e3:.0f} ms/step, {sum(times):.1f} s timed"}
 
 
 def main():
@@ -109,14 +165,32 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grid-update", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager (Python-launched) step instead of a HIP graph")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="launch/rendezvous check only (no GPU work): every rank all-reduces its rank, rank 0 "
+                         "prints {world, backend, sum}")
     args = ap.parse_args()
 
-    from ncnerf_amd import _lib, distributed
+    from ncnerf_amd import distributed
+
+    rank, world = distributed.init_from_env()
+    backend = dist.get_backend() if world > 1 else None
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s)", file=sys.stderr)
+        sys.exit(3)
+    if args.dist_selftest:
+        t = torch.tensor([float(rank)])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"world": world, "backend": backend, "rank_sum": float(t.item())}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    from ncnerf_amd import _lib
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.synthetic import SyntheticScene
     from ncnerf_amd.trainer import Trainer
-
-    rank, world = distributed.init_from_env()
     # (modulo: a 1-GPU rehearsal of the N>1 path with NCN_DIST_BACKEND=gloo puts every rank on cuda:0)
     local_rank = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -156,8 +230,11 @@ def main():
         # so the captured body is run eagerly for `steps` more steps with HIP events on the launch
         # stream around each hot kernel (GPU spin in front: see _lib.TIMING).
         _lib.TIMING = {n: [] for n in TIMED}
+        step_t = torch.full((), step0, dtype=torch.int64, device=dev)
         for k in range(args.steps):
-            trainer._body(batches[k % n_batches], torch.full((), step0, dtype=torch.int64, device=dev), True)
+            trainer._body(batches[k % n_batches], step_t, trainer._with_opt)
+            if not trainer._with_opt:
+                trainer.opt.step(grad_scale=distributed.reduce_gradients(model))
         torch.cuda.synchronize()
     timing = _lib.TIMING
     _lib.TIMING = None
@@ -165,7 +242,11 @@ def main():
     vr = sum(torch.as_tensor(b).double().sum() for _, b in counts)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     tot = torch.stack([rm, vr]).reshape(2)
+    rank_ms = [round(1e3 * (t1 - t0) / args.steps, 3)]
     if world > 1:
+        gathered = [torch.zeros_like(elapsed) for _ in range(world)]
+        dist.all_gather(gathered, elapsed)
+        rank_ms = [round(1e3 * float(g.item()) / args.steps, 3) for g in gathered]
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     el = float(elapsed.item())
@@ -191,6 +272,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * el / args.steps, 3),
+        "world": world,
+        "backend": backend,
+        "rank_ms_per_step": rank_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -175,6 +175,17 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
                   float* level_max /* 16 * ncn_field_bwd_blocks(n) floats of workspace (per-level max |dE|) */,
                   void* stream);
+/* ncn_field_bwd in its two passes (the data-parallel step overlaps the gradient all-reduce of one
+ * level range with the scatter of the others): the MLP pass (weight-gradient slabs, dE_ws,
+ * level_max), then the table scatter of the levels [level_lo, level_hi) into grad_table (+=).
+ * max_blocks > 0 caps the scatter's workgroups (one per CU otherwise), leaving CUs to a concurrent
+ * collective. */
+int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const uint16_t* weights_packed,
+                      const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* slab,
+                      float* dE_ws, float* level_max, void* stream);
+int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const uint32_t* levels, float xyz_min,
+                      float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
+                      int max_blocks, float* grad_table, void* stream);
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream);
 
 /* ---- normal clustering loss path: replaces _extract_normals_from_ray_batch
@@ -217,6 +228,10 @@ int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opaci
  *   before its first use and reused across calls (every call leaves its barrier words at zero);
  *   one workspace per stream (two concurrent calls must not share one). */
 int64_t ncn_cluster_workspace_words(int K);
+/* Index (in 32-bit words) of the workspace's sticky error word: non-zero once a grid barrier or a
+ * Lloyd hand-off of any call on this workspace timed out (its results are then wrong).  The
+ * caller reads it outside the hot loop (the training step: every few steps) and fails. */
+int64_t ncn_cluster_status_offset(int K);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,
                      float sched_start, float sched_grow, const float* photo_loss, float* out_losses,
@@ -246,10 +261,11 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
  * 0, the hash grid), the rest wd1.  The gradient used is grads * grad_scale (1/world after an
  * all-reduce SUM: the average of DDP without a separate division pass), clipped by its L2 norm.  step_dev is incremented (device step counter) and drives the
  * bias corrections; work holds ncn_adam_step_work_floats() floats, zero before the first call (its
- * arrival counter is left zero by every call).  Buffers 16-byte aligned. */
-int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+ * arrival counter is left zero by every call).  zero_grads != 0: the Adam pass also writes zeros over
+ * the gradient it consumed (the next step's zero_grad folded in).  Buffers 16-byte aligned. */
+int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
                   float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, void* stream);
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, void* stream);
 int64_t ncn_adam_step_work_floats(void);
 
 #ifdef __cplusplus

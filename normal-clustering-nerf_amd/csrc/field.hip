@@ -1024,7 +1024,8 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    float xyz_min, float xyz_extent,
                                                                    const float2* __restrict__ dE,
                                                                    float* __restrict__ grad,
-                                                                   const float* __restrict__ level_max, int lm_rows) {
+                                                                   const float* __restrict__ level_max, int lm_rows,
+                                                                   int level_lo, int level_hi) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
     __shared__ float wmax[SC_WAVES];
     __shared__ int fill;
@@ -1043,17 +1044,20 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     nrm.ext = xyz_extent;
     nrm.inv = 1.0f / xyz_extent;
     nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
-    // units, level-major: run levels in spans of 8192 samples (8 per lane), direct levels in spans
-    // of 2048 (2 per lane)
+    // units, level-major over the levels [level_lo, level_hi): run levels in spans of
+    // 1024 * SC_C_RUN samples, direct levels in spans of 2048 (2 per lane)
     constexpr int C_RUN = SC_C_RUN, C_DIR = 2;
     const int64_t ur = (n + SC_THREADS * C_RUN - 1) / (SC_THREADS * C_RUN);
     const int64_t ud = (n + SC_THREADS * C_DIR - 1) / (SC_THREADS * C_DIR);
-    const int64_t n_units = SC_RUN_LEVELS * ur + (16 - SC_RUN_LEVELS) * ud;
+    const int run_lo = level_lo, run_hi = min(level_hi, SC_RUN_LEVELS);
+    const int dir_lo = max(level_lo, SC_RUN_LEVELS), dir_hi = level_hi;
+    const int64_t n_run = run_hi > run_lo ? (int64_t)(run_hi - run_lo) * ur : 0;
+    const int64_t n_units = n_run + (dir_hi > dir_lo ? (int64_t)(dir_hi - dir_lo) * ud : 0);
     // (grid-stride: a workgroup takes its run units first, then its direct ones: one layout switch)
     int layout = -1;
     ScShared sh;
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-        const int run = u < SC_RUN_LEVELS * ur;
+        const int run = u < n_run;
         if (run != layout) {  // (re)initialise the table of the new layout
             lds_barrier();
             sh = sc_layout(arena, wmax, &fill, run);
@@ -1067,13 +1071,13 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
             layout = run;
         }
         if (run) {
-            const int l = (int)(u / ur);
-            const int64_t s0 = (u - l * ur) * (SC_THREADS * C_RUN), s1 = min(n, s0 + SC_THREADS * C_RUN);
+            const int li = (int)(u / ur), l = run_lo + li;
+            const int64_t s0 = (u - li * ur) * (SC_THREADS * C_RUN), s1 = min(n, s0 + SC_THREADS * C_RUN);
             sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, lmax_s[l], grad);
         } else {
-            const int64_t v = u - SC_RUN_LEVELS * ur;
-            const int l = SC_RUN_LEVELS + (int)(v / ud);
-            const int64_t s0 = (v - (l - SC_RUN_LEVELS) * ud) * (SC_THREADS * C_DIR), s1 = min(n, s0 + SC_THREADS * C_DIR);
+            const int64_t v = u - n_run;
+            const int li = (int)(v / ud), l = dir_lo + li;
+            const int64_t s0 = (v - li * ud) * (SC_THREADS * C_DIR), s1 = min(n, s0 + SC_THREADS * C_DIR);
             sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, lmax_s[l], grad);
         }
     }
@@ -1137,6 +1141,36 @@ int ncn_field_bwd_blocks(int64_t n) {
 
 int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(int64_t)3) : 0; }
 
+int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const uint16_t* weights_packed,
+                      const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* slab,
+                      float* dE_ws, float* level_max, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0, hipErrorInvalidValue, "ncn_field_bwd_mlp: dE_ws must be 16-byte aligned");
+    NCN_REQUIRE(level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp: level_max workspace required");
+    hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
+                       dirs, n, n_dev, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas,
+                       dL_drgbs, dE_ws, slab, level_max);
+    NCN_LAUNCH_CHECK("ncn_field_bwd_mlp");
+    return 0;
+}
+
+int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const uint32_t* levels, float xyz_min,
+                      float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
+                      int max_blocks, float* grad_table, void* stream) {
+    if (n <= 0 || level_hi <= level_lo) return 0;
+    NCN_REQUIRE(0 <= level_lo && level_hi <= 16, hipErrorInvalidValue, "ncn_field_scatter: levels must lie in [0, 16)");
+    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
+                "ncn_field_scatter: dE_ws and xyzs must be 16-byte aligned");
+    const LevelTable Lt = make_table(levels);
+    int grid = scatter_grid(n);
+    if (max_blocks > 0) grid = std::min(grid, max_blocks);
+    hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
+                       xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
+                       level_lo, level_hi);
+    NCN_LAUNCH_CHECK("ncn_field_scatter");
+    return 0;
+}
+
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
                   float xyz_min,
                   float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
@@ -1145,17 +1179,11 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
     if (n <= 0) return 0;
     NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
                 "ncn_field_bwd: dE_ws and xyzs must be 16-byte aligned");
-    NCN_REQUIRE(level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd: level_max workspace required");
-    const LevelTable Lt = make_table(levels);
-    hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
-                       dirs, n, n_dev, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas,
-                       dL_drgbs, dE_ws, slab, level_max);
-    NCN_LAUNCH_CHECK("ncn_field_bwd");
-    hipLaunchKernelGGL(field_scatter_kernel, dim3(scatter_grid(n)), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n,
-                       n_dev, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max,
-                       ncn_field_bwd_blocks(n));
-    NCN_LAUNCH_CHECK("ncn_field_bwd (scatter)");
-    return 0;
+    const int e = ncn_field_bwd_mlp(dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs, slab, dE_ws,
+                                    level_max, stream);
+    if (e) return e;
+    return ncn_field_scatter(xyzs, n, n_dev, levels, xyz_min, xyz_extent, dE_ws, level_max, 0, 16, 0, grad_table,
+                             stream);
 }
 
 

@@ -319,8 +319,16 @@ __device__ __forceinline__ void st_c(long long* p, long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Grid barrier number `phase` (1, 2, ...) over the KM_BLOCKS co-resident workgroups.  The spin is
-// bounded: a barrier that does not complete within ~2^22 polls sets the error word and lets the
-// workgroup run on (wrong numbers, reported by ncn_cluster_loss's caller check), never a hang.
+// bounded: a barrier that does not complete within ~2^22 polls sets the error word (sync[2],
+// sticky; ncn_cluster_status_offset) and lets the workgroup run on (wrong numbers, never a hang);
+// the training step reads the word every few steps and raises (losses.check_cluster_status).
+// NCN_KM_SPIN_LIMIT / NCN_KM_POLL_LIMIT: diagnostic builds force the flag with a limit of 1.
+#ifndef NCN_KM_SPIN_LIMIT
+#define NCN_KM_SPIN_LIMIT (1u << 22)
+#endif
+#ifndef NCN_KM_POLL_LIMIT
+#define NCN_KM_POLL_LIMIT (1u << 20)
+#endif
 __device__ __forceinline__ void km_grid_sync(unsigned* sync, unsigned phase) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -330,7 +338,7 @@ __device__ __forceinline__ void km_grid_sync(unsigned* sync, unsigned phase) {
         unsigned spins = 0;
         while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins == (1u << 22)) {
+            if (++spins >= NCN_KM_SPIN_LIMIT) {
                 __hip_atomic_store(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
@@ -405,7 +413,7 @@ __device__ __forceinline__ float sum_rows_tagged(const long long* __restrict__ p
 #pragma unroll
         for (int b = 0; b < KM_BLOCKS; b++) ready &= ((unsigned long long)v[b] >> KM_TAG_SHIFT) == tag;
         if (ready) break;
-        if (spins == (1u << 20)) {
+        if (spins + 1 >= NCN_KM_POLL_LIMIT) {
             __hip_atomic_store(&sync[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
@@ -911,6 +919,11 @@ using namespace ncn;
 extern "C" {
 
 int64_t ncn_cluster_workspace_words(int K) { return km_ws_words(K); }
+
+int64_t ncn_cluster_status_offset(int K) {
+    float* base = nullptr;
+    return (int64_t)((float*)(km_ws(base, K).sync + 2) - base);
+}
 
 int ncn_photo_loss_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
                        float* loss, void* stream) {

@@ -87,22 +87,29 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 //     (arrival counter) adds the partials in a fixed order and writes the step's scalars — clip
 //     factor, bias corrections of the incremented device step, lr — then resets the counter;
 //  2. adam_apply_kernel: Adam of both groups (index < n_group0: weight decay wd0, else wd1) with
-//     16-B accesses, reading the four scalars.
-// Replaces sumsq + one Adam launch per group (each of whose workgroups re-summed the partials).
-constexpr int ADAM_BLOCKS = 2048;  // max workgroups of adam_prep (partials)
-constexpr int ADAM_UNROLL = 8;
-__global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float gscale, float max_norm,
-                                                        float b1, float b2, float lr, const float* __restrict__ lr_dev,
-                                                        int* __restrict__ step_dev, float* __restrict__ work) {
+//     16-B accesses, reading the four scalars; optionally zeroes the gradient it has consumed
+//     (the next step's zero_grad fill folded into this pass: +4 B/param instead of a 4 B/param
+//     fill launch).
+// adam_prep runs ONE 1024-thread workgroup per CU (256 on MI355X): every arrival is an atomic on
+// the same counter word, and same-address atomics serialise at the memory side (MI355X_MICROARCH.md
+// "Global float atomics", contention row), so 2048 arrivals cost ~15-20 us where 256 cost ~2.
+constexpr int ADAM_BLOCKS = 256;     // workgroups of adam_prep (partials)
+constexpr int ADAM_THREADS = 1024;
+constexpr int ADAM_UNROLL = 12;      // float4 loads in flight per thread (45.8 MB: 11 per thread)
+__global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float gscale,
+                                                               float max_norm, float b1, float b2, float lr,
+                                                               const float* __restrict__ lr_dev,
+                                                               int* __restrict__ step_dev, float* __restrict__ work) {
     float* part = work;                                // [ADAM_BLOCKS]
     unsigned* cnt = (unsigned*)(work + ADAM_BLOCKS);   // arrival counter (left zero)
     float* sc = work + ADAM_BLOCKS + 4;                // cf, bc1, bc2, lr
-    __shared__ float red[4];
+    constexpr int NW = ADAM_THREADS / 64;
+    __shared__ float red[NW];
     __shared__ bool last;
-    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * ADAM_THREADS;
     const float4* g4 = (const float4*)g;
     float s = 0.f;
-    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n4; b += ADAM_UNROLL * stride) {
+    for (int64_t b = (int64_t)blockIdx.x * ADAM_THREADS + threadIdx.x; b < n4; b += ADAM_UNROLL * stride) {
         float4 x[ADAM_UNROLL];  // ADAM_UNROLL independent loads in flight per thread
 #pragma unroll
         for (int u = 0; u < ADAM_UNROLL; u++) x[u] = b + u * stride < n4 ? g4[b + u * stride] : make_float4(0, 0, 0, 0);
@@ -112,51 +119,53 @@ __global__ __launch_bounds__(256) void adam_prep_kernel(const float* __restrict_
         }
     }
     if (blockIdx.x == 0)
-        for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) s = fmaf(g[i], g[i], s);
+        for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += ADAM_THREADS) s = fmaf(g[i], g[i], s);
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    // hand-off with agent-scope (sc1) accesses only (MI355X_MICROARCH.md inter-workgroup visibility):
-    // store the partial, wait for it, then one arrival add.  No __threadfence(): a device-scope
-    // release writes the L2 back, which right after the table-gradient scatter costs ~40 us.
+    // Hand-off in the sc1 form of MI355X_MICROARCH.md "Correctness boundaries" (inter-workgroup
+    // visibility): the partial is stored with an agent-scope (sc1) store and drained (vmcnt(0))
+    // before the arrival add, and the last workgroup reads the partials with agent-scope (sc1)
+    // loads.  This relies on gfx9's in-order completion of one wave's vector memory operations
+    // after vmcnt(0), not on a HIP release/acquire pair: an agent-scope release fence writes back
+    // the whole L2 (buffer_wbl2), which right after the table-gradient scatter measured ~40 us.
+    // (The asm's "memory" clobber keeps the compiler from moving the store past the add.)
     if (threadIdx.x == 0) {
-        __hip_atomic_store(&part[blockIdx.x], red[0] + red[1] + red[2] + red[3], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; w++) t += red[w];
+        __hip_atomic_store(&part[blockIdx.x], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
-    // the gridDim.x (<= ADAM_BLOCKS) partials: every thread loads its share at once (one round
-    // trip), fixed-order sums
-    float t = 0.f;
-    {
-        float q[ADAM_BLOCKS / 256];
+    // the gridDim.x (<= ADAM_BLOCKS) partials, fixed-order sum in wave 0
+    if (threadIdx.x < 64) {
+        float q[ADAM_BLOCKS / 64];
 #pragma unroll
-        for (int u = 0; u < ADAM_BLOCKS / 256; u++) {
-            const int i = u * 256 + threadIdx.x;
+        for (int u = 0; u < ADAM_BLOCKS / 64; u++) {
+            const int i = u * 64 + threadIdx.x;
             q[u] = i < (int)gridDim.x ? __hip_atomic_load(&part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
         }
+        float t = 0.f;
 #pragma unroll
-        for (int u = 0; u < ADAM_BLOCKS / 256; u++) t += q[u];
-    }
-    t = wave_sum(t);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        t = red[0] + red[1] + red[2] + red[3];
-        const float c = max_norm / (sqrtf(t) * gscale + 1e-6f);  // norm of the scaled gradient
-        const int st = *step_dev + 1;  // device step counter
-        *step_dev = st;
-        sc[0] = (max_norm > 0.f ? fminf(c, 1.0f) : 1.0f) * gscale;
-        sc[1] = 1.0f - powf(b1, (float)st);
-        sc[2] = 1.0f - powf(b2, (float)st);
-        sc[3] = lr_dev ? *lr_dev : lr;
-        *cnt = 0u;
+        for (int u = 0; u < ADAM_BLOCKS / 64; u++) t += q[u];
+        t = wave_sum(t);
+        if (threadIdx.x == 0) {
+            const float c = max_norm / (sqrtf(t) * gscale + 1e-6f);  // norm of the scaled gradient
+            const int st = *step_dev + 1;  // device step counter
+            *step_dev = st;
+            sc[0] = (max_norm > 0.f ? fminf(c, 1.0f) : 1.0f) * gscale;
+            sc[1] = 1.0f - powf(b1, (float)st);
+            sc[2] = 1.0f - powf(b2, (float)st);
+            sc[3] = lr_dev ? *lr_dev : lr;
+            *cnt = 0u;
+        }
     }
 }
-__global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, const float* __restrict__ g,
+template <bool ZERO>
+__global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                          int64_t n0, float b1, float b2, float eps, float wd0,
                                                          float wd1, const float* __restrict__ sc) {
@@ -181,8 +190,12 @@ __global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, 
         ((float4*)p)[i] = P;
         ((float4*)m)[i] = M;
         ((float4*)v)[i] = V;
+        if (ZERO) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (int64_t i = 4 * n4 + tid; i < n; i += nth) upd(p[i], g[i], m[i], v[i], i < n0 ? wd0 : wd1);
+    for (int64_t i = 4 * n4 + tid; i < n; i += nth) {
+        upd(p[i], g[i], m[i], v[i], i < n0 ? wd0 : wd1);
+        if (ZERO) g[i] = 0.f;
+    }
 }
 }  // namespace ncn
 
@@ -211,22 +224,26 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
     return 0;
 }
 
-int ncn_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
                   float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, void* stream) {
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
                 hipErrorInvalidValue, "ncn_adam_step: buffers must be 16-byte aligned");
     NCN_REQUIRE(step_dev != nullptr && work != nullptr, hipErrorInvalidValue,
                 "ncn_adam_step: needs the device step counter and the work buffer");
-    const int prep_blocks = (int)std::min<int64_t>(ADAM_BLOCKS, std::max<int64_t>(1, cdiv(n / 4, 256 * ADAM_UNROLL)));
-    hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(256), 0, (hipStream_t)stream, grads, n, grad_scale, max_norm,
-                       beta1, beta2, lr, lr_dev, step_dev, work);
+    const int prep_blocks = (int)std::min<int64_t>(ADAM_BLOCKS, std::max<int64_t>(1, cdiv(n / 4, ADAM_THREADS * 4)));
+    hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, grads, n,
+                       grad_scale, max_norm, beta1, beta2, lr, lr_dev, step_dev, work);
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
     // two float4 per thread (8 loads of p/g/m/v in flight): ~n/2048 workgroups
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 16384);
-    hipLaunchKernelGGL(adam_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
-                       exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
+    if (zero_grads)
+        hipLaunchKernelGGL(adam_apply_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
+                           exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
+    else
+        hipLaunchKernelGGL(adam_apply_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
+                           exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
     NCN_LAUNCH_CHECK("ncn_adam_step");
     return 0;
 }

@@ -39,6 +39,19 @@ def _cluster_workspace(dev, K):
     return ws
 
 
+def check_cluster_status(dev=None):
+    """Raise if a clustering launch on any workspace (of `dev`, or all) hit its barrier/hand-off
+    timeout (the kernel's sticky error word, ncn_cluster_status_offset): its losses and gradients
+    were computed from incomplete partial sums.  One device read per workspace (host sync)."""
+    for (d, K), ws in _WS.items():
+        if dev is not None and d != str(dev):
+            continue
+        off = int(_lib.lib().ncn_cluster_status_offset(I32(K)))
+        if int(ws.view(torch.int32)[off].item()) != 0:
+            raise _lib.NcnError(f"ncn_cluster_loss on {d} (K={K}): a grid barrier / Lloyd hand-off timed out "
+                                f"(co-residency of its {32} workgroups failed); cluster losses are invalid")
+
+
 class _Normals(torch.autograd.Function):
     """hypersim_src/utils.py:504-541: n = normalize(cross(P2-P1, P3-P1)), P = rays_o + rays_d*depth."""
 

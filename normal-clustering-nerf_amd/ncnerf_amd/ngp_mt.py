@@ -106,10 +106,20 @@ class _FieldFunction(torch.autograd.Function):
         dE_ws = torch.empty(int(_lib.lib().ncn_field_bwd_dE_floats(I64(n))), dtype=torch.float32, device=x.device)
         c = lambda t: None if t is None else t.contiguous().float()
         dsig, drgb = c(dL_dsigmas), c(dL_drgbs)
-        call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
-             F32(model._xyz_extent),
-             ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()),
-             stream())
+        split = model.scatter_split
+        if split is None:
+            call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
+                 F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab),
+                 ptr(dE_ws), ptr(model._level_max()), stream())
+        else:
+            # data-parallel step: the levels [split, 16) are scattered now, [0, split) later by
+            # run_deferred_scatter() while the all-reduce of the first bucket is in flight
+            lmax = model._level_max()
+            call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb),
+                 ptr(slab), ptr(dE_ws), ptr(lmax), stream())
+            call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
+                 F32(model._xyz_extent), ptr(dE_ws), ptr(lmax), I32(split), I32(16), I32(0), ptr(g_table), stream())
+            model._deferred = (x, n, n_dev, dE_ws, lmax, g_table)
         call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
         return None, None, None, None, None, None, None, None
 
@@ -160,6 +170,10 @@ class NGPMT(nn.Module):
         self.rgb_net = _ParamHolder(flat[n_table + W_SIGMA:])
         self._flat_grad = None
         self._packed = None
+        # None: the backward scatters every level.  An int L (data-parallel step): levels [L, 16)
+        # are scattered in the backward, [0, L) by run_deferred_scatter() (grad_buckets(L)).
+        self.scatter_split = None
+        self._deferred = None
 
     # -- flat buffers --------------------------------------------------------------------------
     def _apply(self, fn, recurse=True):
@@ -200,6 +214,23 @@ class NGPMT(nn.Module):
                     v.zero_()
                 p.grad = v
         return fg[:n_table], fg[n_table:]
+
+    def grad_buckets(self, split):
+        """The flat gradient as (levels [split, 16) of the table + the MLP weights, levels [0, split)):
+        two contiguous views, the all-reduce buckets of the split data-parallel step."""
+        fg = self.flat_grad()
+        cut = 2 * self.levels[split]["offset"]
+        return fg[cut:], fg[:cut]
+
+    def run_deferred_scatter(self, max_blocks=0):
+        """Scatter of the levels [0, scatter_split) left by the last backward (same tensors; inside a
+        captured step they are the graph's static buffers, refilled by every replay)."""
+        if self._deferred is None:
+            raise RuntimeError("run_deferred_scatter: no deferred scatter (scatter_split unset or no backward yet)")
+        x, n, n_dev, dE_ws, lmax, g_table = self._deferred
+        call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), self._levels_ptr, F32(self._xyz_min),
+             F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(0), I32(self.scatter_split), I32(max_blocks),
+             ptr(g_table), stream())
 
     def prepare_weights(self):
         """Pack the MLP weights now (after the optimizer step) so the next forward reuses them."""

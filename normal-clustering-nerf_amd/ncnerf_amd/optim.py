@@ -2,9 +2,11 @@
 
 Reference: apex FusedAdam (AdamW mode, eps 1e-15) with two groups — hash-grid features (weight
 decay 0) and MLP weights (weight decay 1e-6) — (train_nerf.py:262-285), gradient clipping by global
-L2 norm 0.05 (train_nerf.py:955), CosineAnnealingLR over epochs (:286-288).  One launch per step
-(ncn_adam_step: sum of squares, grid barrier, Adam of both groups); the clip factor never leaves
-the device.
+L2 norm 0.05 (train_nerf.py:955), CosineAnnealingLR(T_max=num_epochs, eta_min=0) stepped once per
+epoch (:286-288; `set_epoch`).  Two launches per step (ncn_adam_step: sum of squares whose last
+workgroup forms the clip factor and step scalars, then Adam of both groups); the clip factor never
+leaves the device.  With `zero_grad_on_step` the Adam pass also zeroes the gradient it consumed, so
+the next step needs no zero_grad fill (PL's zero_grad before every backward, folded in).
 """
 import math
 
@@ -16,7 +18,7 @@ from ._lib import F32, I32, I64, call, ptr, stream
 
 class FlatAdam:
     def __init__(self, model, lr=1e-2, betas=(0.9, 0.999), eps=1e-15, weight_decay=(0.0, 1e-6), max_norm=0.05,
-                 num_epochs=None):
+                 num_epochs=None, zero_grad_on_step=False):
         self.model = model
         self.base_lr = self.lr = lr
         self.betas, self.eps, self.wd, self.max_norm = betas, eps, weight_decay, max_norm
@@ -32,13 +34,18 @@ class FlatAdam:
         self.lr_dev = torch.full((), float(lr), dtype=torch.float32, device=flat.device)
         self.num_epochs = num_epochs
         self.n_table = model._n_table
+        self.zero_grad_on_step = zero_grad_on_step
+        self.epoch = 0
 
     def zero_grad(self):
         self.model.flat_grad().zero_()
 
     def set_epoch(self, epoch):
-        """CosineAnnealingLR(T_max=num_epochs, eta_min=0) stepped per epoch (train_nerf.py:286-288)."""
-        if self.num_epochs:
+        """CosineAnnealingLR(T_max=num_epochs, eta_min=0) stepped per epoch (train_nerf.py:286-288):
+        lr(e) = base_lr * (1 + cos(pi * e / T_max)) / 2.  Writes the device lr the step kernels read
+        (also inside a captured graph); a no-op when the epoch is unchanged."""
+        if self.num_epochs and epoch != self.epoch:
+            self.epoch = epoch
             self.lr = 0.5 * self.base_lr * (1 + math.cos(math.pi * epoch / self.num_epochs))
             self.lr_dev.fill_(self.lr)
 
@@ -50,7 +57,7 @@ class FlatAdam:
         b1, b2 = self.betas
         call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
              F32(grad_scale), F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
-             ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), stream())
+             ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), I32(1 if self.zero_grad_on_step else 0), stream())
 
     def state_tensors(self):
         """Every tensor the step mutates (parameters, moments, device counters)."""

@@ -1,13 +1,17 @@
 """One training step of the reference NeRFSystem (train_nerf.py:165-358) on the HIP hot path:
 render (intersect -> march -> field -> composite) -> NeRFMTLoss (rgb + opacity + normal
 clustering) -> backward -> [RCCL gradient all-reduce] -> clip + Adam, plus the occupancy-grid
-refresh every 16 steps (train_nerf.py:314-320) when `update_grid` is on.
+refresh every 16 steps (train_nerf.py:314-320) when `update_grid` is on, and the per-epoch cosine
+learning rate (CosineAnnealingLR(T_max=num_epochs), train_nerf.py:286-288; an epoch is the
+training set's 1000 items, base.py:78-81, split over the ranks by DDP's DistributedSampler).
 
 Hyper-parameters default to the Hypersim config (experiments/hypersim/hyperparameters.py)."""
+import math
+
 import torch
 
 from . import distributed
-from .losses import NeRFMTLoss
+from .losses import NeRFMTLoss, check_cluster_status
 from .optim import FlatAdam
 from .rendering import render
 
@@ -25,11 +29,21 @@ class Trainer:
     warmup_steps = 256
     update_interval = 16
 
-    def __init__(self, model, hparams=None, update_grid=False, use_graph=False):
+    epoch_items = 1000  # base.py:78-81 (training "epoch" = 1000 batches)
+
+    def __init__(self, model, hparams=None, update_grid=False, use_graph=False, scatter_split=None):
         self.h = dict(HYPERSIM_HPARAMS, **(hparams or {}))
         self.model = model
         self.loss = NeRFMTLoss(self.h)
-        self.opt = FlatAdam(model, lr=self.h["lr"], max_norm=self.h["grad_clip"], num_epochs=self.h["num_epochs"])
+        # the Adam pass zeroes the gradient it consumed: no zero_grad fill in the step
+        self.opt = FlatAdam(model, lr=self.h["lr"], max_norm=self.h["grad_clip"], num_epochs=self.h["num_epochs"],
+                            zero_grad_on_step=True)
+        self.world = distributed.world_size()
+        self.steps_per_epoch = math.ceil(self.epoch_items / self.world)  # DistributedSampler split
+        # data-parallel step: all-reduce the gradient in two buckets, the table levels
+        # [scatter_split, 16) + MLP weights while the levels [0, scatter_split) are scattered
+        if self.world > 1:
+            model.scatter_split = distributed.DEFAULT_SCATTER_SPLIT if scatter_split is None else scatter_split
         self.update_grid = update_grid
         self.render_kwargs = dict(near_distance=self.h["rend_near_dist"], max_samples=self.h["rend_max_samples"],
                                   test_time=False, random_bg=False, anneal_strategy="none", anneal_steps=0)
@@ -53,7 +67,6 @@ class Trainer:
     # run eagerly around it.
     def _body(self, batch, step_dev, with_opt):
         m = self.model
-        self.opt.zero_grad()
         kw = dict(self.render_kwargs, global_step=0, static_shapes=True)
         if "march_noise" in batch:
             kw["march_noise"] = batch["march_noise"]
@@ -76,7 +89,8 @@ class Trainer:
             raise NotImplementedError("ray-range annealing is step-dependent host control flow")
         self._static = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in batch.items()}
         self._step_dev = torch.zeros((), dtype=torch.int64, device=dev)
-        self._with_opt = not distributed.is_distributed()
+        # the optimizer is in the graph unless the gradient is reduced (or its scatter finished) outside
+        self._with_opt = not distributed.is_distributed() and self.model.scatter_split is None
         state = self.opt.state_tensors()
         saved = [t.clone() for t in state]  # warm-up steps must not advance training
         saved_count = self.opt.step_count
@@ -92,6 +106,7 @@ class Trainer:
         for t, v in zip(state, saved):
             t.copy_(v)
         self.opt.step_count = saved_count
+        self.model.flat_grad().zero_()  # (the warm-ups without the optimizer left gradients behind)
 
     def _graph_step(self, batch, global_step):
         if self.graph is None:
@@ -106,22 +121,26 @@ class Trainer:
         self._step_dev.fill_(global_step)
         self.graph.replay()
         if not self._with_opt:
-            self.opt.step(grad_scale=distributed.allreduce_grads(self.model.flat_grad(), average=False))
+            self.opt.step(grad_scale=distributed.reduce_gradients(self.model))
         else:
             self.opt.step_count += 1
         return self._out
 
+    status_interval = 100  # steps between reads of the clustering kernel's error word
+
     def step(self, batch, global_step):
         m = self.model
+        if global_step % self.status_interval == 0:
+            check_cluster_status(m.flat_params().device)  # (raises if an earlier launch timed out)
         self._maybe_update_grid(global_step)
+        self.opt.set_epoch(global_step // self.steps_per_epoch)
         if self.use_graph:
             return self._graph_step(batch, global_step)
-        self.opt.zero_grad()
         kw = dict(self.render_kwargs, global_step=global_step)
         if "march_noise" in batch:
             kw["march_noise"] = batch["march_noise"]
         results = render(m, batch["rays_o"], batch["rays_d"], **kw)
         loss_d = self.loss(results, batch, global_step=global_step)
         loss_d["total"].backward()
-        self.opt.step(grad_scale=distributed.allreduce_grads(m.flat_grad(), average=False))
+        self.opt.step(grad_scale=distributed.reduce_gradients(m))
         return results, loss_d

@@ -17,11 +17,7 @@ Deliberate differences (DESIGN.md "Parity contract"):
 import torch
 
 from . import _lib
-from ._lib import I64, call, check_dtype, check_input, ptr, stream
-
-I64 = _lib.I64
-I32 = _lib.I32
-F32 = _lib.F32
+from ._lib import F32, I32, I64, call, check_dtype, check_input, ptr, stream
 
 
 def ray_aabb_intersect(rays_o, rays_d, centers, half_sizes, max_hits, near_distance=None):

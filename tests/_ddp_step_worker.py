@@ -1,8 +1,13 @@
-"""Worker of tests/test_gpu_ddp.py (not a test module): under torchrun, every rank trains the same
-model on the SAME batch through Trainer(use_graph=True) — the N>1 path: graph-captured step
-without the optimizer, all-reduce SUM of the flat gradient, Adam with grad_scale = 1/world — and
-rank 0 saves the parameters.  With identical batches the averaged gradient equals the
-single-process gradient, so the result must match a 1-process run of the same steps."""
+"""Worker of tests/test_gpu_ddp.py (not a test module).
+
+`run` — under torchrun every rank trains the model through Trainer(use_graph=True) on ITS OWN
+batches (seeded by rank and step): the N>1 path — graph-captured step without the optimizer, the
+two-bucket gradient all-reduce (SUM) overlapped with the deferred coarse-level table scatter, Adam
+with grad_scale = 1/world — and rank 0 saves the parameters.
+
+`run_reference` — one process, the eager step: for every step the gradients of all ranks' batches
+are accumulated into the flat gradient (one backward per batch, no optimizer in between), then one
+Adam step with grad_scale = 1/world, i.e. DDP's average computed without any collective."""
 import os
 import sys
 
@@ -11,20 +16,32 @@ sys.path[:0] = [os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT]
 
 import torch  # noqa: E402
 
+N_RAYS = 1024
 
-def run(steps, device, out=None):
+
+def _setup(device):
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.synthetic import SyntheticScene
-    from ncnerf_amd.trainer import Trainer
     scene = SyntheticScene()
     torch.manual_seed(0)
     model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(device))
     model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(device))
+    return scene, model
+
+
+def _batch(scene, rank, k, device):
+    batch = scene.torch_batch(N_RAYS, seed=1000 * rank + 10 + k, device=device)
+    g = torch.Generator().manual_seed(1000 * rank + k)
+    batch["march_noise"] = torch.rand(N_RAYS, generator=g).to(device)
+    return batch
+
+
+def run(steps, device, out=None, rank=0):
+    from ncnerf_amd.trainer import Trainer
+    scene, model = _setup(device)
     tr = Trainer(model, use_graph=True)
     for k in range(steps):
-        batch = scene.torch_batch(1024, seed=10 + k, device=device)
-        batch["march_noise"] = torch.rand(1024, generator=torch.Generator().manual_seed(k)).to(device)
-        tr.step(batch, global_step=3000 + k)
+        tr.step(_batch(scene, rank, k, device), global_step=3000 + k)
     torch.cuda.synchronize()
     flat = model.flat_params().detach().cpu().clone()
     if out:
@@ -32,10 +49,28 @@ def run(steps, device, out=None):
     return flat
 
 
+def run_reference(steps, device, world):
+    from ncnerf_amd.rendering import render
+    from ncnerf_amd.trainer import Trainer
+    scene, model = _setup(device)
+    tr = Trainer(model, use_graph=False)
+    for k in range(steps):
+        tr.opt.set_epoch((3000 + k) // -(-tr.epoch_items // world))  # the ranks' epoch (DistributedSampler)
+        for r in range(world):
+            batch = _batch(scene, r, k, device)
+            kw = dict(tr.render_kwargs, global_step=3000 + k, march_noise=batch["march_noise"])
+            results = render(model, batch["rays_o"], batch["rays_d"], **kw)
+            tr.loss(results, batch, global_step=3000 + k)["total"].backward()
+        tr.opt.step(grad_scale=1.0 / world)
+    torch.cuda.synchronize()
+    return model.flat_params().detach().cpu().clone()
+
+
 if __name__ == "__main__":
     from ncnerf_amd import distributed
     rank, world = distributed.init_from_env(backend=os.environ.get("DDP_BACKEND", "gloo"))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)) % torch.cuda.device_count())
-    run(int(sys.argv[2]), torch.device("cuda", torch.cuda.current_device()), sys.argv[1] if rank == 0 else None)
+    run(int(sys.argv[2]), torch.device("cuda", torch.cuda.current_device()), sys.argv[1] if rank == 0 else None,
+        rank=rank)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

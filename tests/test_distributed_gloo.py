@@ -1,5 +1,6 @@
-"""Multi-rank logic on CPU with gloo (world_size 2): gradient averaging of the flat buffer,
-patch sharding, occupancy broadcast."""
+"""Multi-rank logic on CPU with gloo (world_size 2): gradient averaging of the flat buffer, the
+two-bucket reduction overlapped with the deferred table scatter, patch sharding, occupancy
+broadcast."""
 import os
 import socket
 
@@ -22,6 +23,29 @@ class _Model:
         self.density_bitfield = torch.full((8,), rank, dtype=torch.uint8)
 
 
+class _SplitModel:
+    """Stands in for NGPMT in reduce_gradients: a flat gradient [coarse levels | fine levels + W],
+    a split, and a deferred scatter that adds into the coarse bucket (it must land before that
+    bucket is reduced, and the fine bucket must not see it)."""
+
+    def __init__(self, rank):
+        self.scatter_split = 3
+        self.g = torch.arange(12, dtype=torch.float32) + 100 * rank
+        self._deferred = True
+        self.calls = []
+
+    def flat_grad(self):
+        return self.g
+
+    def grad_buckets(self, split):
+        cut = 2 * split  # (2 floats per level in this stand-in)
+        return self.g[cut:], self.g[:cut]
+
+    def run_deferred_scatter(self, max_blocks=0):
+        self.calls.append(max_blocks)
+        self.g[: 2 * self.scatter_split] += 1000.0
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from ncnerf_amd import distributed
@@ -32,6 +56,13 @@ def _worker(rank, world, port, q):
     g2 = torch.ones(4) * (rank + 1)
     scale = distributed.allreduce_grads(g2, average=False)  # sum; the 1/world goes to the optimizer
     assert scale == 0.5 and g2.tolist() == [3.0] * 4
+    sm = _SplitModel(rank)
+    assert distributed.reduce_gradients(sm) == 0.5
+    assert sm.calls == [distributed.DP_SCATTER_BLOCKS]
+    base = torch.arange(12, dtype=torch.float32) * 2 + 100  # sum over ranks 0, 1 of arange + 100 r
+    want_split = base.clone()
+    want_split[:6] += 2000.0
+    assert torch.equal(sm.g, want_split), sm.g
     m = _Model(rank)
     distributed.broadcast_occupancy(m)
     lo, hi = distributed.shard_patches(1024, rank, world)

@@ -1,10 +1,13 @@
-"""The multi-rank training path (Trainer with world_size 2: graph without the optimizer, RCCL-style
-all-reduce SUM of the flat gradient, Adam with grad_scale 1/world) on the one GPU of the test box:
-two torchrun ranks share cuda:0 over gloo, both train on the same batches, and the parameters must
-equal a single-process run of the same steps (identical gradients: sum * 1/2 is exact).  The table
-gradient's float-atomic summation order differs run to run (and Adam turns the sign of a near-zero
-gradient into a full lr step), so the bound is the run-to-run floor of two single-process runs:
-entries off by > 1e-4 at most 3x the floor + 1e-6 of the table, everything else within 1e-6."""
+"""The multi-rank training path (Trainer with world_size 2: graph without the optimizer, two-bucket
+all-reduce SUM of the flat gradient overlapped with the deferred coarse-level scatter, Adam with
+grad_scale 1/world) on the one GPU of the test box: two torchrun ranks share cuda:0 over gloo, each
+trains on ITS OWN batches, and the parameters must equal a single-process run that accumulates the
+gradients of both ranks' batches and steps once with grad_scale 1/2 (DDP's average without a
+collective).  So a skipped or doubled all-reduce, a lost 1/world or a missing deferred scatter all
+fail.  The table gradient's float-atomic summation order differs run to run (and Adam turns the sign
+of a near-zero gradient into a full lr step), so the bound is the run-to-run floor of two
+single-process runs: entries off by > 1e-4 at most 3x the floor + 1e-6 of all, and at most 0.1 %
+off by more than 1e-6."""
 import os
 import socket
 import subprocess
@@ -35,9 +38,9 @@ def test_two_rank_step_matches_single_process(dev, tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     dist_flat = torch.load(out, weights_only=True)
     sys.path.insert(0, HERE)
-    from _ddp_step_worker import run
-    single = run(steps, dev)
-    single2 = run(steps, dev)
+    from _ddp_step_worker import run_reference
+    single = run_reference(steps, dev, world=2)
+    single2 = run_reference(steps, dev, world=2)
     assert torch.isfinite(single).all()
     floor = int(((single2 - single).abs() > 1e-4).sum())
     d = (dist_flat - single).abs()

@@ -188,3 +188,50 @@ def test_cluster_after_unclustered_call(dev):
     C, a = losses_ref.spherical_kmeans(X[valid], K=20, niter=20, seed=1234)
     _, labels, cents, _ = L.cluster_losses(torch.from_numpy(X).to(dev), K=20, niter=20, seed=1234, t_similar=0.99)
     np.testing.assert_allclose(cents.cpu().numpy(), C, atol=1e-5)
+
+
+_STATUS_CHILD = r"""
+import os, sys
+sys.path[:0] = [os.path.join(sys.argv[1], "normal-clustering-nerf_amd"), sys.argv[1]]
+import numpy as np, torch
+from ncnerf_amd import losses as L, _lib
+rng = np.random.default_rng(0)
+x = rng.normal(size=(6272, 3)).astype(np.float32)
+x /= np.linalg.norm(x, axis=1, keepdims=True)
+L.cluster_losses(torch.from_numpy(x).cuda(), K=20, niter=20)
+torch.cuda.synchronize()
+try:
+    L.check_cluster_status()
+except _lib.NcnError as e:
+    print("RAISED", e)
+    sys.exit(0)
+print("NOT RAISED")
+sys.exit(1)
+"""
+
+
+def test_cluster_status_word(dev):
+    """The clustering kernel's sticky error word reaches the caller: clean after normal launches;
+    a diagnostic build whose barrier / hand-off spin limits are 1 (libncnerf_diag_kmspin.so) sets it
+    in a real launch and check_cluster_status raises; a set word raises on the product library."""
+    import os
+    import subprocess
+    import sys
+    from ncnerf_amd import _lib
+    L.check_cluster_status()  # the launches of the tests above left it clear
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    diag = os.path.join(root, "normal-clustering-nerf_amd", "ncnerf_amd", "libncnerf_diag_kmspin.so")
+    assert os.path.exists(diag), "build the diagnostic library (make -C normal-clustering-nerf_amd)"
+    r = subprocess.run([sys.executable, "-c", _STATUS_CHILD, root], env=dict(os.environ, NCN_LIB_PATH=diag),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "RAISED" in r.stdout, r.stdout + r.stderr[-2000:]
+    # product library: a set word is reported
+    x = torch.from_numpy(_manhattan_normals(512, 3)).to(dev)
+    L.cluster_losses(x, K=20, niter=20)
+    ws = L._WS[(str(dev), 20)]
+    off = int(_lib.lib().ncn_cluster_status_offset(20))
+    ws.view(torch.int32)[off] = 1
+    with pytest.raises(_lib.NcnError):
+        L.check_cluster_status(dev)
+    ws.view(torch.int32)[off] = 0
+    L.check_cluster_status(dev)

@@ -1,0 +1,86 @@
+"""ncn_adam_step (FlatAdam) element-wise against torch: clip_grad_norm_(max_norm) on the scaled
+gradient, then torch.optim.AdamW with the reference's two groups (hash grid wd 0, nets wd 1e-6,
+eps 1e-15; train_nerf.py:262-285, 955).  apex FusedAdam's AdamW update (the reference optimizer)
+and torch's differ only in rounding order: tolerance 2e-6 relative on the parameters + 1e-9.
+Covers grad_scale != 1 (DDP's 1/world), an odd n (scalar tail), an odd group boundary, clipped and
+unclipped norms, n beyond one grid-stride of the Adam launch, and the zero_grad fold."""
+import math
+
+import pytest
+import torch
+
+from ncnerf_amd.optim import FlatAdam
+
+pytestmark = pytest.mark.gpu
+
+
+class _Flat:
+    def __init__(self, p, n_table):
+        self._p, self._g, self._n_table = p, torch.zeros_like(p), n_table
+
+    def flat_params(self):
+        return self._p
+
+    def flat_grad(self):
+        return self._g
+
+
+def _torch_reference(p0, grads, n0, scale, lr, max_norm, wd=(0.0, 1e-6)):
+    a = p0[:n0].clone().requires_grad_(True)
+    b = p0[n0:].clone().requires_grad_(True)
+    opt = torch.optim.AdamW([{"params": [a], "weight_decay": wd[0]}, {"params": [b], "weight_decay": wd[1]}],
+                            lr=lr, betas=(0.9, 0.999), eps=1e-15, foreach=False)
+    for g in grads:
+        gs = g * scale
+        a.grad, b.grad = gs[:n0].clone(), gs[n0:].clone()
+        torch.nn.utils.clip_grad_norm_([a, b], max_norm)
+        opt.step()
+    return torch.cat([a.detach(), b.detach()])
+
+
+@pytest.mark.parametrize("n,n0,scale,gmag,steps", [
+    (100003, 70001, 0.5, 1e-2, 3),       # clipped (norm >> 0.05), odd sizes, DDP scale
+    (100003, 70001, 1.0, 1e-5, 3),       # unclipped
+    (4096, 4096, 0.25, 1.0, 3),          # one group only
+    (34_000_003, 22_000_001, 0.5, 1e-3, 1),  # beyond 16384 workgroups x 2048 elements
+])
+def test_adam_step_matches_torch_adamw(dev, n, n0, scale, gmag, steps):
+    g = torch.Generator(device=dev).manual_seed(n)
+    p0 = torch.randn(n, device=dev, generator=g) * 0.1
+    grads = [torch.randn(n, device=dev, generator=g) * gmag for _ in range(steps)]
+    m = _Flat(p0.clone(), n0)
+    opt = FlatAdam(m, lr=1e-2, max_norm=0.05, zero_grad_on_step=True)
+    for gr in grads:
+        m.flat_grad().copy_(gr)
+        opt.step(grad_scale=scale)
+        assert int(m.flat_grad().count_nonzero()) == 0  # gradient consumed and zeroed
+    ref = _torch_reference(p0, grads, n0, scale, 1e-2, 0.05)
+    err = (m.flat_params() - ref).abs()
+    tol = 2e-6 * ref.abs() + 1e-9
+    bad = int((err > tol).sum())
+    assert bad == 0, (bad, float(err.max()))
+    assert int(opt.step_dev.item()) == steps
+
+
+def test_adam_step_keeps_grad_without_fold(dev):
+    m = _Flat(torch.zeros(1000, device=dev), 500)
+    opt = FlatAdam(m, lr=1e-2, max_norm=0.05)
+    m.flat_grad().fill_(1.0)
+    opt.step()
+    assert bool((m.flat_grad() == 1.0).all())
+
+
+def test_trainer_sets_cosine_epoch_lr(dev):
+    """Trainer.step applies CosineAnnealingLR(T_max=30) per 1000-step epoch (train_nerf.py:286-288)."""
+    from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
+    from ncnerf_amd.synthetic import SyntheticScene
+    from ncnerf_amd.trainer import Trainer
+    scene = SyntheticScene()
+    model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+    model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+    tr = Trainer(model)
+    batch = scene.torch_batch(256, seed=0, device=dev)
+    for step, epoch in ((999, 0), (1000, 1), (14999, 14), (15000, 15)):
+        tr.step(batch, global_step=step)
+        want = 0.5 * 1e-2 * (1 + math.cos(math.pi * epoch / 30))
+        assert abs(tr.opt.lr - want) < 1e-12 and abs(float(tr.opt.lr_dev.item()) - want) < 1e-9

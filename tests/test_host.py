@@ -71,3 +71,30 @@ def test_vren_rejects_cpu_tensors():
     from ncnerf_amd import vren
     with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
         vren.composite_train_multi_fw(*(torch.zeros(4) for _ in range(4)), torch.zeros(1, 3, dtype=torch.long), 1e-4)
+
+
+def test_flat_adam_set_epoch_is_cosine_annealing():
+    """FlatAdam.set_epoch == torch CosineAnnealingLR(T_max=num_epochs, eta_min=0) stepped per epoch
+    (train_nerf.py:286-288); runs on CPU tensors (no kernel call)."""
+    import torch
+    from ncnerf_amd.optim import FlatAdam
+
+    class _M:
+        _n_table = 4
+
+        def __init__(self):
+            self.p = torch.zeros(8)
+
+        def flat_params(self):
+            return self.p
+
+    opt = FlatAdam(_M(), lr=1e-2, num_epochs=30)
+    p = torch.nn.Parameter(torch.zeros(1))
+    ref_opt = torch.optim.SGD([p], lr=1e-2)
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(ref_opt, 30, 0)
+    for e in range(30):
+        opt.set_epoch(e)
+        assert abs(opt.lr - ref_opt.param_groups[0]["lr"]) < 1e-12, e
+        assert abs(float(opt.lr_dev) - opt.lr) < 1e-9
+        ref_opt.step()
+        sch.step()
