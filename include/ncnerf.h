@@ -264,7 +264,7 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
  * arrival counter is left zero by every call).  zero_grads != 0: the Adam pass also writes zeros over
  * the gradient it consumed (the next step's zero_grad folded in).  Buffers 16-byte aligned. */
 int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
-                  float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
+                  float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
                   const float* lr_dev, int* step_dev, float* work, int zero_grads, void* stream);
 int64_t ncn_adam_step_work_floats(void);
 

@@ -97,7 +97,7 @@ constexpr int ADAM_BLOCKS = 256;     // workgroups of adam_prep (partials)
 constexpr int ADAM_THREADS = 1024;
 constexpr int ADAM_UNROLL = 12;      // float4 loads in flight per thread (45.8 MB: 11 per thread)
 __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float gscale,
-                                                               float max_norm, float b1, float b2, float lr,
+                                                               float max_norm, double b1, double b2, float lr,
                                                                const float* __restrict__ lr_dev,
                                                                int* __restrict__ step_dev, float* __restrict__ work) {
     float* part = work;                                // [ADAM_BLOCKS]
@@ -157,8 +157,10 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
             const int st = *step_dev + 1;  // device step counter
             *step_dev = st;
             sc[0] = (max_norm > 0.f ? fminf(c, 1.0f) : 1.0f) * gscale;
-            sc[1] = 1.0f - powf(b1, (float)st);
-            sc[2] = 1.0f - powf(b2, (float)st);
+            // bias corrections in double from the double betas, as apex's host code forms them
+            // (1 - beta ** step in Python): 1 - 0.999f in f32 is off by 1.3e-5 relative
+            sc[1] = (float)(1.0 - pow(b1, (double)st));
+            sc[2] = (float)(1.0 - pow(b2, (double)st));
             sc[3] = lr_dev ? *lr_dev : lr;
             *cnt = 0u;
         }
@@ -225,7 +227,7 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
 }
 
 int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
-                  float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps, float wd0, float wd1,
+                  float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
                   const float* lr_dev, int* step_dev, float* work, int zero_grads, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
@@ -240,10 +242,12 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 16384);
     if (zero_grads)
         hipLaunchKernelGGL(adam_apply_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
-                           exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
+                           exp_avg, exp_avg_sq, n, n_group0, (float)beta1, (float)beta2, eps, wd0, wd1,
+                           work + ADAM_BLOCKS + 4);
     else
         hipLaunchKernelGGL(adam_apply_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
-                           exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0, wd1, work + ADAM_BLOCKS + 4);
+                           exp_avg, exp_avg_sq, n, n_group0, (float)beta1, (float)beta2, eps, wd0, wd1,
+                           work + ADAM_BLOCKS + 4);
     NCN_LAUNCH_CHECK("ncn_adam_step");
     return 0;
 }

@@ -58,7 +58,7 @@ SIGNATURES = {
     "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
-    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F32, F32, F32, F32, F32, P, P, P, I32, P],
+    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P],
     "ncn_adam_step_work_floats": [],
     "ncn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "ncn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],

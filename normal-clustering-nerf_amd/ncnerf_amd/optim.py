@@ -56,7 +56,7 @@ class FlatAdam:
         g = self.model.flat_grad()
         b1, b2 = self.betas
         call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
-             F32(grad_scale), F32(self.max_norm), F32(self.lr), F32(b1), F32(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
+             F32(grad_scale), F32(self.max_norm), F32(self.lr), _lib.F64(b1), _lib.F64(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
              ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), I32(1 if self.zero_grad_on_step else 0), stream())
 
     def state_tensors(self):
