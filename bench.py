@@ -165,6 +165,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grid-update", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager (Python-launched) step instead of a HIP graph")
+    ap.add_argument("--precision", choices=("fp16", "bf16"), default="fp16",
+                    help="MFMA operand type of the field MLP (fp16 = tcnn's FullyFusedMLP, the reference's AMP run)")
+    ap.add_argument("--no-bf16-line", action="store_true",
+                    help="skip the second measurement of configs[2] with bf16 MLP operands")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="launch/rendezvous check only (no GPU work): every rank all-reduces its rank, rank 0 "
                          "prints {world, backend, sum}")
@@ -197,59 +201,66 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.manual_seed(1234 + rank)
 
-    scene = SyntheticScene()
-    model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
-    with torch.no_grad():
-        model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
-        model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
-    trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph)
-    n_batches = 8
-    batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
-    step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
-    if trainer.update_grid:  # first-call costs of the refresh path stay out of the timed region
-        model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
-    for k in range(args.warmup):
-        trainer.step(batches[k % n_batches], global_step=step0 + k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    counts = []  # per-step device counts (copied: graph outputs are overwritten by the next replay)
-    if args.no_graph:
-        _lib.TIMING = {n: [] for n in TIMED}
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        results, _ = trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k)
-        counts.append((results["rm_samples"].clone(), results["vr_samples"].clone()))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    if not args.no_graph:
-        # Per-kernel durations (the `kernels` table): a graph replay has no host launch to bracket,
-        # so the captured body is run eagerly for `steps` more steps with HIP events on the launch
-        # stream around each hot kernel (GPU spin in front: see _lib.TIMING).
-        _lib.TIMING = {n: [] for n in TIMED}
-        step_t = torch.full((), step0, dtype=torch.int64, device=dev)
-        for k in range(args.steps):
-            trainer._body(batches[k % n_batches], step_t, trainer._with_opt)
-            if not trainer._with_opt:
-                trainer.opt.step(grad_scale=distributed.reduce_gradients(model))
+    def measure(precision, steps, kernel_table):
+        """Build the model in `precision`, warm up, time `steps` graph-replayed training steps
+        (barrier + synchronize on both sides), max over ranks."""
+        scene = SyntheticScene()
+        model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
+        with torch.no_grad():
+            model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
+            model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+        trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph)
+        n_batches = 8
+        batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
+        step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
+        if trainer.update_grid:  # first-call costs of the refresh path stay out of the timed region
+            model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
+        for k in range(args.warmup):
+            trainer.step(batches[k % n_batches], global_step=step0 + k)
         torch.cuda.synchronize()
-    timing = _lib.TIMING
-    _lib.TIMING = None
-    rm = sum(torch.as_tensor(a).double().sum() for a, _ in counts)
-    vr = sum(torch.as_tensor(b).double().sum() for _, b in counts)
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    tot = torch.stack([rm, vr]).reshape(2)
-    rank_ms = [round(1e3 * (t1 - t0) / args.steps, 3)]
-    if world > 1:
-        gathered = [torch.zeros_like(elapsed) for _ in range(world)]
-        dist.all_gather(gathered, elapsed)
-        rank_ms = [round(1e3 * float(g.item()) / args.steps, 3) for g in gathered]
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    el = float(elapsed.item())
+        if world > 1:
+            dist.barrier()
+        counts = []  # per-step device counts (copied: graph outputs are overwritten by the next replay)
+        if args.no_graph and kernel_table:
+            _lib.TIMING = {n: [] for n in TIMED}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            results, _ = trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k)
+            counts.append((results["rm_samples"].clone(), results["vr_samples"].clone()))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        if not args.no_graph and kernel_table:
+            # Per-kernel durations (the `kernels` table): a graph replay has no host launch to bracket,
+            # so the captured body is run eagerly for `steps` more steps with HIP events on the launch
+            # stream around each hot kernel (GPU spin in front: see _lib.TIMING).
+            _lib.TIMING = {n: [] for n in TIMED}
+            step_t = torch.full((), step0, dtype=torch.int64, device=dev)
+            for k in range(steps):
+                trainer._body(batches[k % n_batches], step_t, trainer._with_opt)
+                if not trainer._with_opt:
+                    trainer.opt.step(grad_scale=distributed.reduce_gradients(model))
+            torch.cuda.synchronize()
+        timing = _lib.TIMING or {}
+        _lib.TIMING = None
+        rm = sum(torch.as_tensor(a).double().sum() for a, _ in counts)
+        vr = sum(torch.as_tensor(b).double().sum() for _, b in counts)
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        tot = torch.stack([rm, vr]).reshape(2)
+        rank_ms = [round(1e3 * (t1 - t0) / steps, 3)]
+        if world > 1:
+            gathered = [torch.zeros_like(elapsed) for _ in range(world)]
+            dist.all_gather(gathered, elapsed)
+            rank_ms = [round(1e3 * float(g.item()) / steps, 3) for g in gathered]
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        return dict(el=float(elapsed.item()), tot=tot, rank_ms=rank_ms, timing=timing, model=model, batches=batches)
+
+    main_run = measure(args.precision, args.steps, True)
+    el, tot, rank_ms, timing = main_run["el"], main_run["tot"], main_run["rank_ms"], main_run["timing"]
+    model, batches = main_run["model"], main_run["batches"]
     kern = {}
     for name, evs in timing.items():
         if evs:
@@ -257,6 +268,17 @@ def main():
             kern[name] = {"avg_us": round(1e3 * float(np.mean(ms)), 2), "launches": len(ms)}
     cf_bytes_per_launch, cf_us = composite_fw_roofline(model, batches[0], dev)
     traffic, traffic_src = pmc_traffic()
+    del main_run, model, batches
+    second = None
+    if not args.no_bf16_line:  # the same step with the other MLP operand type (configs[2] asks for bf16)
+        prec2 = "bf16" if args.precision == "fp16" else "fp16"
+        r2 = measure(prec2, args.steps, False)
+        second = {"precision": prec2, "value": round(args.rays * world * args.steps / r2["el"], 1), "unit": "rays/s",
+                  "ms_per_step": round(1e3 * r2["el"] / args.steps, 3),
+                  "samples_per_s": round(float(r2["tot"][0].item()) / r2["el"], 1),
+                  "workload": "configs[2]: the same full training step (normal clustering on), " + prec2 +
+                              "-operand MFMA in the field MLP"}
+        del r2
     achieved = cf_bytes_per_launch / (cf_us * 1e-6) / 1e9
     if rank != 0:
         if world > 1:
@@ -278,7 +300,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32 (march/composite/losses); fp16-operand MFMA with fp32 accumulate in the field MLP",
+        "dtype": f"fp32 (march/composite/losses); {args.precision}-operand MFMA with fp32 accumulate in the field MLP",
         "data": "synthetic Hypersim-shaped batches (ai_001_001 box, 8x8 patches, procedural room occupancy); "
                 "random-init NGPMT",
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
@@ -297,6 +319,8 @@ def main():
                                "stream, host launch latency hidden behind a GPU spin"},
         "kernels": kern,
     }
+    if second is not None:
+        out["other_precision"] = second
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     print(json.dumps(out))

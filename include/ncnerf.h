@@ -146,22 +146,29 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
  *      (ngp_mt.py:70-113, 157-229; custom_functions.py:162-173).
  * Hash grid geometry (16 levels, 2 features) is described by `levels` = 16 x {scale f32 bits,
  *   resolution, params, offset} as uint32 (see ncnerf_amd/ngp_mt.py:grid_levels).
- * weights_packed: fp16 MFMA fragments produced by ncn_field_pack_weights from the fp32 masters
- *   W1 (64,32) W2 (16,64) W3 (64,19) W4 (64,64) W5 (3,64) concatenated (size NCN_FIELD_NW floats).
- * enc_cache: fp16 encoding cache for the backward, NCN_ENC_BYTES_PER_SAMPLE bytes per sample
- *   (rounded up to 16 samples); may be NULL for inference.
+ * Weights: fp32 masters in tcnn's padded shapes, concatenated (NCN_FIELD_NW floats): sigma_net
+ *   W1 (64,32) W2 (16,64); rgb_net W3 (64,32) W4 (64,64) W5 (16,64) — tcnn pads rgb_net's 19 inputs
+ *   cat[d/|d|, h] to 32 with constant 1.0 (columns 19..31 of W3 act as a bias) and its 3 outputs
+ *   to 16 (rows 3..15 of W5 are parameters whose outputs are discarded).
+ * precision: NCN_PREC_F16 (tcnn's FullyFusedMLP precision) or NCN_PREC_BF16 — the MFMA operand
+ *   type of weights_packed, enc_cache and the activations; accumulation is fp32 either way.
+ * weights_packed: NCN_FIELD_PACKED_HALVES 16-bit MFMA fragments (16-byte aligned) produced by
+ *   ncn_field_pack_weights(precision) from the fp32 masters.
+ * enc_cache: encoding cache for the backward in the operand precision, NCN_ENC_BYTES_PER_SAMPLE
+ *   bytes per sample (rounded up to 16 samples, 16-byte aligned); may be NULL for inference.
  * mode 0: full (sigmas + rgbs), mode 1: density only (sigmas; dirs/rgbs ignored).
  * n_dev: NULL, or a device int32 holding the real sample count (<= n): then n is the capacity of
  *   the buffers (static-shape / graph-captured step, where the host never reads the marcher's
  *   counter); grids are sized from n, the kernels stop at *n_dev. ---- */
-#define NCN_FIELD_NW (64 * 32 + 16 * 64 + 64 * 19 + 64 * 64 + 3 * 64)
+#define NCN_FIELD_NW (64 * 32 + 16 * 64 + 64 * 32 + 64 * 64 + 16 * 64)
 #define NCN_FIELD_PACKED_HALVES 19456
 #define NCN_ENC_BYTES_PER_SAMPLE 64
-int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void* stream);
+#define NCN_PREC_F16 0
+#define NCN_PREC_BF16 1
+int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int precision, void* stream);
 int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const float* table,
-                  const uint32_t* levels,
-                  float xyz_min, float xyz_extent, const uint16_t* weights_packed, int mode,
-                  float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
+                  const uint32_t* levels, float xyz_min, float xyz_extent, const uint16_t* weights_packed,
+                  int precision, int mode, float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
 /* Backward: accumulates (+=) into grad_table (n_entries,2) and writes per-block weight-gradient
  * slabs (n_blocks x NCN_FIELD_NW) into `slab`; ncn_field_reduce_wgrad sums them into grad_w (+=).
  * n_blocks is returned by ncn_field_bwd_blocks(n).  dE_ws is a device workspace of
@@ -170,9 +177,9 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
 int ncn_field_bwd_blocks(int64_t n);
 int64_t ncn_field_bwd_dE_floats(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
-                  float xyz_min,
-                  float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
-                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
+                  float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision,
+                  const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* grad_table,
+                  float* slab, float* dE_ws,
                   float* level_max /* 16 * ncn_field_bwd_blocks(n) floats of workspace (per-level max |dE|) */,
                   void* stream);
 /* ncn_field_bwd in its two passes (the data-parallel step overlaps the gradient all-reduce of one
@@ -181,8 +188,8 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * max_blocks > 0 caps the scatter's workgroups (one per CU otherwise), leaving CUs to a concurrent
  * collective. */
 int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const uint16_t* weights_packed,
-                      const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* slab,
-                      float* dE_ws, float* level_max, void* stream);
+                      int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
+                      float* slab, float* dE_ws, float* level_max, void* stream);
 int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
                       int max_blocks, float* grad_table, void* stream);
@@ -211,9 +218,20 @@ int ncn_photo_loss_fwd(const float* rgb, const float* rgb_gt, const float* opaci
                        float* loss, void* stream);
 int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
                        const float* loss, const float* upstream, float* dL_drgb, float* dL_dopacity, void* stream);
+/* faiss k-means plan: the random draws of faiss's Clustering::train for every valid-point count
+ * nx <= n_tri, built on the HOST with std::mt19937 (faiss's RandomGenerator engine):
+ * subsample_training_set's rand_perm(seed) membership when nx > K*256, the init picks (first K of
+ * rand_perm(seed + 1) of the training set, as indices into the valid points), and 4096 floats of
+ * split_clusters' RandomGenerator(1234).  ncn_kmeans_plan_words(n_tri, K) 32-bit words; the caller
+ * copies the filled host buffer to the device once and passes it to every ncn_cluster_loss call
+ * with the same (n_tri, K).  seed: faiss ClusteringParameters::seed (1234 in the reference). */
+int64_t ncn_kmeans_plan_words(int n_tri, int K);
+int ncn_kmeans_plan_fill(int n_tri, int K, uint32_t seed, uint32_t* host_out);
 /* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations), cluster selection,
  * the three cluster losses and their gradient w.r.t. the normals, scaled by w_ort / w_dot / w_l1,
  * in ONE launch of 32 co-resident workgroups (grid barriers between the phases).  n_tri <= 16384.
+ * kmeans_plan: device copy of ncn_kmeans_plan_fill(n_tri, K, seed) (a mismatched plan sets the
+ * status word, ncn_cluster_status_offset).
  * out_losses (11 floats): [0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter;
  * [3] = valid n; [4..6] = the weighted terms; [7..9] = the weights used; [10] = total (only when
  * photo_loss is given: photo_loss[0] + photo_loss[1] + [4] + [5] + [6], losses.py's sum over the
@@ -232,7 +250,8 @@ int64_t ncn_cluster_workspace_words(int K);
  * Lloyd hand-off of any call on this workspace timed out (its results are then wrong).  The
  * caller reads it outside the hot loop (the training step: every few steps) and fails. */
 int64_t ncn_cluster_status_offset(int K);
-int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
+int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, const uint32_t* kmeans_plan,
+                     float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,
                      float sched_start, float sched_grow, const float* photo_loss, float* out_losses,
                      int32_t* out_labels, float* out_centroids, float* dL_dnormals, float* workspace, void* stream);

@@ -1,17 +1,23 @@
 // NGPMT field for gfx950: multires hash-grid encoding (tiny-cuda-nn Grid/Hash semantics) fused
-// with sigma_net (32->64->16), TruncExp, and rgb_net (cat[d/|d|, h] 19->64->64->3, Sigmoid).
-// Replaces tcnn Encoding + two FullyFusedMLPs (reference models/ngp_mt.py:70-113, 157-229) and
-// TruncExp (models/custom_functions.py:162-173).
+// with sigma_net (32->64->16), TruncExp, and rgb_net, replacing tcnn Encoding + two FullyFusedMLPs
+// (reference models/ngp_mt.py:70-113, 157-229) and TruncExp (models/custom_functions.py:162-173).
+// rgb_net is tcnn's network as built by the reference: `tcnn.Network(n_input_dims=19, ...)` wraps
+// an Identity encoding that pads the 19 inputs cat[d/|d|, h] to the FullyFusedMLP's 16-alignment
+// (32) with the value 1.0 (a learned bias in the padded columns), and pads the 3 outputs to 16:
+// W3 is 64x32, W5 16x64 (rgb_net.params = 7168, sigma_net.params = 3072, as tcnn).
 //
-// Layout ("transposed activations"): every layer is computed as  Y^T = W . X^T  with
-// v_mfma_f32_16x16x16_f16, samples on the MFMA column (lane & 15) and features on the rows.
-// The accumulator of one layer (lane (g,r) holds rows 4g..4g+3 of column r) is *exactly* the
-// B-operand layout of a K=16 step of the next layer, so activations never leave registers.
-// A wave owns 16 samples per step; lane (g = lane>>4, r = lane&15) encodes hash levels
-// {2g, 2g+1, 8+2g, 9+2g} of sample r — i.e. the two K=16 steps of layer 1 — and in the backward
-// scatters the gradient of exactly those levels.  Weights live in LDS as pre-packed fp16 MFMA
-// fragments (ncn_field_pack_weights), 8 bytes per lane per fragment (ds_read_b64).
-// Numerics: fp32 hash table + fp32 trilinear interpolation, fp16 MFMA operands, fp32 accumulate.
+// Layout ("transposed activations"): every layer is computed as  Y^T = W . X^T  with the gfx950
+// v_mfma_f32_16x16x32_{f16,bf16} (K = 32 per instruction), samples on the MFMA column (lane & 15),
+// features on the rows.  The accumulator of a layer (lane (g,r) holds rows 4g..4g+3 of column r)
+// is the B operand of the next layer with no data movement: two 16-row accumulator tiles side by
+// side form a K = 32 operand whose element j of lane group g is feature phi(g,j) = 4g+j (j < 4, the
+// first tile) or 16+4g+j-4 (the second), and the A fragments (weights) are packed in the same
+// permuted K order.  A wave owns 16 samples per step; lane (g,r) encodes hash levels
+// {2g, 2g+1, 8+2g, 9+2g} of sample r — exactly features phi(g, 0..7) of the encoding, i.e. the
+// layer-1 B operand — and in the backward scatters the gradient of those levels.  Weights live in
+// LDS as pre-packed MFMA fragments (ncn_field_pack_weights, 16 B per lane per K=32 fragment).
+// Operand precision is a template parameter: fp16 (tcnn's FullyFusedMLP precision) or bf16
+// (config #3); fp32 hash table + fp32 trilinear interpolation, fp32 accumulation either way.
 #include <algorithm>
 #include <cstring>
 #include "common.h"
@@ -19,78 +25,123 @@
 
 namespace ncn {
 
-typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float4_t mfma16(half4_t a, half4_t b, float4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ half4_t to_h4(float4_t v) {
-    half4_t h;
-    h[0] = (_Float16)v[0]; h[1] = (_Float16)v[1]; h[2] = (_Float16)v[2]; h[3] = (_Float16)v[3];
-    return h;
-}
-__device__ __forceinline__ half4_t relu_h4(float4_t v) {
-    half4_t h;
-#pragma unroll
-    for (int i = 0; i < 4; i++) h[i] = (_Float16)fmaxf(v[i], 0.0f);
-    return h;
-}
+// MFMA operand traits: T = _Float16 or __bf16; v4 = one K=16 / half a K=32 fragment, v8 = K=32.
+template <typename T> struct Mfma;
+template <> struct Mfma<_Float16> {
+    typedef _Float16 v4 __attribute__((ext_vector_type(4)));
+    typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+    static __device__ __forceinline__ float4_t k32(v8 a, v8 b, float4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ float4_t k16(v4 a, v4 b, float4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct Mfma<__bf16> {
+    typedef __bf16 v4 __attribute__((ext_vector_type(4)));
+    typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+    static __device__ __forceinline__ float4_t k32(v8 a, v8 b, float4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ float4_t k16(v4 a, v4 b, float4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+    }
+};
+
 __device__ __forceinline__ float4_t zero4() { return float4_t{0.f, 0.f, 0.f, 0.f}; }
-// ReLU backward on a gradient tile: keep v where the saved fp16 activation is > 0, as fp16
-__device__ __forceinline__ half4_t relu_mask_h4(float4_t v, half4_t x) {
-    half4_t h;
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::v4 cvt4(float4_t v) {  // round to the operand type (RNE)
+    typename Mfma<T>::v4 h;
 #pragma unroll
-    for (int i = 0; i < 4; i++) h[i] = x[i] > (_Float16)0.0f ? (_Float16)v[i] : (_Float16)0.0f;
+    for (int i = 0; i < 4; i++) h[i] = (T)v[i];
     return h;
 }
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::v4 relu4(float4_t v) {
+    typename Mfma<T>::v4 h;
+#pragma unroll
+    for (int i = 0; i < 4; i++) h[i] = (T)fmaxf(v[i], 0.0f);
+    return h;
+}
+// ReLU backward on a gradient tile: keep v where the saved (rounded) activation is > 0
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::v4 relu_mask4(float4_t v, typename Mfma<T>::v4 x) {
+    typename Mfma<T>::v4 h;
+#pragma unroll
+    for (int i = 0; i < 4; i++) h[i] = (float)x[i] > 0.0f ? (T)v[i] : (T)0.0f;
+    return h;
+}
+template <typename V8, typename V4>
+__device__ __forceinline__ V8 cat8(V4 a, V4 b) {
+    return V8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
 
-// ---- packed weight fragment table (units: fragments of 64 lanes x 4 halves = 512 B) ----
+// ---- packed weight fragments ----
+// K=32 fragments (64 lanes x 8 values = 1 KB; lane (g,r) element j = A[row r][k phi(g,j)])
 // forward (A = W, rows = out, K = in)
-constexpr int F_L1 = 0;    // [t 0..3][ks 0..1]     W1[16t+r][16ks+4g+j]
-constexpr int F_L2 = 8;    // [ks 0..3]             W2[r][16ks+4g+j]
-constexpr int F_L3 = 12;   // [t 0..3][ks 0..1]     ks0: W3[16t+r][3+4g+j] (h), ks1: g==0&&j<3 ? W3[16t+r][j] (d)
-constexpr int F_L4 = 20;   // [t 0..3][ks 0..3]     W4[16t+r][16ks+4g+j]
-constexpr int F_L5 = 36;   // [ks 0..3]             r<3 ? W5[r][16ks+4g+j]
-constexpr int N_FWD_FRAGS = 40;
+constexpr int F_L1 = 0;    // [t 0..3]          W1[16t+r][phi]
+constexpr int F_L2 = 4;    // [s 0..1]          W2[r][32s+phi]
+constexpr int F_L3 = 6;    // [t 0..3]          W3[16t+r][psi]   (psi: the padded-input order, below)
+constexpr int F_L4 = 10;   // [t 0..3][s 0..1]  W4[16t+r][32s+phi]
+constexpr int F_L5 = 18;   // [s 0..1]          W5[r][32s+phi]   (all 16 padded output rows)
+constexpr int N_FWD32 = 20;
 // backward (A = W^T, rows = in, K = out)
-constexpr int B_L5 = 40;   // [t 0..3]              4g+j<3 ? W5[4g+j][16t+r]
-constexpr int B_L4 = 44;   // [t 0..3][ks 0..3]     W4[16ks+4g+j][16t+r]
-constexpr int B_L3 = 60;   // [ks 0..3]             W3[16ks+4g+j][3+r]       (rows = h only)
-constexpr int B_L2 = 64;   // [t 0..3]              W2[4g+j][16t+r]
-constexpr int B_L1 = 68;   // [t 0..1][ks 0..3]     W1[16ks+4g+j][16t+r]
-constexpr int N_FRAGS = 76;
-static_assert(N_FRAGS * 256 == NCN_FIELD_PACKED_HALVES, "packed size");
+constexpr int B_L4 = 20;   // [t 0..3][s 0..1]  W4[32s+phi][16t+r]
+constexpr int B_L3 = 28;   // [s 0..1]          W3[32s+phi][3+r]   (rows = h only)
+constexpr int B_L1 = 30;   // [t 0..1][s 0..1]  W1[32s+phi][16t+r]
+constexpr int N_FRAG32 = 34;
+// K=16 fragments (64 lanes x 4 values = 512 B; lane (g,r) element j = A[row r][k 4g+j]) of the two
+// products whose K is a 16-wide layer output (the K=32 form would be half zeros)
+constexpr int B_L5 = 0;    // [t 0..3]          W5[4g+j][16t+r]
+constexpr int B_L2 = 4;    // [t 0..3]          W2[4g+j][16t+r]
+constexpr int N_FRAG16 = 8;
+constexpr int PACKED_HALVES = N_FRAG32 * 512 + N_FRAG16 * 256;
+static_assert(PACKED_HALVES == NCN_FIELD_PACKED_HALVES, "packed size");
 
-// master weight offsets (floats) inside the concatenated fp32 buffer
-constexpr int W1_OFF = 0, W2_OFF = W1_OFF + 64 * 32, W3_OFF = W2_OFF + 16 * 64, W4_OFF = W3_OFF + 64 * 19,
-              W5_OFF = W4_OFF + 64 * 64, W_TOTAL = W5_OFF + 3 * 64;
+// master weight offsets (floats) inside the concatenated fp32 buffer (tcnn's padded shapes)
+constexpr int W1_OFF = 0, W2_OFF = W1_OFF + 64 * 32, W3_OFF = W2_OFF + 16 * 64, W4_OFF = W3_OFF + 64 * 32,
+              W5_OFF = W4_OFF + 64 * 64, W_TOTAL = W5_OFF + 16 * 64;
 static_assert(W_TOTAL == NCN_FIELD_NW, "weights size");
 
-__device__ float frag_value(const float* __restrict__ W, int f, int lane, int j) {
-    const int g = lane >> 4, r = lane & 15;
-    const int k4 = 4 * g + j;
-    if (f < F_L2) { const int t = (f - F_L1) >> 1, ks = (f - F_L1) & 1; return W[W1_OFF + (16 * t + r) * 32 + 16 * ks + k4]; }
-    if (f < F_L3) { const int ks = f - F_L2; return W[W2_OFF + r * 64 + 16 * ks + k4]; }
-    if (f < F_L4) {
-        const int t = (f - F_L3) >> 1, ks = (f - F_L3) & 1;
-        if (ks == 0) return W[W3_OFF + (16 * t + r) * 19 + 3 + k4];
-        return (g == 0 && j < 3) ? W[W3_OFF + (16 * t + r) * 19 + j] : 0.f;
-    }
-    if (f < F_L5) { const int t = (f - F_L4) >> 2, ks = (f - F_L4) & 3; return W[W4_OFF + (16 * t + r) * 64 + 16 * ks + k4]; }
-    if (f < B_L5) { const int ks = f - F_L5; return r < 3 ? W[W5_OFF + r * 64 + 16 * ks + k4] : 0.f; }
-    if (f < B_L4) { const int t = f - B_L5; return k4 < 3 ? W[W5_OFF + k4 * 64 + 16 * t + r] : 0.f; }
-    if (f < B_L3) { const int t = (f - B_L4) >> 2, ks = (f - B_L4) & 3; return W[W4_OFF + (16 * ks + k4) * 64 + 16 * t + r]; }
-    if (f < B_L2) { const int ks = f - B_L3; return W[W3_OFF + (16 * ks + k4) * 19 + 3 + r]; }
-    if (f < B_L1) { const int t = f - B_L2; return W[W2_OFF + k4 * 64 + 16 * t + r]; }
-    const int t = (f - B_L1) >> 2, ks = (f - B_L1) & 3;
-    return W[W1_OFF + (16 * ks + k4) * 32 + 16 * t + r];
+__host__ __device__ constexpr int phi(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
+// rgb_net input index of K element (g,j) of the layer-3 B operand [h tile | d,pad tile]:
+// j < 4: h feature 4g+j = input 3+4g+j; j >= 4: q = 4g+j-4, input q (d, q < 3) or 16+q (padding)
+__host__ __device__ constexpr int psi(int g, int j) {
+    return j < 4 ? 3 + 4 * g + j : ((4 * g + j - 4) < 3 ? (4 * g + j - 4) : 16 + (4 * g + j - 4));
 }
 
-__global__ void pack_weights_kernel(const float* __restrict__ W, _Float16* __restrict__ out) {
+__device__ float frag32_value(const float* __restrict__ W, int f, int lane, int j) {
+    const int g = lane >> 4, r = lane & 15, k = phi(g, j);
+    if (f < F_L2) return W[W1_OFF + (16 * (f - F_L1) + r) * 32 + k];
+    if (f < F_L3) return W[W2_OFF + r * 64 + 32 * (f - F_L2) + k];
+    if (f < F_L4) return W[W3_OFF + (16 * (f - F_L3) + r) * 32 + psi(g, j)];
+    if (f < F_L5) { const int t = (f - F_L4) >> 1, s = (f - F_L4) & 1; return W[W4_OFF + (16 * t + r) * 64 + 32 * s + k]; }
+    if (f < B_L4) return W[W5_OFF + r * 64 + 32 * (f - F_L5) + k];
+    if (f < B_L3) { const int t = (f - B_L4) >> 1, s = (f - B_L4) & 1; return W[W4_OFF + (32 * s + k) * 64 + 16 * t + r]; }
+    if (f < B_L1) return W[W3_OFF + (32 * (f - B_L3) + k) * 32 + 3 + r];
+    const int t = (f - B_L1) >> 1, s = (f - B_L1) & 1;
+    return W[W1_OFF + (32 * s + k) * 32 + 16 * t + r];
+}
+__device__ float frag16_value(const float* __restrict__ W, int f, int lane, int j) {
+    const int g = lane >> 4, r = lane & 15, k = 4 * g + j;
+    if (f < B_L2) return W[W5_OFF + k * 64 + 16 * (f - B_L5) + r];
+    return W[W2_OFF + k * 64 + 16 * (f - B_L2) + r];
+}
+
+template <typename T>
+__global__ void pack_weights_kernel(const float* __restrict__ W, T* __restrict__ out) {
     const int f = blockIdx.x, lane = threadIdx.x;
+    if (f < N_FRAG32) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) out[(f * 64 + lane) * 4 + j] = (_Float16)frag_value(W, f, lane, j);
+        for (int j = 0; j < 8; j++) out[(f * 64 + lane) * 8 + j] = (T)frag32_value(W, f, lane, j);
+    } else {
+        const int f16 = f - N_FRAG32;
+#pragma unroll
+        for (int j = 0; j < 4; j++) out[N_FRAG32 * 512 + (f16 * 64 + lane) * 4 + j] = (T)frag16_value(W, f16, lane, j);
+    }
 }
 
 // ---- hash grid ----
@@ -182,61 +233,56 @@ __device__ __forceinline__ void run_sum(float& v, const int (&link)[4]) {
     if (link[K]) v += t;
 }
 
-__device__ __forceinline__ half4_t frag(const half4_t* __restrict__ lds_frags, int f, int lane) {
-    return lds_frags[f * 64 + lane];
-}
-
-// Shared per-group forward (16 samples).  Produces every intermediate the backward needs.
-struct FwdState {
-    half4_t x2[4];     // relu(H1) tiles (B operands of L2)
-    float4_t h;        // sigma_net output tile (rows 4g..4g+3)
-    half4_t x3h, x3d;  // L3 B operands (h tile, d tile)
-    half4_t x4[4];     // relu(G1)
-    half4_t x5[4];     // relu(G2)
-    float4_t out;      // rgb pre-activation tile (rows 0..2 valid on g==0)
+// LDS fragment tables: K=32 fragments as v8 per lane, then the K=16 ones as v4 per lane
+template <typename T>
+struct Frags {
+    typedef typename Mfma<T>::v4 v4;
+    typedef typename Mfma<T>::v8 v8;
+    const v8* f32;
+    const v4* f16;
+    __device__ __forceinline__ v8 a32(int f, int lane) const { return f32[f * 64 + lane]; }
+    __device__ __forceinline__ v4 a16(int f, int lane) const { return f16[f * 64 + lane]; }
 };
 
-__device__ __forceinline__ void mlp_sigma(const half4_t* F, int lane, half4_t e0, half4_t e1, FwdState& st) {
+// Shared per-group forward (16 samples).  Produces every intermediate the backward needs.
+template <typename T>
+struct FwdState {
+    typedef typename Mfma<T>::v4 v4;
+    v4 x2[4];       // relu(H1) tiles (B operands of L2)
+    float4_t h;     // sigma_net output tile (rows 4g..4g+3)
+    v4 x3h, x3d;    // L3 B operand halves: h tile, [d, 1-padding] tile
+    v4 x4[4];       // relu(G1)
+    v4 x5[4];       // relu(G2)
+    float4_t out;   // rgb pre-activation tile (rows 0..2 valid on g==0)
+};
+
+template <typename T>
+__device__ __forceinline__ void mlp_sigma(const Frags<T>& F, int lane, typename Mfma<T>::v8 e, FwdState<T>& st) {
+    typedef Mfma<T> M;
+    typedef typename M::v8 v8;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        float4_t acc = zero4();
-        acc = mfma16(frag(F, F_L1 + 2 * t, lane), e0, acc);
-        acc = mfma16(frag(F, F_L1 + 2 * t + 1, lane), e1, acc);
-        st.x2[t] = relu_h4(acc);
-    }
-    float4_t h = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) h = mfma16(frag(F, F_L2 + ks, lane), st.x2[ks], h);
-    st.h = h;
+    for (int t = 0; t < 4; t++) st.x2[t] = relu4<T>(M::k32(F.a32(F_L1 + t, lane), e, zero4()));
+    float4_t h = M::k32(F.a32(F_L2, lane), cat8<v8>(st.x2[0], st.x2[1]), zero4());
+    st.h = M::k32(F.a32(F_L2 + 1, lane), cat8<v8>(st.x2[2], st.x2[3]), h);
 }
 
-__device__ __forceinline__ void mlp_rgb(const half4_t* F, int lane, float dnx, float dny, float dnz, FwdState& st) {
+template <typename T>
+__device__ __forceinline__ void mlp_rgb(const Frags<T>& F, int lane, float dnx, float dny, float dnz, FwdState<T>& st) {
+    typedef Mfma<T> M;
+    typedef typename M::v8 v8;
     const int g = lane >> 4;
-    st.x3h = to_h4(st.h);
-    half4_t xd;
-    xd[0] = (_Float16)(g == 0 ? dnx : 0.f);
-    xd[1] = (_Float16)(g == 0 ? dny : 0.f);
-    xd[2] = (_Float16)(g == 0 ? dnz : 0.f);
-    xd[3] = (_Float16)0.f;
-    st.x3d = xd;
+    st.x3h = cvt4<T>(st.h);
+    // [d, 1-padding]: element i of lane group g is padded-input q = 4g+i: d[q] for q < 3, else 1.0
+    st.x3d = cvt4<T>(float4_t{g == 0 ? dnx : 1.f, g == 0 ? dny : 1.f, g == 0 ? dnz : 1.f, 1.f});
+    const v8 b3 = cat8<v8>(st.x3h, st.x3d);
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        float4_t acc = zero4();
-        acc = mfma16(frag(F, F_L3 + 2 * t, lane), st.x3h, acc);
-        acc = mfma16(frag(F, F_L3 + 2 * t + 1, lane), st.x3d, acc);
-        st.x4[t] = relu_h4(acc);
-    }
+    for (int t = 0; t < 4; t++) st.x4[t] = relu4<T>(M::k32(F.a32(F_L3 + t, lane), b3, zero4()));
+    const v8 b4a = cat8<v8>(st.x4[0], st.x4[1]), b4b = cat8<v8>(st.x4[2], st.x4[3]);
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        float4_t acc = zero4();
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++) acc = mfma16(frag(F, F_L4 + 4 * t + ks, lane), st.x4[ks], acc);
-        st.x5[t] = relu_h4(acc);
-    }
-    float4_t o = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) o = mfma16(frag(F, F_L5 + ks, lane), st.x5[ks], o);
-    st.out = o;
+    for (int t = 0; t < 4; t++)
+        st.x5[t] = relu4<T>(M::k32(F.a32(F_L4 + 2 * t + 1, lane), b4b, M::k32(F.a32(F_L4 + 2 * t, lane), b4a, zero4())));
+    const float4_t o = M::k32(F.a32(F_L5, lane), cat8<v8>(st.x5[0], st.x5[1]), zero4());
+    st.out = M::k32(F.a32(F_L5 + 1, lane), cat8<v8>(st.x5[2], st.x5[3]), o);
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
@@ -253,17 +299,19 @@ __device__ __forceinline__ void load_levels(LevelTable& Ls, const LevelTable& La
 
 // ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
+template <typename T>
 __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                         int64_t n, const int32_t* __restrict__ n_dev,
                                                         const float2* __restrict__ table, LevelTable Lt,
                                                         float xyz_min, float xyz_extent,
-                                                        const half4_t* __restrict__ wpacked, int mode,
+                                                        const typename Mfma<T>::v8* __restrict__ wpacked, int mode,
                                                         float* __restrict__ sigmas, float* __restrict__ rgbs,
-                                                        half4_t* __restrict__ enc_cache) {
-    __shared__ half4_t F[N_FWD_FRAGS * 64];
+                                                        typename Mfma<T>::v8* __restrict__ enc_cache) {
+    typedef typename Mfma<T>::v8 v8;
+    __shared__ v8 Fs[N_FWD32 * 64];
     __shared__ LevelTable L;
     if (n_dev) n = min<int64_t>(n, *n_dev);  // device-resident count (static-capacity buffers)
-    for (int i = threadIdx.x; i < N_FWD_FRAGS * 64; i += 256) F[i] = wpacked[i];
+    for (int i = threadIdx.x; i < N_FWD32 * 64; i += 256) Fs[i] = wpacked[i];
     load_levels(L, Lt);
     __syncthreads();
     const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
@@ -271,7 +319,9 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
     const int64_t wave0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t n_waves = (int64_t)gridDim.x * 4;
     for (int64_t grp = wave0; grp < n_groups; grp += n_waves) {
-        const half4_t* Fl = F + opaque_zero();  // fragments re-read from LDS every group (not hoisted)
+        Frags<T> F;
+        F.f32 = Fs + opaque_zero();  // fragments re-read from LDS every group (not hoisted)
+        F.f16 = nullptr;
         const int64_t s = grp * 16 + r;
         const bool valid = s < n;
         float x = 0.f, y = 0.f, z = 0.f;
@@ -284,15 +334,10 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
         const float2 e01 = encode_level(table, L, 2 * g + 1, x, y, z);
         const float2 e10 = encode_level(table, L, 8 + 2 * g, x, y, z);
         const float2 e11 = encode_level(table, L, 9 + 2 * g, x, y, z);
-        half4_t b0, b1;
-        b0[0] = (_Float16)e00.x; b0[1] = (_Float16)e00.y; b0[2] = (_Float16)e01.x; b0[3] = (_Float16)e01.y;
-        b1[0] = (_Float16)e10.x; b1[1] = (_Float16)e10.y; b1[2] = (_Float16)e11.x; b1[3] = (_Float16)e11.y;
-        if (enc_cache) {
-            enc_cache[(grp * 2 + 0) * 64 + lane] = b0;
-            enc_cache[(grp * 2 + 1) * 64 + lane] = b1;
-        }
-        FwdState st;
-        mlp_sigma(Fl, lane, b0, b1, st);
+        const v8 e = v8{(T)e00.x, (T)e00.y, (T)e01.x, (T)e01.y, (T)e10.x, (T)e10.y, (T)e11.x, (T)e11.y};
+        if (enc_cache) enc_cache[grp * 64 + lane] = e;
+        FwdState<T> st;
+        mlp_sigma<T>(F, lane, e, st);
         if (g == 0 && valid) sigmas[s] = __expf(st.h[0]);  // TruncExp forward = exp
         if (mode == 1) continue;
         float dx = 0.f, dy = 0.f, dz = 0.f;
@@ -301,7 +346,7 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
             const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
             dx /= nrm; dy /= nrm; dz /= nrm;
         }
-        mlp_rgb(Fl, lane, dx, dy, dz, st);
+        mlp_rgb<T>(F, lane, dx, dy, dz, st);
         if (g == 0 && valid) {
             rgbs[3 * s] = sigmoidf_(st.out[0]);
             rgbs[3 * s + 1] = sigmoidf_(st.out[1]);
@@ -315,15 +360,15 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
 // samples per step.  Phase 1, every wave on its own group (inputs prefetched one step ahead):
 // recompute the MLP forward from the cached encoding, back-propagate through the five layers
 // (transposed products with the W^T fragments from LDS), write the encoding gradient level-major
-// for the scatter pass, and put the 30 operand fragments of the weight gradient (dY and X tiles
-// of every layer, transposed so that the samples are on K) into an LDS exchange area.  Phase 2,
-// after a barrier: wave w owns 5 of the 40 dW tiles and accumulates them over the step's 8
-// groups straight from the exchange area.  So no wave holds all of dW (the old one-wave-per-SIMD
-// layout kept 160 accumulator registers per wave), the two waves of a SIMD overlap their MFMA
-// chains, and every tile is written once per workgroup into its slab row at the end.
+// for the scatter pass, and put the 30 operand tiles of the weight gradient (dY and X tiles of
+// every layer, transposed so that the samples are on K) into an LDS exchange area.  Phase 2,
+// after a barrier: wave w owns 5 of the 40 dW tiles and accumulates them over the step's groups
+// straight from the exchange area, two groups (32 samples) per K=32 MFMA.  So no wave holds all
+// of dW, the two waves of a SIMD overlap their MFMA chains, and every tile is written once per
+// workgroup into its slab row at the end.
 constexpr int BWD_WAVES = 8;
 constexpr int BWD_THREADS = 64 * BWD_WAVES;
-// exchange fragments per group: dW operands, A = dY^T, B = X^T (16x16 fp16 MFMA fragments)
+// exchange tiles per group: dW operands, A = dY^T, B = X^T (16 features x 16 samples)
 constexpr int XA5 = 0, XB5 = 1, XA4 = 5, XB4 = 9, XA3 = 13, XB3D = 17, XB3H = 18, XA2 = 19, XB2 = 20, XA1 = 24,
               XB1 = 28, N_XFRAG = 30;
 
@@ -331,32 +376,35 @@ constexpr int XA5 = 0, XB5 = 1, XA4 = 5, XB4 = 9, XA3 = 13, XB3D = 17, XB3H = 18
 // stored as a [sample][feature] image (16 rows of 32 B; lane (g,r) writes 8 B at row r, chunk g,
 // chunks XOR-swizzled by row>>2 against write bank conflicts) and read back with the gfx950
 // transposed read ds_read_b64_tr_b16: lane 4q+p of group g addresses row 4g+q, chunk p, and lane
-// (g,i) receives column i of rows 4g..4g+3, i.e. [feature i][samples 4g..4g+3] — the A/B fragment
-// of a product that sums over the samples.  (EXEC must be all ones at the read.)
-typedef short short4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void x_put(_Float16* tile, int lane, half4_t v) {
+// (g,i) receives column i of rows 4g..4g+3, i.e. [feature i][samples 4g..4g+3] — half of the A/B
+// fragment of a product that sums over samples (the two halves of a K=32 fragment are the images
+// of two groups).  (EXEC must be all ones at the read.)
+template <typename V>
+__device__ __forceinline__ void x_put(uint16_t* tile, int lane, V v) {
     const int g = lane >> 4, r = lane & 15;
-    *(half4_t*)(tile + r * 16 + 4 * (g ^ (r >> 2))) = v;
+    *(V*)(tile + r * 16 + 4 * (g ^ (r >> 2))) = v;
 }
-__device__ __forceinline__ half4_t x_get(const _Float16* tile, int lane) {
+template <typename V>
+__device__ __forceinline__ V x_get(const uint16_t* tile, int lane) {
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
     const short4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (__attribute__((address_space(3))) short4_t*)(tile + (4 * g + q) * 16 + 4 * (p ^ g)));
-    return __builtin_bit_cast(half4_t, v);
+    return __builtin_bit_cast(V, v);
 }
 
 // Per-group inputs of the backward (prefetched one step ahead).
+template <typename T>
 struct BwdIn {
-    half4_t e0, e1;
+    typename Mfma<T>::v8 e;
     float dx, dy, dz, dsig, dr0, dr1, dr2;
 };
-__device__ __forceinline__ void bwd_load(BwdIn& in, int64_t grp, int64_t n, int lane, const half4_t* __restrict__ enc,
-                                         const float* __restrict__ dirs, const float* __restrict__ dL_dsig,
-                                         const float* __restrict__ dL_drgb) {
+template <typename T>
+__device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, int lane,
+                                         const typename Mfma<T>::v8* __restrict__ enc, const float* __restrict__ dirs,
+                                         const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb) {
     const int64_t s = grp * 16 + (lane & 15);
     const bool valid = s < n;
-    in.e0 = enc[(grp * 2 + 0) * 64 + lane];
-    in.e1 = enc[(grp * 2 + 1) * 64 + lane];
+    in.e = enc[grp * 64 + lane];
     in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
     if (valid) {
         in.dx = dirs[3 * s]; in.dy = dirs[3 * s + 1]; in.dz = dirs[3 * s + 2];
@@ -369,9 +417,13 @@ __device__ __forceinline__ void bwd_load(BwdIn& in, int64_t grp, int64_t n, int 
 __device__ __forceinline__ float lmax_upd(float m, float a, float b) {  // non-finite -> INF
     return (isfinite(a) && isfinite(b)) ? fmaxf(m, fmaxf(fabsf(a), fabsf(b))) : INFINITY;
 }
-__device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const BwdIn& cur,
-                                          int64_t grp, int64_t n, int64_t n_stride, int lane,
-                                          float* __restrict__ dE_out, float (&lm)[4]) {
+template <typename T>
+__device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const BwdIn<T>& cur, int64_t grp,
+                                          int64_t n, int64_t n_stride, int lane, float* __restrict__ dE_out,
+                                          float (&lm)[4]) {
+    typedef Mfma<T> M;
+    typedef typename M::v4 v4;
+    typedef typename M::v8 v8;
     const int g = lane >> 4, r = lane & 15;
     const int64_t s = grp * 16 + r;
     const bool valid = s < n;
@@ -380,10 +432,10 @@ __device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const
         const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
         dx /= nrm; dy /= nrm; dz /= nrm;
     }
-    FwdState st;
-    mlp_sigma(Fl, lane, cur.e0, cur.e1, st);
-    mlp_rgb(Fl, lane, dx, dy, dz, st);
-    // dY5: d(pre-sigmoid) = drgb * s(1-s), rows 0..2 on g==0
+    FwdState<T> st;
+    mlp_sigma<T>(F, lane, cur.e, st);
+    mlp_rgb<T>(F, lane, dx, dy, dz, st);
+    // dY5: d(pre-sigmoid) = drgb * s(1-s), rows 0..2 on g==0 (the padded output rows get zero)
     float4_t dy5 = zero4();
     if (g == 0) {
         const float s0 = sigmoidf_(st.out[0]), s1 = sigmoidf_(st.out[1]), s2 = sigmoidf_(st.out[2]);
@@ -391,58 +443,53 @@ __device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const
         dy5[1] = cur.dr1 * s1 * (1.f - s1);
         dy5[2] = cur.dr2 * s2 * (1.f - s2);
     }
-    const half4_t dy5h = to_h4(dy5);
+    const v4 dy5h = cvt4<T>(dy5);
     x_put(Xw + XA5 * 256, lane, dy5h);
 #pragma unroll
     for (int b = 0; b < 4; b++) x_put(Xw + (XB5 + b) * 256, lane, st.x5[b]);
     // L5 backward -> dG2, ReLU(x5) mask -> dD4
-    half4_t dD4h[4];
+    v4 dD4[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) dD4h[t] = relu_mask_h4(mfma16(frag(Fl, B_L5 + t, lane), dy5h, zero4()), st.x5[t]);
+    for (int t = 0; t < 4; t++) dD4[t] = relu_mask4<T>(M::k16(F.a16(B_L5 + t, lane), dy5h, zero4()), st.x5[t]);
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-        x_put(Xw + (XA4 + t) * 256, lane, dD4h[t]);
+        x_put(Xw + (XA4 + t) * 256, lane, dD4[t]);
         x_put(Xw + (XB4 + t) * 256, lane, st.x4[t]);
     }
     // L4 backward -> dG1, ReLU(x4) mask -> dD3
-    half4_t dD3h[4];
+    const v8 d4a = cat8<v8>(dD4[0], dD4[1]), d4b = cat8<v8>(dD4[2], dD4[3]);
+    v4 dD3[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        float4_t v = zero4();
+    for (int t = 0; t < 4; t++)
+        dD3[t] = relu_mask4<T>(M::k32(F.a32(B_L4 + 2 * t + 1, lane), d4b, M::k32(F.a32(B_L4 + 2 * t, lane), d4a, zero4())),
+                                st.x4[t]);
 #pragma unroll
-        for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L4 + 4 * t + ks, lane), dD4h[ks], v);
-        dD3h[t] = relu_mask_h4(v, st.x4[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < 4; t++) x_put(Xw + (XA3 + t) * 256, lane, dD3h[t]);
+    for (int t = 0; t < 4; t++) x_put(Xw + (XA3 + t) * 256, lane, dD3[t]);
     x_put(Xw + XB3D * 256, lane, st.x3d);
     x_put(Xw + XB3H * 256, lane, st.x3h);
     // L3 backward -> dh (rgb path) ; + TruncExp backward on h[0]
-    float4_t dh = zero4();
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) dh = mfma16(frag(Fl, B_L3 + ks, lane), dD3h[ks], dh);
+    float4_t dh = M::k32(F.a32(B_L3, lane), cat8<v8>(dD3[0], dD3[1]), zero4());
+    dh = M::k32(F.a32(B_L3 + 1, lane), cat8<v8>(dD3[2], dD3[3]), dh);
     if (g == 0) dh[0] += cur.dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
-    const half4_t dhh = to_h4(dh);
+    const v4 dhh = cvt4<T>(dh);
     x_put(Xw + XA2 * 256, lane, dhh);
 #pragma unroll
     for (int b = 0; b < 4; b++) x_put(Xw + (XB2 + b) * 256, lane, st.x2[b]);
     // L2 backward -> dH1, ReLU(x2) mask -> dD1
-    half4_t dD1h[4];
+    v4 dD1[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) dD1h[t] = relu_mask_h4(mfma16(frag(Fl, B_L2 + t, lane), dhh, zero4()), st.x2[t]);
+    for (int t = 0; t < 4; t++) dD1[t] = relu_mask4<T>(M::k16(F.a16(B_L2 + t, lane), dhh, zero4()), st.x2[t]);
 #pragma unroll
-    for (int t = 0; t < 4; t++) x_put(Xw + (XA1 + t) * 256, lane, dD1h[t]);
-    x_put(Xw + XB1 * 256, lane, cur.e0);
-    x_put(Xw + (XB1 + 1) * 256, lane, cur.e1);
+    for (int t = 0; t < 4; t++) x_put(Xw + (XA1 + t) * 256, lane, dD1[t]);
+    const v4 e0 = v4{cur.e[0], cur.e[1], cur.e[2], cur.e[3]}, e1 = v4{cur.e[4], cur.e[5], cur.e[6], cur.e[7]};
+    x_put(Xw + XB1 * 256, lane, e0);
+    x_put(Xw + (XB1 + 1) * 256, lane, e1);
     // L1 backward -> dE (tile t holds levels 8t+2g, 8t+2g+1)
+    const v8 d1a = cat8<v8>(dD1[0], dD1[1]), d1b = cat8<v8>(dD1[2], dD1[3]);
     float4_t dE[2];
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
-        float4_t v = zero4();
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++) v = mfma16(frag(Fl, B_L1 + 4 * t + ks, lane), dD1h[ks], v);
-        dE[t] = v;
-    }
+    for (int t = 0; t < 2; t++)
+        dE[t] = M::k32(F.a32(B_L1 + 2 * t + 1, lane), d1b, M::k32(F.a32(B_L1 + 2 * t, lane), d1a, zero4()));
     // per-level max |dE| of this lane's levels (2g, 2g+1, 8+2g, 9+2g): the scatter's fixed-point scale
     lm[0] = lmax_upd(lm[0], dE[0][0], dE[0][1]);
     lm[1] = lmax_upd(lm[1], dE[0][2], dE[0][3]);
@@ -457,41 +504,53 @@ __device__ __forceinline__ void bwd_group(const half4_t* Fl, _Float16* Xw, const
     }
 }
 
-// Phase 2: the dW tiles owned by wave `wid`, accumulated over the exchange fragments of `ng`
-// groups.  Ownership (5 tiles each): waves 0-3: W4 row-block a = wid (4 tiles) + W5 column block
-// wid; waves 4-5: W3 row-blocks 2(wid-4), +1 (d and h tiles) + W2 block wid-4; waves 6-7: W1
-// row-blocks 2(wid-6), +1 (two K tiles) + W2 block wid-4.
-__device__ __forceinline__ void bwd_dw(const _Float16* X, int ng, int wid, int lane, float4_t (&acc)[5]) {
-    for (int q = 0; q < ng; q++) {
-        const _Float16* Xq = X + q * N_XFRAG * 256;
+// Phase 2: the dW tiles owned by wave `wid`, accumulated over the exchange tiles of `ng` groups,
+// two groups per K=32 MFMA (an odd last group is paired with zeros).  Ownership (5 tiles each):
+// waves 0-3: W4 row-block a = wid (4 tiles) + W5 column block wid; waves 4-5: W3 row-blocks
+// 2(wid-4), +1 (d/pad and h tiles) + W2 block wid-4; waves 6-7: W1 row-blocks 2(wid-6), +1 (two K
+// tiles) + W2 block wid-4.
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::v8 x_pair(const uint16_t* X, int q, int ng, int tile, int lane) {
+    typedef typename Mfma<T>::v4 v4;
+    const v4 a = x_get<v4>(X + (q * N_XFRAG + tile) * 256, lane);
+    const v4 b = q + 1 < ng ? x_get<v4>(X + ((q + 1) * N_XFRAG + tile) * 256, lane) : v4{0, 0, 0, 0};
+    return cat8<typename Mfma<T>::v8>(a, b);
+}
+template <typename T>
+__device__ __forceinline__ void bwd_dw(const uint16_t* X, int ng, int wid, int lane, float4_t (&acc)[5]) {
+    typedef Mfma<T> M;
+    typedef typename M::v8 v8;
+    for (int q = 0; q < ng; q += 2) {
         if (wid < 4) {
-            const half4_t A4 = x_get(Xq + (XA4 + wid) * 256, lane);
+            const v8 A4 = x_pair<T>(X, q, ng, XA4 + wid, lane);
 #pragma unroll
-            for (int b = 0; b < 4; b++) acc[b] = mfma16(A4, x_get(Xq + (XB4 + b) * 256, lane), acc[b]);
-            acc[4] = mfma16(x_get(Xq + XA5 * 256, lane), x_get(Xq + (XB5 + wid) * 256, lane), acc[4]);
+            for (int b = 0; b < 4; b++) acc[b] = M::k32(A4, x_pair<T>(X, q, ng, XB4 + b, lane), acc[b]);
+            acc[4] = M::k32(x_pair<T>(X, q, ng, XA5, lane), x_pair<T>(X, q, ng, XB5 + wid, lane), acc[4]);
         } else if (wid < 6) {
-            const half4_t Bd = x_get(Xq + XB3D * 256, lane), Bh = x_get(Xq + XB3H * 256, lane);
+            const v8 Bd = x_pair<T>(X, q, ng, XB3D, lane), Bh = x_pair<T>(X, q, ng, XB3H, lane);
 #pragma unroll
             for (int aa = 0; aa < 2; aa++) {
-                const half4_t A3 = x_get(Xq + (XA3 + 2 * (wid - 4) + aa) * 256, lane);
-                acc[2 * aa] = mfma16(A3, Bd, acc[2 * aa]);
-                acc[2 * aa + 1] = mfma16(A3, Bh, acc[2 * aa + 1]);
+                const v8 A3 = x_pair<T>(X, q, ng, XA3 + 2 * (wid - 4) + aa, lane);
+                acc[2 * aa] = M::k32(A3, Bd, acc[2 * aa]);
+                acc[2 * aa + 1] = M::k32(A3, Bh, acc[2 * aa + 1]);
             }
-            acc[4] = mfma16(x_get(Xq + XA2 * 256, lane), x_get(Xq + (XB2 + wid - 4) * 256, lane), acc[4]);
+            acc[4] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid - 4, lane), acc[4]);
         } else {
-            const half4_t B0 = x_get(Xq + XB1 * 256, lane), B1 = x_get(Xq + (XB1 + 1) * 256, lane);
+            const v8 B0 = x_pair<T>(X, q, ng, XB1, lane), B1 = x_pair<T>(X, q, ng, XB1 + 1, lane);
 #pragma unroll
             for (int aa = 0; aa < 2; aa++) {
-                const half4_t A1 = x_get(Xq + (XA1 + 2 * (wid - 6) + aa) * 256, lane);
-                acc[2 * aa] = mfma16(A1, B0, acc[2 * aa]);
-                acc[2 * aa + 1] = mfma16(A1, B1, acc[2 * aa + 1]);
+                const v8 A1 = x_pair<T>(X, q, ng, XA1 + 2 * (wid - 6) + aa, lane);
+                acc[2 * aa] = M::k32(A1, B0, acc[2 * aa]);
+                acc[2 * aa + 1] = M::k32(A1, B1, acc[2 * aa + 1]);
             }
-            acc[4] = mfma16(x_get(Xq + XA2 * 256, lane), x_get(Xq + (XB2 + wid - 4) * 256, lane), acc[4]);
+            acc[4] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid - 4, lane), acc[4]);
         }
     }
 }
 
 // The owned tiles (C layout: lane (g,r) = rows 4g+i, column r) into the workgroup's slab row.
+// W3 columns: the h tile's column r is input 3+r; the [d, pad] tile's column q is input q (d) or
+// 16+q (the 13 constant-1 padding inputs, whose gradient is the plain sum of dY).
 __device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, int lane, const float4_t (&acc)[5]) {
     const int g = lane >> 4, r = lane & 15;
 #pragma unroll
@@ -500,13 +559,13 @@ __device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, i
         if (wid < 4) {
 #pragma unroll
             for (int b = 0; b < 4; b++) out[W4_OFF + (16 * wid + row) * 64 + 16 * b + r] = acc[b][i];
-            if (row < 3) out[W5_OFF + row * 64 + 16 * wid + r] = acc[4][i];
+            out[W5_OFF + row * 64 + 16 * wid + r] = acc[4][i];
         } else if (wid < 6) {
 #pragma unroll
             for (int aa = 0; aa < 2; aa++) {
                 const int orow = 16 * (2 * (wid - 4) + aa) + row;
-                if (r < 3) out[W3_OFF + orow * 19 + r] = acc[2 * aa][i];
-                out[W3_OFF + orow * 19 + 3 + r] = acc[2 * aa + 1][i];
+                out[W3_OFF + orow * 32 + (r < 3 ? r : 16 + r)] = acc[2 * aa][i];
+                out[W3_OFF + orow * 32 + 3 + r] = acc[2 * aa + 1][i];
             }
             out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
         } else {
@@ -521,15 +580,25 @@ __device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, i
     }
 }
 
+template <typename T>
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
-    const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const half4_t* __restrict__ wpacked,
-    const half4_t* __restrict__ enc_cache, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
-    float* __restrict__ dE_out, float* __restrict__ slab, float* __restrict__ level_max) {
+    const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const uint16_t* __restrict__ wpacked,
+    const typename Mfma<T>::v8* __restrict__ enc_cache, const float* __restrict__ dL_dsig,
+    const float* __restrict__ dL_drgb, float* __restrict__ dE_out, float* __restrict__ slab,
+    float* __restrict__ level_max) {
+    typedef typename Mfma<T>::v4 v4;
+    typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     if (n_dev) n = min<int64_t>(n, *n_dev);
-    __shared__ half4_t F[N_FRAGS * 64];                    // 38.9 KB weight fragments
-    __shared__ __attribute__((aligned(16))) _Float16 X[BWD_WAVES * N_XFRAG * 256];  // 120 KB dW operand images
-    for (int i = threadIdx.x; i < N_FRAGS * 64; i += BWD_THREADS) F[i] = wpacked[i];
+    __shared__ v8 F32s[N_FRAG32 * 64];                                              // 34 KB
+    __shared__ v4 F16s[N_FRAG16 * 64];                                              // 4 KB
+    __shared__ __attribute__((aligned(16))) uint16_t X[BWD_WAVES * N_XFRAG * 256];  // 120 KB dW operand images
+    {
+        const v8* w32 = (const v8*)wpacked;
+        const v4* w16 = (const v4*)(wpacked + N_FRAG32 * 512);
+        for (int i = threadIdx.x; i < N_FRAG32 * 64; i += BWD_THREADS) F32s[i] = w32[i];
+        for (int i = threadIdx.x; i < N_FRAG16 * 64; i += BWD_THREADS) F16s[i] = w16[i];
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     float4_t acc[5];
@@ -539,23 +608,22 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t n_groups = (n + 15) / 16;
     const int64_t stride = (int64_t)gridDim.x * BWD_WAVES;
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
-    BwdIn nxt;
-    if (base + wid < n_groups) bwd_load(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+    BwdIn<T> nxt;
+    if (base + wid < n_groups) bwd_load<T>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
     for (; base < n_groups; base += stride) {
         const int64_t grp = base + wid;
         const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
-        const BwdIn cur = nxt;
-        if (grp + stride < n_groups) bwd_load(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
-#ifndef NCN_DIAG_BWD_NO_P1
-        if (grp < n_groups)
-            bwd_group(F + opaque_zero(), X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm);
-#else
-        if (cur.dsig == 1234.5f) dE_out[grp] = 0.f;
-#endif
+        const BwdIn<T> cur = nxt;
+        if (grp + stride < n_groups) bwd_load<T>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+        if (grp < n_groups) {
+            Frags<T> F;
+            const int z = opaque_zero();
+            F.f32 = F32s + z;
+            F.f16 = F16s + z;
+            bwd_group<T>(F, X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm);
+        }
         lds_barrier();  // (the dE stores and the next step's loads stay in flight)
-#ifndef NCN_DIAG_BWD_NO_DW
-        bwd_dw(X, ng, wid, lane, acc);
-#endif
+        bwd_dw<T>(X, ng, wid, lane, acc);
         lds_barrier();
     }
     bwd_store_dw(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc);
@@ -1109,9 +1177,15 @@ using namespace ncn;
 
 extern "C" {
 
-int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void* stream) {
-    hipLaunchKernelGGL(pack_weights_kernel, dim3(N_FRAGS), dim3(64), 0, (hipStream_t)stream, w_master,
-                       (_Float16*)weights_packed);
+int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int precision, void* stream) {
+    NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,
+                "ncn_field_pack_weights: precision must be NCN_PREC_F16 or NCN_PREC_BF16");
+    if (precision == NCN_PREC_F16)
+        hipLaunchKernelGGL(pack_weights_kernel<_Float16>, dim3(N_FRAG32 + N_FRAG16), dim3(64), 0, (hipStream_t)stream,
+                           w_master, (_Float16*)weights_packed);
+    else
+        hipLaunchKernelGGL(pack_weights_kernel<__bf16>, dim3(N_FRAG32 + N_FRAG16), dim3(64), 0, (hipStream_t)stream,
+                           w_master, (__bf16*)weights_packed);
     NCN_LAUNCH_CHECK("ncn_field_pack_weights");
     return 0;
 }
@@ -1119,16 +1193,24 @@ int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, void
 // `levels` is a HOST array of 16 x {scale f32 bits, resolution, params, offset}.
 int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const float* table,
                   const uint32_t* levels,
-                  float xyz_min, float xyz_extent, const uint16_t* weights_packed, int mode, float* sigmas,
-                  float* rgbs, uint16_t* enc_cache, void* stream) {
+                  float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision, int mode,
+                  float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(mode == 0 || mode == 1, hipErrorInvalidValue, "ncn_field_fwd: mode must be 0 or 1");
-    NCN_REQUIRE(((uintptr_t)table & 7) == 0 && ((uintptr_t)enc_cache & 7) == 0, hipErrorInvalidValue,
-                "ncn_field_fwd: table / enc_cache must be 8-byte aligned");
+    NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,
+                "ncn_field_fwd: precision must be NCN_PREC_F16 or NCN_PREC_BF16");
+    NCN_REQUIRE(((uintptr_t)table & 7) == 0 && ((uintptr_t)enc_cache & 15) == 0 && ((uintptr_t)weights_packed & 15) == 0,
+                hipErrorInvalidValue, "ncn_field_fwd: table 8-byte, enc_cache / weights_packed 16-byte aligned");
     const LevelTable Lt = make_table(levels);
-    hipLaunchKernelGGL(field_fwd_kernel, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs, n, n_dev,
-                       (const float2*)table, Lt, xyz_min, xyz_extent, (const half4_t*)weights_packed, mode, sigmas,
-                       rgbs, (half4_t*)enc_cache);
+    if (precision == NCN_PREC_F16)
+        hipLaunchKernelGGL(field_fwd_kernel<_Float16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
+                           n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,
+                           (const Mfma<_Float16>::v8*)weights_packed, mode, sigmas, rgbs,
+                           (Mfma<_Float16>::v8*)enc_cache);
+    else
+        hipLaunchKernelGGL(field_fwd_kernel<__bf16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
+                           n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,
+                           (const Mfma<__bf16>::v8*)weights_packed, mode, sigmas, rgbs, (Mfma<__bf16>::v8*)enc_cache);
     NCN_LAUNCH_CHECK("ncn_field_fwd");
     return 0;
 }
@@ -1142,14 +1224,22 @@ int ncn_field_bwd_blocks(int64_t n) {
 int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(int64_t)3) : 0; }
 
 int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const uint16_t* weights_packed,
-                      const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* slab,
-                      float* dE_ws, float* level_max, void* stream) {
+                      int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
+                      float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
-    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0, hipErrorInvalidValue, "ncn_field_bwd_mlp: dE_ws must be 16-byte aligned");
+    NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,
+                "ncn_field_bwd_mlp: precision must be NCN_PREC_F16 or NCN_PREC_BF16");
+    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)enc_cache & 15) == 0 && ((uintptr_t)weights_packed & 15) == 0,
+                hipErrorInvalidValue, "ncn_field_bwd_mlp: dE_ws / enc_cache / weights_packed must be 16-byte aligned");
     NCN_REQUIRE(level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp: level_max workspace required");
-    hipLaunchKernelGGL(field_bwd_kernel, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0, (hipStream_t)stream,
-                       dirs, n, n_dev, (const half4_t*)weights_packed, (const half4_t*)enc_cache, dL_dsigmas,
-                       dL_drgbs, dE_ws, slab, level_max);
+    if (precision == NCN_PREC_F16)
+        hipLaunchKernelGGL(field_bwd_kernel<_Float16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
+                           (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<_Float16>::v8*)enc_cache,
+                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max);
+    else
+        hipLaunchKernelGGL(field_bwd_kernel<__bf16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
+                           (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<__bf16>::v8*)enc_cache,
+                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max);
     NCN_LAUNCH_CHECK("ncn_field_bwd_mlp");
     return 0;
 }
@@ -1172,15 +1262,12 @@ int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const 
 }
 
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
-                  float xyz_min,
-                  float xyz_extent, const uint16_t* weights_packed, const uint16_t* enc_cache,
-                  const float* dL_dsigmas, const float* dL_drgbs, float* grad_table, float* slab, float* dE_ws,
-                  float* level_max, void* stream) {
+                  float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision,
+                  const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* grad_table,
+                  float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
-    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
-                "ncn_field_bwd: dE_ws and xyzs must be 16-byte aligned");
-    const int e = ncn_field_bwd_mlp(dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs, slab, dE_ws,
-                                    level_max, stream);
+    const int e = ncn_field_bwd_mlp(dirs, n, n_dev, weights_packed, precision, enc_cache, dL_dsigmas, dL_drgbs, slab,
+                                    dE_ws, level_max, stream);
     if (e) return e;
     return ncn_field_scatter(xyzs, n, n_dev, levels, xyz_min, xyz_extent, dE_ws, level_max, 0, 16, 0, grad_table,
                              stream);

@@ -6,6 +6,11 @@
 //    reference copies the normals to the host for faiss, losses.py:434).
 #pragma clang fp contract(off)
 
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <vector>
 #include "common.h"
 #include "../../include/ncnerf.h"
 
@@ -228,19 +233,10 @@ __global__ void nerf_loss_bwd_kernel(const float* __restrict__ rgb, const float*
 }
 
 // ---- clustering ----
-// Pipeline (one stream, no host round trip, every kernel but prep is KM_BLOCKS workgroups):
-//   prep   (1 WG)  : validity filter + ordered compaction (losses.py:427-430), seeded init
-//   iter   (niter+1 launches): C_i = update(partials_{i-1}, C_{i-1}) (i>0), assign every valid
-//                    point to argmax <x, C_i>, per-workgroup partial sums (x, y, z, count) per
-//                    cluster; the last launch (i = niter) is faiss's final search and keeps the
-//                    assignment
-//   select         : cluster selection (losses.py:75-166) -> label per point, flipped per-cluster
-//                    partial sums (losses.py:441-468)
-//   sums           : per-cluster partials of x.c, |x-c|_1, sign(x-c)
-//   grad           : the three cluster losses, their analytic gradient per point (losses.py:469-478),
-//                    labels (-9 invalid) and the zero gradient of every unselected/invalid point
-// Every workgroup reduces the same partials in the same fixed order, so all of them hold
-// bit-identical centroids/statistics and the result is run-to-run deterministic.
+// faiss.Kmeans(3, K, niter, spherical=True) + index.search (losses.py:86-89) restated on the device
+// (the algorithm of oracle/losses_ref.py:spherical_kmeans; its random draws — subsample
+// permutation, init picks, split walk — come precomputed from a host-built plan).  The kernel
+// layout is described at cluster_kernel.
 constexpr int CL_MAX_TRI = 16384;
 constexpr int NCN_MAX_NQ = 80;       // K * 4 at K = 20
 #ifndef KM_THREADS_CFG
@@ -253,11 +249,6 @@ constexpr int KM_THREADS = KM_THREADS_CFG;  // threads per workgroup of the clus
 constexpr int KM_BLOCKS = KM_BLOCKS_CFG;    // co-resident workgroups (grid barriers)
 constexpr int KM_CHUNK_MAX = CL_MAX_TRI / KM_BLOCKS;
 
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x = (x ^ (x >> 16)) * 0x7FEB352Du;
-    x = (x ^ (x >> 15)) * 0x846CA68Bu;
-    return x ^ (x >> 16);
-}
 
 __device__ __forceinline__ bool valid_normal(float a, float b, float c) {
     const bool zero = (fabsf(a) + fabsf(b) + fabsf(c)) == 0.0f;
@@ -439,9 +430,43 @@ struct KmUpdLds {
     int any_empty;
 };
 
+// faiss's k-means plan (host-built by ncn_kmeans_plan_fill; the faiss restatement of
+// oracle/losses_ref.py): header words, init picks per point count, training-set membership masks
+// per point count above the subsampling cap, split_clusters' RandomGenerator(1234) floats.
+struct KmPlan {
+    const uint32_t* p;
+    __device__ __forceinline__ int n_tri() const { return (int)p[1]; }
+    __device__ __forceinline__ int K() const { return (int)p[2]; }
+    __device__ __forceinline__ int cap() const { return (int)p[3]; }
+    __device__ __forceinline__ int n_rand() const { return (int)p[4]; }
+    __device__ __forceinline__ int init(int nx, int k) const {
+        return (int)((const uint16_t*)(p + p[5]))[(int64_t)nx * p[2] + k];
+    }
+    __device__ __forceinline__ bool member(int nx, int rank) const {
+        if (nx <= (int)p[3]) return true;
+        const int mw = ((int)p[1] + 31) >> 5;
+        return (p[p[6] + (int64_t)(nx - (int)p[3] - 1) * mw + (rank >> 5)] >> (rank & 31)) & 1u;
+    }
+    __device__ __forceinline__ float rnd(int i) const { return __uint_as_float(p[p[7] + i]); }
+};
+
+// faiss fvec_renorm_L2 of one 3-vector: x *= (float)(1.0 / sqrtf(|x|^2)) when |x|^2 > 0
+__device__ __forceinline__ void faiss_renorm3(float* x) {
+    const float nr = x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
+    if (nr > 0.f) {
+        const float inv = (float)(1.0 / (double)sqrtf(nr));
+        x[0] *= inv; x[1] *= inv; x[2] *= inv;
+    }
+}
+
+// One faiss iteration's update (Clustering.cpp compute_centroids + split_clusters +
+// post_process_centroids): centroid = sum * (1 / count); each empty cluster ci, in order, takes
+// the cluster cj found by walking cj = 0, 1, ... (mod K) until RandomGenerator(1234).rand_float()
+// < (count_cj - 1) / (n_train - K), a +-1/1024 perturbation splits the two, and the counts halve
+// (float); then every centroid is L2-renormalised.  The random floats come from the plan.
 template <int K>
 __device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmUpdLds<K>& L, unsigned tag,
-                          unsigned* sync) {
+                          unsigned* sync, const KmPlan& plan, int n_train) {
     if (threadIdx.x < K * 4) L.sums[threadIdx.x] = sum_rows_tagged(part, K * 4, threadIdx.x, tag, sync);
     if (threadIdx.x == 0) L.any_empty = 0;
     __syncthreads();
@@ -449,35 +474,44 @@ __device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmU
         const int k = threadIdx.x;
         const float n = L.sums[4 * k + 3];
         L.cnt[k] = n;
+        const float inv = n > 0.f ? 1.0f / n : 0.f;
 #pragma unroll
-        for (int q = 0; q < 3; q++) L.nc[k][q] = n > 0.f ? L.sums[4 * k + q] / n : C[k][q];
+        for (int q = 0; q < 3; q++) L.nc[k][q] = L.sums[4 * k + q] * inv;  // (0 for an empty cluster)
         if (n == 0.f) L.any_empty = 1;
     }
     __syncthreads();
     if (L.any_empty && threadIdx.x == 0) {
         const float EPS = 1.0f / 1024.0f;
-        for (int k = 0; k < K; k++) {
-            if (L.cnt[k] == 0.f) {
-                int j = 0;
-                for (int q = 1; q < K; q++)
-                    if (L.cnt[q] > L.cnt[j]) j = q;
-                for (int q = 0; q < 3; q++) {
-                    if (q % 2 == 0) { L.nc[k][q] = L.nc[j][q] * (1 + EPS); L.nc[j][q] = L.nc[j][q] * (1 - EPS); }
-                    else { L.nc[k][q] = L.nc[j][q] * (1 - EPS); L.nc[j][q] = L.nc[j][q] * (1 + EPS); }
+        const double denom = (double)(float)(n_train - K);
+        int ri = 0;
+        const int nr = plan.n_rand();
+        for (int ci = 0; ci < K; ci++) {
+            if (L.cnt[ci] != 0.f) continue;
+            int cj = 0;
+            for (;; cj = (cj + 1) % K) {
+                const float pr = (float)(((double)L.cnt[cj] - 1.0) / denom);
+                if (ri >= nr) {  // (a split walk longer than the plan's table: flag and take cj)
+                    __hip_atomic_store(&sync[2], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
                 }
-                const float half = floorf(L.cnt[j] * 0.5f);
-                L.cnt[k] = half;
-                L.cnt[j] -= half;
+                if (plan.rnd(ri++) < pr) break;
             }
+            for (int q = 0; q < 3; q++) {
+                L.nc[ci][q] = L.nc[cj][q];
+                if (q % 2 == 0) { L.nc[ci][q] *= 1 + EPS; L.nc[cj][q] *= 1 - EPS; }
+                else { L.nc[ci][q] *= 1 - EPS; L.nc[cj][q] *= 1 + EPS; }
+            }
+            L.cnt[ci] = L.cnt[cj] / 2;
+            L.cnt[cj] -= L.cnt[ci];
         }
     }
     __syncthreads();
     if (threadIdx.x < K) {
         const int k = threadIdx.x;
-        const float nr =
-            fmaxf(sqrtf(L.nc[k][0] * L.nc[k][0] + L.nc[k][1] * L.nc[k][1] + L.nc[k][2] * L.nc[k][2]), 1e-30f);
+        float c[3] = {L.nc[k][0], L.nc[k][1], L.nc[k][2]};
+        faiss_renorm3(c);
 #pragma unroll
-        for (int q = 0; q < 3; q++) C[k][q] = L.nc[k][q] / nr;
+        for (int q = 0; q < 3; q++) C[k][q] = c[q];
     }
     __syncthreads();
 }
@@ -590,8 +624,10 @@ struct ClusterLds {
     int label_map[K];
     int wcnt[CL_MAX_TRI / KM_THREADS][KM_THREADS / 64];
     int woff[CL_MAX_TRI / KM_THREADS][KM_THREADS / 64];
-    int pick[K];
+    int pick[K];       // init picks (ranks), sorted ascending
+    int pick_ord[K];   // the centroid index of sorted pick k
     int picki[K];
+    unsigned char pmem[KM_CHUNK_MAX];  // training-set membership of the chunk's points (faiss subsampling)
     int total;
     KmUpdLds<K> upd;
     SelLds<K> sel;
@@ -603,7 +639,8 @@ struct ClusterLds {
 // The whole clustering pipeline in ONE launch of KM_BLOCKS co-resident workgroups, the phases
 // separated by grid barriers instead of kernel boundaries (23 of them at niter = 20):
 //   compaction  (no barrier: every workgroup ranks all normals itself and keeps its chunk in LDS)
-//               validity filter + ordered compaction (losses.py:427-430) and the seeded init picks
+//               validity filter + ordered compaction (losses.py:427-430), faiss's training-set
+//               membership and init picks from the plan
 //   niter + 1 Lloyd rounds: C_i = update(partials_{i-1}, C_{i-1}) (i > 0), assign every point to
 //               argmax <x, C_i>, per-workgroup partial sums (x, y, z, count) per cluster; the last
 //               round (i = niter) is faiss's final search and keeps the assignment
@@ -622,7 +659,8 @@ __device__ unsigned long long ncn_cl_times[64];
 #endif
 template <int K>
 __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
-    const float* __restrict__ normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort, float w_dot,
+    const float* __restrict__ normals, int n_tri, int niter, const uint32_t* __restrict__ plan_words, float t_sim,
+    float w_ort, float w_dot,
     float w_l1, const float* __restrict__ w_dev, const int64_t* __restrict__ step_dev, float sched_start,
     float sched_grow, const float* __restrict__ photo, float* __restrict__ wsb, float* __restrict__ out_losses,
     int32_t* __restrict__ out_labels, float* __restrict__ out_centroids, float* __restrict__ dn) {
@@ -677,12 +715,24 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     const bool clustered = nv >= K;
     int m0, len;
     km_chunk(nv, m0, len);
-    if (tid < K && clustered) {  // init: one seeded pick per stratum (oracle/losses_ref.py:kmeans_init_indices)
-        const int lo = (int)(((int64_t)tid * nv) / K), hi = (int)(((int64_t)(tid + 1) * nv) / K);
-        const int span = max(hi - lo, 1);
-        const uint32_t h = mix32(seed * 0x9E3779B1u + (uint32_t)tid * 0x85EBCA77u + 1u);
-        L.pick[tid] = lo + (int)(h % (uint32_t)span);
+    KmPlan plan;
+    plan.p = plan_words;
+    const bool plan_ok = plan.n_tri() == n_tri && plan.K() == K;
+    if (!plan_ok && tid == 0) __hip_atomic_store(&ws.sync[2], 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // faiss: training set = rand_perm(seed) subsample of nv > K*256 points; nv == K is its copy corner
+    // case (centroids = the points, no iteration)
+    const int n_train = (plan_ok && nv > plan.cap()) ? plan.cap() : nv;
+    const int niter_eff = n_train == K ? 0 : niter;
+    if (tid == 0 && clustered) {  // init picks (plan: first K of rand_perm(seed + 1)), sorted with their index
+        for (int k = 0; k < K; k++) {
+            const int v = plan_ok ? plan.init(nv, k) : k;
+            int j = k;
+            for (; j > 0 && L.pick[j - 1] > v; j--) { L.pick[j] = L.pick[j - 1]; L.pick_ord[j] = L.pick_ord[j - 1]; }
+            L.pick[j] = v;
+            L.pick_ord[j] = k;
+        }
     }
+    for (int j = tid; j < len; j += KM_THREADS) L.pmem[j] = plan_ok ? plan.member(nv, m0 + j) : 1;
     __syncthreads();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int picks[K];
@@ -706,7 +756,7 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
             const int i = r * KM_THREADS + tid;
             if (rank >= m0 && rank < m0 + len) L.pidx[rank - m0] = i;
             for (int k = kbeg; k < kend; k++)  // usually none or one
-                if (picks[k] == rank) L.picki[k] = i;
+                if (picks[k] == rank) L.picki[L.pick_ord[k]] = i;
         } else if (r * KM_THREADS + tid < n_tri && r % KM_BLOCKS == (int)blockIdx.x) {  // invalid: label -9, zero grad
             const int i = r * KM_THREADS + tid;
             out_labels[i] = -9;
@@ -720,12 +770,17 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
 #pragma unroll
         for (int q = 0; q < 3; q++) L.pv[q][j] = normals[3 * i + q];
     }
-    if (clustered && tid < 3 * K) L.C[tid / 3][tid % 3] = normals[3 * L.picki[tid / 3] + tid % 3];
+    if (clustered && tid < K) {  // faiss: centroids = the picked points, post-processed (renormalised)
+        float c[3] = {normals[3 * L.picki[tid]], normals[3 * L.picki[tid] + 1], normals[3 * L.picki[tid] + 2]};
+        if (niter_eff > 0) faiss_renorm3(c);
+#pragma unroll
+        for (int q = 0; q < 3; q++) L.C[tid][q] = c[q];
+    }
     __syncthreads();
     CL_STAMP(1);
     unsigned phase = 0;
     const unsigned seq = __hip_atomic_load(&ws.sync[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!clustered || niter == 0) {  // the buffers the Lloyd rounds do not write get void words
+    if (!clustered || niter_eff == 0) {  // the buffers the Lloyd rounds do not write get void words
         const long long vw = km_tagged(km_round_tag(seq, KM_VOID_ROUND), 0);
         for (int q = tid; q < K * 4; q += KM_THREADS) {
             if (!clustered) st_c(ws.part + blockIdx.x * K * 4 + q, vw);
@@ -735,17 +790,20 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     if (clustered) {
         // ---- Lloyd rounds (tagged partials, no grid barrier) ----
         constexpr int NQ = K * 4;
-        for (int it = 0; it <= niter; it++) {
+        for (int it = 0; it <= niter_eff; it++) {
             if (it > 0)
-                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, km_round_tag(seq, it - 1), ws.sync);
+                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, km_round_tag(seq, it - 1), ws.sync,
+                             plan, n_train);
             CL_STAMP(2 + 2 * it);
-            // assignment + per-cluster (x, y, z, count) sums of the chunk (fixed point, LDS u64 atomics)
+            // assignment + per-cluster (x, y, z, count) sums of the chunk (fixed point, LDS u64 atomics):
+            // training rounds over the training set, the final search (it == niter_eff) over all points
             if (tid < NQ) L.acc[tid] = 0ull;
             __syncthreads();
             for (int j = tid; j < len; j += KM_THREADS) {
                 const float x = L.pv[0][j], y = L.pv[1][j], z = L.pv[2][j];
                 const int a = nearest<K>(L.C, x, y, z);
                 L.pk[j] = a;
+                if (it < niter_eff && !L.pmem[j]) continue;
                 atomicAdd(&L.acc[4 * a], km_fixl(x));
                 atomicAdd(&L.acc[4 * a + 1], km_fixl(y));
                 atomicAdd(&L.acc[4 * a + 2], km_fixl(z));
@@ -759,8 +817,8 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
         }
         // ---- select: final cluster sizes = count column of the final-search partials ----
         if (tid < K)
-            L.cnt[tid] = sum_rows_tagged(ws.part + (niter & 1) * KM_BLOCKS * NQ, NQ, 4 * tid + 3, km_round_tag(seq, niter),
-                                         ws.sync);
+            L.cnt[tid] = sum_rows_tagged(ws.part + (niter_eff & 1) * KM_BLOCKS * NQ, NQ, 4 * tid + 3,
+                                         km_round_tag(seq, niter_eff), ws.sync);
         __syncthreads();
         CL_STAMP(57);
         select_clusters<K>(L.C, L.cnt, t_sim, L.sel, L.label_map);
@@ -903,11 +961,11 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
 }
 
 template <int K>
-static void launch_cluster(const float* normals, int n_tri, int niter, uint32_t seed, float t_sim, float w_ort,
+static void launch_cluster(const float* normals, int n_tri, int niter, const uint32_t* plan, float t_sim, float w_ort,
                            float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev, float sched_start,
                            float sched_grow, const float* photo, float* out_losses, int32_t* out_labels,
                            float* out_centroids, float* dn, float* ws, hipStream_t s) {
-    hipLaunchKernelGGL(cluster_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, seed, t_sim,
+    hipLaunchKernelGGL(cluster_kernel<K>, dim3(KM_BLOCKS), dim3(KM_THREADS), 0, s, normals, n_tri, niter, plan, t_sim,
                        w_ort, w_dot, w_l1, w_dev, step_dev, sched_start, sched_grow, photo, ws, out_losses, out_labels,
                        out_centroids, dn);
 }
@@ -919,6 +977,63 @@ using namespace ncn;
 extern "C" {
 
 int64_t ncn_cluster_workspace_words(int K) { return km_ws_words(K); }
+
+// ---- faiss k-means plan (host) ----
+static constexpr int KMP_MAX_PTS = 256;  // faiss ClusteringParameters::max_points_per_centroid
+static constexpr int KMP_N_RAND = 4096;
+static int64_t kmp_init_words(int n_tri, int K) { return ((int64_t)(n_tri + 1) * K + 1) / 2; }
+static int64_t kmp_mask_rows(int n_tri, int K) { return std::max<int64_t>(0, n_tri - (int64_t)K * KMP_MAX_PTS); }
+
+int64_t ncn_kmeans_plan_words(int n_tri, int K) {
+    if (n_tri < 0 || K <= 0) return 0;
+    return 8 + kmp_init_words(n_tri, K) + kmp_mask_rows(n_tri, K) * ((n_tri + 31) / 32) + KMP_N_RAND;
+}
+
+// faiss rand_perm(perm, n, seed) (utils/random.cpp) for its first m steps: Fisher-Yates with
+// RandomGenerator::rand_int(max) = mt() % max over std::mt19937((unsigned)seed).
+static void kmp_rand_perm(std::vector<int>& perm, int n, uint32_t seed, int m) {
+    perm.resize(n);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::mt19937 mt(seed);
+    for (int i = 0; i < std::min(m, n - 1); i++) {
+        const int i2 = i + (int)(mt() % (uint32_t)(n - i));
+        std::swap(perm[i], perm[i2]);
+    }
+}
+
+int ncn_kmeans_plan_fill(int n_tri, int K, uint32_t seed, uint32_t* out) {
+    NCN_REQUIRE(out != nullptr && n_tri >= 0 && n_tri < 65536 && K > 0, hipErrorInvalidValue,
+                "ncn_kmeans_plan_fill: bad arguments");
+    const int cap = K * KMP_MAX_PTS, mw = (n_tri + 31) / 32;
+    const int64_t init_off = 8, mask_off = init_off + kmp_init_words(n_tri, K);
+    const int64_t rand_off = mask_off + kmp_mask_rows(n_tri, K) * mw;
+    std::fill(out, out + ncn_kmeans_plan_words(n_tri, K), 0u);
+    const uint32_t head[8] = {0x4B4D5031u, (uint32_t)n_tri, (uint32_t)K, (uint32_t)cap, (uint32_t)KMP_N_RAND,
+                              (uint32_t)init_off, (uint32_t)mask_off, (uint32_t)rand_off};
+    std::copy(head, head + 8, out);
+    uint16_t* init = (uint16_t*)(out + init_off);
+    std::vector<int> perm, perm1;
+    kmp_rand_perm(perm1, std::max(cap, 1), seed + 1, K);  // init picks of a subsampled training set
+    for (int nx = K; nx <= n_tri; nx++) {
+        if (nx == K) {  // faiss's nx == k corner case: the points themselves, in order
+            for (int k = 0; k < K; k++) init[(int64_t)nx * K + k] = (uint16_t)k;
+        } else if (nx <= cap) {
+            kmp_rand_perm(perm, nx, seed + 1, K);  // redo 0: seed + 1 + 0 * 15486557
+            for (int k = 0; k < K; k++) init[(int64_t)nx * K + k] = (uint16_t)perm[k];
+        } else {
+            kmp_rand_perm(perm, nx, seed, cap);  // subsample_training_set
+            uint32_t* mask = out + mask_off + (int64_t)(nx - cap - 1) * mw;
+            for (int i = 0; i < cap; i++) mask[perm[i] >> 5] |= 1u << (perm[i] & 31);
+            for (int k = 0; k < K; k++) init[(int64_t)nx * K + k] = (uint16_t)perm[perm1[k]];
+        }
+    }
+    std::mt19937 mt(1234u);  // split_clusters: RandomGenerator rng(1234); rand_float = mt() / float(mt.max())
+    for (int i = 0; i < KMP_N_RAND; i++) {
+        const float r = (float)mt() / (float)mt.max();
+        memcpy(out + rand_off + i, &r, 4);
+    }
+    return 0;
+}
 
 int64_t ncn_cluster_status_offset(int K) {
     float* base = nullptr;
@@ -992,7 +1107,7 @@ int ncn_diag_cl_times(unsigned long long* host) {
 }
 #endif
 
-int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint32_t seed, float t_similar,
+int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, const uint32_t* kmeans_plan, float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,
                      float sched_start, float sched_grow, const float* photo_loss, float* out_losses,
                      int32_t* out_labels, float* out_centroids, float* dL_dnormals, float* workspace,
@@ -1000,13 +1115,14 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, uint
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
                 "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
     NCN_REQUIRE(niter >= 0 && niter <= 30, hipErrorInvalidValue, "ncn_cluster_loss: niter must be in [0, 30]");
+    NCN_REQUIRE(kmeans_plan != nullptr, hipErrorInvalidValue, "ncn_cluster_loss: kmeans_plan required (ncn_kmeans_plan_fill)");
     hipStream_t s = (hipStream_t)stream;
     if (K == 20)
-        launch_cluster<20>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
+        launch_cluster<20>(normals, (int)n_tri, niter, kmeans_plan, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
                            sched_grow, photo_loss, out_losses, out_labels,
                            out_centroids, dL_dnormals, workspace, s);
     else if (K == 10)
-        launch_cluster<10>(normals, (int)n_tri, niter, seed, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
+        launch_cluster<10>(normals, (int)n_tri, niter, kmeans_plan, t_similar, w_ort, w_dot, w_l1, w_dev, step_dev, sched_start,
                            sched_grow, photo_loss, out_losses, out_labels,
                            out_centroids, dL_dnormals, workspace, s);
     else

@@ -39,12 +39,12 @@ SIGNATURES = {
     "ncn_composite_train_fw_bg": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, F32, P, P],
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
-    "ncn_field_pack_weights": [P, P, P],
-    "ncn_field_fwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P],
+    "ncn_field_pack_weights": [P, P, I32, P],
+    "ncn_field_fwd": [P, P, I64, P, P, P, F32, F32, P, I32, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
     "ncn_field_bwd_dE_floats": [I64],
-    "ncn_field_bwd": [P, P, I64, P, P, F32, F32, P, P, P, P, P, P, P, P, P],
-    "ncn_field_bwd_mlp": [P, I64, P, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd": [P, P, I64, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd_mlp": [P, I64, P, P, I32, P, P, P, P, P, P, P],
     "ncn_field_scatter": [P, I64, P, P, F32, F32, P, P, I32, I32, I32, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
@@ -54,7 +54,9 @@ SIGNATURES = {
     "ncn_photo_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P],
     "ncn_cluster_workspace_words": [I32],
     "ncn_cluster_status_offset": [I32],
-    "ncn_cluster_loss": [P, I64, I32, I32, U32, F32, F32, F32, F32, P, P, F32, F32, P, P, P, P, P, P, P],
+    "ncn_kmeans_plan_words": [I32, I32],
+    "ncn_kmeans_plan_fill": [I32, I32, U32, P],
+    "ncn_cluster_loss": [P, I64, I32, I32, P, F32, F32, F32, F32, P, P, F32, F32, P, P, P, P, P, P, P],
     "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
@@ -97,6 +99,7 @@ def lib():
             fn.restype = ctypes.c_int
         L.ncn_cluster_workspace_words.restype = ctypes.c_int64
         L.ncn_cluster_status_offset.restype = ctypes.c_int64
+        L.ncn_kmeans_plan_words.restype = ctypes.c_int64
         L.ncn_field_bwd_dE_floats.restype = ctypes.c_int64
         L.ncn_adam_step_work_floats.restype = ctypes.c_int64
         L.ncn_grid_work_bytes.restype = ctypes.c_int64

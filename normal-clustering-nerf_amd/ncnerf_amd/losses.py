@@ -39,6 +39,25 @@ def _cluster_workspace(dev, K):
     return ws
 
 
+_PLANS = {}
+
+
+def kmeans_plan(dev, n_tri, K, seed=1234):
+    """faiss's k-means draws for (n_tri, K, seed) (ncn_kmeans_plan_fill, built on the host once with
+    std::mt19937 and kept on `dev`): subsample membership, init picks, split floats."""
+    key = (str(dev), int(n_tri), int(K), int(seed))
+    plan = _PLANS.get(key)
+    if plan is None:
+        words = int(_lib.lib().ncn_kmeans_plan_words(I32(n_tri), I32(K)))
+        host = torch.zeros(words, dtype=torch.int32)
+        rc = _lib.lib().ncn_kmeans_plan_fill(I32(n_tri), I32(K), U32(seed), ptr(host))
+        if rc != 0:
+            raise _lib.NcnError("ncn_kmeans_plan_fill failed: " + _lib.lib().ncn_last_error().decode())
+        plan = host.to(dev)
+        _PLANS[key] = plan
+    return plan
+
+
 def check_cluster_status(dev=None):
     """Raise if a clustering launch on any workspace (of `dev`, or all) hit its barrier/hand-off
     timeout (the kernel's sticky error word, ncn_cluster_status_offset): its losses and gradients
@@ -99,7 +118,7 @@ class _ClusterLoss(torch.autograd.Function):
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = _cluster_workspace(dev, K)
         hw, w_dev = _split_weights(w)
-        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), ptr(kmeans_plan(dev, T, K, seed)), F32(t_sim), F32(hw[0]),
              F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(None), F32(0.0), F32(1.0), ptr(None), ptr(out), ptr(labels),
              ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(dn)
@@ -153,7 +172,7 @@ class _NormalsClusterLoss(torch.autograd.Function):
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = _cluster_workspace(dev, K)
         hw, w_dev = _split_weights(w)
-        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(hw[0]),
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), ptr(kmeans_plan(dev, T, K, seed)), F32(t_sim), F32(hw[0]),
              F32(hw[1]), F32(hw[2]), ptr(w_dev), ptr(None), F32(0.0), F32(1.0), ptr(None), ptr(out), ptr(labels),
              ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(rays_o, rays_d, depth, x1, x2, x3, dn)
@@ -243,7 +262,7 @@ class _NeRFLossFused(torch.autograd.Function):
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
         dn = torch.empty(3, T, 3, dtype=torch.float32, device=dev)
         ws = _cluster_workspace(dev, K)
-        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), U32(seed), F32(t_sim), F32(w[0]),
+        call("ncn_cluster_loss", ptr(normals), I64(T), I32(K), I32(niter), ptr(kmeans_plan(dev, T, K, seed)), F32(t_sim), F32(w[0]),
              F32(w[1]), F32(w[2]), ptr(None), ptr(step_dev), F32(sched[0]), F32(sched[1]), ptr(photo), ptr(out),
              ptr(labels), ptr(cents), ptr(dn), ptr(ws), stream())
         ctx.save_for_backward(rgb, opacity, depth, rays_o, rays_d, rgb_gt, photo, dn)

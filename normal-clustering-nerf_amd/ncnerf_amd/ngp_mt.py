@@ -9,7 +9,8 @@ update_density_grid, mark_invisible_cells).  Parameter names keep tcnn's `<modul
 ('xyz_encoder' in name -> no weight decay, train_nerf.py:262-274) applies unchanged.
 
 Memory layout (MI355X): all parameters live in ONE flat fp32 buffer
-  [hash table (n_entries x 2) | W1 (64,32) | W2 (16,64) | W3 (64,19) | W4 (64,64) | W5 (3,64)]
+  [hash table (n_entries x 2) | W1 (64,32) | W2 (16,64) | W3 (64,32) | W4 (64,64) | W5 (16,64)]
+(tcnn's padded rgb_net: 19 inputs cat[d/|d|, h] + 13 constant-1 inputs, 3 outputs + 13 unused rows)
 and their gradients in a second flat buffer of the same layout, so the gradient all-reduce is a
 single RCCL call and the optimizer a single pass.  The backward accumulates straight into
 `param.grad` (views of the flat gradient buffer): hash-table gradients by f32 atomics, weight
@@ -29,7 +30,11 @@ from . import _lib, vren
 from ._lib import I32, I64, F32, call, ptr, stream
 
 L_LEVELS, F_PER_LEVEL, LOG2_T, N_MIN = 16, 2, 19, 16  # ngp_mt.py:40
-N_W = 64 * 32 + 16 * 64 + 64 * 19 + 64 * 64 + 3 * 64  # NCN_FIELD_NW
+# tcnn's padded shapes (ngp_mt.py:83-113 through tcnn.Network): sigma_net W1 (64,32) W2 (16,64);
+# rgb_net's 19 inputs padded to 32 with 1.0, 3 outputs padded to 16: W3 (64,32) W4 (64,64) W5 (16,64)
+MLP_SHAPES = ((64, 32), (16, 64), (64, 32), (64, 64), (16, 64))
+N_W = sum(o * i for o, i in MLP_SHAPES)  # NCN_FIELD_NW (10240: sigma_net 3072 + rgb_net 7168)
+PRECISIONS = {"fp16": 0, "bf16": 1}  # NCN_PREC_F16 / NCN_PREC_BF16
 N_PACKED_HALVES = 19456  # NCN_FIELD_PACKED_HALVES
 ENC_BYTES = 64  # NCN_ENC_BYTES_PER_SAMPLE
 W_SIGMA = 64 * 32 + 16 * 64
@@ -84,8 +89,8 @@ class _FieldFunction(torch.autograd.Function):
             enc = torch.empty(((n + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev)
         packed = model._take_packed()
         call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(n_dev), ptr(table),
-             model._levels_ptr,
-             F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(mode), ptr(sigmas),
+             model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(model._prec), I32(mode),
+             ptr(sigmas),
              ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
         if need_grad:
             ctx.save_for_backward(x, d, enc, packed, n_dev)
@@ -109,13 +114,14 @@ class _FieldFunction(torch.autograd.Function):
         split = model.scatter_split
         if split is None:
             call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
-                 F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table), ptr(slab),
-                 ptr(dE_ws), ptr(model._level_max()), stream())
+                 F32(model._xyz_extent), ptr(packed), I32(model._prec), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table),
+                 ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
         else:
             # data-parallel step: the levels [split, 16) are scattered now, [0, split) later by
             # run_deferred_scatter() while the all-reduce of the first bucket is in flight
             lmax = model._level_max()
-            call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb),
+            call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(packed), I32(model._prec), ptr(enc), ptr(dsig),
+                 ptr(drgb),
                  ptr(slab), ptr(dE_ws), ptr(lmax), stream())
             call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), model._levels_ptr, F32(model._xyz_min),
                  F32(model._xyz_extent), ptr(dE_ws), ptr(lmax), I32(split), I32(16), I32(0), ptr(g_table), stream())
@@ -132,8 +138,15 @@ class NGPMT(nn.Module):
             self._lmax = torch.empty(16 * 256, dtype=torch.float32, device=dev)
         return self._lmax
 
-    def __init__(self, scale, grid_size, rgb_act="Sigmoid", pred_sem=False, pred_norm=False, seed=1337, **kwargs):
+    def __init__(self, scale, grid_size, rgb_act="Sigmoid", pred_sem=False, pred_norm=False, seed=1337,
+                 precision="fp16", **kwargs):
+        """precision: MFMA operand type of the MLPs, "fp16" (tcnn's FullyFusedMLP, the reference's AMP
+        run) or "bf16" (config #3); parameters, table and accumulation stay fp32."""
         super().__init__()
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        self.precision = precision
+        self._prec = PRECISIONS[precision]
         if rgb_act != "Sigmoid":
             raise NotImplementedError("rgb_act='None' (exposure tonemappers) is off in every reference config")
         if pred_sem or pred_norm:
@@ -160,7 +173,7 @@ class NGPMT(nn.Module):
         g = torch.Generator().manual_seed(seed)
         flat[:n_table] = (torch.rand(n_table, generator=g) * 2 - 1) * 1e-4  # tcnn grid init U(-1e-4, 1e-4)
         off = n_table
-        for o, i in ((64, 32), (16, 64), (64, 19), (64, 64), (3, 64)):  # Xavier-uniform MLP weights
+        for o, i in MLP_SHAPES:  # Xavier-uniform MLP weights (tcnn initialises the padded matrices)
             a = math.sqrt(6.0 / (o + i))
             flat[off:off + o * i] = (torch.rand(o * i, generator=g) * 2 - 1) * a
             off += o * i
@@ -246,7 +259,7 @@ class NGPMT(nn.Module):
     def _pack_weights(self):
         if self._packed is None or self._packed.device != self._flat.device:
             self._packed = torch.empty(N_PACKED_HALVES, dtype=torch.float16, device=self._flat.device)
-        call("ncn_field_pack_weights", ptr(self._flat[self._n_table:]), ptr(self._packed), stream())
+        call("ncn_field_pack_weights", ptr(self._flat[self._n_table:]), ptr(self._packed), I32(self._prec), stream())
         return self._packed
 
     # -- field -----------------------------------------------------------------------------------
@@ -382,7 +395,7 @@ class NGPMT(nn.Module):
                  _lib.U64((seed + 0x9E3779B97F4A7C15 * c) % 2 ** 64), F32(decay), ptr(cc), ptr(ws["xyzs"]),
                  ptr(ws["idx"]), ptr(n_list), ptr(ws["work"]), stream())
             call("ncn_field_fwd", ptr(ws["xyzs"]), ptr(None), I64(N), ptr(n_list), ptr(table), self._levels_ptr,
-                 F32(self._xyz_min), F32(self._xyz_extent), ptr(packed), I32(1), ptr(ws["sigmas"]), ptr(None),
+                 F32(self._xyz_min), F32(self._xyz_extent), ptr(packed), I32(self._prec), I32(1), ptr(ws["sigmas"]), ptr(None),
                  ptr(None), stream())
             call("ncn_grid_apply", ptr(dgc), ptr(ws["idx"]), ptr(ws["sigmas"]), ptr(n_list), I64(N), F32(decay),
                  ptr(cc), stream())

@@ -6,7 +6,10 @@ Pure-PyTorch (CPU, fp32) restatement of the NGPMT field (reference models/ngp_mt
   * sigma_net 32 -> 64 (ReLU) -> 16, no bias (ngp_mt.py:83-92) and sigma = TruncExp(h[:,0])
     (ngp_mt.py:168-169, custom_functions.py:162-173);
   * rgb_net cat([d/|d|, h]) 19 -> 64 -> 64 -> 3, ReLU hidden, Sigmoid output, no bias
-    (ngp_mt.py:103-113, 206-209).
+    (ngp_mt.py:103-113, 206-209), in tcnn's padded form: `tcnn.Network(n_input_dims=19)` runs an
+    Identity encoding that pads the input to the FullyFusedMLP's 16-alignment (32) with the value
+    1.0, and the output layer is padded to 16 rows, so W3 is (64, 32) and W5 (16, 64) (7168
+    rgb_net parameters, as tcnn reports) and only rows 0..2 of W5 produce outputs.
 
 tiny-cuda-nn is NOT vendored in the reference (README.md:17, `pip install git+...tiny-cuda-nn` at
 no pinned commit) and is not importable here, so this restates tcnn's published algorithm:
@@ -19,8 +22,9 @@ no pinned commit) and is not importable here, so this restates tcnn's published 
   feature        = sum over the 8 corners of trilinear weight * table[index]
 PARITY UNPINNED for this file: no reference test or fixture pins tcnn's numerics.  The documented
 deviations from tcnn (fp32 table + fp32 interpolation instead of fp16) are listed in DESIGN.md.
-`emulate_f16=True` rounds the MLP operands to fp16 at the same points the HIP kernel does
-(fp16 MFMA inputs, fp32 accumulation), so the HIP path can be checked tightly.
+`emulate_f16=True` (or emulate="bf16") rounds the MLP operands to fp16 (bf16) at the same points
+the HIP kernel does (MFMA inputs in that type, fp32 accumulation), so the HIP path can be checked
+tightly in either precision.
 """
 import math
 
@@ -98,12 +102,16 @@ def hash_encode(x01, table, levels):
     return (wts * g).sum(2).reshape(n, L * F_PER_LEVEL)
 
 
-def _f16(t, on):
-    return t.half().float() if on else t
+def _rounder(emulate_f16=False, emulate=None):
+    mode = emulate or ("fp16" if emulate_f16 else None)
+    if mode is None:
+        return lambda t: t
+    dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[mode]
+    return lambda t: t.to(dt).float()
 
 
 class FieldParams:
-    """fp32 master parameters: table (n_entries,2), W1 (64,32), W2 (16,64), W3 (64,19), W4 (64,64), W5 (3,64)."""
+    """fp32 master parameters: table (n_entries,2), W1 (64,32), W2 (16,64), W3 (64,32), W4 (64,64), W5 (16,64)."""
 
     def __init__(self, table, W1, W2, W3, W4, W5):
         self.table, self.W1, self.W2, self.W3, self.W4, self.W5 = table, W1, W2, W3, W4, W5
@@ -112,20 +120,24 @@ class FieldParams:
         return [self.table, self.W1, self.W2, self.W3, self.W4, self.W5]
 
 
-def field_forward(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False):
+def rgb_input(d, h):
+    """tcnn Identity encoding of rgb_net's 19 inputs cat[d/|d|, h], padded to 32 with 1.0."""
+    return torch.cat([d, h, torch.ones(d.shape[0], 32 - 19, dtype=h.dtype)], dim=1)
+
+
+def field_forward(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=None):
     """NGPMT.forward (ngp_mt.py:196-229) with density() (ngp_mt.py:157-171).
     Returns sigmas (N), rgbs (N,3), h (N,16)."""
+    q = _rounder(emulate_f16, emulate)
     x01 = (xyzs - (-scale)) / (2 * scale)  # (x - xyz_min)/(xyz_max - xyz_min), ngp_mt.py:166
     enc = hash_encode(x01, P.table, levels)
-    e = _f16(enc, emulate_f16)
-    h1 = torch.relu(e @ _f16(P.W1, emulate_f16).t())
-    h = _f16(h1, emulate_f16) @ _f16(P.W2, emulate_f16).t()
+    h1 = torch.relu(q(enc) @ q(P.W1).t())
+    h = q(h1) @ q(P.W2).t()
     sig = torch.exp(h[:, 0])  # TruncExp forward
     d = dirs / torch.norm(dirs, dim=1, keepdim=True)
-    xin = torch.cat([d, h], dim=1)
-    g1 = torch.relu(_f16(xin, emulate_f16) @ _f16(P.W3, emulate_f16).t())
-    g2 = torch.relu(_f16(g1, emulate_f16) @ _f16(P.W4, emulate_f16).t())
-    rgb = torch.sigmoid(_f16(g2, emulate_f16) @ _f16(P.W5, emulate_f16).t())
+    g1 = torch.relu(q(rgb_input(d, h)) @ q(P.W3).t())
+    g2 = torch.relu(q(g1) @ q(P.W4).t())
+    rgb = torch.sigmoid((q(g2) @ q(P.W5).t())[:, :3])
     return sig, rgb, h
 
 
@@ -143,19 +155,19 @@ class _TruncExp(torch.autograd.Function):
         return g * torch.exp(x.clamp(-15, 15))
 
 
-def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False):
+def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=None):
     """Same as field_forward with TruncExp's clamped backward, differentiable w.r.t. P.  With
-    emulate_f16 the forward operands are rounded to fp16 where the HIP kernel rounds them (the
-    rounding is straight-through in the backward), so ReLU masks match the kernel's."""
-    q = lambda t: _f16(t, emulate_f16)
+    emulation the forward operands are rounded where the HIP kernel rounds them (the rounding is
+    straight-through in the backward), so ReLU masks match the kernel's."""
+    q = _rounder(emulate_f16, emulate)
     x01 = (xyzs - (-scale)) / (2 * scale)
     enc = hash_encode(x01, P.table, levels)
     h = q(torch.relu(q(enc) @ q(P.W1).t())) @ q(P.W2).t()
     sig = _TruncExp.apply(h[:, 0])
     d = dirs / torch.norm(dirs, dim=1, keepdim=True)
-    g = torch.relu(q(torch.cat([d, h], 1)) @ q(P.W3).t())
+    g = torch.relu(q(rgb_input(d, h)) @ q(P.W3).t())
     g = torch.relu(q(g) @ q(P.W4).t())
-    rgb = torch.sigmoid(q(g) @ q(P.W5).t())
+    rgb = torch.sigmoid((q(g) @ q(P.W5).t())[:, :3])
     return sig, rgb, h
 
 
@@ -169,5 +181,5 @@ def init_params(seed=0, scale=0.5, table_init=1e-4):
         return (torch.rand(o, i, generator=g) * 2 - 1) * a
 
     table = (torch.rand(n_entries, 2, generator=g) * 2 - 1) * table_init
-    P = FieldParams(table, xavier(64, 32), xavier(16, 64), xavier(64, 19), xavier(64, 64), xavier(3, 64))
+    P = FieldParams(table, xavier(64, 32), xavier(16, 64), xavier(64, 32), xavier(64, 64), xavier(16, 64))
     return P, levels

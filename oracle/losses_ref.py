@@ -4,11 +4,19 @@ CPU restatement of the normal-clustering loss path:
   * `normals_from_depth`  — datasets/hypersim_src/utils.py:504-541 (_extract_normals_from_ray_batch)
   * `patch_triangles`     — datasets/base.py:35-66 (x1/x2/x3 local offsets of an 8x8 patch) and
                             losses.py:307-313 (get_patch_triang_idx)
-  * `spherical_kmeans`    — the k-means behind losses.py:433-440 (faiss.Kmeans(3, k=20, niter=20,
-                            spherical=True)).  faiss is not installed here and its version is unpinned
-                            (not in README/requirements; imported at losses.py:8-9), so this is OUR
-                            deterministic Lloyd spherical k-means (see `spherical_kmeans` doc) — PARITY
-                            UNPINNED w.r.t. faiss.  The HIP kernel implements exactly this algorithm.
+  * `spherical_kmeans`    — the k-means behind losses.py:86-89 (faiss.Kmeans(3, k=20, niter=20,
+                            spherical=True) + index.search).  faiss is not installed here and its
+                            version is unpinned (not in README/requirements; imported at
+                            losses.py:8-9): this RESTATES faiss's published Clustering::train
+                            (faiss/Clustering.cpp, utils/random.cpp of the 1.7 line) — subsampling
+                            to k*max_points_per_centroid (256) points by rand_perm(seed 1234),
+                            init = the first k points of rand_perm(seed 1235), search / centroid
+                            mean / split_clusters (RandomGenerator(1234) per iteration) / L2
+                            renormalisation per iteration, then a final search of all points —
+                            with std::mt19937 restated below.  PARITY UNPINNED w.r.t. faiss itself
+                            (no fixture of faiss output exists); float summation order differs
+                            (faiss sums centroids in f32, the HIP kernel in exact fixed point).
+                            The HIP kernel implements exactly this algorithm.
   * `cluster_select`      — losses.py:47-166 (_cluster_indices, _find_opposite, _normals_clustering),
                             pinned by golden vectors from the reference code (tests/golden).
   * `cluster_losses`      — losses.py:420-478 + the weight schedule losses.py:217 and the validity
@@ -52,58 +60,151 @@ def valid_normals_mask(n):
     return ~inv
 
 
-def _mix32(x):
-    x = (x ^ (x >> 16)) * 0x7FEB352D & 0xFFFFFFFF
-    x = (x ^ (x >> 15)) * 0x846CA68B & 0xFFFFFFFF
-    return (x ^ (x >> 16)) & 0xFFFFFFFF
+class Mt19937:
+    """std::mt19937 (faiss RandomGenerator's engine: `mt((unsigned int)seed)`)."""
+
+    def __init__(self, seed):
+        mt = [0] * 624
+        mt[0] = seed & 0xFFFFFFFF
+        for i in range(1, 624):
+            mt[i] = (1812433253 * (mt[i - 1] ^ (mt[i - 1] >> 30)) + i) & 0xFFFFFFFF
+        self.mt, self.i = np.array(mt, np.uint64), 624
+
+    def _twist(self):
+        mt = self.mt
+        for i in range(624):
+            y = (int(mt[i]) & 0x80000000) | (int(mt[(i + 1) % 624]) & 0x7FFFFFFF)
+            v = int(mt[(i + 397) % 624]) ^ (y >> 1)
+            if y & 1:
+                v ^= 0x9908B0DF
+            mt[i] = v
+        self.i = 0
+
+    def __call__(self):
+        if self.i >= 624:
+            self._twist()
+        y = int(self.mt[self.i])
+        self.i += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        y ^= y >> 18
+        return y & 0xFFFFFFFF
 
 
-def kmeans_init_indices(n, K, seed):
-    """Stratified seeded init: one pick per stratum [k*n/K, (k+1)*n/K) (the HIP kernel uses the same)."""
-    idx = []
-    for k in range(K):
-        lo = (k * n) // K
-        hi = ((k + 1) * n) // K
-        span = max(hi - lo, 1)
-        idx.append(lo + _mix32((seed * 0x9E3779B1 + k * 0x85EBCA77 + 1) & 0xFFFFFFFF) % span)
-    return np.array(idx, dtype=np.int64)
+def rand_perm_prefix(n, seed, m):
+    """faiss rand_perm(perm, n, seed) (utils/random.cpp): Fisher-Yates with
+    i2 = i + RandomGenerator::rand_int(n - i) = i + mt() % (n - i); only the first m steps (the
+    first m entries are final after them)."""
+    perm = np.arange(n, dtype=np.int64)
+    rng = Mt19937(seed)
+    for i in range(min(m, n - 1)):
+        i2 = i + rng() % (n - i)
+        perm[i], perm[i2] = perm[i2], perm[i]
+    return perm[:m]
 
 
-def spherical_kmeans(X, K=KM_K, niter=KM_NITER, seed=0):
-    """Deterministic spherical Lloyd k-means (float32, numpy).
+def rand_floats(seed, count):
+    """RandomGenerator::rand_float() = mt() / float(mt.max()) in f32."""
+    rng = Mt19937(seed)
+    return np.array([np.float32(np.float32(rng()) / np.float32(4294967295.0)) for _ in range(count)], np.float32)
 
-    init: X[kmeans_init_indices]; each of `niter` iterations: assign every point to the centroid of
-    largest inner product (ties -> lowest index), centroid = mean of its members, empty clusters
-    are split from the largest cluster with faiss's perturbation (+/- 1/1024 on alternating
-    coordinates), then every centroid is L2-normalised (spherical).  The returned assignment is a
-    final search against the final centroids, as losses.py:436 does with kmeans.index.search.
-    Returns (centroids (K,3) f32, assign (n,) i64)."""
+
+MAX_POINTS_PER_CENTROID = 256  # faiss ClusteringParameters default
+N_RAND = 4096
+
+
+def faiss_training_set(nx, K, seed=1234):
+    """(indices of the training points in subsample order, init picks as indices into the input)."""
+    cap = K * MAX_POINTS_PER_CENTROID
+    if nx > cap:
+        sub = rand_perm_prefix(nx, seed, cap)  # subsample_training_set
+    else:
+        sub = np.arange(nx, dtype=np.int64)
+    picks = rand_perm_prefix(len(sub), seed + 1, K)  # init (redo 0: seed + 1 + 0 * 15486557)
+    return sub, sub[picks]
+
+
+def plan_mask_row(nx, K, seed=1234):
+    """Training-set membership bits (uint32 words, bit i = point i) of nx > K*256 points."""
+    sub, _ = faiss_training_set(nx, K, seed)
+    bits = np.zeros(((nx + 31) // 32) * 32, np.uint64)
+    bits[sub] = 1
+    return (bits.reshape(-1, 32) << np.arange(32, dtype=np.uint64)).sum(1).astype(np.uint32)
+
+
+def _renorm(C):
+    """faiss fvec_renorm_L2: x *= (float)(1.0 / sqrtf(|x|^2)) (a double division) when |x|^2 > 0;
+    |x|^2 in f32 as ((x0 x0 + x1 x1) + x2 x2)."""
+    C = C.astype(np.float32).copy()
+    for k in range(C.shape[0]):
+        nr = np.float32(np.float32(C[k, 0] * C[k, 0]) + np.float32(C[k, 1] * C[k, 1]))
+        nr = np.float32(nr + np.float32(C[k, 2] * C[k, 2]))
+        if nr > 0:
+            C[k] = C[k] * np.float32(1.0 / float(np.sqrt(nr, dtype=np.float32)))
+    return C
+
+
+def _dots(X, C):
+    """<x, c> in f32 without FMA as ((x0 c0 + x1 c1) + x2 c2): the HIP kernel's association (faiss
+    itself uses BLAS sgemm: unpinned at the last bit)."""
+    X = X.astype(np.float32)
+    C = C.astype(np.float32)
+    return (X[:, None, 0] * C[None, :, 0] + X[:, None, 1] * C[None, :, 1]) + X[:, None, 2] * C[None, :, 2]
+
+
+KM_FXL = 2.0 ** 39
+
+
+def _fixed_sum(X):
+    """Sum of rows as the HIP kernel forms it: every coordinate rounded to 2^-39 (half to even),
+    exact int64 sums, one rounding to f32 (faiss sums in f32 in point order: unpinned)."""
+    q = np.rint(X.astype(np.float64) * KM_FXL).astype(np.int64).sum(0)
+    return (q.astype(np.float64) * (1.0 / KM_FXL)).astype(np.float32)
+
+
+def spherical_kmeans(X, K=KM_K, niter=KM_NITER, seed=1234):
+    """faiss.Kmeans(3, K, niter, spherical=True).train(X) + index.search(X, 1) (losses.py:86-89),
+    restated (module doc) with the HIP kernel's arithmetic (_dots, _fixed_sum), so the device
+    result is reproduced bit for bit.  Returns (centroids (K,3) f32, assign (n,) i64)."""
     X = np.ascontiguousarray(X, dtype=np.float32)
     n = X.shape[0]
-    C = X[kmeans_init_indices(n, K, seed)].copy()
-    EPS = np.float32(1.0 / 1024.0)
+    sub, picks = faiss_training_set(n, K, seed)
+    Xt = X[sub]
+    nt = Xt.shape[0]
+    if nt == K:  # faiss's nx == k corner case: the points are the centroids, no iteration
+        C = X[:K].copy()
+        return C, np.argmax(_dots(X, C), axis=1).astype(np.int64)
+    C = _renorm(X[picks])
+    EPS = 1.0 / 1024.0
     for _ in range(niter):
-        a = np.argmax(X @ C.T, axis=1)
-        cnt = np.bincount(a, minlength=K).astype(np.int64)
-        S = np.zeros((K, 3), np.float64)
-        np.add.at(S, a, X.astype(np.float64))
-        newC = C.copy()
+        a = np.argmax(_dots(Xt, C), axis=1)  # IndexFlatIP search, ties -> lowest index
+        cnt = np.bincount(a, minlength=K).astype(np.float32)  # hassign
+        newC = np.zeros((K, 3), np.float32)
         for k in range(K):
             if cnt[k] > 0:
-                newC[k] = (S[k] / cnt[k]).astype(np.float32)
-        for k in range(K):  # split empty clusters from the (current) largest one
-            if cnt[k] == 0:
-                j = int(np.argmax(cnt))
+                newC[k] = _fixed_sum(Xt[a == k]) * (np.float32(1.0) / cnt[k])
+        rng, r_i = rand_floats(1234, N_RAND), 0  # split_clusters: RandomGenerator rng(1234), per call
+        for ci in range(K):
+            if cnt[ci] == 0:
+                cj = 0
+                while True:
+                    p = np.float32((float(cnt[cj]) - 1.0) / float(np.float32(nt - K)))
+                    r = rng[r_i]
+                    r_i += 1
+                    if r < p:
+                        break
+                    cj = (cj + 1) % K
+                newC[ci] = newC[cj]
                 for dd in range(3):
                     if dd % 2 == 0:
-                        newC[k, dd] = newC[j, dd] * (1 + EPS); newC[j, dd] = newC[j, dd] * (1 - EPS)
+                        newC[ci, dd] *= np.float32(1 + EPS); newC[cj, dd] *= np.float32(1 - EPS)
                     else:
-                        newC[k, dd] = newC[j, dd] * (1 - EPS); newC[j, dd] = newC[j, dd] * (1 + EPS)
-                cnt[k] = cnt[j] // 2
-                cnt[j] = cnt[j] - cnt[k]
-        nrm = np.sqrt((newC.astype(np.float64) ** 2).sum(1, keepdims=True))
-        C = (newC / np.maximum(nrm, 1e-30)).astype(np.float32)
-    a = np.argmax(X @ C.T, axis=1).astype(np.int64)
+                        newC[ci, dd] *= np.float32(1 - EPS); newC[cj, dd] *= np.float32(1 + EPS)
+                cnt[ci] = cnt[cj] / np.float32(2)
+                cnt[cj] -= cnt[ci]
+        C = _renorm(newC)
+    a = np.argmax(_dots(X, C), axis=1).astype(np.int64)  # kmeans.index.search(normals_np, 1)
     return C, a
 
 

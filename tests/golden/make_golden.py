@@ -93,6 +93,9 @@ class _Encoding(nn.Module):
 
 
 class _Network(nn.Module):
+    """tcnn.Network as the reference builds it: an Identity encoding pads the input to a multiple of
+    16 with 1.0 and the FullyFusedMLP's output layer is padded to 16 rows (sliced back)."""
+
     def __init__(self, n_input_dims, n_output_dims, network_config, **kw):
         super().__init__()
         if n_input_dims == 32:
@@ -101,11 +104,16 @@ class _Network(nn.Module):
             Ws = [_P.W3, _P.W4, _P.W5]
         else:
             raise NotImplementedError(n_input_dims)
+        self.n_in, self.n_out = n_input_dims, n_output_dims
         self.shapes = [tuple(w.shape) for w in Ws]
+        assert self.shapes[0][1] == -(-n_input_dims // 16) * 16 and self.shapes[-1][0] == -(-n_output_dims // 16) * 16
         self.out_act = network_config["output_activation"]
         self.params = nn.Parameter(torch.cat([w.reshape(-1) for w in Ws]).clone())
 
     def forward(self, x):
+        pad = self.shapes[0][1] - x.shape[1]
+        if pad:
+            x = torch.cat([x, torch.ones(x.shape[0], pad, dtype=x.dtype)], dim=1)
         off, h = 0, x
         for i, (o, n) in enumerate(self.shapes):
             W = self.params[off:off + o * n].view(o, n)
@@ -115,7 +123,7 @@ class _Network(nn.Module):
                 h = torch.relu(h)
         if self.out_act == "Sigmoid":
             h = torch.sigmoid(h)
-        return h
+        return h[:, :self.n_out]
 
 
 def _tcnn_module():
