@@ -105,9 +105,9 @@ _TEX = np.array([[11.0, 7.0, -5.0], [-6.0, 13.0, 8.0], [9.0, -4.0, 12.0]], np.fl
 _TEX_PHASE = np.array([0.3, 2.2, 4.1], np.float32)
 
 
-def texture_rgb(p):
-    """Albedo of the room surfaces at points p (N,3): smooth procedural texture in [0.1, 0.9]."""
-    return (0.5 + 0.4 * np.sin(p @ _TEX.T + _TEX_PHASE)).astype(np.float32)
+def texture_rgb(p, lo=0.1, hi=0.9):
+    """Albedo of the room surfaces at points p (N,3): smooth procedural texture in [lo, hi]."""
+    return (0.5 * (hi + lo) + 0.5 * (hi - lo) * np.sin(p @ _TEX.T + _TEX_PHASE)).astype(np.float32)
 
 
 def first_hit(occ, rays_o, rays_d, scale=0.5, step_vox=0.25, t_max=2.0, chunk=64):
@@ -135,13 +135,13 @@ def first_hit(occ, rays_o, rays_d, scale=0.5, step_vox=0.25, t_max=2.0, chunk=64
     return t_hit
 
 
-def surface_rgb(occ, rays_o, rays_d, scale=0.5):
+def surface_rgb(occ, rays_o, rays_d, scale=0.5, lo=0.1, hi=0.9):
     """Target colour of a ray (gt="surface", default): texture_rgb at its first occupied voxel,
     white (the reference's background, rendering.py:232-240) if it hits nothing."""
     t = first_hit(occ, rays_o, rays_d, scale)
     rgb = np.ones((rays_o.shape[0], 3), np.float32)
     m = np.isfinite(t)
-    rgb[m] = texture_rgb(rays_o[m] + rays_d[m] * t[m, None])
+    rgb[m] = texture_rgb(rays_o[m] + rays_d[m] * t[m, None], lo, hi)
     return rgb
 
 
@@ -174,7 +174,12 @@ class SyntheticScene:
         P = self.poses[cam]
         rays_d = np.einsum("nij,nj->ni", P[:, :, :3], dcam).astype(np.float32)
         rays_o = P[:, :, 3].astype(np.float32)
-        rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale) if gt == "surface" else _gt_color(rays_d)
+        if gt == "surface":
+            rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale)
+        elif gt == "surface_bright":
+            rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale, 0.45, 0.95)
+        else:
+            rgb = _gt_color(rays_d)
         return {"rays_o": rays_o, "rays_d": rays_d, "rgb": rgb, "patch_area": PATCH * PATCH,
                 "x1_offsets_local": self.x1_off, "x2_offsets_local": self.x2_off, "x3_offsets_local": self.x3_off}
 

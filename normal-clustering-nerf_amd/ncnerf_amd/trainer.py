@@ -50,12 +50,15 @@ class Trainer:
         self.use_graph = use_graph
         self.graph = None
         self._rng_seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # marcher jitter stream (CPU generator)
+        # optional seed of each grid refresh (global_step -> int); default: drawn from torch's CPU generator
+        self.grid_seed = None
 
     def _maybe_update_grid(self, global_step):
         m = self.model
         if self.update_grid and global_step % self.update_interval == 0:
             thr = 0.01 * self.h["rend_max_samples"] / 3 ** 0.5 * self.h["density_tresh_decay"]
-            m.update_density_grid(thr, warmup=global_step < self.warmup_steps)
+            seed = self.grid_seed(global_step) if self.grid_seed is not None else None
+            m.update_density_grid(thr, warmup=global_step < self.warmup_steps, seed=seed)
             distributed.broadcast_occupancy(m)
 
     # -- graph-captured step ---------------------------------------------------------------------

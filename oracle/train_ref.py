@@ -7,6 +7,8 @@ Same step as ncnerf_amd/trainer.py, built only from the oracle restatements:
   white background (rendering.py:232-240) -> rgb MSE + opacity + normals-from-depth + clustering
   losses (losses_ref) -> backward -> global-norm clip 0.05 + AdamW(eps 1e-15) (train_nerf.py:262-285).
 """
+import math
+
 import numpy as np
 import torch
 
@@ -51,7 +53,7 @@ def render_train_ref(P, levels, rays_o, rays_d, bitfield, noise, near=0.01, max_
 class CPUTrainer:
     """Hypersim config: scale 0.5, G 128, max_samples 1024, near 0.01, loss weights as the trainer."""
 
-    def __init__(self, bitfield, seed=0, lr=1e-2, w_cluster=2e-3, opacity_w=1e-3):
+    def __init__(self, bitfield, seed=0, lr=1e-2, w_cluster=2e-3, opacity_w=1e-3, num_epochs=None, epoch_steps=1000):
         P, self.levels = field_ref.init_params(seed=seed)
         self.params = [t.requires_grad_(True) for t in P.tensors()]
         self.P = field_ref.FieldParams(*self.params)
@@ -59,6 +61,17 @@ class CPUTrainer:
         self.opt = torch.optim.AdamW([{"params": self.params[:1], "weight_decay": 0.0},
                                       {"params": self.params[1:], "weight_decay": 1e-6}], lr=lr, eps=1e-15)
         self.w_cluster, self.opacity_w = w_cluster, opacity_w
+        # CosineAnnealingLR(T_max=num_epochs) stepped per epoch of `epoch_steps` steps
+        # (train_nerf.py:286-288; base.py:78-81); None keeps lr constant
+        self.base_lr, self.num_epochs, self.epoch_steps = lr, num_epochs, epoch_steps
+
+    def set_lr_for_step(self, global_step):
+        if not self.num_epochs:
+            return
+        e = global_step // self.epoch_steps
+        lr = 0.5 * self.base_lr * (1 + math.cos(math.pi * e / self.num_epochs))
+        for g in self.opt.param_groups:
+            g["lr"] = lr
 
     def step(self, batch, global_step=3000, noise=None):
         """One training step; `noise` (R,) injects the marcher's perturbation (default torch.rand)."""
@@ -69,6 +82,7 @@ class CPUTrainer:
         near = (ht[:, 0] >= 0) & (ht[:, 0] < 0.01)
         ht[near, 0] = 0.01
         noise = torch.rand(R).numpy() if noise is None else np.ascontiguousarray(noise, np.float32)
+        self.set_lr_for_step(global_step)
         rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, self.bitfield, 1, 0.5, 0.0,
                                                                              noise, 128, 1024)
         self.opt.zero_grad()

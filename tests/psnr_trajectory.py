@@ -1,0 +1,185 @@
+"""PSNR parity after equal steps, long form (BASELINE.json north_star: "PSNR within +-0.05 dB of
+reference after equal steps") — test infrastructure, not product code.
+
+The reference trajectory is the oracle CPU step (oracle/train_ref.py: the reference algorithm in
+plain PyTorch fp32 + the C marcher/compositor; AdamW + clip 0.05; cosine LR per 1000-step epoch)
+with the occupancy grid maintained as train_nerf.py does it (mark_invisible_cells at the start,
+update_density_grid every 16 steps, all cells for the first 256 steps; oracle/grid_ref.py, the
+device's sampling restated).  The HIP trajectory is the product step (ncnerf_amd.trainer.Trainer,
+whole step in a HIP graph, grid refresh on the device) fed the SAME batches (synthetic room,
+8192-ray patch batches, gt "surface_bright"), the same marcher noise and the same refresh seeds,
+from the same initial parameters (step 0: the clustering weight ramps in from step 500 as
+losses.py:217 schedules it).
+
+Two halves, so the slow one needs no GPU:
+  python tests/psnr_trajectory.py ref --steps 3000 --out profiles/round2/psnr_ref_trajectory.json   (CPU)
+  python tests/psnr_trajectory.py hip --ref profiles/round2/psnr_ref_trajectory.json \
+         --out profiles/round2/psnr_parity_trajectory.json                                              (GPU)
+PSNR is measured at the same checkpoints on the same held-out rays: the oracle side with the oracle
+renderer (train path, zero noise), the HIP side with the HIP test renderer (the two renderers agree
+on the same parameters: tests/test_gpu_psnr.py).  The HIP side runs twice with identical inputs:
+the difference between those two runs (float-atomic summation order only) is the run-to-run floor
+the reference-vs-HIP difference is read against.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+N_RAYS = 8192
+GT = "surface_bright"
+EVAL_SEEDS = (90_000, 90_001)
+INIT_SEED = 4
+THRESHOLD = 0.01 * 1024 / 3 ** 0.5  # train_nerf.py:316 (density_tresh_decay 1)
+
+
+def batch_seed(k):
+    return 10_000 + k
+
+
+def noise_of(k, n=N_RAYS):
+    return torch.rand(n, generator=torch.Generator().manual_seed(20_000 + k))
+
+
+def grid_seed(k):
+    return 30_000 + k
+
+
+def camera_K():
+    from ncnerf_amd import synthetic
+    fx = (synthetic.IMG_W / 2) / math.tan(synthetic.HFOV / 2)
+    return np.array([[fx, 0, synthetic.IMG_W / 2], [0, fx, synthetic.IMG_H / 2], [0, 0, 1]], np.float32)
+
+
+def _psnr(se, n):
+    return -10.0 * math.log10(max(se / n, 1e-12))
+
+
+def run_ref(steps, every, threads, log, out=None):
+    from oracle import field_ref, grid_ref
+    from oracle.train_ref import CPUTrainer, render_train_ref
+    from ncnerf_amd import synthetic
+    from ncnerf_amd.synthetic import SyntheticScene
+    torch.set_num_threads(threads)
+    scene = SyntheticScene()
+    cpu = CPUTrainer(scene.bitfield, seed=INIT_SEED, num_epochs=30, epoch_steps=1000)
+    grid, _ = grid_ref.mark_invisible_cells(camera_K(), scene.poses, (synthetic.IMG_W, synthetic.IMG_H), 0.01, 128,
+                                            0.5)
+    ev = [scene.batch(N_RAYS, seed=s, gt=GT) for s in EVAL_SEEDS]
+    curve, t0 = [], time.time()
+    for k in range(steps):
+        if k % 16 == 0:
+            dens = lambda x: field_ref.density(torch.from_numpy(x), cpu.P, cpu.levels).numpy()  # noqa: E731
+            grid, thr, bf = grid_ref.grid_refresh(grid, dens, THRESHOLD, k < 256, grid_seed(k), 128, 0.5)
+            cpu.bitfield = np.ascontiguousarray(bf, np.uint8)
+        b = scene.batch(N_RAYS, seed=batch_seed(k), gt=GT)
+        loss, S = cpu.step(b, global_step=k, noise=noise_of(k).numpy())
+        if (k + 1) % every == 0 or k + 1 == steps:
+            se, n = 0.0, 0
+            with torch.no_grad():
+                for e in ev:
+                    r = render_train_ref(cpu.P, cpu.levels, e["rays_o"], e["rays_d"], cpu.bitfield,
+                                         np.zeros(N_RAYS, np.float32))
+                    se += float(((r["rgb"].clamp(0, 1) - torch.from_numpy(e["rgb"])) ** 2).sum())
+                    n += e["rgb"].size
+            curve.append({"step": k + 1, "psnr": _psnr(se, n), "loss": loss, "samples": S,
+                          "occupied_frac": float(np.unpackbits(cpu.bitfield).mean()), "t_s": round(time.time() - t0, 1)})
+            log(json.dumps(curve[-1]))
+            res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": N_RAYS, "gt": GT,
+                   "init_seed": INIT_SEED, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
+                   "curve": curve}
+            if out:  # the trajectory so far (a partial run is usable up to its last checkpoint)
+                with open(out, "w") as f:
+                    f.write(json.dumps(res) + "\n")
+    return res
+
+
+def run_hip(steps, every, log):
+    from ncnerf_amd import synthetic
+    from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
+    from ncnerf_amd.rendering import render
+    from ncnerf_amd.synthetic import SyntheticScene
+    from ncnerf_amd.trainer import Trainer
+    from oracle import field_ref
+    dev = torch.device("cuda:0")
+    scene = SyntheticScene()
+    P, _ = field_ref.init_params(seed=INIT_SEED)
+    ev = [scene.torch_batch(N_RAYS, seed=s, device=dev, gt=GT) for s in EVAL_SEEDS]
+    m = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+    flat, off = m.flat_params(), 0
+    with torch.no_grad():
+        for W in P.tensors():
+            flat[off:off + W.numel()].copy_(W.reshape(-1))
+            off += W.numel()
+    m.mark_invisible_cells(torch.from_numpy(camera_K()), dev, torch.from_numpy(scene.poses).to(dev),
+                           (synthetic.IMG_W, synthetic.IMG_H), 0.01)
+    tr = Trainer(m, update_grid=True, use_graph=True)
+    tr.grid_seed = grid_seed
+    curve, t0 = [], time.time()
+    for k in range(steps):
+        b = scene.torch_batch(N_RAYS, seed=batch_seed(k), device=dev, gt=GT)
+        b["march_noise"] = noise_of(k).to(dev)
+        _, ld = tr.step(b, global_step=k)
+        if (k + 1) % every == 0 or k + 1 == steps:
+            se, n = 0.0, 0
+            with torch.no_grad():
+                for e in ev:
+                    r = render(m, e["rays_o"], e["rays_d"], near_distance=0.01, max_samples=1024, test_time=True)
+                    se += float(((r["rgb"].clamp(0, 1) - e["rgb"]) ** 2).sum())
+                    n += e["rgb"].numel()
+            curve.append({"step": k + 1, "psnr": _psnr(se, n), "loss": float(ld["total"].detach()),
+                          "occupied_frac": float((m.density_bitfield.cpu().numpy()[:, None] >> np.arange(8) & 1).mean()),
+                          "t_s": round(time.time() - t0, 1)})
+            log(json.dumps(curve[-1]))
+    return {"side": "HIP", "curve": curve}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("side", choices=("ref", "hip"))
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--every", type=int, default=500)
+    ap.add_argument("--threads", type=int, default=6)
+    ap.add_argument("--ref", default=None, help="(hip) the oracle trajectory JSON")
+    ap.add_argument("--repeats", type=int, default=2, help="(hip) identical-input HIP runs")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    log = lambda s: print(s, flush=True)  # noqa: E731
+    if a.side == "ref":
+        res = run_ref(a.steps, a.every, a.threads, log, a.out)
+    else:
+        ref = json.load(open(a.ref)) if a.ref else None
+        steps = ref["steps"] if ref else a.steps
+        runs = [run_hip(steps, a.every, log) for _ in range(a.repeats)]
+        res = {"steps": steps, "rays_per_step": N_RAYS, "gt": GT, "hip_runs": runs}
+        last = [r["curve"][-1]["psnr"] for r in runs]
+        res["psnr_hip"] = last
+        res["hip_run_to_run_db"] = max(last) - min(last)
+        if ref:
+            res["ref"] = ref
+            res["psnr_ref"] = ref["curve"][-1]["psnr"]
+            res["delta_db"] = [p - res["psnr_ref"] for p in last]
+            # per-checkpoint deltas (same steps on both sides)
+            rc = {c["step"]: c["psnr"] for c in ref["curve"]}
+            res["delta_curve"] = [[c["step"], round(c["psnr"] - rc[c["step"]], 4)] for c in runs[0]["curve"]
+                                  if c["step"] in rc]
+    line = json.dumps(res)
+    print(line)
+    if a.out:
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
