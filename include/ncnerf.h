@@ -166,7 +166,15 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
 #define NCN_PREC_F16 0
 #define NCN_PREC_BF16 1
 int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int precision, void* stream);
-int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const float* table,
+/* Processing order of a training batch (no reference counterpart: tcnn evaluates in input order):
+ * every window of 4096 consecutive samples sorted by the 30-bit Morton code of its normalised
+ * positions; order[p] = the sample evaluated at position p (n int32, a permutation of each window).
+ * `order` of ncn_field_fwd / _bwd / _bwd_mlp / _scatter: NULL (identity) or this array; enc_cache
+ * and dE_ws are then in processing order, sigmas / rgbs / dL_d* stay in sample order. */
+int ncn_field_sort_windows(const float* xyzs, int64_t n, const int32_t* n_dev, float xyz_min, float xyz_extent,
+                           int32_t* order, void* stream);
+int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                  const float* table,
                   const uint32_t* levels, float xyz_min, float xyz_extent, const uint16_t* weights_packed,
                   int precision, int mode, float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
 /* Backward: accumulates (+=) into grad_table (n_entries,2) and writes per-block weight-gradient
@@ -176,7 +184,8 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * LDS-aggregating table scatter pass). */
 int ncn_field_bwd_blocks(int64_t n);
 int64_t ncn_field_bwd_dE_floats(int64_t n);
-int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
+int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                  const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision,
                   const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* grad_table,
                   float* slab, float* dE_ws,
@@ -187,10 +196,12 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * level_max), then the table scatter of the levels [level_lo, level_hi) into grad_table (+=).
  * max_blocks > 0 caps the scatter's workgroups (one per CU otherwise), leaving CUs to a concurrent
  * collective. */
-int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const uint16_t* weights_packed,
+int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                      const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
                       float* slab, float* dE_ws, float* level_max, void* stream);
-int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const uint32_t* levels, float xyz_min,
+int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                      const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
                       int max_blocks, float* grad_table, void* stream);
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream);

@@ -298,6 +298,64 @@ __device__ __forceinline__ void load_levels(LevelTable& Ls, const LevelTable& La
 }
 
 // ---------------------------------------------------------------------------------------------
+// Processing order of the training step's samples (ncn_field_sort_windows).  The marcher packs
+// samples ray by ray (the compositors need each ray's segment contiguous); the field does not care
+// about order, and the table scatter of its backward aggregates the gradients of samples that share
+// hash-grid corners — which, across the ~60 neighbouring rays of a patch, are samples at the same
+// place in space, far apart in ray order.  So every window of SORT_W consecutive samples is sorted
+// by the 30-bit Morton code of its normalised positions (10 bits per axis, the finest hash level's
+// resolution): `order[p]` is the sample processed at position p.  The forward evaluates samples in
+// that order (neighbouring lanes gather neighbouring table entries), the MLP backward writes the
+// encoding gradient in it, and the scatter's units (one window) see long runs of equal cells on
+// every level.  Keys carry the in-window index (unique keys, bitonic sort in LDS): the order is a
+// deterministic function of the positions.
+constexpr int SORT_W = 4096, SORT_THREADS = 1024;
+__device__ __forceinline__ uint32_t sort_spread10(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t sort_q10(float v, float mn, float inv) {
+    const float q = (v - mn) * inv * 1024.0f;
+    return (uint32_t)(int)fminf(fmaxf(q, 0.0f), 1023.0f);  // (NaN -> 0)
+}
+__global__ __launch_bounds__(SORT_THREADS) void sort_windows_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                                    const int32_t* __restrict__ n_dev, float mn,
+                                                                    float inv, int32_t* __restrict__ order) {
+    __shared__ unsigned long long k[SORT_W];
+    if (n_dev) n = min<int64_t>(n, *n_dev);
+    const int64_t base = (int64_t)blockIdx.x * SORT_W;
+    if (base >= n) return;  // (uniform)
+    const int cnt = (int)min<int64_t>(SORT_W, n - base);
+    for (int i = threadIdx.x; i < SORT_W; i += SORT_THREADS) {
+        unsigned long long key = ~0ull;  // empty slots sort last
+        if (i < cnt) {
+            const float* x = xyzs + 3 * (base + i);
+            const uint32_t m = sort_spread10(sort_q10(x[0], mn, inv)) | (sort_spread10(sort_q10(x[1], mn, inv)) << 1) |
+                               (sort_spread10(sort_q10(x[2], mn, inv)) << 2);
+            key = ((unsigned long long)m << 12) | (unsigned long long)i;
+        }
+        k[i] = key;
+    }
+    __syncthreads();
+    for (int size = 2; size <= SORT_W; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < SORT_W / 2; t += SORT_THREADS) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;  // pair (lo, hi), lo's bit `stride` clear
+                const bool up = (lo & size) == 0;
+                const unsigned long long a = k[lo], b = k[hi];
+                if ((a > b) == up) { k[lo] = b; k[hi] = a; }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < cnt; i += SORT_THREADS) order[base + i] = (int32_t)(base + (int64_t)(k[i] & 0xFFFull));
+}
+
+// ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
 template <typename T>
 __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
@@ -306,7 +364,8 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
                                                         float xyz_min, float xyz_extent,
                                                         const typename Mfma<T>::v8* __restrict__ wpacked, int mode,
                                                         float* __restrict__ sigmas, float* __restrict__ rgbs,
-                                                        typename Mfma<T>::v8* __restrict__ enc_cache) {
+                                                        typename Mfma<T>::v8* __restrict__ enc_cache,
+                                                        const int32_t* __restrict__ order) {
     typedef typename Mfma<T>::v8 v8;
     __shared__ v8 Fs[N_FWD32 * 64];
     __shared__ LevelTable L;
@@ -322,8 +381,9 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
         Frags<T> F;
         F.f32 = Fs + opaque_zero();  // fragments re-read from LDS every group (not hoisted)
         F.f16 = nullptr;
-        const int64_t s = grp * 16 + r;
-        const bool valid = s < n;
+        const int64_t pos = grp * 16 + r;  // processing position; s = the sample it evaluates
+        const bool valid = pos < n;
+        const int64_t s = valid && order ? (int64_t)order[pos] : pos;
         float x = 0.f, y = 0.f, z = 0.f;
         if (valid) {
             x = (xyzs[3 * s] - xyz_min) / xyz_extent;
@@ -401,12 +461,14 @@ struct BwdIn {
 template <typename T>
 __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, int lane,
                                          const typename Mfma<T>::v8* __restrict__ enc, const float* __restrict__ dirs,
-                                         const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb) {
-    const int64_t s = grp * 16 + (lane & 15);
-    const bool valid = s < n;
+                                         const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
+                                         const int32_t* __restrict__ order) {
+    const int64_t pos = grp * 16 + (lane & 15);  // processing position (enc_cache / dE order)
+    const bool valid = pos < n;
     in.e = enc[grp * 64 + lane];
     in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
     if (valid) {
+        const int64_t s = order ? (int64_t)order[pos] : pos;
         in.dx = dirs[3 * s]; in.dy = dirs[3 * s + 1]; in.dz = dirs[3 * s + 2];
         in.dsig = dL_dsig ? dL_dsig[s] : 0.f;
         if (dL_drgb) { in.dr0 = dL_drgb[3 * s]; in.dr1 = dL_drgb[3 * s + 1]; in.dr2 = dL_drgb[3 * s + 2]; }
@@ -585,7 +647,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const uint16_t* __restrict__ wpacked,
     const typename Mfma<T>::v8* __restrict__ enc_cache, const float* __restrict__ dL_dsig,
     const float* __restrict__ dL_drgb, float* __restrict__ dE_out, float* __restrict__ slab,
-    float* __restrict__ level_max) {
+    float* __restrict__ level_max, const int32_t* __restrict__ order) {
     typedef typename Mfma<T>::v4 v4;
     typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
@@ -609,12 +671,12 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t stride = (int64_t)gridDim.x * BWD_WAVES;
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
     BwdIn<T> nxt;
-    if (base + wid < n_groups) bwd_load<T>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+    if (base + wid < n_groups) bwd_load<T>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order);
     for (; base < n_groups; base += stride) {
         const int64_t grp = base + wid;
         const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
         const BwdIn<T> cur = nxt;
-        if (grp + stride < n_groups) bwd_load<T>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb);
+        if (grp + stride < n_groups) bwd_load<T>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order);
         if (grp < n_groups) {
             Frags<T> F;
             const int z = opaque_zero();
@@ -727,6 +789,12 @@ __device__ __forceinline__ long long sc_fix(float v, int k) {
 #ifndef SC_C_RUN
 #define SC_C_RUN 4  // samples per lane on the run levels (unit = 1024 * SC_C_RUN samples)
 #endif
+#ifndef SC_BATCH
+#define SC_BATCH 2  // corners per batch of set reads in sc_add (2: 232 us, 4: 238 us (spills), 8: 298 us)
+#endif
+#ifndef SC_C_DIR
+#define SC_C_DIR 4  // samples per lane on the direct levels (unit = one sort window)
+#endif
 
 struct ScRec {
     uint32_t k0, k1, pad0, pad1;  // cell: k0 = px | py << 16, k1 = pz
@@ -800,43 +868,82 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
         }
         return;
     }
-    // per corner: one ds_read_b128 of the set; a hit adds, a miss claims the first empty way with
-    // ds_cmpst (a uniform branch skips the claim step when no lane of the wave misses: the common
-    // case on coarse levels); a full set falls back to a global atomic.  Lanes with no
-    // contribution (v == 0: beyond the span / zero dE) take part with nothing to add.
-    const bool act = (v[0] != 0.f) | (v[1] != 0.f) | (v[2] != 0.f) | (v[3] != 0.f) | (v[4] != 0.f) | (v[5] != 0.f) |
-                     (v[6] != 0.f) | (v[7] != 0.f) | (v[8] != 0.f) | (v[9] != 0.f) | (v[10] != 0.f) |
-                     (v[11] != 0.f) | (v[12] != 0.f) | (v[13] != 0.f) | (v[14] != 0.f) | (v[15] != 0.f);
+    // Corners in batches of SC_BATCH: the batch's set reads (ds_read_b128) are issued together and
+    // waited for once, then the hits and claims are resolved, then the batch's fixed-point adds
+    // (ds_add_u64, no return) are issued back to back — a few LDS round trips per record instead of
+    // two per corner.  A miss claims the first empty way of its set with ds_cmpst (a uniform branch
+    // skips the claim step when no lane of the wave misses); a lost claim re-reads the set once;
+    // a full set falls back to a global atomic.  Zero corners (beyond the span / zero dE / a lane
+    // with no finished run) take part with nothing to add.
     uint32_t newmask = 0;
     int slot[8];
-#pragma unroll 2
-    for (int c = 0; c < 8; c++) {
-        const int p0 = SC_WAYS * sc_set(e[c], sh.sets);
-        const uint4 kk = *(const uint4*)&sh.keys[p0];
-        int sl = kk.x == e[c] ? p0 : kk.y == e[c] ? p0 + 1 : kk.z == e[c] ? p0 + 2 : kk.w == e[c] ? p0 + 3 : -1;
-        const int cl = (!act || sl >= 0) ? -1
-                     : kk.x == SC_EMPTY ? p0 : kk.y == SC_EMPTY ? p0 + 1 : kk.z == SC_EMPTY ? p0 + 2
-                     : kk.w == SC_EMPTY ? p0 + 3 : -1;
-        if (__ballot(cl >= 0)) {  // uniform
-            if (cl >= 0) {
-                const uint32_t got = atomicCAS(&sh.keys[cl], SC_EMPTY, e[c]);
-                if (got == SC_EMPTY) { sl = cl; newmask |= 1u << c; }
-                else if (got == e[c]) sl = cl;
+#pragma unroll
+    for (int c0 = 0; c0 < 8; c0 += SC_BATCH) {
+        uint4 kk[SC_BATCH];
+        int p0[SC_BATCH];
+#pragma unroll
+        for (int b = 0; b < SC_BATCH; b++) {
+            p0[b] = SC_WAYS * sc_set(e[c0 + b], sh.sets);
+            kk[b] = *(const uint4*)&sh.keys[p0[b]];
+        }
+        int sl[SC_BATCH];
+        bool vc[SC_BATCH], miss = false;
+#pragma unroll
+        for (int b = 0; b < SC_BATCH; b++) {
+            const uint32_t k = e[c0 + b];
+            vc[b] = (v[2 * (c0 + b)] != 0.f) | (v[2 * (c0 + b) + 1] != 0.f);
+            sl[b] = kk[b].x == k ? p0[b] : kk[b].y == k ? p0[b] + 1 : kk[b].z == k ? p0[b] + 2
+                  : kk[b].w == k ? p0[b] + 3 : -1;
+            miss |= vc[b] && sl[b] < 0;
+        }
+        if (__ballot(miss)) {  // uniform
+#pragma unroll
+            for (int b = 0; b < SC_BATCH; b++) {
+                if (vc[b] && sl[b] < 0) {
+                    const uint32_t k = e[c0 + b];
+#pragma unroll
+                    for (int attempt = 0; attempt < 2 && sl[b] < 0; attempt++) {
+                        if (attempt) {  // lost a claim: look again
+                            asm volatile("" ::: "memory");
+                            kk[b] = *(const uint4*)&sh.keys[p0[b]];
+                        }
+                        sl[b] = kk[b].x == k ? p0[b] : kk[b].y == k ? p0[b] + 1 : kk[b].z == k ? p0[b] + 2
+                              : kk[b].w == k ? p0[b] + 3 : -1;
+                        if (sl[b] >= 0) break;
+                        const int cl = kk[b].x == SC_EMPTY ? p0[b] : kk[b].y == SC_EMPTY ? p0[b] + 1
+                                     : kk[b].z == SC_EMPTY ? p0[b] + 2 : kk[b].w == SC_EMPTY ? p0[b] + 3 : -1;
+                        if (cl < 0) break;  // set full
+                        const uint32_t got = atomicCAS(&sh.keys[cl], SC_EMPTY, k);
+                        if (got == SC_EMPTY) { sl[b] = cl; newmask |= 1u << (c0 + b); }
+                        else if (got == k) sl[b] = cl;
+                    }
+                }
             }
         }
-        slot[c] = act ? sl : SC_TS_NONE;
-        if (act && sl >= 0) {
+#pragma unroll
+        for (int b = 0; b < SC_BATCH; b++) {
+            const int c = c0 + b;
+            slot[c] = sl[b];
+            if (vc[b] && sl[b] >= 0) {
 #ifndef NCN_DIAG_SC_NO_LDSADD
-            atomicAdd((unsigned long long*)&sh.valx[sl], (unsigned long long)sc_fix(v[2 * c], L.k));
-            atomicAdd((unsigned long long*)&sh.valy[sl], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
+                atomicAdd((unsigned long long*)&sh.valx[sl[b]], (unsigned long long)sc_fix(v[2 * c], L.k));
+                atomicAdd((unsigned long long*)&sh.valy[sl[b]], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
 #endif
+            }
         }
-        if (__ballot(act && sl < 0)) {  // uniform: some lane's set is full of other entries
-            if (act && sl < 0) {
+        bool full = false;
+#pragma unroll
+        for (int b = 0; b < SC_BATCH; b++) full |= vc[b] && sl[b] < 0;
+        if (__ballot(full)) {  // uniform: some lane's set is full of other entries
+#pragma unroll
+            for (int b = 0; b < SC_BATCH; b++) {
+                const int c = c0 + b;
+                if (vc[b] && sl[b] < 0) {
 #ifndef NCN_DIAG_SC_NO_FALLBACK
-                atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
-                atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
+                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
+                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
 #endif
+                }
             }
         }
     }
@@ -923,10 +1030,40 @@ struct ScChunk {
 // cycles per touched cache line).  A partial last chunk falls back to per-sample loads.
 template <int C>
 __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
-                                               const float2* __restrict__ dEl, const ScNorm& nrm) {
+                                               const float2* __restrict__ dEl, const ScNorm& nrm,
+                                               const int32_t* __restrict__ order) {
     static_assert(C == 2 || C == 4, "chunk of 2 or 4 samples");
     float xs[3 * C];
-    if (sb + C <= s1) {
+    if (order) {  // positions sb.. in processing order: dE contiguous, positions gathered
+        int64_t src[C];
+#pragma unroll
+        for (int i = 0; i < C; i++) src[i] = sb + i < s1 ? (int64_t)order[sb + i] : -1;
+        if (sb + C <= s1) {
+            if constexpr (C == 4) {
+                const float4* pg = (const float4*)(dEl + sb);
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const float4 v = pg[q];
+                    ch.g[2 * q] = make_float2(v.x, v.y);
+                    ch.g[2 * q + 1] = make_float2(v.z, v.w);
+                }
+            } else {
+                const float4 v = *(const float4*)(dEl + sb);
+                ch.g[0] = make_float2(v.x, v.y);
+                ch.g[1] = make_float2(v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < C; i++) ch.g[i] = src[i] >= 0 ? dEl[sb + i] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            const int64_t sc = src[i] >= 0 ? src[i] : 0;
+            xs[3 * i] = xyzs[3 * sc];
+            xs[3 * i + 1] = xyzs[3 * sc + 1];
+            xs[3 * i + 2] = xyzs[3 * sc + 2];
+        }
+    } else if (sb + C <= s1) {
         if constexpr (C == 4) {
             const float4* px = (const float4*)(xyzs + 3 * sb);
 #pragma unroll
@@ -1004,18 +1141,37 @@ __device__ __forceinline__ void sc_phase_a(ScShared& sh, int wid, int lane, ScCh
     }
 }
 
-// Direct form (fine levels): every sample's 8 corners go to the table as they are.
+// Direct form (fine levels, no record staging): the lane's consecutive samples in the same cell are
+// summed in registers (a run), and a run's 8 corners go to the table when the cell changes (sc_add
+// is called by the whole wave; lanes without a finished run take part with zeros).
 template <int C>
 __device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
                                           float* __restrict__ grad) {
+    float v[16];
 #pragma unroll
-    for (int i = 0; i < C; i++) {
-        const LevelPos p = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
-        float v[16];
+    for (int j = 0; j < 16; j++) v[j] = 0.f;
+    LevelPos p = level_pos(L.scale, ch.x[0], ch.y[0], ch.z[0]);
+    sc_corner_sums(p, ch.g[0], v);
 #pragma unroll
-        for (int j = 0; j < 16; j++) v[j] = 0.f;
-        sc_corner_sums(p, ch.g[i], v);
-        sc_add(sh, lane, p.px, p.py, p.pz, v, L, grad);
+    for (int i = 1; i <= C; i++) {
+        LevelPos q = p;
+        bool emit = true;
+        if (i < C) {
+            q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
+            emit = q.px != p.px || q.py != p.py || q.pz != p.pz;
+        }
+        if (__ballot(emit)) {  // uniform
+            float ve[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) ve[j] = emit ? v[j] : 0.f;
+            sc_add(sh, lane, p.px, p.py, p.pz, ve, L, grad);
+        }
+        if (i < C) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = emit ? 0.f : v[j];
+            sc_corner_sums(q, ch.g[i], v);
+        }
+        p = q;
     }
 }
 
@@ -1032,14 +1188,14 @@ __device__ unsigned long long ncn_sc_times[256][8];  // per workgroup, wave 0: c
 template <int C, bool RUNS>
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const float2* __restrict__ dEl,
-                                        const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad) {
+                                        const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
+                                        const int32_t* __restrict__ order) {
     SC_TNOW(t0);
-#ifdef NCN_DIAG_SC_LEVELS_MASK
-    if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
-#endif
-    if (m == 0.f) return;  // uniform: nothing to add on this level
     ScChunk<C> ch;
-    sc_load_chunk<C>(ch, s0 + (int64_t)threadIdx.x * C, s1, xyzs, dEl, nrm);
+    // chunk of lane t of wave w: t * SC_WAVES + w — the 64 lanes of one wave-instruction hold chunks
+    // SC_WAVES * C positions apart, so in the Morton processing order (where neighbouring positions
+    // share cells) they rarely address the same LDS slot at once (same-address LDS atomics serialise)
+    sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, nrm, order);
     ScLevel L;
     L.scale = Lt.scale[l];
     L.res = Lt.res[l];
@@ -1061,24 +1217,24 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     SC_TNOW(t2);
     lds_barrier();
     SC_TNOW(t3);
-    // flush: the claimed slots, two lanes per slot (x and y of one entry are adjacent floats)
+    // flush: the claimed slots, two lanes per slot (x and y of one entry are adjacent floats, one
+    // 8-B piece of one 64-B granule per lane pair); each lane resets the half it read (the even
+    // lane the key and x, the odd one y), so one barrier closes the unit
     const int nf = *sh.fill;
     for (int i = threadIdx.x; i < 2 * nf; i += SC_THREADS) {
         const int slot = sh.used[i >> 1];
         const uint32_t key = sh.keys[slot];
-        const long long q = (i & 1) ? sh.valy[slot] : sh.valx[slot];
+        long long* pv = (i & 1) ? &sh.valy[slot] : &sh.valx[slot];
+        const long long q = *pv;
+        *pv = 0;
 #ifndef NCN_DIAG_SC_NO_FLUSH
         if (q != 0) atomicAdd(grad + 2 * (size_t)(L.off + key) + (i & 1), (float)ldexp((double)q, -L.k));
 #endif
+        if (!(i & 1)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the odd lane has read the key: same wave)
+            sh.keys[slot] = SC_EMPTY;
+        }
     }
-    lds_barrier();  // every lane has read its slots
-    for (int i = threadIdx.x; i < nf; i += SC_THREADS) {
-        const int slot = sh.used[i];
-        sh.keys[slot] = SC_EMPTY;
-        sh.valx[slot] = 0;
-        sh.valy[slot] = 0;
-    }
-    if (threadIdx.x == 0) *sh.fill = 0;
     lds_barrier();
     SC_TNOW(t4);
     SC_TADD(0, t0, t1);
@@ -1093,10 +1249,11 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    const float2* __restrict__ dE,
                                                                    float* __restrict__ grad,
                                                                    const float* __restrict__ level_max, int lm_rows,
-                                                                   int level_lo, int level_hi) {
+                                                                   int level_lo, int level_hi,
+                                                                   const int32_t* __restrict__ order) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
     __shared__ float wmax[SC_WAVES];
-    __shared__ int fill;
+    __shared__ int fill[2];  // claimed-slot counts, alternating per unit (reset one unit ahead)
     // per-level max |dE| over the MLP pass's workgroup rows (the fixed-point scale of each level);
     // visible to every thread at the first layout barrier
     __shared__ float lmax_s[16];
@@ -1114,7 +1271,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
     // units, level-major over the levels [level_lo, level_hi): run levels in spans of
     // 1024 * SC_C_RUN samples, direct levels in spans of 2048 (2 per lane)
-    constexpr int C_RUN = SC_C_RUN, C_DIR = 2;
+    constexpr int C_RUN = SC_C_RUN, C_DIR = SC_C_DIR;
     const int64_t ur = (n + SC_THREADS * C_RUN - 1) / (SC_THREADS * C_RUN);
     const int64_t ud = (n + SC_THREADS * C_DIR - 1) / (SC_THREADS * C_DIR);
     const int run_lo = level_lo, run_hi = min(level_hi, SC_RUN_LEVELS);
@@ -1122,32 +1279,51 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     const int64_t n_run = run_hi > run_lo ? (int64_t)(run_hi - run_lo) * ur : 0;
     const int64_t n_units = n_run + (dir_hi > dir_lo ? (int64_t)(dir_hi - dir_lo) * ud : 0);
     // (grid-stride: a workgroup takes its run units first, then its direct ones: one layout switch)
-    int layout = -1;
+    int layout = -1, par = 0;
     ScShared sh;
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
         const int run = u < n_run;
         if (run != layout) {  // (re)initialise the table of the new layout
             lds_barrier();
-            sh = sc_layout(arena, wmax, &fill, run);
+            sh = sc_layout(arena, wmax, fill, run);
             for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) {
                 sh.keys[i] = SC_EMPTY;
                 sh.valx[i] = 0;
                 sh.valy[i] = 0;
             }
-            if (threadIdx.x == 0) fill = 0;
+            if (threadIdx.x == 0) fill[0] = fill[1] = 0;
             lds_barrier();
             layout = run;
+            par = 0;
         }
+        int l;
+        int64_t s0, s1;
         if (run) {
-            const int li = (int)(u / ur), l = run_lo + li;
-            const int64_t s0 = (u - li * ur) * (SC_THREADS * C_RUN), s1 = min(n, s0 + SC_THREADS * C_RUN);
-            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, lmax_s[l], grad);
+            const int li = (int)(u / ur);
+            l = run_lo + li;
+            s0 = (u - li * ur) * (SC_THREADS * C_RUN);
+            s1 = min(n, s0 + SC_THREADS * C_RUN);
         } else {
             const int64_t v = u - n_run;
-            const int li = (int)(v / ud), l = dir_lo + li;
-            const int64_t s0 = (v - li * ud) * (SC_THREADS * C_DIR), s1 = min(n, s0 + SC_THREADS * C_DIR);
-            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, lmax_s[l], grad);
+            const int li = (int)(v / ud);
+            l = dir_lo + li;
+            s0 = (v - li * ud) * (SC_THREADS * C_DIR);
+            s1 = min(n, s0 + SC_THREADS * C_DIR);
         }
+        float m = lmax_s[l];
+#ifdef NCN_DIAG_SC_LEVELS_MASK
+        if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
+#endif
+        if (m == 0.f) continue;  // uniform: nothing to add on this level (no barrier, parity kept)
+        // the unit claims into fill[par]; fill[par ^ 1] (read by every lane before the previous
+        // unit's closing barrier) is reset here for the next unit
+        sh.fill = fill + par;
+        if (threadIdx.x == 0) fill[par ^ 1] = 0;
+        par ^= 1;
+        if (run)
+            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, m, grad, order);
+        else
+            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, m, grad, order);
     }
 }
 
@@ -1191,7 +1367,18 @@ int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int 
 }
 
 // `levels` is a HOST array of 16 x {scale f32 bits, resolution, params, offset}.
-int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const float* table,
+int ncn_field_sort_windows(const float* xyzs, int64_t n, const int32_t* n_dev, float xyz_min, float xyz_extent,
+                           int32_t* order, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(xyz_extent > 0.f, hipErrorInvalidValue, "ncn_field_sort_windows: xyz_extent must be positive");
+    hipLaunchKernelGGL(sort_windows_kernel, dim3((unsigned)cdiv(n, SORT_W)), dim3(SORT_THREADS), 0, (hipStream_t)stream,
+                       xyzs, n, n_dev, xyz_min, 1.0f / xyz_extent, order);
+    NCN_LAUNCH_CHECK("ncn_field_sort_windows");
+    return 0;
+}
+
+int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                  const float* table,
                   const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision, int mode,
                   float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream) {
@@ -1206,11 +1393,12 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
         hipLaunchKernelGGL(field_fwd_kernel<_Float16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
                            n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,
                            (const Mfma<_Float16>::v8*)weights_packed, mode, sigmas, rgbs,
-                           (Mfma<_Float16>::v8*)enc_cache);
+                           (Mfma<_Float16>::v8*)enc_cache, order);
     else
         hipLaunchKernelGGL(field_fwd_kernel<__bf16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
                            n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,
-                           (const Mfma<__bf16>::v8*)weights_packed, mode, sigmas, rgbs, (Mfma<__bf16>::v8*)enc_cache);
+                           (const Mfma<__bf16>::v8*)weights_packed, mode, sigmas, rgbs, (Mfma<__bf16>::v8*)enc_cache,
+                           order);
     NCN_LAUNCH_CHECK("ncn_field_fwd");
     return 0;
 }
@@ -1223,7 +1411,8 @@ int ncn_field_bwd_blocks(int64_t n) {
 
 int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(int64_t)3) : 0; }
 
-int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const uint16_t* weights_packed,
+int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                      const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
                       float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
@@ -1235,16 +1424,17 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
     if (precision == NCN_PREC_F16)
         hipLaunchKernelGGL(field_bwd_kernel<_Float16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
                            (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<_Float16>::v8*)enc_cache,
-                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max);
+                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max, order);
     else
         hipLaunchKernelGGL(field_bwd_kernel<__bf16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
                            (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<__bf16>::v8*)enc_cache,
-                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max);
+                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max, order);
     NCN_LAUNCH_CHECK("ncn_field_bwd_mlp");
     return 0;
 }
 
-int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const uint32_t* levels, float xyz_min,
+int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                      const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
                       int max_blocks, float* grad_table, void* stream) {
     if (n <= 0 || level_hi <= level_lo) return 0;
@@ -1256,21 +1446,22 @@ int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const 
     if (max_blocks > 0) grid = std::min(grid, max_blocks);
     hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
                        xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
-                       level_lo, level_hi);
+                       level_lo, level_hi, order);
     NCN_LAUNCH_CHECK("ncn_field_scatter");
     return 0;
 }
 
-int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const uint32_t* levels,
+int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                  const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision,
                   const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* grad_table,
                   float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
-    const int e = ncn_field_bwd_mlp(dirs, n, n_dev, weights_packed, precision, enc_cache, dL_dsigmas, dL_drgbs, slab,
-                                    dE_ws, level_max, stream);
+    const int e = ncn_field_bwd_mlp(dirs, n, n_dev, order, weights_packed, precision, enc_cache, dL_dsigmas, dL_drgbs,
+                                    slab, dE_ws, level_max, stream);
     if (e) return e;
-    return ncn_field_scatter(xyzs, n, n_dev, levels, xyz_min, xyz_extent, dE_ws, level_max, 0, 16, 0, grad_table,
-                             stream);
+    return ncn_field_scatter(xyzs, n, n_dev, order, levels, xyz_min, xyz_extent, dE_ws, level_max, 0, 16, 0,
+                             grad_table, stream);
 }
 
 

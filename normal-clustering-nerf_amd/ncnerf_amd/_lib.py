@@ -40,12 +40,13 @@ SIGNATURES = {
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, I32, P],
-    "ncn_field_fwd": [P, P, I64, P, P, P, F32, F32, P, I32, I32, P, P, P, P],
+    "ncn_field_sort_windows": [P, I64, P, F32, F32, P, P],
+    "ncn_field_fwd": [P, P, I64, P, P, P, P, F32, F32, P, I32, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
     "ncn_field_bwd_dE_floats": [I64],
-    "ncn_field_bwd": [P, P, I64, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P],
-    "ncn_field_bwd_mlp": [P, I64, P, P, I32, P, P, P, P, P, P, P],
-    "ncn_field_scatter": [P, I64, P, P, F32, F32, P, P, I32, I32, I32, P, P],
+    "ncn_field_bwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd_mlp": [P, I64, P, P, P, I32, P, P, P, P, P, P, P],
+    "ncn_field_scatter": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],

@@ -17,7 +17,7 @@ def declared_symbols():
 def test_header_declares_the_hot_path():
     syms = declared_symbols()
     for s in ("ncn_ray_aabb_intersect", "ncn_march_train_walk", "ncn_march_train_scan", "ncn_march_train_pack",
-              "ncn_composite_train_fw", "ncn_composite_train_bw", "ncn_field_fwd", "ncn_field_bwd",
+              "ncn_composite_train_fw", "ncn_composite_train_bw", "ncn_field_fwd", "ncn_field_bwd", "ncn_field_sort_windows",
               "ncn_normals_fwd", "ncn_cluster_loss", "ncn_adam", "ncn_last_error"):
         assert s in syms
 

@@ -127,3 +127,51 @@ def test_field_backward_accumulates(dev):
     out["rgbs"].sum().backward()
     assert torch.allclose(g2, 2 * m.flat_grad(), rtol=1e-4, atol=1e-7)
     assert m.xyz_encoder.params.grad.data_ptr() == m.flat_grad().data_ptr()
+
+
+@pytest.mark.parametrize("n", [8192, 13000])
+def test_field_morton_window_order(dev, n):
+    """ncn_field_sort_windows: `order` is a permutation of every 4096-sample window sorted by the
+    Morton code of the positions (checked on the host), and the field evaluated in that processing
+    order gives the same outputs (bitwise: each sample's arithmetic does not depend on its position)
+    and the same gradients (summation order only) as in sample order."""
+    from ncnerf_amd import _lib
+    from ncnerf_amd._lib import F32, I64, ptr, stream
+    P, _ = field_ref.init_params(seed=5, table_init=0.5)
+    m = _model_from_oracle(P, dev)
+    x, d = _inputs(n, 3)
+    x, d = x.to(dev), d.to(dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    assert _lib.lib().ncn_field_sort_windows(ptr(x), I64(n), ptr(None), F32(m._xyz_min), F32(m._xyz_extent),
+                                             ptr(order), stream()) == 0
+    o = order.cpu().numpy().astype(np.int64)
+    xc = x.cpu().numpy()
+    q = np.clip(((xc - m._xyz_min) / m._xyz_extent * 1024).astype(np.int64), 0, 1023)
+
+    def spread(v):
+        r = np.zeros_like(v)
+        for b in range(10):
+            r |= ((v >> b) & 1) << (3 * b)
+        return r
+    code = spread(q[:, 0]) | (spread(q[:, 1]) << 1) | (spread(q[:, 2]) << 2)
+    for w0 in range(0, n, 4096):
+        win = o[w0:w0 + 4096]
+        assert np.array_equal(np.sort(win), np.arange(w0, min(n, w0 + 4096)))
+        key = code[win] * 4096 + (win - w0)
+        assert np.all(np.diff(key) > 0)
+
+    def run(sort):
+        m.sort_samples = sort
+        m.flat_grad().zero_()
+        xs, ds = x.clone(), d.clone()
+        out = m(xs, ds)
+        (out["sigmas"] * 0.01 + (out["rgbs"] * torch.linspace(-1, 1, 3, device=dev)).sum(1)).sum().backward()
+        return out["sigmas"].detach().clone(), out["rgbs"].detach().clone(), m.flat_grad().clone()
+
+    s0, r0, g0 = run(False)
+    s1, r1, g1 = run(True)
+    m.sort_samples = False
+    assert torch.equal(s0, s1) and torch.equal(r0, r1)
+    nt = m._n_table
+    for a, b in ((g0[:nt], g1[:nt]), (g0[nt:], g1[nt:])):
+        assert float((a - b).norm() / a.norm()) < 1e-5

@@ -1,0 +1,126 @@
+"""Diagnostic: time ncn_field_scatter alone (and diagnostic builds of it) on realistic marched
+samples: the bench batch is marched, the field run forward and the MLP backward pass once, then
+the scatter is timed per library (main + tools/_build/field_*.so).  Not part of the product."""
+import ctypes
+import glob
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from ncnerf_amd import _lib  # noqa: E402
+from ncnerf_amd._lib import F32, I32, I64, ptr, stream  # noqa: E402
+from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers  # noqa: E402
+from ncnerf_amd.rendering import march_train_fused  # noqa: E402
+from ncnerf_amd.synthetic import SyntheticScene  # noqa: E402
+
+dev = torch.device("cuda:0")
+scene = SyntheticScene()
+model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+b = scene.torch_batch(8192, seed=1, device=dev)
+o, d = b["rays_o"].contiguous(), b["rays_d"].contiguous()
+mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(8192, device=dev))
+n = int(mk["counter"][0].item())
+xyzs, dirs = mk["xyzs"][:n].contiguous(), mk["dirs"][:n].contiguous()
+print("samples", n, flush=True)
+main = _lib.lib()
+packed = model._pack_weights()
+enc = torch.empty(((n + 15) // 16) * 64 * 8, dtype=torch.float16, device=dev)
+sig = torch.empty(n, device=dev)
+rgb = torch.empty(n, 3, device=dev)
+table = model.flat_params()[: model._n_table]
+gen = torch.Generator(device="cuda").manual_seed(0)
+dsig = torch.randn(n, device=dev, generator=gen) * 1e-3
+drgb = torch.randn(n, 3, device=dev, generator=gen) * 1e-3
+nb = main.ncn_field_bwd_blocks(I64(n))
+slab = torch.empty(nb * 19712, device=dev)
+dE = torch.empty(int(main.ncn_field_bwd_dE_floats(I64(n))), device=dev)
+lmax = torch.empty(16 * 256, device=dev)
+gtab = torch.zeros_like(table)
+order = torch.empty(n, dtype=torch.int32, device=dev)
+ORDER = [None]
+
+
+def ev_time(f, reps=20):
+    f()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, e in evs:
+        torch.cuda._sleep(100000)
+        a.record()
+        assert f() == 0
+        e.record()
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(e) for a, e in evs]) * 1e3)
+
+
+def prepare(sorted_):
+    """fwd + MLP backward in the chosen processing order (dE in that order)."""
+    ORDER[0] = order if sorted_ else None
+    o = ORDER[0]
+    srt = lambda: main.ncn_field_sort_windows(ptr(xyzs), I64(n), ptr(None), F32(model._xyz_min),  # noqa: E731
+                                              F32(model._xyz_extent), ptr(order), stream())
+    if sorted_:
+        print(f"  sort_windows {ev_time(srt):7.1f} us", flush=True)
+    fwd = lambda: main.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(o), ptr(table),  # noqa: E731
+                                     model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed),
+                                     I32(0), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
+    mlp = lambda: main.ncn_field_bwd_mlp(ptr(dirs), I64(n), ptr(None), ptr(o), ptr(packed), I32(0), ptr(enc),  # noqa: E731
+                                         ptr(dsig), ptr(drgb), ptr(slab), ptr(dE), ptr(lmax), stream())
+    print(f"  field_fwd {ev_time(fwd):7.1f} us   bwd_mlp {ev_time(mlp):7.1f} us", flush=True)
+    return sig.clone(), rgb.clone()
+
+
+def scat(lib, lo=0, hi=16):
+    return lib.ncn_field_scatter(ptr(xyzs), I64(n), ptr(None), ptr(ORDER[0]), model._levels_ptr, F32(model._xyz_min),
+                                 F32(model._xyz_extent), ptr(dE), ptr(lmax), I32(lo), I32(hi), I32(0), ptr(gtab),
+                                 stream())
+
+
+def timeit(lib, reps=20, **kw):
+    return ev_time(lambda: scat(lib, **kw), reps)
+
+
+libs = [("main", main)]
+for so in sorted(glob.glob(os.path.join(ROOT, "tools", "_build", "field_*.so"))):
+    L = ctypes.CDLL(so)
+    L.ncn_field_scatter.argtypes = _lib.SIGNATURES["ncn_field_scatter"]
+    L.ncn_field_scatter.restype = ctypes.c_int
+    libs.append((os.path.basename(so)[6:-3], L))
+gref = None
+for sorted_ in (False, True):
+    print("order:", "Morton windows" if sorted_ else "ray (identity)", flush=True)
+    so = prepare(sorted_)
+    if sorted_:
+        print(f"  fwd outputs vs identity order: max|dsigma| {float((so[0] - s0[0]).abs().max()):.3e} "
+              f"max|drgb| {float((so[1] - s0[1]).abs().max()):.3e}")
+    else:
+        s0 = so
+    for name, L in libs:
+        gtab.zero_()
+        assert scat(L) == 0
+        torch.cuda.synchronize()
+        g1 = gtab.clone()
+        msg = ""
+        if gref is None:
+            gref = g1
+        else:
+            rel = ((g1 - gref).norm() / gref.norm()).item()
+            msg = f"rel-L2 vs first {rel:.2e}"
+        t = timeit(L)
+        coarse = timeit(L, lo=0, hi=10)
+        fine = timeit(L, lo=10, hi=16)
+        print(f"  {name:24s} all {t:7.1f} us  levels0-9 {coarse:7.1f}  levels10-15 {fine:7.1f}  {msg}", flush=True)
+        if hasattr(L, "ncn_diag_sc_times"):
+            buf = (ctypes.c_ulonglong * (256 * 8))()
+            L.ncn_diag_sc_times(buf, 1)
+            assert scat(L) == 0
+            torch.cuda.synchronize()
+            L.ncn_diag_sc_times(buf, 0)
+            a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8).astype(np.float64)
+            names = ["load", "work", "barrier", "flush"]
+            print("     cycles per WG (wave 0, mean), run | direct:",
+                  "  ".join(f"{nm} {a[:, 2 * i].mean():.0f}|{a[:, 2 * i + 1].mean():.0f}" for i, nm in enumerate(names)))
