@@ -86,41 +86,77 @@ def pmc_traffic():
     return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def composite_fw_roofline(model, batch, dev, reps=50):
-    """Live HIP-event measurement of the roofline kernel (composite_train_fw) on one bench batch:
-    the batch is marched and the field evaluated once, then `reps` launches of the kernel are queued
-    back to back behind a GPU spin (so host launch latency is hidden) between two events on the
-    launch stream.  Returns (algorithmic bytes per launch, average launch duration in us)."""
+def composite_fw_roofline(model, batches, dev, reps=48, n_sets=24):
+    """Live HIP-event measurement of the roofline kernel, the training step's compositor
+    (ncn_composite_train_fw_bg over the fused marcher's rays_a, long rays first).  `n_sets` input
+    sets (the bench batches marched with different jitter and run through the field as in the step,
+    ~16.5 MB each: n_sets x that > the 256 MiB Infinity Cache) are prepared; then
+      hbm:     `reps` back-to-back launches cycling through the sets behind a GPU spin: every launch
+               reads inputs the launches between evicted from the caches (HBM-bound), the average
+               launch duration -> `achieved` / `frac`;
+      warm:    `reps` back-to-back launches on ONE set (its inputs cache-resident);
+      in_step: one launch right behind the field forward that wrote its inputs, bracketed by its own
+               event pair (includes the launch ramp and the event overhead), mean over the batches.
+    Returns (algorithmic bytes per launch (mean over the sets), {hbm, warm, in_step} us)."""
     from ncnerf_amd import _lib
     from ncnerf_amd._lib import F32, I32, I64, ptr, stream
     from ncnerf_amd.rendering import march_train_fused
+    fn = _lib.lib().ncn_composite_train_fw_bg
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    sets, t_in = [], []
     with torch.no_grad():
-        o, d = batch["rays_o"].contiguous(), batch["rays_d"].contiguous()
-        R = o.shape[0]
-        # the training step's marcher (its rays_a row order: long rays first)
-        mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(R, device=dev))
-        S = int(mk["counter"][0].item())
-        rays_a, xyzs, dirs, deltas, ts = mk["rays_a"], mk["xyzs"][:S], mk["dirs"][:S], mk["deltas"][:S], mk["ts"][:S]
-        out = model(xyzs, dirs)
-        sig, rgb = out["sigmas"].contiguous(), out["rgbs"].contiguous()
-        S = sig.shape[0]
-        res = [torch.empty(R, dtype=torch.int64, device=dev), torch.empty(R, device=dev), torch.empty(R, device=dev),
-               torch.empty(R, 3, device=dev), torch.empty(S, device=dev)]
-        fn = _lib.lib().ncn_composite_train_fw
-        args = [ptr(sig), ptr(rgb), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S), I32(3), F32(1e-4)] + \
-               [ptr(t) for t in res] + [stream()]
-        assert fn(*args) == 0
+        for j in range(n_sets):
+            batch = batches[j % len(batches)]
+            o, d = batch["rays_o"].contiguous(), batch["rays_d"].contiguous()
+            R = o.shape[0]
+            mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(R, device=dev))
+            S = int(mk["counter"][0].item())
+            out = model(mk["xyzs"], mk["dirs"], n_samples_dev=mk["counter"])
+            res = [torch.empty(R, dtype=torch.int64, device=dev), torch.empty(R, device=dev), torch.empty(R, device=dev),
+                   torch.empty(R, 3, device=dev), torch.empty(S, device=dev), torch.empty(R, 3, device=dev)]
+            if j < len(batches):  # in-step: right behind the field forward that produced the inputs
+                args = [ptr(out["sigmas"]), ptr(out["rgbs"]), ptr(mk["deltas"]), ptr(mk["ts"]), ptr(mk["rays_a"]),
+                        I64(R), I64(S), I32(3), F32(1e-4)] + [ptr(t) for t in res[:5]] + [F32(1.0), ptr(res[5]),
+                                                                                          stream()]
+                for rep in range(2):  # (rep 0 warms up)
+                    if rep:
+                        out = model(mk["xyzs"], mk["dirs"], n_samples_dev=mk["counter"])
+                    a, b = ev(), ev()
+                    a.record()
+                    assert fn(*args) == 0
+                    b.record()
+                    torch.cuda.synchronize()
+                t_in.append(a.elapsed_time(b) * 1e3)
+            # compact copies (S rows) so the sets are disjoint, cache-sized data
+            keep = {"sig": out["sigmas"][:S].clone(), "rgb": out["rgbs"][:S].clone(), "dl": mk["deltas"][:S].clone(),
+                    "ts": mk["ts"][:S].clone(), "ra": mk["rays_a"].clone(), "res": res}
+            keep["args"] = [ptr(keep["sig"]), ptr(keep["rgb"]), ptr(keep["dl"]), ptr(keep["ts"]), ptr(keep["ra"]),
+                            I64(R), I64(S), I32(3), F32(1e-4)] + [ptr(t) for t in res[:5]] + [F32(1.0),
+                                                                                          ptr(res[5]), stream()]
+            sets.append(keep)
+            del out, mk
+        for k in sets:  # (first-call costs, and the algorithmic bytes of each set)
+            assert fn(*k["args"]) == 0
         torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(2_000_000)  # ~1 ms: every launch below is queued before the first runs
-        a.record()
-        for _ in range(reps):
-            fn(*args)
-        b.record()
-        torch.cuda.synchronize()
-        us = a.elapsed_time(b) * 1e3 / reps
-        S_vr = float(res[0].sum().item())
-    return 24.0 * S_vr + 4.0 * S + 52.0 * R, us
+        nbytes = [24.0 * float(k["res"][0].sum().item()) + 4.0 * k["sig"].shape[0] + 52.0 * k["ra"].shape[0]
+                  for k in sets]
+
+        def b2b(arg_list):
+            torch.cuda.synchronize()
+            a, b = ev(), ev()
+            torch.cuda._sleep(2_000_000)  # ~1 ms: every launch below is queued before the first runs
+            a.record()
+            for i in range(reps):
+                fn(*arg_list[i % len(arg_list)])
+            b.record()
+            torch.cuda.synchronize()
+            return a.elapsed_time(b) * 1e3 / reps
+
+        t_hbm = b2b([k["args"] for k in sets])
+        t_warm = b2b([sets[0]["args"]])
+    mean_bytes = float(np.mean([nbytes[i % len(sets)] for i in range(reps)]))
+    return mean_bytes, {"hbm": t_hbm, "warm": t_warm, "in_step": float(np.mean(t_in)),
+                        "warm_bytes": nbytes[0]}
 
 
 def cpu_baseline(n_rays=2048, steps=20, warmup=3):
@@ -210,6 +246,10 @@ def main():
             model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
             model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
         trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph)
+        # marched / composited sample counts accumulated on the device by the step itself
+        # (ncn_count_samples: no per-step copies in the timed region)
+        count_acc = torch.zeros(2, dtype=torch.float64, device=dev)
+        trainer.render_kwargs["count_acc"] = count_acc
         n_batches = 8
         batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
         step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
@@ -220,18 +260,18 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        counts = []  # per-step device counts (copied: graph outputs are overwritten by the next replay)
+        count_acc.zero_()
         if args.no_graph and kernel_table:
             _lib.TIMING = {n: [] for n in TIMED}
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(steps):
-            results, _ = trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k)
-            counts.append((results["rm_samples"].clone(), results["vr_samples"].clone()))
+            trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
+        tot = count_acc.clone()
         if not args.no_graph and kernel_table:
             # Per-kernel durations (the `kernels` table): a graph replay has no host launch to bracket,
             # so the captured body is run eagerly for `steps` more steps with HIP events on the launch
@@ -245,10 +285,7 @@ def main():
             torch.cuda.synchronize()
         timing = _lib.TIMING or {}
         _lib.TIMING = None
-        rm = sum(torch.as_tensor(a).double().sum() for a, _ in counts)
-        vr = sum(torch.as_tensor(b).double().sum() for _, b in counts)
         elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-        tot = torch.stack([rm, vr]).reshape(2)
         rank_ms = [round(1e3 * (t1 - t0) / steps, 3)]
         if world > 1:
             gathered = [torch.zeros_like(elapsed) for _ in range(world)]
@@ -266,7 +303,8 @@ def main():
         if evs:
             ms = [a.elapsed_time(b) for a, b in evs]
             kern[name] = {"avg_us": round(1e3 * float(np.mean(ms)), 2), "launches": len(ms)}
-    cf_bytes_per_launch, cf_us = composite_fw_roofline(model, batches[0], dev)
+    cf_bytes_per_launch, cf_t = composite_fw_roofline(model, batches, dev)
+    cf_us = cf_t["hbm"]
     traffic, traffic_src = pmc_traffic()
     del main_run, model, batches
     second = None
@@ -310,13 +348,21 @@ def main():
         "samples_per_s": round(float(tot[0].item()) / el, 1),
         "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),
-        "roofline": {"kernel": "composite_train_fw", "bound": "hbm", "achieved": round(achieved, 1),
+        "roofline": {"kernel": "composite_train_fw (ncn_composite_train_fw_bg, the step's compositor)",
+                     "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(cf_bytes_per_launch),
                      "avg_launch_us": round(cf_us, 2),
-                     "method": "50 back-to-back launches on one bench batch between HIP events on the launch "
-                               "stream, host launch latency hidden behind a GPU spin"},
+                     "warm_us": round(cf_t["warm"], 2),
+                     "frac_warm": round(cf_t["warm_bytes"] / (cf_t["warm"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                     "in_step_us": round(cf_t["in_step"], 2),
+                     "method": "avg_launch_us (-> achieved, frac): 48 back-to-back launches cycling through 24 "
+                               "input sets (~16.5 MB each, 24x > the 256 MiB Infinity Cache: every launch reads "
+                               "from HBM), HIP events on the launch stream around all of them behind a GPU spin; "
+                               "warm_us: the same on one set (cache-resident); in_step_us: one launch right behind "
+                               "the field forward that produced its inputs, its own event pair (launch ramp and "
+                               "event overhead included). Algorithmic bytes 24*S_vr + 4*S + 52*R (SURVEY 8d)"},
         "kernels": kern,
     }
     if second is not None:

@@ -124,6 +124,12 @@ int ncn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, con
                            int64_t n_samples, int n_rend, const float* opacity, const float* depth,
                            const float* rend, float T_threshold, float* dL_dsigmas, float* dL_draws, void* stream);
 
+/* VolumeRenderer.forward's total_samples.sum() (custom_functions.py:139-146) -> *sum_out (int64),
+ * one workgroup; with acc != NULL also acc[0] += counter[0] (the marcher's sample count; counter may
+ * be NULL) and acc[1] += the sum: device-resident throughput counters of a captured step. */
+int ncn_count_samples(const int64_t* total_samples, int64_t n_rays, const int32_t* counter, int64_t* sum_out,
+                      double* acc, void* stream);
+
 /* render()'s white/zero background fused into the compositor (rendering.py:232-240, used by the
  * train path when exp_step_factor == 0): the forward additionally writes rgb_bg = rend + bg *
  * (1 - opacity) (R, n_rend); the backward takes dL/drgb_bg in place of dL/drend and adds the

@@ -766,7 +766,6 @@ constexpr int sc_layout_bytes(int sets, bool staging) {
 constexpr int SC_ARENA = sc_layout_bytes(SC_SETS_RUN, true) > sc_layout_bytes(SC_SETS_DIR, false)
                              ? sc_layout_bytes(SC_SETS_RUN, true) : sc_layout_bytes(SC_SETS_DIR, false);
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
-constexpr int SC_TS_NONE = -2;  // slot[] of an inactive lane
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
 

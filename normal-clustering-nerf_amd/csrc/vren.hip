@@ -1195,6 +1195,34 @@ __global__ void morton3D_invert_kernel(const int32_t* __restrict__ idx, int64_t 
     c[3 * i + 1] = (int32_t)morton3D_invert((uint32_t)(ind >> 1));
     c[3 * i + 2] = (int32_t)morton3D_invert((uint32_t)(ind >> 2));
 }
+// total_samples.sum() of VolumeRenderer.forward (custom_functions.py:139-146) in one workgroup,
+// optionally adding the marcher's count and that sum into a running f64 pair (throughput counters
+// that stay on the device: no per-step copies).
+__global__ __launch_bounds__(1024) void count_samples_kernel(const int64_t* __restrict__ total, int64_t R,
+                                                             const int32_t* __restrict__ counter,
+                                                             int64_t* __restrict__ sum_out, double* __restrict__ acc) {
+    __shared__ long long part[16];
+    long long v = 0;
+    for (int64_t i = threadIdx.x; i < R; i += 1024) v += total[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)v, off, 64), hi = __shfl_xor((unsigned)((unsigned long long)v >> 32), off, 64);
+        v += (long long)(((unsigned long long)hi << 32) | lo);
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) t += part[w];
+        *sum_out = t;
+        if (acc) {
+            acc[0] += counter ? (double)counter[0] : 0.0;
+            acc[1] += (double)t;
+        }
+    }
+}
+
 __global__ void packbits_kernel(const float4* __restrict__ grid, int64_t n_bytes, float thr,
                                 uint8_t* __restrict__ bitfield) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1227,6 +1255,14 @@ int ncn_morton3D_invert(const int32_t* indices, int64_t n, int32_t* coords, void
     hipLaunchKernelGGL(morton3D_invert_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, indices, n,
                        coords);
     NCN_LAUNCH_CHECK("ncn_morton3D_invert");
+    return 0;
+}
+
+int ncn_count_samples(const int64_t* total_samples, int64_t n_rays, const int32_t* counter, int64_t* sum_out,
+                      double* acc, void* stream) {
+    hipLaunchKernelGGL(count_samples_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, total_samples, n_rays,
+                       counter, sum_out, acc);
+    NCN_LAUNCH_CHECK("ncn_count_samples");
     return 0;
 }
 

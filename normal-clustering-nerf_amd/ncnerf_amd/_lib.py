@@ -37,6 +37,7 @@ SIGNATURES = {
     "ncn_composite_train_fw": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, P],
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
     "ncn_composite_train_fw_bg": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, F32, P, P],
+    "ncn_count_samples": [P, I64, P, P, P, P],
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, I32, P],

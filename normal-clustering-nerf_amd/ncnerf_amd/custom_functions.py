@@ -74,7 +74,7 @@ class VolumeRenderer(torch.autograd.Function):
         ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
         ctx.T_threshold = T_threshold
         ctx.set_materialize_grads(False)
-        return total_samples.sum(), opacity, depth, rend, ws
+        return vren.count_samples(total_samples), opacity, depth, rend, ws
 
     @staticmethod
     @custom_bwd(device_type="cuda")
@@ -94,14 +94,16 @@ class VolumeRendererBg(torch.autograd.Function):
 
     @staticmethod
     @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg):
+    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg, count=None):
         sigmas = sigmas.contiguous(); raws = raws.contiguous()
         total_samples, opacity, depth, rend, ws, rgb = vren.composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a,
                                                                                        T_threshold, bg=bg)
         ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
         ctx.T_threshold, ctx.bg = T_threshold, bg
         ctx.set_materialize_grads(False)
-        return total_samples.sum(), opacity, depth, rgb, ws
+        # count = (the marcher's device counter, a float64 (2,) accumulator) or None (ncn_count_samples)
+        cnt = vren.count_samples(total_samples, *(count if count is not None else ()))
+        return cnt, opacity, depth, rgb, ws
 
     @staticmethod
     @custom_bwd(device_type="cuda")
@@ -111,7 +113,7 @@ class VolumeRendererBg(torch.autograd.Function):
         dL_dsigmas, dL_draws = vren.composite_train_multi_bw(c(dL_dopacity), c(dL_ddepth), c(dL_drgb), c(dL_dws),
                                                              sigmas, raws, ws, deltas, ts, rays_a, opacity, depth,
                                                              rend, ctx.T_threshold, bg=ctx.bg)
-        return dL_dsigmas, dL_draws, None, None, None, None, None
+        return dL_dsigmas, dL_draws, None, None, None, None, None, None
 
 
 class TruncExp(torch.autograd.Function):

@@ -142,7 +142,7 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
             rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
             model.grid_size, max_samples, kwargs.get("march_noise"), static)
     for k, v in list(kwargs.items()):  # rendering.py:198-200
-        if isinstance(v, torch.Tensor) and k not in ("march_noise", "premarched", "march_rng"):
+        if isinstance(v, torch.Tensor) and k not in ("march_noise", "premarched", "march_rng", "count_acc"):
             if static:
                 raise NotImplementedError(f"per-ray tensor kwarg {k!r} on the static-shape path")
             kwargs[k] = torch.repeat_interleave(v[rays_a[:, 0]], rays_a[:, 2], 0)
@@ -158,6 +158,10 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     fuse_bg = exp_step_factor == 0 and raws.shape[1] == 3  # white background, rgb only
     renderer = VolumeRendererBg if fuse_bg else VolumeRenderer
     extra = (1.0,) if fuse_bg else ()
+    if fuse_bg and kwargs.get("count_acc") is not None:  # (extension) device-side throughput counters
+        rm = results["rm_samples"]
+        rm = rm if isinstance(rm, torch.Tensor) and rm.dtype == torch.int32 and rm.is_cuda else None
+        extra = (1.0, (rm, kwargs["count_acc"]))
     (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = renderer.apply(
         sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4), *extra)
     i = 3
@@ -203,7 +207,8 @@ def _fused_march_ok(model, kw, n_rays):
     return (kw.get("static_shapes", False) and not kw.get("test_time", False)
             and kw.get("exp_step_factor", 0.0) == 0 and kw.get("anneal_strategy", "none") == "none"
             and getattr(model, "_aabb", None) is not None and n_rays <= 16384
-            and not any(isinstance(v, torch.Tensor) for k, v in kw.items() if k not in ("march_noise", "march_rng")))
+            and not any(isinstance(v, torch.Tensor) for k, v in kw.items()
+                        if k not in ("march_noise", "march_rng", "count_acc")))
 
 
 @torch.no_grad()

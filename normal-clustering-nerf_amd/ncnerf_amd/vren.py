@@ -132,6 +132,16 @@ def raymarching_test(rays_o, rays_d, hits_t, alive_indices, density_bitfield, ca
     return [xyzs, dirs, deltas, ts, n_eff]
 
 
+def count_samples(total_samples, counter=None, acc=None):
+    """total_samples.sum() (int64 scalar tensor) in one kernel (ncn_count_samples); with acc (a device
+    float64 (2,) tensor) also acc += (counter[0], the sum): throughput counters kept on the device."""
+    check_input(total_samples, "total_samples")
+    out = torch.empty((), dtype=torch.int64, device=total_samples.device)
+    call("ncn_count_samples", ptr(total_samples), I64(total_samples.shape[0]), ptr(counter), ptr(out), ptr(acc),
+         stream())
+    return out
+
+
 def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold, bg=None):
     """volumerendering.cu:140-176 -> [total_samples i64 (R), opacity (R), depth (R), rend (R,C), ws (S)]
     Extension: bg (float) also returns rgb_bg = rend + bg * (1 - opacity) as a sixth output."""

@@ -58,7 +58,8 @@ def run_reference(steps, device, world):
         tr.opt.set_epoch((3000 + k) // -(-tr.epoch_items // world))  # the ranks' epoch (DistributedSampler)
         for r in range(world):
             batch = _batch(scene, r, k, device)
-            kw = dict(tr.render_kwargs, global_step=3000 + k, march_noise=batch["march_noise"])
+            # the graph step's kernels (fused marcher, sample-order compositor) on the eager path
+            kw = dict(tr.render_kwargs, global_step=3000 + k, march_noise=batch["march_noise"], static_shapes=True)
             results = render(model, batch["rays_o"], batch["rays_d"], **kw)
             tr.loss(results, batch, global_step=3000 + k)["total"].backward()
         tr.opt.step(grad_scale=1.0 / world)
