@@ -753,15 +753,32 @@ __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb, floa
 //  * at the end of the unit the claimed slots (the `used` list) are flushed with one f32 global
 //    atomic per non-zero sum and reset.  A unit whose gradient is not finite adds every record
 //    straight to global memory (NaN/Inf propagate as in the f32 path).
-constexpr int SC_THREADS = 1024;
+#ifndef NCN_SC_THREADS
+#define NCN_SC_THREADS 1024
+#endif
+constexpr int SC_THREADS = NCN_SC_THREADS;  // workgroups per CU: 1024 / SC_THREADS (tables scale with it)
 constexpr int SC_WAVES = SC_THREADS / 64;
 constexpr int SC_WAYS = 4;                 // 4-way set associative: one ds_read_b128 per lookup
 constexpr int SC_REC = 64;                 // staged run records per wave (80 B each: 80 KB)
-// Two LDS layouts over one arena: run levels 768 sets (3072 slots, 66 KB) + the record staging
-// (80 KB); direct levels 1536 sets (6144 slots, 132 KB) and no staging.
-constexpr int SC_SETS_RUN = 768, SC_SETS_DIR = 1536;
+// Slot value: NCN_SC_PACK = 1 keeps the (x, y) sums of an entry as two 32-bit fixed-point halves of
+// ONE 64-bit word (y * 2^32 + x: one ds_add_u64 per corner, 14 B per slot); 0 keeps two 64-bit sums
+// (22 B per slot).
+#ifndef NCN_SC_PACK
+#define NCN_SC_PACK 1
+#endif
+constexpr bool SC_PACK = NCN_SC_PACK != 0;
+constexpr int SC_SLOT_BYTES = SC_PACK ? 4 + 8 + 2 : 4 + 8 + 8 + 2;
+// Two LDS layouts over one arena: run levels (sets + the record staging, 80 KB at 1024 threads);
+// direct levels (sets only).  Unpacked: 768 / 1536 sets (66 / 132 KB); packed: 1152 / 2560.
+#ifndef NCN_SC_SETS_RUN
+#define NCN_SC_SETS_RUN (SC_PACK ? 1152 : 768)
+#endif
+#ifndef NCN_SC_SETS_DIR
+#define NCN_SC_SETS_DIR (SC_PACK ? 2560 : 1536)
+#endif
+constexpr int SC_SETS_RUN = NCN_SC_SETS_RUN * SC_THREADS / 1024, SC_SETS_DIR = NCN_SC_SETS_DIR * SC_THREADS / 1024;
 constexpr int sc_layout_bytes(int sets, bool staging) {
-    return sets * SC_WAYS * (4 + 8 + 8 + 2) + (staging ? SC_WAVES * SC_REC * 80 : 0);
+    return sets * SC_WAYS * SC_SLOT_BYTES + (staging ? SC_WAVES * SC_REC * 80 : 0);
 }
 constexpr int SC_ARENA = sc_layout_bytes(SC_SETS_RUN, true) > sc_layout_bytes(SC_SETS_DIR, false)
                              ? sc_layout_bytes(SC_SETS_RUN, true) : sc_layout_bytes(SC_SETS_DIR, false);
@@ -776,6 +793,19 @@ __device__ __forceinline__ long long sc_fix(float v, int k) {
     const double magic = 6755399441055744.0;  // 1.5 * 2^52
     const double y = fma((double)v, __longlong_as_double((long long)(1023 + k) << 52), magic);
     return __double_as_longlong(y) - __double_as_longlong(magic);
+}
+
+// (packed slots) round(x * 2^k) + round(y * 2^k) * 2^32 as one 64-bit addend: with x_i < 0 the high
+// half borrows one, so sums of addends are sum(y_i) * 2^32 + sum(x_i) exactly while |sum| < 2^31
+// (the scale k guarantees it); sc_unpack recovers both sums.
+__device__ __forceinline__ unsigned long long sc_fix2(float x, float y, int k) {
+    const int xi = __float2int_rn(ldexpf(x, k)), yi = __float2int_rn(ldexpf(y, k));
+    return ((unsigned long long)(uint32_t)(yi + (xi >> 31)) << 32) | (uint32_t)xi;
+}
+__device__ __forceinline__ float sc_q(float v, int k) { return ldexpf(rintf(ldexpf(v, k)), -k); }
+__device__ __forceinline__ void sc_unpack(long long q, int& xs, int& ys) {
+    xs = (int)(uint32_t)q;
+    ys = (int)((q - (long long)xs) >> 32);
 }
 
 // samples per lane (log2) and span of a unit on level l
@@ -816,7 +846,7 @@ __device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fil
     sh.sets = run ? SC_SETS_RUN : SC_SETS_DIR;
     sh.slots = (int)sh.sets * SC_WAYS;
     sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used, records (16-B aligned)
-    sh.valy = sh.valx + sh.slots;
+    sh.valy = SC_PACK ? sh.valx : sh.valx + sh.slots;  // (packed: one value array)
     sh.keys = (uint32_t*)(sh.valy + sh.slots);
     sh.used = (uint16_t*)(sh.keys + sh.slots);
     sh.rec = (ScRec*)(sh.used + sh.slots);
@@ -925,8 +955,12 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
             slot[c] = sl[b];
             if (vc[b] && sl[b] >= 0) {
 #ifndef NCN_DIAG_SC_NO_LDSADD
-                atomicAdd((unsigned long long*)&sh.valx[sl[b]], (unsigned long long)sc_fix(v[2 * c], L.k));
-                atomicAdd((unsigned long long*)&sh.valy[sl[b]], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
+                if constexpr (SC_PACK) {
+                    atomicAdd((unsigned long long*)&sh.valx[sl[b]], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
+                } else {
+                    atomicAdd((unsigned long long*)&sh.valx[sl[b]], (unsigned long long)sc_fix(v[2 * c], L.k));
+                    atomicAdd((unsigned long long*)&sh.valy[sl[b]], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
+                }
 #endif
             }
         }
@@ -939,8 +973,10 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
                 const int c = c0 + b;
                 if (vc[b] && sl[b] < 0) {
 #ifndef NCN_DIAG_SC_NO_FALLBACK
-                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
-                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
+                    // (packed: rounded to the table's fixed-point grid like every LDS addend, so which
+                    // corners fall back — claim order — moves the result by float-add order only)
+                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]), SC_PACK ? sc_q(v[2 * c], L.k) : v[2 * c]);
+                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, SC_PACK ? sc_q(v[2 * c + 1], L.k) : v[2 * c + 1]);
 #endif
                 }
             }
@@ -1204,7 +1240,11 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     L.direct = !isfinite(m);
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
-    L.k = 46 - e2;
+    // An entry's sum over the unit is at most (unit samples) * m (a sample's 8 corner weights sum
+    // to 1), plus half a unit of rounding per addend: 64-bit sums take k = 46 - e2 (a record sums
+    // at most 8 samples, an entry at most 8192); packed 32-bit halves k = 30 - log2(samples) - e2.
+    constexpr int lg_unit = 31 - __builtin_clz(SC_THREADS * C);
+    L.k = SC_PACK ? 30 - lg_unit - e2 : 46 - e2;
     SC_TNOW(t1);
     if (RUNS) {
         int staged = 0;
@@ -1225,9 +1265,18 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
         const uint32_t key = sh.keys[slot];
         long long* pv = (i & 1) ? &sh.valy[slot] : &sh.valx[slot];
         const long long q = *pv;
-        *pv = 0;
+        float gv;
+        if constexpr (SC_PACK) {  // both lanes of the pair read the word; the odd one resets it
+            int xs, ys;
+            sc_unpack(q, xs, ys);
+            gv = ldexpf((float)((i & 1) ? ys : xs), -L.k);
+            if (i & 1) *pv = 0;
+        } else {
+            gv = (float)ldexp((double)q, -L.k);
+            *pv = 0;
+        }
 #ifndef NCN_DIAG_SC_NO_FLUSH
-        if (q != 0) atomicAdd(grad + 2 * (size_t)(L.off + key) + (i & 1), (float)ldexp((double)q, -L.k));
+        if (gv != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + key) + (i & 1), gv);
 #endif
         if (!(i & 1)) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the odd lane has read the key: same wave)
@@ -1327,7 +1376,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
 }
 
 static int scatter_grid(int64_t n_cap) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(256, (n_cap + 255) / 256));  // one per CU
+    return (int)std::max<int64_t>(1, std::min<int64_t>(256 * 1024 / SC_THREADS, (n_cap + 255) / 256));  // 1024 threads per CU
 }
 
 static LevelTable make_table(const uint32_t* levels) {

@@ -85,13 +85,13 @@ def timeit(lib, reps=20, **kw):
 
 
 libs = [("main", main)]
-for so in sorted(glob.glob(os.path.join(ROOT, "tools", "_build", "field_*.so"))):
+for so in [] if os.environ.get("SCATTER_PROBE_MAIN_ONLY") else sorted(glob.glob(os.path.join(ROOT, "tools", "_build", "field_*.so"))):
     L = ctypes.CDLL(so)
     L.ncn_field_scatter.argtypes = _lib.SIGNATURES["ncn_field_scatter"]
     L.ncn_field_scatter.restype = ctypes.c_int
     libs.append((os.path.basename(so)[6:-3], L))
 gref = None
-for sorted_ in (False, True):
+for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") else (False, True):
     print("order:", "Morton windows" if sorted_ else "ray (identity)", flush=True)
     so = prepare(sorted_)
     if sorted_:
