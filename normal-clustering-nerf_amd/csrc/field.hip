@@ -780,8 +780,19 @@ constexpr int SC_SETS_RUN = NCN_SC_SETS_RUN * SC_THREADS / 1024, SC_SETS_DIR = N
 constexpr int sc_layout_bytes(int sets, bool staging) {
     return sets * SC_WAYS * SC_SLOT_BYTES + (staging ? SC_WAVES * SC_REC * 80 : 0);
 }
-constexpr int SC_ARENA = sc_layout_bytes(SC_SETS_RUN, true) > sc_layout_bytes(SC_SETS_DIR, false)
-                             ? sc_layout_bytes(SC_SETS_RUN, true) : sc_layout_bytes(SC_SETS_DIR, false);
+// Cell-keyed layout (the coarse levels [0, SC_CELL_HI)): a slot is one grid CELL of the level and
+// holds the packed sums of its 8 corners (corner-major: vals[c * slots + slot]); 70 B per slot.
+#ifndef SC_CELL_HI
+#define SC_CELL_HI 10
+#endif
+#ifndef NCN_SC_SETS_CELL
+#define NCN_SC_SETS_CELL 512
+#endif
+constexpr int SC_SETS_CELL = NCN_SC_SETS_CELL * SC_THREADS / 1024;
+constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + 8 * 8 + 2); }
+constexpr int sc_max(int a, int b) { return a > b ? a : b; }
+constexpr int SC_ARENA = sc_max(sc_cell_bytes(SC_SETS_CELL),
+                                sc_max(sc_layout_bytes(SC_SETS_RUN, true), sc_layout_bytes(SC_SETS_DIR, false)));
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
@@ -841,12 +852,15 @@ struct ScShared {
     float* wmax;
     int* fill;
 };
-__device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fill, bool run) {
+enum { SC_MODE_DIR = 0, SC_MODE_RUN = 1, SC_MODE_CELL = 2 };
+__device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fill, int mode) {
     ScShared sh;
-    sh.sets = run ? SC_SETS_RUN : SC_SETS_DIR;
+    const bool run = mode == SC_MODE_RUN;
+    sh.sets = mode == SC_MODE_CELL ? SC_SETS_CELL : run ? SC_SETS_RUN : SC_SETS_DIR;
     sh.slots = (int)sh.sets * SC_WAYS;
     sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used, records (16-B aligned)
-    sh.valy = SC_PACK ? sh.valx : sh.valx + sh.slots;  // (packed: one value array)
+    // (packed: one value array; cell mode: 8 corner arrays)
+    sh.valy = mode == SC_MODE_CELL ? sh.valx + 7 * sh.slots : SC_PACK ? sh.valx : sh.valx + sh.slots;
     sh.keys = (uint32_t*)(sh.valy + sh.slots);
     sh.used = (uint16_t*)(sh.keys + sh.slots);
     sh.rec = (ScRec*)(sh.used + sh.slots);
@@ -1210,10 +1224,142 @@ __device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<
     }
 }
 
+// ---- cell-keyed form (coarse levels) ----
+// One LDS lookup per run record instead of one per corner: the record's cell (px, py, pz) is the
+// key (px | py << 11 | pz << 22; cells outside that range go straight to global memory) and its 8
+// corner sums are 8 packed ds_add_u64 into the slot's corner arrays.  The flush forms each claimed
+// cell's corner entries and adds them to the table gradient (a corner shared by several cells of
+// the unit gets one global add per cell: coarse levels have few cells per unit).
+__device__ __forceinline__ uint32_t sc_corner_entry(const ScLevel& L, uint32_t px, uint32_t py, uint32_t pz, int c) {
+    const uint32_t x = px + (c & 1), y = py + ((c >> 1) & 1), z = pz + ((c >> 2) & 1);
+    if (L.dense) {
+        const uint32_t e = x + L.res * y + L.res * L.res * z;
+        return e < L.params ? e : e % L.params;
+    }
+    return (x ^ (y * 2654435761u) ^ (z * 805459861u)) & (L.params - 1);
+}
+
+__device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, uint32_t px, uint32_t py, uint32_t pz,
+                                            const float (&v)[16], const ScLevel& L, float* __restrict__ grad) {
+    const bool inkey = px < 2048u && py < 2048u && pz < 1024u;
+    const uint32_t key = px | (py << 11) | (pz << 22);
+    const bool go = act && inkey;
+    const int p0 = SC_WAYS * (int)sc_set(key, sh.sets);
+    int sl = -1;
+    bool isnew = false;
+    uint4 kk = make_uint4(0u, 0u, 0u, 0u);
+    if (go) {
+        kk = *(const uint4*)&sh.keys[p0];
+        sl = kk.x == key ? p0 : kk.y == key ? p0 + 1 : kk.z == key ? p0 + 2 : kk.w == key ? p0 + 3 : -1;
+    }
+    if (__ballot(go && sl < 0)) {  // uniform: some lane claims
+        if (go && sl < 0) {
+#pragma unroll
+            for (int attempt = 0; attempt < 2 && sl < 0; attempt++) {
+                if (attempt) {  // lost a claim: look again
+                    asm volatile("" ::: "memory");
+                    kk = *(const uint4*)&sh.keys[p0];
+                    sl = kk.x == key ? p0 : kk.y == key ? p0 + 1 : kk.z == key ? p0 + 2 : kk.w == key ? p0 + 3 : -1;
+                    if (sl >= 0) break;
+                }
+                const int cl = kk.x == SC_EMPTY ? p0 : kk.y == SC_EMPTY ? p0 + 1 : kk.z == SC_EMPTY ? p0 + 2
+                             : kk.w == SC_EMPTY ? p0 + 3 : -1;
+                if (cl < 0) break;  // set full
+                const uint32_t got = atomicCAS(&sh.keys[cl], SC_EMPTY, key);
+                if (got == SC_EMPTY) { sl = cl; isnew = true; }
+                else if (got == key) sl = cl;
+            }
+        }
+    }
+    if (go && sl >= 0) {
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            if (v[2 * c] != 0.f || v[2 * c + 1] != 0.f)
+                atomicAdd((unsigned long long*)&sh.valx[c * sh.slots + sl], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
+    }
+    const bool fb = act && sl < 0;
+    if (__ballot(fb)) {  // uniform: set full or cell outside the key range: straight to the table
+        if (fb) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const uint32_t e = L.off + sc_corner_entry(L, px, py, pz, c);
+                if (v[2 * c] != 0.f) atomicAdd(grad + 2 * (size_t)e, sc_q(v[2 * c], L.k));
+                if (v[2 * c + 1] != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, sc_q(v[2 * c + 1], L.k));
+            }
+        }
+    }
+    // append the claimed slot to `used`: one LDS atomic per wave
+    const uint64_t nm = __ballot(isnew);
+    if (nm) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(sh.fill, (int)__popcll(nm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (isnew)
+            sh.used[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0))] =
+                (uint16_t)sl;
+    }
+}
+
+// A lane's C consecutive samples: consecutive samples in the same cell are summed in registers and
+// a finished run goes to sc_add_cell (called by the whole wave when some lane has one).
+template <int C>
+__device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
+                                         float* __restrict__ grad) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = 0.f;
+    LevelPos p = level_pos(L.scale, ch.x[0], ch.y[0], ch.z[0]);
+    bool any = ch.g[0].x != 0.f || ch.g[0].y != 0.f;
+    sc_corner_sums(p, ch.g[0], v);
+#pragma unroll
+    for (int i = 1; i <= C; i++) {
+        LevelPos q = p;
+        bool emit = true;
+        if (i < C) {
+            q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
+            emit = q.px != p.px || q.py != p.py || q.pz != p.pz;
+        }
+        if (__ballot(emit && any)) sc_add_cell(sh, lane, emit && any, p.px, p.py, p.pz, v, L, grad);  // uniform
+        if (i < C) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = emit ? 0.f : v[j];
+            any = (emit ? false : any) || ch.g[i].x != 0.f || ch.g[i].y != 0.f;
+            sc_corner_sums(q, ch.g[i], v);
+        }
+        p = q;
+    }
+}
+
+// Flush of a cell unit: 8 lanes per claimed cell (one corner each: decode the packed sums, form the
+// corner's entry, two f32 global adds); the corner-0 lane resets the key, each lane its value.
+__device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, float* __restrict__ grad) {
+    const int nf = *sh.fill;
+    for (int i = threadIdx.x; i < 8 * nf; i += SC_THREADS) {
+        const int slot = sh.used[i >> 3], c = i & 7;
+        const uint32_t key = sh.keys[slot];
+        long long* pv = &sh.valx[c * sh.slots + slot];
+        const long long q = *pv;
+        *pv = 0;
+#ifndef NCN_DIAG_SC_NO_FLUSH
+        if (q != 0) {
+            int xs, ys;
+            sc_unpack(q, xs, ys);
+            const uint32_t e = L.off + sc_corner_entry(L, key & 2047u, (key >> 11) & 2047u, key >> 22, c);
+            if (xs) atomicAdd(grad + 2 * (size_t)e, ldexpf((float)xs, -L.k));
+            if (ys) atomicAdd(grad + 2 * (size_t)e + 1, ldexpf((float)ys, -L.k));
+        }
+#endif
+        if (c == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the other 7 lanes have read the key: same wave)
+            sh.keys[slot] = SC_EMPTY;
+        }
+    }
+}
+
 // One unit: load the chunk, phase A/B or direct, flush.  The fixed-point scale is per level, from
 // the max |dE| the MLP pass recorded (level_max): no per-unit reduction or barrier.
 #ifdef NCN_DIAG_SC_TIMES
-__device__ unsigned long long ncn_sc_times[256][8];  // per workgroup, wave 0: cycles per phase x {run, dir}
+__device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: cycles per phase x {run, dir}
 #define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
 #define SC_TADD(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2 + (RUNS ? 0 : 1)] += (b) - (a)
 #else
@@ -1254,6 +1400,10 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
         sc_direct<C>(sh, lane, ch, L, grad);
     }
     SC_TNOW(t2);
+#ifdef NCN_DIAG_SC_TIMES
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (diagnostic: the wave's own LDS ops drain)
+#endif
+    SC_TNOW(t2b);
     lds_barrier();
     SC_TNOW(t3);
     // flush: the claimed slots, two lanes per slot (x and y of one entry are adjacent floats, one
@@ -1287,8 +1437,58 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     SC_TNOW(t4);
     SC_TADD(0, t0, t1);
     SC_TADD(1, t1, t2);
-    SC_TADD(2, t2, t3);
-    SC_TADD(3, t3, t4);
+    SC_TADD(2, t2, t2b);
+    SC_TADD(3, t2b, t3);
+    SC_TADD(4, t3, t4);
+}
+
+// Cell units: `rounds` consecutive chunks of 1024 x C samples per unit (no barrier between them),
+// then one flush.  Rounds per level: coarse levels have few cells, so longer units mean fewer
+// flushes and barriers.
+#ifndef SC_C_CELL
+#define SC_C_CELL 4
+#endif
+#ifndef SC_CELL_ROUNDS_A
+#define SC_CELL_ROUNDS_A 4  // levels 0-5
+#endif
+#ifndef SC_CELL_ROUNDS_B
+#define SC_CELL_ROUNDS_B 2  // levels 6-9
+#endif
+__device__ __forceinline__ int sc_cell_rounds(int l) { return l < 6 ? SC_CELL_ROUNDS_A : l < 10 ? SC_CELL_ROUNDS_B : 1; }
+
+template <int C>
+__device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1, int rounds,
+                                             const float* __restrict__ xyzs, const float2* __restrict__ dEl,
+                                             const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
+                                             const int32_t* __restrict__ order) {
+    ScLevel L;
+    L.scale = Lt.scale[l];
+    L.res = Lt.res[l];
+    L.params = Lt.params[l];
+    L.off = Lt.offset[l];
+    L.dense = (uint64_t)L.res * L.res * L.res <= L.params;
+    L.direct = !isfinite(m);  // (uniform) non-finite gradient: every corner straight to global memory
+    int e2 = 0;
+    (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
+    // packed 32-bit halves: |sum| <= (unit samples) * m * 2^k + rounding < 2^31
+    const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
+    L.k = 30 - lg_unit - e2;
+    ScChunk<C> ch;
+    const int64_t lane_off = (int64_t)(lane * SC_WAVES + wid) * C;
+    sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, nrm, order);
+    for (int r = 0; r < rounds; r++) {
+        ScChunk<C> nx;
+        const bool more = r + 1 < rounds;
+        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * SC_THREADS * C + lane_off, s1, xyzs, dEl, nrm, order);
+        if (L.direct)
+            sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
+        else
+            sc_cells<C>(sh, lane, ch, L, grad);
+        if (more) ch = nx;
+    }
+    lds_barrier();
+    sc_flush_cells(sh, L, grad);
+    lds_barrier();
 }
 
 __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
@@ -1317,42 +1517,63 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     nrm.ext = xyz_extent;
     nrm.inv = 1.0f / xyz_extent;
     nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
-    // units, level-major over the levels [level_lo, level_hi): run levels in spans of
-    // 1024 * SC_C_RUN samples, direct levels in spans of 2048 (2 per lane)
-    constexpr int C_RUN = SC_C_RUN, C_DIR = SC_C_DIR;
+    // units, level-major over the levels [level_lo, level_hi): cell levels [0, SC_CELL_HI) in spans
+    // of 1024 * C_CELL * rounds(l) samples, run levels [SC_CELL_HI, SC_RUN_LEVELS) in spans of
+    // 1024 * SC_C_RUN, direct levels in spans of 1024 * SC_C_DIR
+    constexpr int C_RUN = SC_C_RUN, C_DIR = SC_C_DIR, C_CELL = SC_C_CELL;
     const int64_t ur = (n + SC_THREADS * C_RUN - 1) / (SC_THREADS * C_RUN);
     const int64_t ud = (n + SC_THREADS * C_DIR - 1) / (SC_THREADS * C_DIR);
-    const int run_lo = level_lo, run_hi = min(level_hi, SC_RUN_LEVELS);
-    const int dir_lo = max(level_lo, SC_RUN_LEVELS), dir_hi = level_hi;
+    const int cell_lo = level_lo, cell_hi = min(level_hi, SC_CELL_HI);
+    const int run_lo = max(level_lo, SC_CELL_HI), run_hi = min(level_hi, SC_RUN_LEVELS);
+    const int dir_lo = max(level_lo, max(SC_CELL_HI, SC_RUN_LEVELS)), dir_hi = level_hi;
+    int64_t n_cell = 0;
+    for (int l = cell_lo; l < cell_hi; l++) {
+        const int64_t span = (int64_t)SC_THREADS * C_CELL * sc_cell_rounds(l);
+        n_cell += (n + span - 1) / span;
+    }
     const int64_t n_run = run_hi > run_lo ? (int64_t)(run_hi - run_lo) * ur : 0;
-    const int64_t n_units = n_run + (dir_hi > dir_lo ? (int64_t)(dir_hi - dir_lo) * ud : 0);
-    // (grid-stride: a workgroup takes its run units first, then its direct ones: one layout switch)
+    const int64_t n_units = n_cell + n_run + (dir_hi > dir_lo ? (int64_t)(dir_hi - dir_lo) * ud : 0);
+    // (grid-stride: a workgroup takes its cell units first, then run, then direct: at most two
+    // layout switches)
     int layout = -1, par = 0;
     ScShared sh;
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-        const int run = u < n_run;
-        if (run != layout) {  // (re)initialise the table of the new layout
+        const int mode = u < n_cell ? SC_MODE_CELL : u < n_cell + n_run ? SC_MODE_RUN : SC_MODE_DIR;
+        if (mode != layout) {  // (re)initialise the table of the new layout
             lds_barrier();
-            sh = sc_layout(arena, wmax, fill, run);
-            for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) {
-                sh.keys[i] = SC_EMPTY;
-                sh.valx[i] = 0;
-                sh.valy[i] = 0;
-            }
+            sh = sc_layout(arena, wmax, fill, mode);
+            const int nv = mode == SC_MODE_CELL ? 8 * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
+            for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
+            for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
             if (threadIdx.x == 0) fill[0] = fill[1] = 0;
             lds_barrier();
-            layout = run;
+            layout = mode;
             par = 0;
         }
-        int l;
+        int l, rounds = 1;
         int64_t s0, s1;
-        if (run) {
-            const int li = (int)(u / ur);
+        if (mode == SC_MODE_CELL) {
+            int64_t v = u;
+            l = cell_lo;
+            for (;; l++) {  // (uniform, at most SC_CELL_HI steps)
+                rounds = sc_cell_rounds(l);
+                const int64_t span = (int64_t)SC_THREADS * C_CELL * rounds;
+                const int64_t nu = (n + span - 1) / span;
+                if (v < nu) {
+                    s0 = v * span;
+                    s1 = min(n, s0 + span);
+                    break;
+                }
+                v -= nu;
+            }
+        } else if (mode == SC_MODE_RUN) {
+            const int64_t v = u - n_cell;
+            const int li = (int)(v / ur);
             l = run_lo + li;
-            s0 = (u - li * ur) * (SC_THREADS * C_RUN);
+            s0 = (v - li * ur) * (SC_THREADS * C_RUN);
             s1 = min(n, s0 + SC_THREADS * C_RUN);
         } else {
-            const int64_t v = u - n_run;
+            const int64_t v = u - n_cell - n_run;
             const int li = (int)(v / ud);
             l = dir_lo + li;
             s0 = (v - li * ud) * (SC_THREADS * C_DIR);
@@ -1368,10 +1589,13 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         sh.fill = fill + par;
         if (threadIdx.x == 0) fill[par ^ 1] = 0;
         par ^= 1;
-        if (run)
-            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, m, grad, order);
+        const float2* dEl = dE + (int64_t)l * e_stride;
+        if (mode == SC_MODE_CELL)
+            sc_cell_unit<C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
+        else if (mode == SC_MODE_RUN)
+            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
         else
-            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dE + (int64_t)l * e_stride, nrm, Lt, m, grad, order);
+            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
     }
 }
 
@@ -1516,10 +1740,10 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
 #ifdef NCN_DIAG_SC_TIMES
 int ncn_diag_sc_times(unsigned long long* host, int reset) {
     if (reset) {
-        static unsigned long long zero[256][8];
+        static unsigned long long zero[256][10];
         return (int)hipMemcpyToSymbol(HIP_SYMBOL(ncn_sc_times), zero, sizeof(zero));
     }
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_times), 256 * 8 * sizeof(unsigned long long));
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_times), 256 * 10 * sizeof(unsigned long long));
 }
 #endif
 

@@ -134,7 +134,10 @@ def test_field_morton_window_order(dev, n):
     """ncn_field_sort_windows: `order` is a permutation of every 4096-sample window sorted by the
     Morton code of the positions (checked on the host), and the field evaluated in that processing
     order gives the same outputs (bitwise: each sample's arithmetic does not depend on its position)
-    and the same gradients (summation order only) as in sample order."""
+    and the same gradients as in sample order up to summation order and the table scatter's
+    fixed-point rounding (its addends are per-lane runs of samples sharing a cell, and which samples
+    form a run depends on the processing order: 32-bit sums at 2^-(30 - log2(unit) - e) of the
+    level's max |dE|, so relative L2 <= 2e-4 for the table block, 1e-5 for the MLP weights)."""
     from ncnerf_amd import _lib
     from ncnerf_amd._lib import F32, I64, ptr, stream
     P, _ = field_ref.init_params(seed=5, table_init=0.5)
@@ -173,5 +176,5 @@ def test_field_morton_window_order(dev, n):
     m.sort_samples = False
     assert torch.equal(s0, s1) and torch.equal(r0, r1)
     nt = m._n_table
-    for a, b in ((g0[:nt], g1[:nt]), (g0[nt:], g1[nt:])):
-        assert float((a - b).norm() / a.norm()) < 1e-5
+    for (a, b), tol in (((g0[:nt], g1[:nt]), 2e-4), ((g0[nt:], g1[nt:]), 1e-5)):
+        assert float((a - b).norm() / a.norm()) < tol

@@ -91,7 +91,7 @@ for so in [] if os.environ.get("SCATTER_PROBE_MAIN_ONLY") else sorted(glob.glob(
     L.ncn_field_scatter.restype = ctypes.c_int
     libs.append((os.path.basename(so)[6:-3], L))
 gref = None
-for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") else (False, True):
+for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.environ.get("SCATTER_PROBE_IDENTITY") else (False, True):
     print("order:", "Morton windows" if sorted_ else "ray (identity)", flush=True)
     so = prepare(sorted_)
     if sorted_:
@@ -115,12 +115,12 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") else (False
         fine = timeit(L, lo=10, hi=16)
         print(f"  {name:24s} all {t:7.1f} us  levels0-9 {coarse:7.1f}  levels10-15 {fine:7.1f}  {msg}", flush=True)
         if hasattr(L, "ncn_diag_sc_times"):
-            buf = (ctypes.c_ulonglong * (256 * 8))()
+            buf = (ctypes.c_ulonglong * (256 * 10))()
             L.ncn_diag_sc_times(buf, 1)
             assert scat(L) == 0
             torch.cuda.synchronize()
             L.ncn_diag_sc_times(buf, 0)
-            a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8).astype(np.float64)
-            names = ["load", "work", "barrier", "flush"]
+            a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 10).astype(np.float64)
+            names = ["load", "work", "drain", "barrier", "flush"]
             print("     cycles per WG (wave 0, mean), run | direct:",
                   "  ".join(f"{nm} {a[:, 2 * i].mean():.0f}|{a[:, 2 * i + 1].mean():.0f}" for i, nm in enumerate(names)))
