@@ -66,6 +66,8 @@ if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
     if _gpus > 1:
         sys.exit(spawn_ranks(_gpus, sys.argv[1:]))
 
+import math  # noqa: E402
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -205,6 +207,14 @@ def main():
                     help="MFMA operand type of the field MLP (fp16 = tcnn's FullyFusedMLP, the reference's AMP run)")
     ap.add_argument("--no-bf16-line", action="store_true",
                     help="skip the second measurement of configs[2] with bf16 MLP operands")
+    ap.add_argument("--pretrain", type=int, default=0,
+                    help="untimed training steps from the random init before the warm-up, on the procedural "
+                         "occupancy grid (not refreshed while pretraining); 0 (default) = the random-init weights "
+                         "the contract asks for")
+    ap.add_argument("--no-extra-states", action="store_true",
+                    help="skip the extra measurements of trained states: 500 steps pretrained on the procedural "
+                         "grid (rays terminate early), and the grid train_nerf.py maintains itself "
+                         "(mark_invisible_cells + grid refresh from step 0)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="launch/rendezvous check only (no GPU work): every rank all-reduces its rank, rank 0 "
                          "prints {world, backend, sum}")
@@ -227,7 +237,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    from ncnerf_amd import _lib
+    from ncnerf_amd import _lib, synthetic
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.synthetic import SyntheticScene
     from ncnerf_amd.trainer import Trainer
@@ -237,23 +247,42 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.manual_seed(1234 + rank)
 
-    def measure(precision, steps, kernel_table):
-        """Build the model in `precision`, warm up, time `steps` graph-replayed training steps
-        (barrier + synchronize on both sides), max over ranks."""
+    GT = "surface_bright"  # synthetic target colours (ncnerf_amd.synthetic)
+
+    def measure(precision, steps, kernel_table, pretrain, state="procedural"):
+        """Build the model in `precision`, pretrain it `pretrain` untimed steps, warm up, time `steps`
+        graph-replayed training steps (barrier + synchronize on both sides), max over ranks.
+        state "procedural": the procedural occupancy grid (BASELINE.md §2), fixed while pretraining;
+        "refreshed": mark_invisible_cells, then the grid refreshed from the model every 16 steps from
+        step 0 (all cells for the first 256), as train_nerf.py does."""
         scene = SyntheticScene()
         model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
-        with torch.no_grad():
-            model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
-            model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
         trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph)
         # marched / composited sample counts accumulated on the device by the step itself
         # (ncn_count_samples: no per-step copies in the timed region)
         count_acc = torch.zeros(2, dtype=torch.float64, device=dev)
         trainer.render_kwargs["count_acc"] = count_acc
+        if state == "refreshed":
+            fx = (synthetic.IMG_W / 2) / math.tan(synthetic.HFOV / 2)
+            K = torch.tensor([[fx, 0, synthetic.IMG_W / 2], [0, fx, synthetic.IMG_H / 2], [0, 0, 1]])
+            model.mark_invisible_cells(K, dev, torch.from_numpy(scene.poses).to(dev),
+                                       (synthetic.IMG_W, synthetic.IMG_H), 0.01)
+        else:
+            with torch.no_grad():
+                model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
+                model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+        if pretrain > 0:  # a pool of 64 batches
+            pool = [scene.torch_batch(args.rays, seed=rank * 10007 + 1000 + i, device=dev, gt=GT) for i in range(64)]
+            trainer.update_grid = state == "refreshed"
+            for k in range(pretrain):
+                trainer.step(pool[k % len(pool)], global_step=k)
+            trainer.update_grid = not args.no_grid_update
+            torch.cuda.synchronize()
+            del pool
         n_batches = 8
-        batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev) for i in range(n_batches)]
-        step0 = 3000  # past the clustering ramp (losses.py:217): full 2e-3 weights
-        if trainer.update_grid:  # first-call costs of the refresh path stay out of the timed region
+        batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev, gt=GT) for i in range(n_batches)]
+        step0 = max(3000, pretrain)  # past the clustering ramp (losses.py:217): full 2e-3 weights
+        if trainer.update_grid and state != "refreshed":  # first-call costs of the refresh path stay out of the timed region
             model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
         for k in range(args.warmup):
             trainer.step(batches[k % n_batches], global_step=step0 + k)
@@ -295,7 +324,7 @@ def main():
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         return dict(el=float(elapsed.item()), tot=tot, rank_ms=rank_ms, timing=timing, model=model, batches=batches)
 
-    main_run = measure(args.precision, args.steps, True)
+    main_run = measure(args.precision, args.steps, True, args.pretrain)
     el, tot, rank_ms, timing = main_run["el"], main_run["tot"], main_run["rank_ms"], main_run["timing"]
     model, batches = main_run["model"], main_run["batches"]
     kern = {}
@@ -310,13 +339,37 @@ def main():
     second = None
     if not args.no_bf16_line:  # the same step with the other MLP operand type (configs[2] asks for bf16)
         prec2 = "bf16" if args.precision == "fp16" else "fp16"
-        r2 = measure(prec2, args.steps, False)
+        r2 = measure(prec2, args.steps, False, args.pretrain)
         second = {"precision": prec2, "value": round(args.rays * world * args.steps / r2["el"], 1), "unit": "rays/s",
                   "ms_per_step": round(1e3 * r2["el"] / args.steps, 3),
                   "samples_per_s": round(float(r2["tot"][0].item()) / r2["el"], 1),
                   "workload": "configs[2]: the same full training step (normal clustering on), " + prec2 +
                               "-operand MFMA in the field MLP"}
         del r2
+    extra = {}
+    if not args.no_extra_states:
+        for key, pre, st, what in (
+                ("init_state", 0, "procedural", "random-init NGPMT on the procedural occupancy grid: rays never "
+                                                "terminate early"),
+                ("pretrained_state", 500, "procedural",
+                 "NGPMT trained 500 untimed steps on the procedural occupancy grid (not refreshed meanwhile), then "
+                 "the same timed steps: rays terminate early; the refreshes in the timed steps re-grow the grid "
+                 "from the trained model's densities"),
+                ("refreshed_state", 500, "refreshed",
+                 "the occupancy grid train_nerf.py maintains itself: mark_invisible_cells, then refreshed from the "
+                 "model every 16 steps from step 0 (all cells for 256 steps) over 500 training steps; this "
+                 "synthetic room's grid is then far denser than the procedural one (more samples per ray)")):
+            if pre == args.pretrain and st == "procedural":
+                continue  # (the headline measurement)
+            r3 = measure(args.precision, args.steps, False, pre, st)
+            n_r = args.rays * world * args.steps
+            extra[key] = {"value": round(n_r / r3["el"], 1), "unit": "rays/s",
+                          "ms_per_step": round(1e3 * r3["el"] / args.steps, 3),
+                          "samples_per_s": round(float(r3["tot"][0].item()) / r3["el"], 1),
+                          "vr_samples_per_s": round(float(r3["tot"][1].item()) / r3["el"], 1),
+                          "rm_samples_per_ray": round(float(r3["tot"][0].item()) / n_r, 2),
+                          "pretrain_steps": pre, "state": what}
+            del r3
     achieved = cf_bytes_per_launch / (cf_us * 1e-6) / 1e9
     if rank != 0:
         if world > 1:
@@ -339,8 +392,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": f"fp32 (march/composite/losses); {args.precision}-operand MFMA with fp32 accumulate in the field MLP",
-        "data": "synthetic Hypersim-shaped batches (ai_001_001 box, 8x8 patches, procedural room occupancy); "
-                "random-init NGPMT",
+        "data": "synthetic Hypersim-shaped batches (ai_001_001 box, 8x8 patches, procedural room, "
+                "surface_bright target colours); " + (
+                    f"NGPMT pretrained {args.pretrain} untimed steps from random init on the procedural occupancy "
+                    f"grid (rays terminate early)" if args.pretrain > 0 else
+                    "random-init NGPMT on the procedural occupancy grid (trained states: pretrained_state, "
+                    "refreshed_state)"),
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
@@ -367,6 +424,7 @@ def main():
     }
     if second is not None:
         out["other_precision"] = second
+    out.update(extra)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     print(json.dumps(out))

@@ -210,3 +210,27 @@ def density_grid_update(grid, cells, sigmas, decay, threshold, count_grid=None):
     mean = np.float32(pos.astype(np.float64).mean()) if pos.size else np.float32(np.nan)
     thr = min(float(mean), threshold)
     return new, thr, packbits(new, thr)
+
+
+def segment_csr(src, indptr):
+    """torch_scatter.segment_csr(src, indptr) with reduce="sum" (the reference's RayMarcher.backward,
+    custom_functions.py:107-110): out[i] = src[indptr[i]:indptr[i+1]].sum(0), sequential f32 adds;
+    an empty or inverted segment sums to 0."""
+    src = np.asarray(src, np.float32)
+    out = np.zeros((len(indptr) - 1,) + src.shape[1:], np.float32)
+    for i in range(len(indptr) - 1):
+        acc = np.zeros(src.shape[1:], np.float32)
+        for s in range(int(indptr[i]), int(indptr[i + 1])):
+            acc = acc + src[s]
+        out[i] = acc
+    return out
+
+
+def raymarcher_backward(rays_a, ts, dL_dxyzs, dL_ddirs):
+    """custom_functions.py:102-112: (dL/drays_o, dL/drays_d) of RayMarcher by segment_csr over
+    indptr = [rays_a[:, 1], rays_a[-1, 1] + rays_a[-1, 2]]."""
+    rays_a = np.asarray(rays_a)
+    indptr = np.concatenate([rays_a[:, 1], rays_a[-1:, 1] + rays_a[-1:, 2]])
+    ts = np.asarray(ts, np.float32)
+    gx = np.asarray(dL_dxyzs, np.float32)
+    return segment_csr(gx, indptr), segment_csr(gx * ts[:, None] + np.asarray(dL_ddirs, np.float32), indptr)

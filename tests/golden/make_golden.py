@@ -14,7 +14,7 @@ concat, VolumeRenderer autograd, rays_o := rays_d, white background), NGPMT.forw
 _extract_normals_from_ray_batch, validity filter, _normals_clustering selection/merging/opposites,
 flips, the cluster losses, the weight schedule) and the autograd through all of it.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [render|loss|select|invisible ...]
 """
 import os
 import sys
@@ -289,16 +289,58 @@ def make_select_fixture(losses):
     print("cluster_select.npz", [np.unique(cases[f"labels{i}"]).tolist() for i in range(3)])
 
 
+def ndc_matrices(fx, w, h, near=0.05, far=4.0):
+    """A Hypersim-style K tuple (M_ndc_from_cam 4x4, M_uv_from_ndc 3x4) for the same pinhole: the
+    OpenGL projection of a camera looking down +z, and NDC -> pixel (u, v) with the NDC depth as d."""
+    a, b = (far + near) / (far - near), -2 * far * near / (far - near)
+    M_ndc = np.array([[2 * fx / w, 0, 0, 0], [0, 2 * fx / h, 0, 0], [0, 0, a, b], [0, 0, 1, 0]], np.float32)
+    M_uv = np.array([[w / 2, 0, 0, w / 2], [0, h / 2, 0, h / 2], [0, 0, 1, 0]], np.float32)
+    return M_ndc, M_uv
+
+
+def make_invisible_fixture(ngp_mt, G=32, n_cams=20):
+    """NGPMT.mark_invisible_cells (ngp_mt.py:274-337) of the reference on a G^3 grid: the pinhole K
+    branch and the (M_ndc_from_cam, M_uv_from_ndc, shift, scale) tuple branch, the synthetic
+    scene's first n_cams poses.  Buffers as train_nerf.py:153-157 registers them (kornia
+    create_meshgrid3d order, as ncnerf_amd.ngp_mt.register_grid_buffers)."""
+    from ncnerf_amd import synthetic
+    scene = SyntheticScene()
+    poses = torch.from_numpy(scene.poses[:n_cams].astype(np.float32))
+    fx = (synthetic.IMG_W / 2) / np.tan(synthetic.HFOV / 2)
+    K = torch.tensor([[fx, 0, synthetic.IMG_W / 2], [0, fx, synthetic.IMG_H / 2], [0, 0, 1]], dtype=torch.float32)
+    M_ndc, M_uv = ndc_matrices(fx, synthetic.IMG_W, synthetic.IMG_H)
+    out = dict(G=np.array(G), n_cams=np.array(n_cams), near=np.array(0.01, np.float32), K=K.numpy(), M_ndc=M_ndc,
+               M_uv=M_uv, ndc_scale=np.array(0.5, np.float32))
+    for name, Kx in (("pinhole", K), ("ndc", (torch.from_numpy(M_ndc), torch.from_numpy(M_uv), [0.0, 0.0, 0.0], 0.5))):
+        model = ngp_mt.NGPMT(scale=0.5, grid_size=G)
+        model.register_buffer("density_grid", torch.zeros(model.cascades, G ** 3))
+        r = torch.arange(G, dtype=torch.int32)
+        zz, yy, xx = torch.meshgrid(r, r, r, indexing="ij")
+        model.register_buffer("grid_coords", torch.stack([xx, yy, zz], -1).reshape(-1, 3).contiguous())
+        model.mark_invisible_cells(Kx, torch.device("cpu"), poses, (synthetic.IMG_W, synthetic.IMG_H), 0.01,
+                                   chunk=5000)
+        out[name + "_density"] = model.density_grid.numpy().astype(np.int8)  # 0 / -1
+        out[name + "_count"] = np.rint(model.count_grid.numpy() * n_cams).astype(np.uint8)  # cameras covering
+        print(f"invisible_cells.npz {name}: valid {(model.density_grid == 0).float().mean():.3f}")
+    np.savez_compressed(os.path.join(HERE, "invisible_cells.npz"), **out)
+
+
 def main():
     install_stubs()
     import importlib
     rendering = importlib.import_module("models.rendering")
     ngp_mt = importlib.import_module("models.ngp_mt")
     losses = importlib.import_module("losses")
-    make_render_fixture(rendering, ngp_mt)
-    make_loss_fixture(losses)
-    make_loss_fixture(losses, n_rays=1024, seed=5, name="loss_cluster_ramp.npz", step=1200)
-    make_select_fixture(losses)
+    only = sys.argv[1:]
+    if not only or "render" in only:
+        make_render_fixture(rendering, ngp_mt)
+    if not only or "loss" in only:
+        make_loss_fixture(losses)
+        make_loss_fixture(losses, n_rays=1024, seed=5, name="loss_cluster_ramp.npz", step=1200)
+    if not only or "select" in only:
+        make_select_fixture(losses)
+    if not only or "invisible" in only:
+        make_invisible_fixture(ngp_mt)
 
 
 if __name__ == "__main__":

@@ -136,3 +136,28 @@ def test_grid_refresh_erode(dev):
     n, idx, xyz, sig = _hits(m)
     new_ref, _, _ = vren_ref.density_grid_update(old, idx, sig, 0.95, 1e4, count_grid=cnt)
     np.testing.assert_allclose(m.density_grid.cpu().numpy(), new_ref, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("branch", ["pinhole", "ndc"])
+def test_mark_invisible_cells_golden(dev, branch):
+    """NGPMT.mark_invisible_cells vs the reference's own (tests/golden/invisible_cells.npz, made by
+    tests/golden/make_golden.py from models/ngp_mt.py:274-337 on a 32^3 grid, 20 synthetic poses):
+    the 0 / -1 marks and the per-cell camera counts.  The projections run as fp32 matmuls on the
+    device (the fixture: torch CPU), so a cell projecting within rounding of an image border or of
+    the near plane may flip: at most 0.05 % of the cells."""
+    import os
+    from ncnerf_amd import synthetic
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "invisible_cells.npz"))
+    G, n_cams = int(f["G"]), int(f["n_cams"])
+    m = register_grid_buffers(NGPMT(scale=0.5, grid_size=G).to(dev))
+    scene = synthetic.SyntheticScene()
+    poses = torch.from_numpy(scene.poses[:n_cams].astype(np.float32)).to(dev)
+    K = torch.from_numpy(f["K"]) if branch == "pinhole" else (torch.from_numpy(f["M_ndc"]), torch.from_numpy(f["M_uv"]),
+                                                              [0.0, 0.0, 0.0], float(f["ndc_scale"]))
+    m.mark_invisible_cells(K, dev, poses, (synthetic.IMG_W, synthetic.IMG_H), float(f["near"]), chunk=5000)
+    dens = m.density_grid.cpu().numpy()
+    cnt = np.rint(m.count_grid.cpu().numpy() * n_cams).astype(np.int64)
+    bad_d = int((dens != f[branch + "_density"].astype(np.float32)).sum())
+    bad_c = int((cnt != f[branch + "_count"].astype(np.int64)).sum())
+    assert set(np.unique(dens).tolist()) <= {0.0, -1.0}
+    assert bad_d <= 0.0005 * dens.size and bad_c <= 0.0005 * dens.size, (bad_d, bad_c)

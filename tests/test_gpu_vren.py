@@ -324,3 +324,33 @@ def test_composite_background_fused(dev, scene):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     for a, b in zip(res[0][2:], res[1][2:]):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
+
+
+@pytest.mark.parametrize("n", [512, 1])
+def test_raymarcher_backward_segment_csr(dev, scene, n):
+    """RayMarcher.backward (custom_functions.py:102-112) against the reference's segment_csr
+    restated (oracle.vren_ref.raymarcher_backward), incl. rays with no samples; and against the
+    geometry it differentiates: xyzs = o + t*d, dirs = d."""
+    from ncnerf_amd.custom_functions import RayMarcher
+    o, d, ht, noise = _march_inputs(scene, n, 3 + n, dev)
+    if n > 1:
+        ht[n // 2] = -1.0  # a missed ray (q9): an empty segment in the middle
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    ro, rd = T(o).requires_grad_(), T(d).requires_grad_()
+    rays_a, xyzs, dirs, deltas, ts, total = RayMarcher.apply(ro, rd, T(ht), T(scene.bitfield), 1, 0.5, 0.0, 128, 1024,
+                                                             T(noise))
+    g = torch.Generator(device=dev).manual_seed(n)
+    wx = torch.randn(xyzs.shape, device=dev, generator=g)
+    wd = torch.randn(dirs.shape, device=dev, generator=g)
+    ((xyzs * wx).sum() + (dirs * wd).sum()).backward()
+    ref_o, ref_d = vren_ref.raymarcher_backward(rays_a.cpu().numpy(), ts.detach().cpu().numpy(), wx.cpu().numpy(),
+                                                wd.cpu().numpy())
+    np.testing.assert_allclose(ro.grad.cpu().numpy(), ref_o, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(rd.grad.cpu().numpy(), ref_d, rtol=1e-5, atol=1e-5)
+    if n > 1:
+        assert int(rays_a[n // 2, 2]) == 0 and float(ro.grad[n // 2].abs().sum()) == 0.0
+        # rows are rays in ray order, so segment i is ray i's samples: d/do (o + t d) = I, d/dd = t I
+        ra = rays_a.cpu().numpy()
+        i = int(np.argmax(ra[:, 2]))
+        s0, c = int(ra[i, 1]), int(ra[i, 2])
+        np.testing.assert_allclose(ro.grad[i].cpu().numpy(), wx[s0:s0 + c].sum(0).cpu().numpy(), rtol=1e-5, atol=1e-5)

@@ -90,3 +90,19 @@ def test_cluster_selection_cases():
         lab, cn = losses_ref.cluster_select(C, a, 0.99)
         assert np.array_equal(lab, f[f"labels{i}"]), i
         np.testing.assert_allclose(cn, f[f"centrs{i}"], atol=1e-7)
+
+
+def test_oracle_mark_invisible_cells_golden():
+    """oracle/grid_ref.mark_invisible_cells (the PSNR-trajectory oracle's init) reproduces the
+    reference's NGPMT.mark_invisible_cells on the golden 32^3 grid (pinhole branch): the 0 / -1
+    marks and camera counts, exactly."""
+    import os
+    from oracle import grid_ref
+    from ncnerf_amd import synthetic
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "invisible_cells.npz"))
+    G, n_cams = int(f["G"]), int(f["n_cams"])
+    poses = synthetic.SyntheticScene().poses[:n_cams].astype(np.float32)
+    dens, cnt = grid_ref.mark_invisible_cells(f["K"], poses, (synthetic.IMG_W, synthetic.IMG_H), float(f["near"]), G,
+                                              0.5, chunk=5000)
+    assert np.array_equal(dens, f["pinhole_density"].astype(np.float32))
+    assert np.array_equal(np.rint(cnt * n_cams).astype(np.uint8), f["pinhole_count"])
