@@ -284,6 +284,12 @@ int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacit
                       const float* dL_dnormals, const float* up_total, const float* up_terms, float* dL_drgb,
                       float* dL_dopacity, float* dL_ddepth, void* stream);
 
+/* ---- step inputs (train_nerf.py:208: the batch handed to training_step): copies n_bufs <= 8 device
+ *      buffers (src[b] -> dst[b], n_bytes[b]; HOST arrays of device pointers) and writes `step` to
+ *      *step_dst (may be NULL) in ONE launch — the new batch into a captured step's static inputs. ---- */
+int ncn_step_inputs(int n_bufs, const void* const* src, void* const* dst, const int64_t* n_bytes, int64_t* step_dst,
+                    int64_t step, void* stream);
+
 /* ---- optimizer (train_nerf.py:262-291, 954-955): global-norm clip + Adam over a flat buffer. ---- */
 /* step_inc: NULL, or a device int incremented once (the optimizer step counter of a captured step) */
 int ncn_sumsq(const float* x, int64_t n, float* out_partial /* >= 1024 floats */, int* step_inc, void* stream);

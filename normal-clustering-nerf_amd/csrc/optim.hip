@@ -199,11 +199,52 @@ __global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, 
         if (ZERO) g[i] = 0.f;
     }
 }
+// The step's inputs in one launch: up to NCN_STEP_MAX_BUFS buffer copies (the new batch into the
+// captured graph's static input buffers) plus the device step counter the graph reads — instead of
+// a multi-tensor copy launch and a fill launch ahead of every replay.  Workgroup b copies the 16-B
+// chunks b, b + grid, ... of every buffer (bytes past the last whole chunk: byte copies).
+constexpr int NCN_STEP_MAX_BUFS = 8;
+struct StepCopies {
+    const unsigned char* src[NCN_STEP_MAX_BUFS];
+    unsigned char* dst[NCN_STEP_MAX_BUFS];
+    int64_t bytes[NCN_STEP_MAX_BUFS];
+};
+__global__ __launch_bounds__(256) void step_inputs_kernel(StepCopies c, int nb, int64_t* step_dst, int64_t step) {
+    if (step_dst && blockIdx.x == 0 && threadIdx.x == 0) *step_dst = step;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+    for (int b = 0; b < nb; b++) {
+        const bool al = (((uintptr_t)c.src[b] | (uintptr_t)c.dst[b]) & 15) == 0;
+        const int64_t n16 = al ? c.bytes[b] / 16 : 0;
+        for (int64_t i = tid; i < n16; i += nth) ((uint4*)c.dst[b])[i] = ((const uint4*)c.src[b])[i];
+        for (int64_t i = 16 * n16 + tid; i < c.bytes[b]; i += nth) c.dst[b][i] = c.src[b][i];
+    }
+}
+
 }  // namespace ncn
 
 using namespace ncn;
 
 extern "C" {
+
+int ncn_step_inputs(int n_bufs, const void* const* src, void* const* dst, const int64_t* n_bytes, int64_t* step_dst,
+                    int64_t step, void* stream) {
+    NCN_REQUIRE(n_bufs >= 0 && n_bufs <= NCN_STEP_MAX_BUFS, hipErrorInvalidValue,
+                "ncn_step_inputs: at most 8 buffers");
+    StepCopies c{};
+    int64_t total = 0;
+    for (int b = 0; b < n_bufs; b++) {
+        NCN_REQUIRE(n_bytes[b] >= 0 && (n_bytes[b] == 0 || (src[b] && dst[b])), hipErrorInvalidValue,
+                    "ncn_step_inputs: null buffer");
+        c.src[b] = (const unsigned char*)src[b];
+        c.dst[b] = (unsigned char*)dst[b];
+        c.bytes[b] = n_bytes[b];
+        total += n_bytes[b];
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(256, (total / 16 + 255) / 256));
+    hipLaunchKernelGGL(step_inputs_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, c, n_bufs, step_dst, step);
+    NCN_LAUNCH_CHECK("ncn_step_inputs");
+    return 0;
+}
 
 int ncn_sumsq(const float* x, int64_t n, float* out_partial, int* step_inc, void* stream) {
     hipLaunchKernelGGL(sumsq_kernel, dim3(SUMSQ_BLOCKS), dim3(256), 0, (hipStream_t)stream, x, n, out_partial,

@@ -38,6 +38,7 @@ SIGNATURES = {
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
     "ncn_composite_train_fw_bg": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, F32, P, P],
     "ncn_count_samples": [P, I64, P, P, P, P],
+    "ncn_step_inputs": [I32, P, P, P, P, I64, P],
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, I32, P],
@@ -143,6 +144,18 @@ def ptr(t):
     if t is None:
         return P(None)
     return P(t.data_ptr())
+
+
+def step_inputs(srcs, dsts, step_dev, step):
+    """ncn_step_inputs: copy each srcs[i] into dsts[i] (contiguous CUDA tensors of equal size) and
+    write `step` into the int64 device scalar step_dev, in one launch."""
+    n = len(srcs)
+    VP = ctypes.c_void_p * max(n, 1)
+    src = VP(*[s.data_ptr() for s in srcs])
+    dst = VP(*[d.data_ptr() for d in dsts])
+    nb = (ctypes.c_int64 * max(n, 1))(*[s.numel() * s.element_size() for s in srcs])
+    return call("ncn_step_inputs", I32(n), ctypes.cast(src, P), ctypes.cast(dst, P), ctypes.cast(nb, P),
+                ptr(step_dev), I64(int(step)), stream())
 
 
 def check_input(t, name):

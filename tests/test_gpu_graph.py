@@ -78,3 +78,21 @@ def test_graph_step_matches_eager(dev):
     # the MLP weights (dense, large gradients) agree tightly
     rel_w = float((params[2][n_t:] - params[0][n_t:]).norm() / params[0][n_t:].norm())
     assert rel_w < 1e-3, rel_w
+
+
+def test_step_inputs_copy(dev):
+    """ncn_step_inputs: every buffer copied byte for byte (16-B chunks, byte tails, unaligned views),
+    the device step counter written, in one launch."""
+    from ncnerf_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(0)
+    srcs = [torch.randn(n, device=dev, generator=g) for n in (1, 17, 8192 * 3, 100003)]
+    srcs.append(torch.randint(0, 1 << 40, (777,), device=dev, dtype=torch.int64, generator=g))
+    base = torch.randn(64, device=dev, generator=g)
+    srcs.append(base[1:34])  # (a view at a 4-B offset: byte-copy path)
+    dsts = [torch.full_like(s, -7) for s in srcs]
+    step = torch.zeros((), dtype=torch.int64, device=dev)
+    _lib.step_inputs(srcs, dsts, step, 123456789012)
+    torch.cuda.synchronize()
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(s, d)
+    assert int(step) == 123456789012
