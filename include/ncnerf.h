@@ -185,6 +185,10 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   int precision, int mode, float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream);
 /* Backward: accumulates (+=) into grad_table (n_entries,2) and writes per-block weight-gradient
  * slabs (n_blocks x NCN_FIELD_NW) into `slab`; ncn_field_reduce_wgrad sums them into grad_w (+=).
+ * loss_scale: NULL, or a device float S (a power of two): the AMP loss scale of the reference's
+ * precision=16 run (torch GradScaler, train_nerf.py:954) — the MLP chain runs on the upstream
+ * gradients times S (no fp16 underflow) and the outputs leave divided by S (ncn_adam_step's
+ * amp_state keeps S and its growth/backoff).
  * n_blocks is returned by ncn_field_bwd_blocks(n).  dE_ws is a device workspace of
  * ncn_field_bwd_dE_floats(n) floats (the level-major encoding gradient between the MLP pass and the
  * LDS-aggregating table scatter pass). */
@@ -193,8 +197,8 @@ int64_t ncn_field_bwd_dE_floats(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                   const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision,
-                  const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* grad_table,
-                  float* slab, float* dE_ws,
+                  const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, const float* loss_scale,
+                  float* grad_table, float* slab, float* dE_ws,
                   float* level_max /* 16 * ncn_field_bwd_blocks(n) floats of workspace (per-level max |dE|) */,
                   void* stream);
 /* ncn_field_bwd in its two passes (the data-parallel step overlaps the gradient all-reduce of one
@@ -205,7 +209,7 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
 int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
-                      float* slab, float* dE_ws, float* level_max, void* stream);
+                      const float* loss_scale, float* slab, float* dE_ws, float* level_max, void* stream);
 int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
@@ -307,7 +311,14 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
  * the gradient it consumed (the next step's zero_grad folded in).  Buffers 16-byte aligned. */
 int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
                   float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, int zero_grads, void* stream);
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, void* stream);
+/* amp_state: NULL, or the GradScaler state of an AMP (fp16) run, device floats {scale, growth
+ * tracker}: a gradient whose norm is not finite skips the update (parameters and moments unchanged,
+ * step counter not advanced; the gradient is still zeroed with zero_grads) and halves the scale;
+ * after NCN_AMP_GROWTH_INTERVAL finite steps in a row the scale doubles (torch.cuda.amp.GradScaler
+ * defaults: init 2^16, factors 2 / 0.5, interval 2000). */
+#define NCN_AMP_INIT_SCALE 65536.0f
+#define NCN_AMP_GROWTH_INTERVAL 2000
 int64_t ncn_adam_step_work_floats(void);
 
 #ifdef __cplusplus

@@ -462,7 +462,7 @@ template <typename T>
 __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, int lane,
                                          const typename Mfma<T>::v8* __restrict__ enc, const float* __restrict__ dirs,
                                          const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
-                                         const int32_t* __restrict__ order) {
+                                         const int32_t* __restrict__ order, float S) {
     const int64_t pos = grp * 16 + (lane & 15);  // processing position (enc_cache / dE order)
     const bool valid = pos < n;
     in.e = enc[grp * 64 + lane];
@@ -470,8 +470,8 @@ __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, i
     if (valid) {
         const int64_t s = order ? (int64_t)order[pos] : pos;
         in.dx = dirs[3 * s]; in.dy = dirs[3 * s + 1]; in.dz = dirs[3 * s + 2];
-        in.dsig = dL_dsig ? dL_dsig[s] : 0.f;
-        if (dL_drgb) { in.dr0 = dL_drgb[3 * s]; in.dr1 = dL_drgb[3 * s + 1]; in.dr2 = dL_drgb[3 * s + 2]; }
+        in.dsig = dL_dsig ? dL_dsig[s] * S : 0.f;
+        if (dL_drgb) { in.dr0 = dL_drgb[3 * s] * S; in.dr1 = dL_drgb[3 * s + 1] * S; in.dr2 = dL_drgb[3 * s + 2] * S; }
     }
 }
 
@@ -482,7 +482,7 @@ __device__ __forceinline__ float lmax_upd(float m, float a, float b) {  // non-f
 template <typename T>
 __device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const BwdIn<T>& cur, int64_t grp,
                                           int64_t n, int64_t n_stride, int lane, float* __restrict__ dE_out,
-                                          float (&lm)[4]) {
+                                          float (&lm)[4], float inv_S) {
     typedef Mfma<T> M;
     typedef typename M::v4 v4;
     typedef typename M::v8 v8;
@@ -552,6 +552,10 @@ __device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const
 #pragma unroll
     for (int t = 0; t < 2; t++)
         dE[t] = M::k32(F.a32(B_L1 + 2 * t + 1, lane), d1b, M::k32(F.a32(B_L1 + 2 * t, lane), d1a, zero4()));
+#pragma unroll
+    for (int t = 0; t < 2; t++)  // (loss scale off: an exact power of two)
+#pragma unroll
+        for (int i = 0; i < 4; i++) dE[t][i] *= inv_S;
     // per-level max |dE| of this lane's levels (2g, 2g+1, 8+2g, 9+2g): the scatter's fixed-point scale
     lm[0] = lmax_upd(lm[0], dE[0][0], dE[0][1]);
     lm[1] = lmax_upd(lm[1], dE[0][2], dE[0][3]);
@@ -613,8 +617,12 @@ __device__ __forceinline__ void bwd_dw(const uint16_t* X, int ng, int wid, int l
 // The owned tiles (C layout: lane (g,r) = rows 4g+i, column r) into the workgroup's slab row.
 // W3 columns: the h tile's column r is input 3+r; the [d, pad] tile's column q is input q (d) or
 // 16+q (the 13 constant-1 padding inputs, whose gradient is the plain sum of dY).
-__device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, int lane, const float4_t (&acc)[5]) {
+__device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, int lane, float4_t (&acc)[5], float inv_S) {
     const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 5; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[t][i] *= inv_S;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int row = 4 * g + i;
@@ -646,9 +654,12 @@ template <typename T>
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const uint16_t* __restrict__ wpacked,
     const typename Mfma<T>::v8* __restrict__ enc_cache, const float* __restrict__ dL_dsig,
-    const float* __restrict__ dL_drgb, float* __restrict__ dE_out, float* __restrict__ slab,
-    float* __restrict__ level_max, const int32_t* __restrict__ order) {
+    const float* __restrict__ dL_drgb, const float* __restrict__ loss_scale, float* __restrict__ dE_out,
+    float* __restrict__ slab, float* __restrict__ level_max, const int32_t* __restrict__ order) {
     typedef typename Mfma<T>::v4 v4;
+    // AMP loss scale (GradScaler of the reference's precision=16 run): the fp16 chain sees the
+    // upstream gradients times S (a power of two), dE and dW leave it divided by S
+    const float S = loss_scale ? *loss_scale : 1.f, inv_S = 1.f / S;
     typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     if (n_dev) n = min<int64_t>(n, *n_dev);
@@ -671,24 +682,25 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t stride = (int64_t)gridDim.x * BWD_WAVES;
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
     BwdIn<T> nxt;
-    if (base + wid < n_groups) bwd_load<T>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order);
+    if (base + wid < n_groups) bwd_load<T>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order, S);
     for (; base < n_groups; base += stride) {
         const int64_t grp = base + wid;
         const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
         const BwdIn<T> cur = nxt;
-        if (grp + stride < n_groups) bwd_load<T>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order);
+        if (grp + stride < n_groups)
+            bwd_load<T>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order, S);
         if (grp < n_groups) {
             Frags<T> F;
             const int z = opaque_zero();
             F.f32 = F32s + z;
             F.f16 = F16s + z;
-            bwd_group<T>(F, X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm);
+            bwd_group<T>(F, X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S);
         }
         lds_barrier();  // (the dE stores and the next step's loads stay in flight)
         bwd_dw<T>(X, ng, wid, lane, acc);
         lds_barrier();
     }
-    bwd_store_dw(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc);
+    bwd_store_dw(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc, inv_S);
     // level maxima: the 16 lanes of a row (same g) share their 4 levels; the row leaders of the 8
     // waves meet in LDS and the workgroup writes its row of level_max [blocks][16] (no atomics: the
     // scatter reduces the rows)
@@ -764,7 +776,7 @@ constexpr int SC_REC = 64;                 // staged run records per wave (80 B 
 // ONE 64-bit word (y * 2^32 + x: one ds_add_u64 per corner, 14 B per slot); 0 keeps two 64-bit sums
 // (22 B per slot).
 #ifndef NCN_SC_PACK
-#define NCN_SC_PACK 1
+#define NCN_SC_PACK 0
 #endif
 constexpr bool SC_PACK = NCN_SC_PACK != 0;
 constexpr int SC_SLOT_BYTES = SC_PACK ? 4 + 8 + 2 : 4 + 8 + 8 + 2;
@@ -785,11 +797,13 @@ constexpr int sc_layout_bytes(int sets, bool staging) {
 #ifndef SC_CELL_HI
 #define SC_CELL_HI 10
 #endif
+// Values per cell slot: 8 packed words (SC_PACK) or 16 64-bit sums (x and y of the 8 corners).
+constexpr int SC_CELL_VALS = SC_PACK ? 8 : 16;
 #ifndef NCN_SC_SETS_CELL
-#define NCN_SC_SETS_CELL 512
+#define NCN_SC_SETS_CELL (SC_PACK ? 512 : 256)
 #endif
 constexpr int SC_SETS_CELL = NCN_SC_SETS_CELL * SC_THREADS / 1024;
-constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + 8 * 8 + 2); }
+constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2); }
 constexpr int sc_max(int a, int b) { return a > b ? a : b; }
 constexpr int SC_ARENA = sc_max(sc_cell_bytes(SC_SETS_CELL),
                                 sc_max(sc_layout_bytes(SC_SETS_RUN, true), sc_layout_bytes(SC_SETS_DIR, false)));
@@ -814,6 +828,8 @@ __device__ __forceinline__ unsigned long long sc_fix2(float x, float y, int k) {
     return ((unsigned long long)(uint32_t)(yi + (xi >> 31)) << 32) | (uint32_t)xi;
 }
 __device__ __forceinline__ float sc_q(float v, int k) { return ldexpf(rintf(ldexpf(v, k)), -k); }
+// a non-zero v that rounds to 0 on the grid 2^-k
+__device__ __forceinline__ bool sc_sub_quantum(float v, int k) { return v != 0.f && fabsf(ldexpf(v, k)) < 0.5f; }
 __device__ __forceinline__ void sc_unpack(long long q, int& xs, int& ys) {
     xs = (int)(uint32_t)q;
     ys = (int)((q - (long long)xs) >> 32);
@@ -860,7 +876,7 @@ __device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fil
     sh.slots = (int)sh.sets * SC_WAYS;
     sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used, records (16-B aligned)
     // (packed: one value array; cell mode: 8 corner arrays)
-    sh.valy = mode == SC_MODE_CELL ? sh.valx + 7 * sh.slots : SC_PACK ? sh.valx : sh.valx + sh.slots;
+    sh.valy = mode == SC_MODE_CELL ? sh.valx + (SC_CELL_VALS - 1) * sh.slots : SC_PACK ? sh.valx : sh.valx + sh.slots;
     sh.keys = (uint32_t*)(sh.valy + sh.slots);
     sh.used = (uint16_t*)(sh.keys + sh.slots);
     sh.rec = (ScRec*)(sh.used + sh.slots);
@@ -930,15 +946,23 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
             kk[b] = *(const uint4*)&sh.keys[p0[b]];
         }
         int sl[SC_BATCH];
-        bool vc[SC_BATCH], miss = false;
+        bool vc[SC_BATCH], ex[SC_BATCH], miss = false;
 #pragma unroll
         for (int b = 0; b < SC_BATCH; b++) {
             const uint32_t k = e[c0 + b];
-            vc[b] = (v[2 * (c0 + b)] != 0.f) | (v[2 * (c0 + b) + 1] != 0.f);
+            const float vx = v[2 * (c0 + b)], vy = v[2 * (c0 + b) + 1];
+            // (packed) a non-zero component below half the fixed-point quantum would round to 0: the
+            // corner goes to global memory exactly, so every entry the oracle's f32 sums give a
+            // gradient gets one (Adam with eps 1e-15 steps a tiny gradient by a full lr)
+            ex[b] = SC_PACK && (sc_sub_quantum(vx, L.k) || sc_sub_quantum(vy, L.k));
+            vc[b] = ((vx != 0.f) | (vy != 0.f)) && !ex[b];
             sl[b] = kk[b].x == k ? p0[b] : kk[b].y == k ? p0[b] + 1 : kk[b].z == k ? p0[b] + 2
                   : kk[b].w == k ? p0[b] + 3 : -1;
             miss |= vc[b] && sl[b] < 0;
         }
+#ifdef NCN_DIAG_SC_NO_CLAIM
+        miss = false;  // diagnostic: misses are neither claimed nor added
+#endif
         if (__ballot(miss)) {  // uniform
 #pragma unroll
             for (int b = 0; b < SC_BATCH; b++) {
@@ -980,17 +1004,20 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
         }
         bool full = false;
 #pragma unroll
-        for (int b = 0; b < SC_BATCH; b++) full |= vc[b] && sl[b] < 0;
-        if (__ballot(full)) {  // uniform: some lane's set is full of other entries
+        for (int b = 0; b < SC_BATCH; b++) full |= (vc[b] && sl[b] < 0) || ex[b];
+        if (__ballot(full)) {  // uniform: some lane's set is full of other entries, or an exact corner
 #pragma unroll
             for (int b = 0; b < SC_BATCH; b++) {
                 const int c = c0 + b;
-                if (vc[b] && sl[b] < 0) {
+                if ((vc[b] && sl[b] < 0) || ex[b]) {
 #ifndef NCN_DIAG_SC_NO_FALLBACK
-                    // (packed: rounded to the table's fixed-point grid like every LDS addend, so which
-                    // corners fall back — claim order — moves the result by float-add order only)
-                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]), SC_PACK ? sc_q(v[2 * c], L.k) : v[2 * c]);
-                    atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, SC_PACK ? sc_q(v[2 * c + 1], L.k) : v[2 * c + 1]);
+                    // (packed: a set-full corner is rounded to the table's fixed-point grid like every
+                    // LDS addend, so which corners fall back — claim order — moves the result by
+                    // float-add order only; a sub-quantum one is added exactly)
+                    const float gx = SC_PACK && !ex[b] ? sc_q(v[2 * c], L.k) : v[2 * c];
+                    const float gy = SC_PACK && !ex[b] ? sc_q(v[2 * c + 1], L.k) : v[2 * c + 1];
+                    if (gx != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + e[c]), gx);
+                    if (gy != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, gy);
 #endif
                 }
             }
@@ -1271,20 +1298,39 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
             }
         }
     }
-    if (go && sl >= 0) {
+    // (packed) sub-quantum corners (a non-zero component that would round to 0) go to global
+    // memory exactly
+    uint32_t exm = 0;
+    if constexpr (SC_PACK) {
 #pragma unroll
         for (int c = 0; c < 8; c++)
-            if (v[2 * c] != 0.f || v[2 * c + 1] != 0.f)
+            exm |= (sc_sub_quantum(v[2 * c], L.k) || sc_sub_quantum(v[2 * c + 1], L.k)) ? 1u << c : 0u;
+    }
+    if (go && sl >= 0) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            if ((v[2 * c] == 0.f && v[2 * c + 1] == 0.f) || ((exm >> c) & 1)) continue;
+            if constexpr (SC_PACK) {
                 atomicAdd((unsigned long long*)&sh.valx[c * sh.slots + sl], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
+            } else {  // x and y of corner c: arrays 2c, 2c + 1
+                atomicAdd((unsigned long long*)&sh.valx[(2 * c) * sh.slots + sl], (unsigned long long)sc_fix(v[2 * c], L.k));
+                atomicAdd((unsigned long long*)&sh.valx[(2 * c + 1) * sh.slots + sl],
+                          (unsigned long long)sc_fix(v[2 * c + 1], L.k));
+            }
+        }
     }
     const bool fb = act && sl < 0;
-    if (__ballot(fb)) {  // uniform: set full or cell outside the key range: straight to the table
-        if (fb) {
+    if (__ballot(fb || (act && exm))) {  // uniform: set full / cell outside the key range / exact corners
+        if (fb || (act && exm)) {
 #pragma unroll
             for (int c = 0; c < 8; c++) {
+                const bool exact = (exm >> c) & 1;
+                if (!fb && !exact) continue;
                 const uint32_t e = L.off + sc_corner_entry(L, px, py, pz, c);
-                if (v[2 * c] != 0.f) atomicAdd(grad + 2 * (size_t)e, sc_q(v[2 * c], L.k));
-                if (v[2 * c + 1] != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, sc_q(v[2 * c + 1], L.k));
+                const float gx = exact || !SC_PACK ? v[2 * c] : sc_q(v[2 * c], L.k);
+                const float gy = exact || !SC_PACK ? v[2 * c + 1] : sc_q(v[2 * c + 1], L.k);
+                if (gx != 0.f) atomicAdd(grad + 2 * (size_t)e, gx);
+                if (gy != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, gy);
             }
         }
     }
@@ -1330,27 +1376,34 @@ __device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C
     }
 }
 
-// Flush of a cell unit: 8 lanes per claimed cell (one corner each: decode the packed sums, form the
-// corner's entry, two f32 global adds); the corner-0 lane resets the key, each lane its value.
+// Flush of a cell unit: SC_CELL_VALS lanes per claimed cell (packed: one corner each, decode both
+// sums; 64-bit: one corner component each), form the corner's entry, f32 global adds; lane 0 of
+// the cell resets the key, each lane its value.
 __device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, float* __restrict__ grad) {
     const int nf = *sh.fill;
-    for (int i = threadIdx.x; i < 8 * nf; i += SC_THREADS) {
-        const int slot = sh.used[i >> 3], c = i & 7;
+    constexpr int V = SC_CELL_VALS;
+    for (int i = threadIdx.x; i < V * nf; i += SC_THREADS) {
+        const int slot = sh.used[i / V], j = i % V;
         const uint32_t key = sh.keys[slot];
-        long long* pv = &sh.valx[c * sh.slots + slot];
+        long long* pv = &sh.valx[j * sh.slots + slot];
         const long long q = *pv;
         *pv = 0;
 #ifndef NCN_DIAG_SC_NO_FLUSH
         if (q != 0) {
-            int xs, ys;
-            sc_unpack(q, xs, ys);
+            const int c = SC_PACK ? j : j >> 1;
             const uint32_t e = L.off + sc_corner_entry(L, key & 2047u, (key >> 11) & 2047u, key >> 22, c);
-            if (xs) atomicAdd(grad + 2 * (size_t)e, ldexpf((float)xs, -L.k));
-            if (ys) atomicAdd(grad + 2 * (size_t)e + 1, ldexpf((float)ys, -L.k));
+            if constexpr (SC_PACK) {
+                int xs, ys;
+                sc_unpack(q, xs, ys);
+                if (xs) atomicAdd(grad + 2 * (size_t)e, ldexpf((float)xs, -L.k));
+                if (ys) atomicAdd(grad + 2 * (size_t)e + 1, ldexpf((float)ys, -L.k));
+            } else {
+                atomicAdd(grad + 2 * (size_t)e + (j & 1), (float)ldexp((double)q, -L.k));
+            }
         }
 #endif
-        if (c == 0) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the other 7 lanes have read the key: same wave)
+        if (j == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the cell's other lanes have read the key: same wave)
             sh.keys[slot] = SC_EMPTY;
         }
     }
@@ -1470,9 +1523,9 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     L.direct = !isfinite(m);  // (uniform) non-finite gradient: every corner straight to global memory
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
-    // packed 32-bit halves: |sum| <= (unit samples) * m * 2^k + rounding < 2^31
+    // |sum| <= (unit samples) * m * 2^k + rounding: below 2^31 (packed 32-bit halves) / 2^62 (64-bit)
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
-    L.k = 30 - lg_unit - e2;
+    L.k = (SC_PACK ? 30 : 61) - lg_unit - e2;
     ScChunk<C> ch;
     const int64_t lane_off = (int64_t)(lane * SC_WAVES + wid) * C;
     sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, nrm, order);
@@ -1542,7 +1595,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         if (mode != layout) {  // (re)initialise the table of the new layout
             lds_barrier();
             sh = sc_layout(arena, wmax, fill, mode);
-            const int nv = mode == SC_MODE_CELL ? 8 * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
+            const int nv = mode == SC_MODE_CELL ? SC_CELL_VALS * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
             for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
             for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
             if (threadIdx.x == 0) fill[0] = fill[1] = 0;
@@ -1686,7 +1739,7 @@ int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(in
 int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
-                      float* slab, float* dE_ws, float* level_max, void* stream) {
+                      const float* loss_scale, float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,
                 "ncn_field_bwd_mlp: precision must be NCN_PREC_F16 or NCN_PREC_BF16");
@@ -1696,11 +1749,11 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
     if (precision == NCN_PREC_F16)
         hipLaunchKernelGGL(field_bwd_kernel<_Float16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
                            (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<_Float16>::v8*)enc_cache,
-                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max, order);
+                           dL_dsigmas, dL_drgbs, loss_scale, dE_ws, slab, level_max, order);
     else
         hipLaunchKernelGGL(field_bwd_kernel<__bf16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
                            (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<__bf16>::v8*)enc_cache,
-                           dL_dsigmas, dL_drgbs, dE_ws, slab, level_max, order);
+                           dL_dsigmas, dL_drgbs, loss_scale, dE_ws, slab, level_max, order);
     NCN_LAUNCH_CHECK("ncn_field_bwd_mlp");
     return 0;
 }
@@ -1726,11 +1779,11 @@ int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const 
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                   const uint32_t* levels,
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision,
-                  const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, float* grad_table,
-                  float* slab, float* dE_ws, float* level_max, void* stream) {
+                  const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, const float* loss_scale,
+                  float* grad_table, float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
     const int e = ncn_field_bwd_mlp(dirs, n, n_dev, order, weights_packed, precision, enc_cache, dL_dsigmas, dL_drgbs,
-                                    slab, dE_ws, level_max, stream);
+                                    loss_scale, slab, dE_ws, level_max, stream);
     if (e) return e;
     return ncn_field_scatter(xyzs, n, n_dev, order, levels, xyz_min, xyz_extent, dE_ws, level_max, 0, 16, 0,
                              grad_table, stream);

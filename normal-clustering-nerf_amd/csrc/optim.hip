@@ -99,10 +99,11 @@ constexpr int ADAM_UNROLL = 12;      // float4 loads in flight per thread (45.8 
 __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float gscale,
                                                                float max_norm, double b1, double b2, float lr,
                                                                const float* __restrict__ lr_dev,
-                                                               int* __restrict__ step_dev, float* __restrict__ work) {
+                                                               int* __restrict__ step_dev, float* __restrict__ work,
+                                                               float* __restrict__ amp) {
     float* part = work;                                // [ADAM_BLOCKS]
     unsigned* cnt = (unsigned*)(work + ADAM_BLOCKS);   // arrival counter (left zero)
-    float* sc = work + ADAM_BLOCKS + 4;                // cf, bc1, bc2, lr
+    float* sc = work + ADAM_BLOCKS + 4;                // cf, bc1, bc2, lr, skip (AMP)
     constexpr int NW = ADAM_THREADS / 64;
     __shared__ float red[NW];
     __shared__ bool last;
@@ -154,8 +155,22 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
         t = wave_sum(t);
         if (threadIdx.x == 0) {
             const float c = max_norm / (sqrtf(t) * gscale + 1e-6f);  // norm of the scaled gradient
-            const int st = *step_dev + 1;  // device step counter
+            // GradScaler (AMP runs): a non-finite gradient skips the step and halves the scale;
+            // NCN_AMP_GROWTH_INTERVAL finite steps in a row double it
+            const bool skip = amp && !isfinite(t);
+            if (amp) {
+                float tr = skip ? 0.f : amp[1] + 1.f;
+                float scale = skip ? amp[0] * 0.5f : amp[0];
+                if (tr >= (float)NCN_AMP_GROWTH_INTERVAL) {
+                    scale *= 2.f;
+                    tr = 0.f;
+                }
+                amp[0] = scale;
+                amp[1] = tr;
+            }
+            const int st = *step_dev + (skip ? 0 : 1);  // device step counter
             *step_dev = st;
+            sc[4] = skip ? 1.f : 0.f;
             sc[0] = (max_norm > 0.f ? fminf(c, 1.0f) : 1.0f) * gscale;
             // bias corrections in double from the double betas, as apex's host code forms them
             // (1 - beta ** step in Python): 1 - 0.999f in f32 is off by 1.3e-5 relative
@@ -172,6 +187,14 @@ __global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, 
                                                          int64_t n0, float b1, float b2, float eps, float wd0,
                                                          float wd1, const float* __restrict__ sc) {
     const float cf = sc[0], bc1 = sc[1], bc2 = sc[2], lr = sc[3];
+    if (sc[4] != 0.f) {  // (uniform) skipped AMP step: only the gradient is consumed
+        if (ZERO) {
+            const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+            for (int64_t i = tid; i < n / 4; i += nth) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int64_t i = 4 * (n / 4) + tid; i < n; i += nth) g[i] = 0.f;
+        }
+        return;
+    }
     auto upd = [&](float& pi, float gr, float& mi, float& vi, float wd) {
         const float gi = gr * cf;
         mi = b1 * mi + (1.f - b1) * gi;
@@ -269,7 +292,7 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
 
 int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
                   float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, int zero_grads, void* stream) {
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
                 hipErrorInvalidValue, "ncn_adam_step: buffers must be 16-byte aligned");
@@ -277,7 +300,7 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
                 "ncn_adam_step: needs the device step counter and the work buffer");
     const int prep_blocks = (int)std::min<int64_t>(ADAM_BLOCKS, std::max<int64_t>(1, cdiv(n / 4, ADAM_THREADS * 4)));
     hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, grads, n,
-                       grad_scale, max_norm, beta1, beta2, lr, lr_dev, step_dev, work);
+                       grad_scale, max_norm, beta1, beta2, lr, lr_dev, step_dev, work, amp_state);
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
     // two float4 per thread (8 loads of p/g/m/v in flight): ~n/2048 workgroups
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 16384);
@@ -293,6 +316,6 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     return 0;
 }
 
-int64_t ncn_adam_step_work_floats(void) { return ADAM_BLOCKS + 8; }
+int64_t ncn_adam_step_work_floats(void) { return ADAM_BLOCKS + 12; }
 
 }  // extern "C"

@@ -18,6 +18,7 @@ I32 = ctypes.c_int
 U32 = ctypes.c_uint32
 F32 = ctypes.c_float
 F64 = ctypes.c_double
+AMP_INIT_SCALE = 65536.0  # NCN_AMP_INIT_SCALE (include/ncnerf.h): torch GradScaler's init_scale
 U64 = ctypes.c_uint64
 
 # name -> argtypes (stream last); every function returns int (hipError_t)
@@ -46,8 +47,8 @@ SIGNATURES = {
     "ncn_field_fwd": [P, P, I64, P, P, P, P, F32, F32, P, I32, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
     "ncn_field_bwd_dE_floats": [I64],
-    "ncn_field_bwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P],
-    "ncn_field_bwd_mlp": [P, I64, P, P, P, I32, P, P, P, P, P, P, P],
+    "ncn_field_bwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd_mlp": [P, I64, P, P, P, I32, P, P, P, P, P, P, P, P],
     "ncn_field_scatter": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
@@ -63,7 +64,7 @@ SIGNATURES = {
     "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
-    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P],
+    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P, P],
     "ncn_adam_step_work_floats": [],
     "ncn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "ncn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],

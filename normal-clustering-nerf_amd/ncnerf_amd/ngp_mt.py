@@ -122,14 +122,14 @@ class _FieldFunction(torch.autograd.Function):
         split = model.scatter_split
         if split is None:
             call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), ptr(order), model._levels_ptr, F32(model._xyz_min),
-                 F32(model._xyz_extent), ptr(packed), I32(model._prec), ptr(enc), ptr(dsig), ptr(drgb), ptr(g_table),
-                 ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
+                 F32(model._xyz_extent), ptr(packed), I32(model._prec), ptr(enc), ptr(dsig), ptr(drgb),
+                 ptr(model.amp_state), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
         else:
             # data-parallel step: the levels [split, 16) are scattered now, [0, split) later by
             # run_deferred_scatter() while the all-reduce of the first bucket is in flight
             lmax = model._level_max()
             call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(model._prec), ptr(enc),
-                 ptr(dsig), ptr(drgb),
+                 ptr(dsig), ptr(drgb), ptr(model.amp_state),
                  ptr(slab), ptr(dE_ws), ptr(lmax), stream())
             call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), model._levels_ptr, F32(model._xyz_min),
                  F32(model._xyz_extent), ptr(dE_ws), ptr(lmax), I32(split), I32(16), I32(0), ptr(g_table), stream())
@@ -191,6 +191,12 @@ class NGPMT(nn.Module):
         self.rgb_net = _ParamHolder(flat[n_table + W_SIGMA:])
         self._flat_grad = None
         self._packed = None
+        # AMP GradScaler state {scale, growth tracker} of the fp16 MLP (the reference trains with
+        # precision=16, train_nerf.py:954: the scaled loss keeps tcnn's fp16 backward from
+        # underflowing): the field backward multiplies its upstream gradients by the scale and
+        # divides its outputs by it; ncn_adam_step skips non-finite steps and grows / backs off the
+        # scale.  bf16 operands (fp32's exponent range) run unscaled, as PL's bf16 mode does.
+        self.register_buffer("amp_state", torch.tensor([_lib.AMP_INIT_SCALE, 0.0]) if precision == "fp16" else None)
         # None: the backward scatters every level.  An int L (data-parallel step): levels [L, 16)
         # are scattered in the backward, [0, L) by run_deferred_scatter() (grad_buckets(L)).
         self.scatter_split = None

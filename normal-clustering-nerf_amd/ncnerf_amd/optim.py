@@ -57,8 +57,11 @@ class FlatAdam:
         b1, b2 = self.betas
         call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
              F32(grad_scale), F32(self.max_norm), F32(self.lr), _lib.F64(b1), _lib.F64(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
-             ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), I32(1 if self.zero_grad_on_step else 0), stream())
+             ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), I32(1 if self.zero_grad_on_step else 0),
+             ptr(getattr(self.model, "amp_state", None)), stream())
 
     def state_tensors(self):
         """Every tensor the step mutates (parameters, moments, device counters)."""
-        return [self.model.flat_params(), self.m, self.v, self.step_dev, self.lr_dev]
+        st = [self.model.flat_params(), self.m, self.v, self.step_dev, self.lr_dev]
+        amp = getattr(self.model, "amp_state", None)
+        return st + ([amp] if amp is not None else [])

@@ -102,12 +102,26 @@ def hash_encode(x01, table, levels):
     return (wts * g).sum(2).reshape(n, L * F_PER_LEVEL)
 
 
+class _RoundST(torch.autograd.Function):
+    """Round to fp16/bf16 in the forward, straight-through (fp32, unrounded) in the backward: the
+    oracle's backward models the kernel's loss-scaled chain (no fp16 underflow), not an autograd
+    cast whose backward would round the gradient to fp16 too."""
+
+    @staticmethod
+    def forward(ctx, t, dt):
+        return t.to(dt).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
 def _rounder(emulate_f16=False, emulate=None):
     mode = emulate or ("fp16" if emulate_f16 else None)
     if mode is None:
         return lambda t: t
     dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[mode]
-    return lambda t: t.to(dt).float()
+    return lambda t: _RoundST.apply(t, dt)
 
 
 class FieldParams:

@@ -104,7 +104,7 @@ def run_ref(steps, every, threads, log, out=None):
     return res
 
 
-def run_hip(steps, every, log):
+def run_hip(steps, every, log, cross_check=False):
     from ncnerf_amd import synthetic
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.rendering import render
@@ -131,13 +131,31 @@ def run_hip(steps, every, log):
         b["march_noise"] = noise_of(k).to(dev)
         _, ld = tr.step(b, global_step=k)
         if (k + 1) % every == 0 or k + 1 == steps:
-            se, n = 0.0, 0
+            se, se_tr, se_or, n = 0.0, 0.0, 0.0, 0
+            P_cpu, bf_cpu = None, None
+            if cross_check:  # the same parameters and bitfield through the oracle's renderer (CPU)
+                from oracle.train_ref import render_train_ref
+                flat = m.flat_params().detach().cpu()
+                Pc, levels = field_ref.init_params(seed=INIT_SEED)
+                off, ts_ = 0, []
+                for W in Pc.tensors():
+                    ts_.append(flat[off:off + W.numel()].view_as(W).clone())
+                    off += W.numel()
+                P_cpu, bf_cpu = field_ref.FieldParams(*ts_), m.density_bitfield.cpu().numpy()
             with torch.no_grad():
                 for e in ev:
                     r = render(m, e["rays_o"], e["rays_d"], near_distance=0.01, max_samples=1024, test_time=True)
                     se += float(((r["rgb"].clamp(0, 1) - e["rgb"]) ** 2).sum())
                     n += e["rgb"].numel()
-            curve.append({"step": k + 1, "psnr": _psnr(se, n), "loss": float(ld["total"].detach()),
+                    if cross_check:
+                        rt = render(m, e["rays_o"], e["rays_d"], near_distance=0.01, max_samples=1024,
+                                    test_time=False, march_noise=torch.zeros(N_RAYS, device=dev))
+                        se_tr += float(((rt["rgb"].clamp(0, 1) - e["rgb"]) ** 2).sum())
+                        ro = render_train_ref(P_cpu, levels, e["rays_o"].cpu().numpy(), e["rays_d"].cpu().numpy(),
+                                              bf_cpu, np.zeros(N_RAYS, np.float32))
+                        se_or += float(((ro["rgb"].clamp(0, 1) - e["rgb"].cpu()) ** 2).sum())
+            extra = {"psnr_train_render": _psnr(se_tr, n), "psnr_oracle_render": _psnr(se_or, n)} if cross_check else {}
+            curve.append({"step": k + 1, "psnr": _psnr(se, n), **extra, "loss": float(ld["total"].detach()),
                           "occupied_frac": float((m.density_bitfield.cpu().numpy()[:, None] >> np.arange(8) & 1).mean()),
                           "t_s": round(time.time() - t0, 1)})
             log(json.dumps(curve[-1]))
@@ -153,6 +171,8 @@ def main():
     ap.add_argument("--ref", default=None, help="(hip) the oracle trajectory JSON")
     ap.add_argument("--repeats", type=int, default=2, help="(hip) identical-input HIP runs")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cross-check", action="store_true",
+                    help="(hip) also render the HIP parameters with the train-path renderer and the oracle's")
     a = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     if a.side == "ref":
@@ -160,7 +180,7 @@ def main():
     else:
         ref = json.load(open(a.ref)) if a.ref else None
         steps = ref["steps"] if ref else a.steps
-        runs = [run_hip(steps, a.every, log) for _ in range(a.repeats)]
+        runs = [run_hip(steps, a.every, log, cross_check=(i == 0 and a.cross_check)) for i in range(a.repeats)]
         res = {"steps": steps, "rays_per_step": N_RAYS, "gt": GT, "hip_runs": runs}
         last = [r["curve"][-1]["psnr"] for r in runs]
         res["psnr_hip"] = last

@@ -67,13 +67,14 @@ def test_graph_step_matches_eager(dev):
         params.append(m.flat_params().detach().clone())
     np.testing.assert_allclose(losses[2], losses[0], rtol=1e-4)
     # hash-table entries: the float-atomic summation order differs run to run, and Adam (eps 1e-15)
-    # turns the sign of a near-zero gradient into a full +-lr step, so a handful of the 11.4M
-    # entries may move by ~lr between ANY two runs (eager or graph); everything else agrees
+    # turns the sign of a near-zero gradient into a full +-lr step, so a few hundred of the 11.4M
+    # entries (measured: ~150 between two eager runs) may move by ~lr between ANY two runs (eager or
+    # graph); everything else agrees
     n_t = _model(dev, scene)._n_table
     for other in (1, 2):
         d = (params[other][:n_t] - params[0][:n_t]).abs()
         big = int((d > 1e-4).sum())
-        assert big <= 1e-5 * n_t, (other, big)
+        assert big <= 5e-5 * n_t, (other, big)
         assert float((d > 1e-6).float().mean()) < 1e-3, other
     # the MLP weights (dense, large gradients) agree tightly
     rel_w = float((params[2][n_t:] - params[0][n_t:]).norm() / params[0][n_t:].norm())

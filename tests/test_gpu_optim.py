@@ -106,3 +106,32 @@ def test_trainer_sets_cosine_epoch_lr(dev):
         tr.step(batch, global_step=step)
         want = 0.5 * 1e-2 * (1 + math.cos(math.pi * epoch / 30))
         assert abs(tr.opt.lr - want) < 1e-12 and abs(float(tr.opt.lr_dev.item()) - want) < 1e-9
+
+
+def test_amp_grad_scaler_semantics(dev):
+    """amp_state (torch GradScaler of the reference's fp16 run): a non-finite gradient skips the
+    step (parameters, moments and the device step counter unchanged; the gradient still zeroed)
+    and halves the scale; finite steps count up and the 2000th doubles the scale."""
+    n = 4099
+    p = torch.randn(n, device=dev)
+    f = _Flat(p, 1001)
+    f.amp_state = torch.tensor([65536.0, 0.0], device=dev)
+    opt = FlatAdam(f, lr=1e-2, max_norm=0.05, zero_grad_on_step=True)
+    f._g.copy_(torch.randn(n, device=dev))
+    opt.step()
+    torch.cuda.synchronize()
+    assert f.amp_state.tolist() == [65536.0, 1.0] and int(opt.step_dev) == 1
+    p1, m1, v1 = p.clone(), opt.m.clone(), opt.v.clone()
+    f._g.copy_(torch.randn(n, device=dev))
+    f._g[17] = float("inf")
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(p, p1) and torch.equal(opt.m, m1) and torch.equal(opt.v, v1)
+    assert int(opt.step_dev) == 1 and f.amp_state.tolist() == [32768.0, 0.0]
+    assert float(f._g.abs().max()) == 0.0
+    f.amp_state[1] = 1999.0
+    f._g.copy_(torch.randn(n, device=dev))
+    opt.step()
+    torch.cuda.synchronize()
+    assert f.amp_state.tolist() == [65536.0, 0.0] and int(opt.step_dev) == 2
+    assert not torch.equal(p, p1)

@@ -61,7 +61,8 @@ lmax = torch.empty(16 * 256, device=dev)
 
 def bwd(lib):
     return lib.ncn_field_bwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(None), model._levels_ptr, F32(model._xyz_min),
-                             F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(gtab), ptr(slab),
+                             F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(None), ptr(gtab),
+                             ptr(slab),
                              ptr(dE_ws), ptr(lmax), stream())
 
 
