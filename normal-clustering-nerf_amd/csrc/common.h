@@ -207,6 +207,13 @@ __device__ __forceinline__ int opaque_zero() {
 // not for its outstanding global loads/stores/atomics (vmcnt), which __syncthreads() also drains.
 // For phases that exchange data through LDS while fire-and-forget global stores / atomics or
 // prefetch loads are in flight.
+// XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs (block b runs on
+// XCD b % 8), each with its own L2.  Renumbering blocks so that XCD x takes the contiguous logical
+// range [x * G/8, (x+1) * G/8) keeps neighbouring work — the samples of one ray patch, which
+// gather the same hash-table entries — inside one L2.  Identity when G is not a multiple of 8.
+// (Placement is a performance hint only: nothing may depend on it for correctness.)
+__device__ __forceinline__ int xcd_block(int b, int G) { return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3); }
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
