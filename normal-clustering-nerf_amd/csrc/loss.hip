@@ -240,10 +240,10 @@ __global__ void nerf_loss_bwd_kernel(const float* __restrict__ rgb, const float*
 constexpr int CL_MAX_TRI = 16384;
 constexpr int NCN_MAX_NQ = 80;       // K * 4 at K = 20
 #ifndef KM_THREADS_CFG
-#define KM_THREADS_CFG 256
+#define KM_THREADS_CFG 512
 #endif
 #ifndef KM_BLOCKS_CFG
-#define KM_BLOCKS_CFG 32
+#define KM_BLOCKS_CFG 16
 #endif
 constexpr int KM_THREADS = KM_THREADS_CFG;  // threads per workgroup of the clustering kernel
 constexpr int KM_BLOCKS = KM_BLOCKS_CFG;    // co-resident workgroups (grid barriers)
@@ -627,6 +627,7 @@ struct ClusterLds {
     int pick[K];       // init picks (ranks), sorted ascending
     int pick_ord[K];   // the centroid index of sorted pick k
     int picki[K];
+    float pickv[K][3];  // the init picks' normals (register-resident compaction)
     unsigned char pmem[KM_CHUNK_MAX];  // training-set membership of the chunk's points (faiss subsampling)
     int total;
     KmUpdLds<K> upd;
@@ -672,9 +673,12 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     CL_STAMP(0);
     // ---- compaction: ranks of the valid normals in index order, this workgroup's chunk to LDS ----
     const int R = (n_tri + KM_THREADS - 1) / KM_THREADS;  // <= 64 rounds
+    // R <= 16 (n_tri <= 16 * KM_THREADS: 8192 at 512 threads; config #2 has 6272): the loaded
+    // normals stay in registers and the chunk / init picks are stored from them (no second gather)
+    const bool regs = R <= 16;
     uint64_t flags = 0;
+    float a[16][3];
     for (int r0 = 0; r0 < R; r0 += 16) {  // 16 rounds of loads in flight before their ballots
-        float a[16][3];
 #pragma unroll
         for (int u = 0; u < 16; u++) {
             const int i = (r0 + u) * KM_THREADS + tid;
@@ -739,7 +743,7 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
 #pragma unroll
     for (int k = 0; k < K; k++) picks[k] = clustered ? __builtin_amdgcn_readfirstlane(L.pick[k]) : -1;
     CL_STAMP(56);
-    for (int r = 0; r < R; r++) {
+    auto rank_round = [&](int r, const float* ar) {
         // uniform skip of the rounds that hold neither a rank of this chunk, nor an init pick, nor
         // invalid normals this workgroup labels
         const int rlo = L.woff[r][0], rhi = r + 1 < R ? L.woff[r + 1][0] : nv;
@@ -749,29 +753,51 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
             if (picks[k] >= rlo) kbeg = k;
             if (picks[k] >= rhi) kend = k;
         }
-        if (!(rlo < m0 + len && rhi > m0) && r % KM_BLOCKS != (int)blockIdx.x && kbeg == kend) continue;
+        if (!(rlo < m0 + len && rhi > m0) && r % KM_BLOCKS != (int)blockIdx.x && kbeg == kend) return;
         const bool v = (flags >> r) & 1u;
         const int rank = L.woff[r][wid] + __popcll(__ballot(v) & lt);
         if (v) {
             const int i = r * KM_THREADS + tid;
-            if (rank >= m0 && rank < m0 + len) L.pidx[rank - m0] = i;
+            if (rank >= m0 && rank < m0 + len) {
+                L.pidx[rank - m0] = i;
+                if (ar) {
+#pragma unroll
+                    for (int q = 0; q < 3; q++) L.pv[q][rank - m0] = ar[q];
+                }
+            }
             for (int k = kbeg; k < kend; k++)  // usually none or one
-                if (picks[k] == rank) L.picki[L.pick_ord[k]] = i;
+                if (picks[k] == rank) {
+                    L.picki[L.pick_ord[k]] = i;
+                    if (ar) {
+#pragma unroll
+                        for (int q = 0; q < 3; q++) L.pickv[L.pick_ord[k]][q] = ar[q];
+                    }
+                }
         } else if (r * KM_THREADS + tid < n_tri && r % KM_BLOCKS == (int)blockIdx.x) {  // invalid: label -9, zero grad
             const int i = r * KM_THREADS + tid;
             out_labels[i] = -9;
 #pragma unroll
             for (int q = 0; q < 3; q++) dn[3 * i + q] = dn[T3 + 3 * i + q] = dn[2 * T3 + 3 * i + q] = 0.f;
         }
+    };
+    if (regs) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            if (r < R) rank_round(r, a[r]);  // (uniform; register indices are compile-time)
+    } else {
+        for (int r = 0; r < R; r++) rank_round(r, nullptr);
     }
     __syncthreads();
-    for (int j = tid; j < len; j += KM_THREADS) {  // this chunk's normals and the init centroids
-        const int i = L.pidx[j];
+    if (!regs)
+        for (int j = tid; j < len; j += KM_THREADS) {  // this chunk's normals and the init centroids
+            const int i = L.pidx[j];
 #pragma unroll
-        for (int q = 0; q < 3; q++) L.pv[q][j] = normals[3 * i + q];
-    }
+            for (int q = 0; q < 3; q++) L.pv[q][j] = normals[3 * i + q];
+        }
     if (clustered && tid < K) {  // faiss: centroids = the picked points, post-processed (renormalised)
-        float c[3] = {normals[3 * L.picki[tid]], normals[3 * L.picki[tid] + 1], normals[3 * L.picki[tid] + 2]};
+        float c[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) c[q] = regs ? L.pickv[tid][q] : normals[3 * L.picki[tid] + q];
         if (niter_eff > 0) faiss_renorm3(c);
 #pragma unroll
         for (int q = 0; q < 3; q++) L.C[tid][q] = c[q];
