@@ -853,6 +853,9 @@ __device__ __forceinline__ void sc_unpack(long long q, int& xs, int& ys) {
 #ifndef SC_C_DIR
 #define SC_C_DIR 4  // samples per lane on the direct levels (unit = one sort window)
 #endif
+#ifndef SC_DIR_HALF
+#define SC_DIR_HALF 15  // direct levels from here on: 2 samples per lane (units of 2048; 13: 198, 14: 202, 15: 190, none: 202 us)
+#endif
 
 struct ScRec {
     uint32_t k0, k1, pad0, pad1;  // cell: k0 = px | py << 16, k1 = pz
@@ -1587,7 +1590,13 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
         n_cell += (n + span - 1) / span;
     }
     const int64_t n_run = run_hi > run_lo ? (int64_t)(run_hi - run_lo) * ur : 0;
-    const int64_t n_units = n_cell + n_run + (dir_hi > dir_lo ? (int64_t)(dir_hi - dir_lo) * ud : 0);
+    // direct levels >= SC_DIR_HALF take half-size units (C = 2: their ~1 distinct entry per sample
+    // would overfill the 4-way sets of a 4096-sample unit)
+    const int64_t ud2 = (n + SC_THREADS * 2 - 1) / (SC_THREADS * 2);
+    const int dir_mid = max(dir_lo, min(dir_hi, SC_DIR_HALF));
+    const int64_t n_dir4 = dir_mid > dir_lo ? (int64_t)(dir_mid - dir_lo) * ud : 0;
+    const int64_t n_dir2 = dir_hi > dir_mid ? (int64_t)(dir_hi - dir_mid) * ud2 : 0;
+    const int64_t n_units = n_cell + n_run + n_dir4 + n_dir2;
     // (grid-stride: a workgroup takes its cell units first, then run, then direct: at most two
     // layout switches)
     int layout = -1, par = 0;
@@ -1628,11 +1637,20 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
             s0 = (v - li * ur) * (SC_THREADS * C_RUN);
             s1 = min(n, s0 + SC_THREADS * C_RUN);
         } else {
-            const int64_t v = u - n_cell - n_run;
-            const int li = (int)(v / ud);
-            l = dir_lo + li;
-            s0 = (v - li * ud) * (SC_THREADS * C_DIR);
-            s1 = min(n, s0 + SC_THREADS * C_DIR);
+            int64_t v = u - n_cell - n_run;
+            if (v < n_dir4) {
+                const int li = (int)(v / ud);
+                l = dir_lo + li;
+                s0 = (v - li * ud) * (SC_THREADS * C_DIR);
+                s1 = min(n, s0 + SC_THREADS * C_DIR);
+            } else {
+                v -= n_dir4;
+                const int li = (int)(v / ud2);
+                l = dir_mid + li;
+                s0 = (v - li * ud2) * (SC_THREADS * 2);
+                s1 = min(n, s0 + SC_THREADS * 2);
+                rounds = 2;  // (marks the C = 2 form below)
+            }
         }
         float m = lmax_s[l];
 #ifdef NCN_DIAG_SC_LEVELS_MASK
@@ -1649,6 +1667,8 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
             sc_cell_unit<C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
         else if (mode == SC_MODE_RUN)
             sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+        else if (rounds == 2)
+            sc_unit<2, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
         else
             sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
     }
