@@ -234,6 +234,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-grid-update", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager (Python-launched) step instead of a HIP graph")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="keep each step's optimizer at the end of its own graph (default: it runs in the next "
+                         "step's graph beside the marcher, Trainer(defer_optimizer=True))")
     ap.add_argument("--precision", choices=("fp16", "bf16"), default="fp16",
                     help="MFMA operand type of the field MLP (fp16 = tcnn's FullyFusedMLP, the reference's AMP run)")
     ap.add_argument("--no-bf16-line", action="store_true",
@@ -288,7 +291,8 @@ def main():
         step 0 (all cells for the first 256), as train_nerf.py does."""
         scene = SyntheticScene()
         model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
-        trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph)
+        trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph,
+                          defer_optimizer=not args.no_defer)
         # marched / composited sample counts accumulated on the device by the step itself
         # (ncn_count_samples: no per-step copies in the timed region)
         count_acc = torch.zeros(2, dtype=torch.float64, device=dev)
@@ -317,6 +321,7 @@ def main():
             model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
         for k in range(args.warmup):
             trainer.step(batches[k % n_batches], global_step=step0 + k)
+        trainer.flush_optimizer()  # (the timed region holds exactly `steps` optimizer steps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -327,6 +332,7 @@ def main():
         t0 = time.perf_counter()
         for k in range(steps):
             trainer.step(batches[(args.warmup + k) % n_batches], global_step=step0 + args.warmup + k)
+        trainer.flush_optimizer()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -432,7 +438,8 @@ def main():
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
-                   "step": "eager" if args.no_graph else "hip_graph"},
+                   "step": "eager" if args.no_graph else "hip_graph" + (
+                       "" if args.no_defer else " (optimizer of step k beside the marcher of step k+1)")},
         "samples_per_s": round(float(tot[0].item()) / el, 1),
         "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),

@@ -289,10 +289,11 @@ int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacit
                       float* dL_dopacity, float* dL_ddepth, void* stream);
 
 /* ---- step inputs (train_nerf.py:208: the batch handed to training_step): copies n_bufs <= 8 device
- *      buffers (src[b] -> dst[b], n_bytes[b]; HOST arrays of device pointers) and writes `step` to
- *      *step_dst (may be NULL) in ONE launch — the new batch into a captured step's static inputs. ---- */
+ *      buffers (src[b] -> dst[b], n_bytes[b]; HOST arrays of device pointers), writes `step` to
+ *      *step_dst and `flag` to *flag_dst (either may be NULL) in ONE launch — the new batch into a
+ *      captured step's static inputs (flag: the deferred optimizer step's gate). ---- */
 int ncn_step_inputs(int n_bufs, const void* const* src, void* const* dst, const int64_t* n_bytes, int64_t* step_dst,
-                    int64_t step, void* stream);
+                    int64_t step, int32_t* flag_dst, int32_t flag, void* stream);
 
 /* ---- optimizer (train_nerf.py:262-291, 954-955): global-norm clip + Adam over a flat buffer. ---- */
 /* step_inc: NULL, or a device int incremented once (the optimizer step counter of a captured step) */
@@ -311,8 +312,11 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
  * the gradient it consumed (the next step's zero_grad folded in).  Buffers 16-byte aligned. */
 int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
                   float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, void* stream);
-/* amp_state: NULL, or the GradScaler state of an AMP (fp16) run, device floats {scale, growth
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, const int* gate,
+                  void* stream);
+/* gate: NULL, or a device int: 0 = no gradient pending, the step is skipped (a deferred step of a
+ * captured graph whose previous step has already been applied).
+ * amp_state: NULL, or the GradScaler state of an AMP (fp16) run, device floats {scale, growth
  * tracker}: a gradient whose norm is not finite skips the update (parameters and moments unchanged,
  * step counter not advanced; the gradient is still zeroed with zero_grads) and halves the scale;
  * after NCN_AMP_GROWTH_INTERVAL finite steps in a row the scale doubles (torch.cuda.amp.GradScaler

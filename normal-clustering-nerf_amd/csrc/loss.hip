@@ -727,9 +727,13 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     // case (centroids = the points, no iteration)
     const int n_train = (plan_ok && nv > plan.cap()) ? plan.cap() : nv;
     const int niter_eff = n_train == K ? 0 : niter;
-    if (tid == 0 && clustered) {  // init picks (plan: first K of rand_perm(seed + 1)), sorted with their index
+    // init picks (plan: first K of rand_perm(seed + 1)), loaded by K threads at once, then sorted
+    // with their index by thread 0 from LDS
+    if (clustered && tid < K) L.picki[tid] = plan_ok ? plan.init(nv, tid) : tid;
+    __syncthreads();
+    if (tid == 0 && clustered) {
         for (int k = 0; k < K; k++) {
-            const int v = plan_ok ? plan.init(nv, k) : k;
+            const int v = L.picki[k];
             int j = k;
             for (; j > 0 && L.pick[j - 1] > v; j--) { L.pick[j] = L.pick[j - 1]; L.pick_ord[j] = L.pick_ord[j - 1]; }
             L.pick[j] = v;

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
                                                                float max_norm, double b1, double b2, float lr,
                                                                const float* __restrict__ lr_dev,
                                                                int* __restrict__ step_dev, float* __restrict__ work,
-                                                               float* __restrict__ amp) {
+                                                               float* __restrict__ amp, const int* __restrict__ gate) {
     float* part = work;                                // [ADAM_BLOCKS]
     unsigned* cnt = (unsigned*)(work + ADAM_BLOCKS);   // arrival counter (left zero)
     float* sc = work + ADAM_BLOCKS + 4;                // cf, bc1, bc2, lr, skip (AMP)
@@ -157,8 +157,11 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
             const float c = max_norm / (sqrtf(t) * gscale + 1e-6f);  // norm of the scaled gradient
             // GradScaler (AMP runs): a non-finite gradient skips the step and halves the scale;
             // NCN_AMP_GROWTH_INTERVAL finite steps in a row double it
-            const bool skip = amp && !isfinite(t);
-            if (amp) {
+            // gate == 0: no gradient is pending (a deferred optimizer step with nothing to apply):
+            // the step is skipped without touching the scaler
+            const bool gated_off = gate && *gate == 0;
+            const bool skip = gated_off || (amp && !isfinite(t));
+            if (amp && !gated_off) {
                 float tr = skip ? 0.f : amp[1] + 1.f;
                 float scale = skip ? amp[0] * 0.5f : amp[0];
                 if (tr >= (float)NCN_AMP_GROWTH_INTERVAL) {
@@ -232,8 +235,10 @@ struct StepCopies {
     unsigned char* dst[NCN_STEP_MAX_BUFS];
     int64_t bytes[NCN_STEP_MAX_BUFS];
 };
-__global__ __launch_bounds__(256) void step_inputs_kernel(StepCopies c, int nb, int64_t* step_dst, int64_t step) {
+__global__ __launch_bounds__(256) void step_inputs_kernel(StepCopies c, int nb, int64_t* step_dst, int64_t step,
+                                                         int* flag_dst, int flag) {
     if (step_dst && blockIdx.x == 0 && threadIdx.x == 0) *step_dst = step;
+    if (flag_dst && blockIdx.x == 0 && threadIdx.x == 0) *flag_dst = flag;
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
     for (int b = 0; b < nb; b++) {
         const bool al = (((uintptr_t)c.src[b] | (uintptr_t)c.dst[b]) & 15) == 0;
@@ -250,7 +255,7 @@ using namespace ncn;
 extern "C" {
 
 int ncn_step_inputs(int n_bufs, const void* const* src, void* const* dst, const int64_t* n_bytes, int64_t* step_dst,
-                    int64_t step, void* stream) {
+                    int64_t step, int32_t* flag_dst, int32_t flag, void* stream) {
     NCN_REQUIRE(n_bufs >= 0 && n_bufs <= NCN_STEP_MAX_BUFS, hipErrorInvalidValue,
                 "ncn_step_inputs: at most 8 buffers");
     StepCopies c{};
@@ -264,7 +269,8 @@ int ncn_step_inputs(int n_bufs, const void* const* src, void* const* dst, const 
         total += n_bytes[b];
     }
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(256, (total / 16 + 255) / 256));
-    hipLaunchKernelGGL(step_inputs_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, c, n_bufs, step_dst, step);
+    hipLaunchKernelGGL(step_inputs_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, c, n_bufs, step_dst, step,
+                       flag_dst, flag);
     NCN_LAUNCH_CHECK("ncn_step_inputs");
     return 0;
 }
@@ -292,7 +298,8 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
 
 int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
                   float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, void* stream) {
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, const int* gate,
+                  void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
                 hipErrorInvalidValue, "ncn_adam_step: buffers must be 16-byte aligned");
@@ -300,7 +307,7 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
                 "ncn_adam_step: needs the device step counter and the work buffer");
     const int prep_blocks = (int)std::min<int64_t>(ADAM_BLOCKS, std::max<int64_t>(1, cdiv(n / 4, ADAM_THREADS * 4)));
     hipLaunchKernelGGL(adam_prep_kernel, dim3(prep_blocks), dim3(ADAM_THREADS), 0, (hipStream_t)stream, grads, n,
-                       grad_scale, max_norm, beta1, beta2, lr, lr_dev, step_dev, work, amp_state);
+                       grad_scale, max_norm, beta1, beta2, lr, lr_dev, step_dev, work, amp_state, gate);
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
     // two float4 per thread (8 loads of p/g/m/v in flight): ~n/2048 workgroups
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 16384);

@@ -39,7 +39,7 @@ SIGNATURES = {
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
     "ncn_composite_train_fw_bg": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, F32, P, P],
     "ncn_count_samples": [P, I64, P, P, P, P],
-    "ncn_step_inputs": [I32, P, P, P, P, I64, P],
+    "ncn_step_inputs": [I32, P, P, P, P, I64, P, I32, P],
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, I32, P],
@@ -64,7 +64,7 @@ SIGNATURES = {
     "ncn_nerf_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, P, P, P, P],
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
-    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P, P],
+    "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P, P, P],
     "ncn_adam_step_work_floats": [],
     "ncn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "ncn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],
@@ -147,16 +147,16 @@ def ptr(t):
     return P(t.data_ptr())
 
 
-def step_inputs(srcs, dsts, step_dev, step):
-    """ncn_step_inputs: copy each srcs[i] into dsts[i] (contiguous CUDA tensors of equal size) and
-    write `step` into the int64 device scalar step_dev, in one launch."""
+def step_inputs(srcs, dsts, step_dev, step, flag_dev=None, flag=0):
+    """ncn_step_inputs: copy each srcs[i] into dsts[i] (contiguous CUDA tensors of equal size), write
+    `step` into the int64 device scalar step_dev and `flag` into the int32 flag_dev, in one launch."""
     n = len(srcs)
     VP = ctypes.c_void_p * max(n, 1)
     src = VP(*[s.data_ptr() for s in srcs])
     dst = VP(*[d.data_ptr() for d in dsts])
     nb = (ctypes.c_int64 * max(n, 1))(*[s.numel() * s.element_size() for s in srcs])
     return call("ncn_step_inputs", I32(n), ctypes.cast(src, P), ctypes.cast(dst, P), ctypes.cast(nb, P),
-                ptr(step_dev), I64(int(step)), stream())
+                ptr(step_dev), I64(int(step)), ptr(flag_dev), I32(int(flag)), stream())
 
 
 def check_input(t, name):

@@ -36,6 +36,9 @@ class FlatAdam:
         self.n_table = model._n_table
         self.zero_grad_on_step = zero_grad_on_step
         self.epoch = 0
+        # gate of a deferred step inside a captured graph (Trainer(defer_optimizer=True)): 0 = no
+        # gradient pending, the step is skipped
+        self.gate = torch.ones((), dtype=torch.int32, device=flat.device)
 
     def zero_grad(self):
         self.model.flat_grad().zero_()
@@ -49,8 +52,9 @@ class FlatAdam:
             self.lr = 0.5 * self.base_lr * (1 + math.cos(math.pi * epoch / self.num_epochs))
             self.lr_dev.fill_(self.lr)
 
-    def step(self, grad_scale=1.0):
-        """grad_scale: the gradient used is flat_grad * grad_scale (1/world after an all-reduce SUM)."""
+    def step(self, grad_scale=1.0, gated=False):
+        """grad_scale: the gradient used is flat_grad * grad_scale (1/world after an all-reduce SUM).
+        gated: the step runs only if the device gate is 1 (a deferred step in a captured graph)."""
         self.step_count += 1
         p = self.model.flat_params()
         g = self.model.flat_grad()
@@ -58,7 +62,7 @@ class FlatAdam:
         call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
              F32(grad_scale), F32(self.max_norm), F32(self.lr), _lib.F64(b1), _lib.F64(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
              ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), I32(1 if self.zero_grad_on_step else 0),
-             ptr(getattr(self.model, "amp_state", None)), stream())
+             ptr(getattr(self.model, "amp_state", None)), ptr(self.gate if gated else None), stream())
 
     def state_tensors(self):
         """Every tensor the step mutates (parameters, moments, device counters)."""

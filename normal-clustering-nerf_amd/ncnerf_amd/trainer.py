@@ -13,7 +13,7 @@ import torch
 from . import _lib, distributed
 from .losses import NeRFMTLoss, check_cluster_status
 from .optim import FlatAdam
-from .rendering import render
+from .rendering import march_train_fused, render
 
 HYPERSIM_HPARAMS = dict(
     scale=0.5, grid_size=128, rend_max_samples=1024, rend_near_dist=0.01, density_tresh_decay=1.0,
@@ -31,7 +31,8 @@ class Trainer:
 
     epoch_items = 1000  # base.py:78-81 (training "epoch" = 1000 batches)
 
-    def __init__(self, model, hparams=None, update_grid=False, use_graph=False, scatter_split=None):
+    def __init__(self, model, hparams=None, update_grid=False, use_graph=False, scatter_split=None,
+                 defer_optimizer=False):
         self.h = dict(HYPERSIM_HPARAMS, **(hparams or {}))
         self.model = model
         self.loss = NeRFMTLoss(self.h)
@@ -49,13 +50,27 @@ class Trainer:
                                   test_time=False, random_bg=False, anneal_strategy="none", anneal_steps=0)
         self.use_graph = use_graph
         self.graph = None
+        # defer_optimizer (graph step, one process): the optimizer step of step k runs inside graph
+        # k+1 on a side stream, concurrently with step k+1's marcher (which reads no parameter), and
+        # joins before the field forward; a refresh of the occupancy grid, or flush_optimizer(),
+        # applies a pending step first.  Parameters read between steps are one step behind until
+        # flush_optimizer() is called.
+        self.defer = bool(defer_optimizer) and use_graph and self.world == 1 and model.scatter_split is None
+        self._pending = False
         self._rng_seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # marcher jitter stream (CPU generator)
         # optional seed of each grid refresh (global_step -> int); default: drawn from torch's CPU generator
         self.grid_seed = None
 
+    def flush_optimizer(self):
+        """Apply the deferred optimizer step (defer_optimizer) now, if one is pending."""
+        if self._pending:
+            self.opt.step()
+            self._pending = False
+
     def _maybe_update_grid(self, global_step):
         m = self.model
         if self.update_grid and global_step % self.update_interval == 0:
+            self.flush_optimizer()  # (the refresh reads the parameters)
             thr = 0.01 * self.h["rend_max_samples"] / 3 ** 0.5 * self.h["density_tresh_decay"]
             seed = self.grid_seed(global_step) if self.grid_seed is not None else None
             m.update_density_grid(thr, warmup=global_step < self.warmup_steps, seed=seed)
@@ -75,15 +90,31 @@ class Trainer:
             kw["march_noise"] = batch["march_noise"]
         else:  # jitter drawn on the device from the step counter: no torch RNG node in the graph
             kw["march_rng"] = (self._rng_seed, step_dev)
+        if self.defer:
+            # the previous step's optimizer (gated: skipped when nothing is pending) on a side stream
+            # beside this step's marcher; joined before the field forward reads the parameters
+            cur = torch.cuda.current_stream()
+            side = self._side_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self.opt.step(gated=True)
+            kw["premarched"] = march_train_fused(m, batch["rays_o"], batch["rays_d"], kw["near_distance"],
+                                                 kw["max_samples"], kw.get("march_noise"), kw.get("march_rng"))
+            cur.wait_stream(side)
         results = render(m, batch["rays_o"], batch["rays_d"], **kw)
         loss_d = self.loss(results, batch, global_step=step_dev)
         total = loss_d["total"]
         if getattr(self, "_one", None) is None or self._one.device != total.device:
             self._one = torch.ones((), dtype=total.dtype, device=total.device)
         torch.autograd.backward(total, grad_tensors=self._one)  # (no ones_like fill node per step)
-        if with_opt:
+        if with_opt and not self.defer:
             self.opt.step()
         return results, loss_d
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.model.flat_params().device)
+        return self._side
 
     def _capture(self, batch):
         import torch
@@ -122,15 +153,21 @@ class Trainer:
         fast = len(dst) <= 8 and all(
             s.is_cuda and s.is_contiguous() and d.is_contiguous() and s.dtype == d.dtype and s.shape == d.shape
             for s, d in zip(src, dst))
-        if fast:  # the batch copies and the device step counter in one launch (ncn_step_inputs)
-            _lib.step_inputs(src, dst, self._step_dev, global_step)
+        gate = 1 if self._pending else 0  # (defer: the previous step's gradient awaits its optimizer step)
+        if fast:  # the batch copies, the device step counter and the gate in one launch (ncn_step_inputs)
+            _lib.step_inputs(src, dst, self._step_dev, global_step, self.opt.gate if self.defer else None, gate)
         else:
             if dst:
                 torch._foreach_copy_(dst, src, non_blocking=True)  # one launch for the whole batch
             self._step_dev.fill_(global_step)
+            if self.defer:
+                self.opt.gate.fill_(gate)
         self.graph.replay()
         if not self._with_opt:
             self.opt.step(grad_scale=distributed.reduce_gradients(self.model))
+        elif self.defer:
+            self.opt.step_count += gate
+            self._pending = True
         else:
             self.opt.step_count += 1
         return self._out

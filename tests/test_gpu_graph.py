@@ -97,3 +97,36 @@ def test_step_inputs_copy(dev):
     for s, d in zip(srcs, dsts):
         assert torch.equal(s, d)
     assert int(step) == 123456789012
+
+
+def test_deferred_optimizer_matches_graph_step(dev):
+    """Trainer(defer_optimizer=True): step k's optimizer runs inside graph k+1 beside its marcher
+    (gated off when nothing is pending), a grid refresh flushes it first.  Over 20 steps with
+    refreshes at 0 and 16 the losses and, after flush_optimizer(), the parameters match the plain
+    graph step within the run-to-run floor of test_graph_step_matches_eager; the device step
+    counter counts exactly one optimizer step per training step."""
+    scene = SyntheticScene()
+    batches = []
+    for k in range(4):
+        b = scene.torch_batch(4096, seed=70 + k, device=dev)
+        b["march_noise"] = torch.rand(4096, device=dev, generator=torch.Generator(device=dev).manual_seed(k))
+        batches.append(b)
+    out = []
+    for defer in (False, True):
+        m = _model(dev, scene)
+        tr = Trainer(m, update_grid=True, use_graph=True, defer_optimizer=defer)
+        tr.grid_seed = lambda k: 1000 + k
+        ls = []
+        for k in range(20):
+            _, ld = tr.step(batches[k % 4], global_step=k)
+            ls.append(float(ld["total"]))
+        tr.flush_optimizer()
+        torch.cuda.synchronize()
+        assert int(tr.opt.step_dev) == 20
+        out.append((np.array(ls), m.flat_params().detach().clone(), m.density_bitfield.clone()))
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-3)
+    n_t = _model(dev, scene)._n_table
+    d = (out[1][1][:n_t] - out[0][1][:n_t]).abs()
+    assert int((d > 1e-4).sum()) <= 5e-5 * n_t
+    rel_w = float((out[1][1][n_t:] - out[0][1][n_t:]).norm() / out[0][1][n_t:].norm())
+    assert rel_w < 1e-3, rel_w
