@@ -129,7 +129,7 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
             hits_t[:, 0, 1] = torch.min(depth + n_i * (hits_t[:, 0, 1] - depth), hits_t[:, 0, 1])
         else:
             assert strategy == "none"
-    if hasattr(model, "prepare_weights"):
+    if hasattr(model, "prepare_weights") and not getattr(model, "_packed_fresh", False):
         model.prepare_weights()  # queue the fp16 weight packing ahead of the marcher's host read of S
     static = bool(kwargs.get("static_shapes", False))
     pm = kwargs.get("premarched")

@@ -98,6 +98,8 @@ class Trainer:
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 self.opt.step(gated=True)
+                m._pack_weights()  # the MLP's fp16 fragments of the updated weights, also beside the marcher
+                m._packed_fresh = True
             kw["premarched"] = march_train_fused(m, batch["rays_o"], batch["rays_d"], kw["near_distance"],
                                                  kw["max_samples"], kw.get("march_noise"), kw.get("march_rng"))
             cur.wait_stream(side)
