@@ -169,6 +169,10 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
                 o, d, ht[:, 0].contiguous(), model.density_bitfield, 1, 0.5, 0.0, torch.rand(65536, device=dev), 128,
                 1024)
             S = int(counter[0].item())
+            # rows as the training step's marcher orders them (march_train_place): rays longer than
+            # 256 samples first, the rest in ray order (sample segments unchanged)
+            long_ = ra[:, 2] > 256
+            ra = torch.cat([ra[long_], ra[~long_]]).contiguous()
             mk = {"rays_a": ra, "deltas": deltas, "ts": ts}
             out = model(xyzs, dirs)
             R = 65536

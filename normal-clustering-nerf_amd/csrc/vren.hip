@@ -806,8 +806,8 @@ struct RaySeg {
     int N;
     bool live;
 };
-__device__ __forceinline__ RaySeg load_ray_seg(const int64_t* __restrict__ rays_a, int64_t R) {
-    const int64_t n0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * CF_WPB + (threadIdx.x >> 6)));
+__device__ __forceinline__ RaySeg load_ray_seg(const int64_t* __restrict__ rays_a, int64_t R, int blk) {
+    const int64_t n0 = __builtin_amdgcn_readfirstlane((int)(blk * CF_WPB + (threadIdx.x >> 6)));
     const int64_t n = n0 < R ? n0 : R - 1;
     RaySeg s;
     s.ray = rays_a[3 * n];
@@ -824,13 +824,18 @@ __device__ __forceinline__ RaySeg load_ray_seg(const int64_t* __restrict__ rays_
 // waves/SIMD).  GUARD: rows past N are skipped (uniform branches).  Returns true when the ray
 // stopped in this block (quirk q6: the stopping sample is composited, not counted); the rest of the
 // segment then gets ws = 0 (volumerendering.cu:133 breaks, ws stays 0).
-template <int C, int ROWS, bool GUARD>
+// LOCAL (the single-wave path of rays longer than 256 samples, 4-row blocks): the chain starts at
+// Tc = 1 inside the block and is scaled by `carry` (the product of the preceding blocks) — the same
+// float operations, in the same order, as the one-workgroup path (composite_fw_coop), so a long ray
+// composites bit-identically on either path.
+template <int C, int ROWS, bool GUARD, bool LOCAL = false>
 __device__ __forceinline__ bool composite_fw_block(const __amdgpu_buffer_rsrc_t& r_s,
                                                    const __amdgpu_buffer_rsrc_t& r_d,
                                                    const __amdgpu_buffer_rsrc_t& r_t,
                                                    const __amdgpu_buffer_rsrc_t& r_r,
                                                    const __amdgpu_buffer_rsrc_t& r_w, int base, int N, float T_thr,
-                                                   int lane, float& Tc, float (&acc)[2 + C], int& total) {
+                                                   int lane, float& Tc, float (&acc)[2 + C], int& total,
+                                                   float carry = 1.0f) {
     constexpr int RT = ROWS < 4 ? ROWS : 4;
     float sg[ROWS], dl[ROWS], tt[RT], rr[RT][C];
 #pragma unroll
@@ -866,9 +871,15 @@ __device__ __forceinline__ bool composite_fw_block(const __amdgpu_buffer_rsrc_t&
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
         Tb[r] = Tc * wave_shr1_dpp(p[r], 1.0f);
-        const float Ta = Tb[r] * om[r];
-        stopm[r] = __ballot(Ta <= T_thr);
-        Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
+        if constexpr (LOCAL) {
+            Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tb[r] * om[r]), 63));
+            Tb[r] *= carry;
+            stopm[r] = __ballot(Tb[r] * om[r] <= T_thr);
+        } else {
+            const float Ta = Tb[r] * om[r];
+            stopm[r] = __ballot(Ta <= T_thr);
+            Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
+        }
     }
     int srow = ROWS, slane = 64;  // first sample whose Ta <= T_thr (T is non-increasing)
 #pragma unroll
@@ -925,15 +936,129 @@ __device__ __forceinline__ bool composite_fw_block(const __amdgpu_buffer_rsrc_t&
 
 // Forward (volumerendering.cu:97-176): a ray with N <= 256 samples is one block of 1, 2 or 4 rows
 // (every row non-empty: no guards), a longer one runs in guarded blocks of 8 rows.
+// Long rays (CF_LONG < N <= CF_COOP_MAX samples) are taken by a whole workgroup: wave v composites
+// the ray's samples [256 v, 256 v + 256) as one 4-row block with a local carry of 1, the waves'
+// segment products meet in LDS (carry-in = product of the preceding waves' products), the first
+// stopping sample over the ray is the minimum of the waves' first stops, and the per-wave sums are
+// added in wave order.  Every load of the ray is issued in ONE round (a single wave needs 2-4
+// dependent rounds for 256 < N <= 1024, the tail that bounded the launch); 3 LDS barriers.  The
+// training step's rows hold the long rays first (march_train_place), so workgroup j < n_coop takes
+// row j when it is long; long rays outside the first n_coop rows (eager callers: rows in ray order)
+// stay on the single-wave path.  Float order: T = carry x local prefix (vs one chained product),
+// within the compositor's scan tolerance.
+#define CF_LONG 256
+#define CF_COOP_MAX (256 * CF_WPB)
+template <int C>
+__device__ __forceinline__ void composite_fw_coop(const float* __restrict__ sigmas, const float* __restrict__ raws,
+                                                  const float* __restrict__ deltas, const float* __restrict__ ts,
+                                                  const int64_t* __restrict__ rays_a, int64_t row, float T_thr,
+                                                  int64_t* __restrict__ total_samples, float* __restrict__ opacity,
+                                                  float* __restrict__ depth, float* __restrict__ rend,
+                                                  float* __restrict__ ws, float bg, float* __restrict__ rgb_bg) {
+    __shared__ float sP[CF_WPB];
+    __shared__ int sStop[CF_WPB];
+    __shared__ float sAcc[CF_WPB][2 + C];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t ray = rays_a[3 * row], start = rays_a[3 * row + 1];
+    const int N = (int)rays_a[3 * row + 2];
+    if (N <= CF_LONG || N > CF_COOP_MAX) return;  // workgroup-uniform: no wave reaches a barrier
+    const uint32_t nb = (uint32_t)N * 4u;
+    const auto r_s = buf_rsrc(sigmas + start, nb), r_d = buf_rsrc(deltas + start, nb);
+    const auto r_t = buf_rsrc(ts + start, nb), r_r = buf_rsrc(raws + start * C, nb * C);
+    const auto r_w = buf_rsrc(ws + start, nb);
+    const int base = wv * 256;
+    float sg[4], dl[4], tt[4], rr[4][C];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {  // past N (and whole waves past N) the descriptors read 0
+        const uint32_t k = (uint32_t)(base + r * 64 + lane);
+        sg[r] = buf_load(r_s, k * 4u);
+        dl[r] = buf_load(r_d, k * 4u);
+        tt[r] = buf_load(r_t, k * 4u);
+#pragma unroll
+        for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+    }
+    float a[4], om[4], p[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        a[r] = 1.0f - __expf(-sg[r] * dl[r]);
+        om[r] = p[r] = 1.0f - a[r];
+    }
+    wave_incl_prod_multi<4>(p);
+    float Tb[4], Tc = 1.0f;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        Tb[r] = Tc * wave_shr1_dpp(p[r], 1.0f);
+        Tc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tb[r] * om[r]), 63));
+    }
+    if (lane == 0) sP[wv] = Tc;
+    __syncthreads();
+    float carry = 1.0f;
+    for (int v = 0; v < wv; v++) carry *= sP[v];
+    int stop = INT_MAX;  // first sample (ray position) whose transmittance after it is <= T_thr
+#pragma unroll
+    for (int r = 3; r >= 0; r--) {
+        Tb[r] *= carry;
+        const uint64_t m = __ballot(Tb[r] * om[r] <= T_thr);
+        if (m) stop = base + r * 64 + __builtin_ctzll(m);
+    }
+    if (lane == 0) sStop[wv] = stop;
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < CF_WPB; v++) stop = min(stop, sStop[v]);
+    float acc[2 + C];
+#pragma unroll
+    for (int i = 0; i < 2 + C; i++) acc[i] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int pos = base + r * 64 + lane;
+        const float w = pos <= stop ? a[r] * Tb[r] : 0.f;  // the stopping sample is composited (q6)
+        if (base + r * 64 < N) buf_store(r_w, (uint32_t)pos * 4u, w);
+        acc[0] += w;
+        acc[1] = fmaf(w, tt[r], acc[1]);
+#pragma unroll
+        for (int i = 0; i < C; i++) acc[2 + i] = fmaf(w, rr[r][i], acc[2 + i]);
+    }
+    wave_sum_multi<2 + C>(acc);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 2 + C; i++) sAcc[wv][i] = acc[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < 2 + C; i++) {
+            float t = sAcc[0][i];
+            for (int v = 1; v < CF_WPB; v++) t += sAcc[v][i];
+            acc[i] = t;
+        }
+        opacity[ray] = acc[0];
+        depth[ray] = acc[1];
+#pragma unroll
+        for (int i = 0; i < C; i++) rend[ray * C + i] = acc[2 + i];
+        if (rgb_bg) {
+#pragma unroll
+            for (int i = 0; i < C; i++) rgb_bg[ray * C + i] = acc[2 + i] + bg * (1 - acc[0]);
+        }
+        total_samples[ray] = stop == INT_MAX ? N : stop;
+    }
+}
+
 template <int C>
 __global__ __launch_bounds__(64 * CF_WPB) void composite_fw_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t R, float T_thr,
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
-    float* __restrict__ rend, float* __restrict__ ws, float bg, float* __restrict__ rgb_bg) {
+    float* __restrict__ rend, float* __restrict__ ws, float bg, float* __restrict__ rgb_bg, int n_coop) {
+    if ((int)blockIdx.x < n_coop) {
+        composite_fw_coop<C>(sigmas, raws, deltas, ts, rays_a, blockIdx.x, T_thr, total_samples, opacity, depth,
+                             rend, ws, bg, rgb_bg);
+        return;
+    }
     const int lane = threadIdx.x & 63;
-    const RaySeg g = load_ray_seg(rays_a, R);
+    const RaySeg g = load_ray_seg(rays_a, R, (int)blockIdx.x - n_coop);
     const int N = g.N;
+    const int64_t row = __builtin_amdgcn_readfirstlane((int)((blockIdx.x - n_coop) * CF_WPB + (threadIdx.x >> 6)));
+    if (row < n_coop && N > CF_LONG && N <= CF_COOP_MAX) return;  // taken by workgroup `row` (wave-uniform)
     const uint32_t nb = (uint32_t)N * 4u;
     const auto r_s = buf_rsrc(sigmas + g.start, nb), r_d = buf_rsrc(deltas + g.start, nb);
     const auto r_t = buf_rsrc(ts + g.start, nb), r_r = buf_rsrc(raws + g.start * C, nb * C);
@@ -949,11 +1074,23 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_fw_kernel(
         composite_fw_block<C, 2, false>(r_s, r_d, r_t, r_r, r_w, 0, N, T_thr, lane, Tc, acc, total);
     } else if (N <= 256) {
         composite_fw_block<C, 4, false>(r_s, r_d, r_t, r_r, r_w, 0, N, T_thr, lane, Tc, acc, total);
-    } else {
-        for (int base = 0; base < N; base += 8 * 64)
-            if (composite_fw_block<C, 8, true>(r_s, r_d, r_t, r_r, r_w, base, N, T_thr, lane, Tc, acc, total)) break;
+    } else {  // 4-row blocks with local chains, block sums added in order (as composite_fw_coop)
+        float carry = 1.0f;
+        for (int base = 0; base < N; base += 4 * 64) {
+            float bacc[2 + C];
+#pragma unroll
+            for (int i = 0; i < 2 + C; i++) bacc[i] = 0.f;
+            Tc = 1.0f;
+            const bool stopped =
+                composite_fw_block<C, 4, true, true>(r_s, r_d, r_t, r_r, r_w, base, N, T_thr, lane, Tc, bacc, total, carry);
+            wave_sum_multi<2 + C>(bacc);
+#pragma unroll
+            for (int i = 0; i < 2 + C; i++) acc[i] += bacc[i];
+            carry *= Tc;
+            if (stopped) break;
+        }
     }
-    wave_sum_multi<2 + C>(acc);
+    if (N <= 256) wave_sum_multi<2 + C>(acc);
     if (g.live && lane == 0) {
         opacity[g.ray] = acc[0];
         depth[g.ray] = acc[1];
@@ -1123,6 +1260,147 @@ __device__ __forceinline__ void composite_bw_ray(
 #undef NCN_BW_BLOCK
 }
 
+// Long rays in the backward: one workgroup per ray as in the forward.  Phase 1: every wave loads
+// its 256 samples and publishes its local transmittance product and its local sums of w*t, w*raw
+// (w with a carry-in of 1) and dL_dws*ws; after one barrier wave v has the carries of the waves in
+// front of it (T_in = product of their products; prefix sums = their sums scaled by their T_in;
+// the stop cannot lie in front of the first stopping wave, so their sums are uncut), finds its
+// first stop, and after a second barrier the ray's first stop cuts w as in the single-wave rows.
+template <int C, bool DWS>
+__device__ __forceinline__ void composite_bw_coop(
+    const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
+    const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
+    const int64_t* __restrict__ rays_a, int64_t row, const float* __restrict__ opacity,
+    const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
+    float* __restrict__ dL_draws, float bg) {
+    __shared__ float sS[CF_WPB][3 + C];  // product, sum w*t, sum dL_dws*ws, sums w*raw
+    __shared__ int sStop[CF_WPB];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t ray = rays_a[3 * row], start = rays_a[3 * row + 1];
+    const int N = (int)rays_a[3 * row + 2];
+    if (N <= CF_LONG || N > CF_COOP_MAX) return;  // workgroup-uniform
+    const float dO = dL_dopacity ? dL_dopacity[ray] : 0.f;
+    const float dD = dL_ddepth ? dL_ddepth[ray] : 0.f;
+    const float O = opacity[ray], D = depth[ray];
+    float dR[C], RE[C];
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        dR[i] = dL_drend ? dL_drend[ray * C + i] : 0.f;
+        RE[i] = rend[ray * C + i];
+    }
+    float dOe = dO;
+    if (bg != 0.f) {
+#pragma unroll
+        for (int i = 0; i < C; i++) dOe -= bg * dR[i];
+    }
+    const float gO = dOe * (1 - O);
+    const uint32_t nb = (uint32_t)N * 4u;
+    const auto r_s = buf_rsrc(sigmas + start, nb), r_d = buf_rsrc(deltas + start, nb);
+    const auto r_t = buf_rsrc(ts + start, nb), r_r = buf_rsrc(raws + start * C, nb * C);
+    const auto r_gs = buf_rsrc(dL_dsigmas + start, nb), r_gr = buf_rsrc(dL_draws + start * C, nb * C);
+    const auto r_dw = buf_rsrc(DWS ? dL_dws + start : dL_dsigmas, DWS ? nb : 0u);
+    const auto r_ws = buf_rsrc(DWS ? ws + start : dL_dsigmas, DWS ? nb : 0u);
+    const int base = wv * 256;
+    float sg[4], dl[4], tt[4], rr[4][C], dws[4], pw[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t k = (uint32_t)(base + r * 64 + lane);
+        sg[r] = buf_load(r_s, k * 4u);
+        dl[r] = buf_load(r_d, k * 4u);
+        tt[r] = buf_load(r_t, k * 4u);
+#pragma unroll
+        for (int i = 0; i < C; i++) rr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
+        dws[r] = DWS ? buf_load(r_dw, k * 4u) : 0.f;
+        pw[r] = DWS ? dws[r] * buf_load(r_ws, k * 4u) : 0.f;
+    }
+    float a[4], om[4], p[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        a[r] = 1.0f - __expf(-sg[r] * dl[r]);
+        om[r] = p[r] = 1.0f - a[r];
+    }
+    wave_incl_prod_multi<4>(p);
+    float Tb[4], Tl = 1.0f, ls[2 + C];  // local sums: w*t, dL_dws*ws, w*raw
+#pragma unroll
+    for (int i = 0; i < 2 + C; i++) ls[i] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        Tb[r] = Tl * wave_shr1_dpp(p[r], 1.0f);
+        Tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Tb[r] * om[r]), 63));
+        const float w = a[r] * Tb[r];
+        ls[0] = fmaf(w, tt[r], ls[0]);
+        ls[1] += pw[r];
+#pragma unroll
+        for (int i = 0; i < C; i++) ls[2 + i] = fmaf(w, rr[r][i], ls[2 + i]);
+    }
+    wave_sum_multi<2 + C>(ls);
+    if (lane == 0) {
+        sS[wv][0] = Tl;
+#pragma unroll
+        for (int i = 0; i < 2 + C; i++) sS[wv][1 + i] = ls[i];
+    }
+    __syncthreads();
+    float Tc = 1.0f, cd = 0.f, cpw = 0.f, tot = 0.f, cr[C];
+#pragma unroll
+    for (int i = 0; i < C; i++) cr[i] = 0.f;
+    for (int v = 0; v < CF_WPB; v++) {
+        if (v < wv) {
+            cd = fmaf(Tc, sS[v][1], cd);
+            cpw += sS[v][2];
+#pragma unroll
+            for (int i = 0; i < C; i++) cr[i] = fmaf(Tc, sS[v][3 + i], cr[i]);
+            Tc *= sS[v][0];
+        }
+        tot += sS[v][2];
+    }
+    int stop = INT_MAX;
+    float Ta[4];
+#pragma unroll
+    for (int r = 3; r >= 0; r--) {
+        Tb[r] *= Tc;
+        Ta[r] = Tb[r] * om[r];
+        const uint64_t m = __ballot(Ta[r] <= T_thr);
+        if (m) stop = base + r * 64 + __builtin_ctzll(m);
+    }
+    if (lane == 0) sStop[wv] = stop;
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < CF_WPB; v++) stop = min(stop, sStop[v]);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int pos = base + r * 64 + lane;
+        const bool inc = pos <= stop;
+        const float w = inc ? a[r] * Tb[r] : 0.f;
+        float run_d = w * tt[r], run_r[C];
+#pragma unroll
+        for (int i = 0; i < C; i++) run_r[i] = w * rr[r][i];
+        if constexpr (C == 3) {
+            wave_incl_sum4(run_d, run_r[0], run_r[1], run_r[2]);
+        } else {
+            run_d = wave_incl_sum_dpp(run_d);
+#pragma unroll
+            for (int i = 0; i < C; i++) run_r[i] = wave_incl_sum_dpp(run_r[i]);
+        }
+        run_d += cd;
+#pragma unroll
+        for (int i = 0; i < C; i++) run_r[i] += cr[i];
+        const float run_pw = DWS ? cpw + wave_incl_sum_dpp(pw[r]) : 0.f;
+        float gs = gO + dD * (tt[r] * Ta[r] - (D - run_d)) + Ta[r] * dws[r] - (tot - run_pw);
+        const bool live_row = base + r * 64 < N;
+#pragma unroll
+        for (int i = 0; i < C; i++) {
+            gs += dR[i] * (rr[r][i] * Ta[r] - (RE[i] - run_r[i]));
+            if (live_row) buf_store(r_gr, (uint32_t)pos * (4u * C) + 4u * i, dR[i] * w);
+        }
+        if (live_row) buf_store(r_gs, (uint32_t)pos * 4u, inc ? gs * dl[r] : 0.f);
+        cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_d), 63));
+        if (DWS) cpw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_pw), 63));
+#pragma unroll
+        for (int i = 0; i < C; i++) cr[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run_r[i]), 63));
+    }
+}
+
 template <int C>
 __global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_nodws(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
@@ -1130,8 +1408,15 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_nodws(
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
     const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
-    float* __restrict__ dL_draws, float bg) {
-    const RaySeg g = load_ray_seg(rays_a, R);
+    float* __restrict__ dL_draws, float bg, int n_coop) {
+    if ((int)blockIdx.x < n_coop) {
+        composite_bw_coop<C, false>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a,
+                                   blockIdx.x, opacity, depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+        return;
+    }
+    const RaySeg g = load_ray_seg(rays_a, R, (int)blockIdx.x - n_coop);
+    const int64_t row = __builtin_amdgcn_readfirstlane((int)((blockIdx.x - n_coop) * CF_WPB + (threadIdx.x >> 6)));
+    if (row < n_coop && g.N > CF_LONG && g.N <= CF_COOP_MAX) return;  // taken by workgroup `row`
     composite_bw_ray<C, false>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, g, opacity,
                                depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
 }
@@ -1142,8 +1427,15 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_dws(
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
     const int64_t* __restrict__ rays_a, int64_t R, const float* __restrict__ opacity,
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
-    float* __restrict__ dL_draws, float bg) {
-    const RaySeg g = load_ray_seg(rays_a, R);
+    float* __restrict__ dL_draws, float bg, int n_coop) {
+    if ((int)blockIdx.x < n_coop) {
+        composite_bw_coop<C, true>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a,
+                                   blockIdx.x, opacity, depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+        return;
+    }
+    const RaySeg g = load_ray_seg(rays_a, R, (int)blockIdx.x - n_coop);
+    const int64_t row = __builtin_amdgcn_readfirstlane((int)((blockIdx.x - n_coop) * CF_WPB + (threadIdx.x >> 6)));
+    if (row < n_coop && g.N > CF_LONG && g.N <= CF_COOP_MAX) return;  // taken by workgroup `row`
     composite_bw_ray<C, true>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, g, opacity,
                               depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
 }
@@ -1407,6 +1699,10 @@ int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
     return 0;
 }
 
+// Workgroups for the long rays at the front of rays_a (the training step's rows put them first);
+// the ones whose row is short exit at once.
+static int cf_coop_blocks(int64_t n_rays) { return (int)std::min<int64_t>(n_rays, std::max<int64_t>(64, n_rays / 16)); }
+
 #define NCN_DISPATCH_C(C_RT, KERNEL, ...)                                                       \
     switch (C_RT) {                                                                            \
         case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                             \
@@ -1423,8 +1719,10 @@ int ncn_composite_train_fw_bg(const float* sigmas, const float* raws, const floa
                               float* rgb_bg, void* stream) {
     if (n_rays <= 0) return 0;
     (void)n_samples;
-    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0, (hipStream_t)stream, sigmas, raws,
-                   deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity, depth, rend, ws, bg, rgb_bg);
+    const int n_coop = cf_coop_blocks(n_rays);
+    NCN_DISPATCH_C(n_rend, composite_fw_kernel, dim3(n_coop + cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0,
+                   (hipStream_t)stream, sigmas, raws, deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity,
+                   depth, rend, ws, bg, rgb_bg, n_coop);
     NCN_LAUNCH_CHECK("ncn_composite_train_fw");
     return 0;
 }
@@ -1445,14 +1743,16 @@ int ncn_composite_train_bw_bg(const float* dL_dopacity, const float* dL_ddepth, 
                               void* stream) {
     if (n_rays <= 0) return 0;
     (void)n_samples;
+    const int n_coop = cf_coop_blocks(n_rays);
+    const dim3 grid(n_coop + cdiv(n_rays, CF_WPB));
     if (dL_dws) {
-        NCN_DISPATCH_C(n_rend, composite_bw_kernel_dws, dim3(cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0, (hipStream_t)stream, dL_dopacity,
+        NCN_DISPATCH_C(n_rend, composite_bw_kernel_dws, grid, dim3(64 * CF_WPB), 0, (hipStream_t)stream, dL_dopacity,
                    dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
-                   T_threshold, dL_dsigmas, dL_draws, bg);
+                   T_threshold, dL_dsigmas, dL_draws, bg, n_coop);
     } else {
-        NCN_DISPATCH_C(n_rend, composite_bw_kernel_nodws, dim3(cdiv(n_rays, CF_WPB)), dim3(64 * CF_WPB), 0, (hipStream_t)stream, dL_dopacity,
+        NCN_DISPATCH_C(n_rend, composite_bw_kernel_nodws, grid, dim3(64 * CF_WPB), 0, (hipStream_t)stream, dL_dopacity,
                    dL_ddepth, dL_drgb, dL_dws, sigmas, raws, ws, deltas, ts, rays_a, n_rays, opacity, depth, rend,
-                   T_threshold, dL_dsigmas, dL_draws, bg);
+                   T_threshold, dL_dsigmas, dL_draws, bg, n_coop);
     }
     NCN_LAUNCH_CHECK("ncn_composite_train_bw");
     return 0;

@@ -231,6 +231,64 @@ def test_composite_fw_edge(dev):
         np.testing.assert_allclose(a.cpu().numpy(), r, rtol=2e-4, atol=2e-5)
 
 
+def _long_first_inputs(seed):
+    """Segments of 257..1025 samples in the rows at the front of rays_a (the training step's row
+    order: the compositors take them with one workgroup each), with transmittance that stops in
+    each of the 4 waves' sample ranges or never; then short rays."""
+    rng = np.random.default_rng(seed)
+    lens = [257, 300, 511, 512, 513, 700, 768, 769, 1000, 1024, 1025, 1024, 600, 400] + list(rng.integers(0, 256, 200))
+    stop_at = [None, 100, 280, 500, None, 600, 260, 767, 900, None, 1010, 1023, None, 390]
+    rows, start, sig_parts = [], 0, []
+    for i, n in enumerate(lens):
+        n = int(n)
+        rows.append([i, start, n])
+        s = np.abs(rng.normal(0, 0.2, n)).astype(np.float32)  # T stays well above 1e-4 ...
+        if i < len(stop_at) and stop_at[i] is not None and stop_at[i] < n:
+            s[stop_at[i]] = 1e5  # ... until an opaque sample
+        elif i >= len(stop_at):
+            s = np.abs(rng.normal(0, 20, n)).astype(np.float32)
+        sig_parts.append(s)
+        start += n
+    order = rng.permutation(len(rows))  # segments not in row order (rows of the step: long first, ray order)
+    rays_a = np.array(rows, np.int64)
+    perm = np.concatenate([order[rays_a[order, 2] > 256], order[rays_a[order, 2] <= 256]])
+    rays_a = rays_a[perm]
+    S = start
+    sig = np.concatenate(sig_parts)
+    raws = rng.random((S, 3), dtype=np.float32)
+    deltas = np.full(S, 1.7e-3, np.float32)
+    ts = (np.arange(S) % 977 * 1.7e-3).astype(np.float32)
+    return rays_a, deltas, ts, sig, raws
+
+
+def test_composite_long_rays_workgroup_path(dev):
+    """Rays of 257..1024 samples at the front of rays_a go through the one-workgroup-per-ray path
+    (1025 stays single-wave): fw exact counts and 2e-4 values, bw at the parity tolerance."""
+    rays_a, deltas, ts, sig, raws = _long_first_inputs(3)
+    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = vren.composite_train_multi_fw(T(sig), T(raws), T(deltas), T(ts), T(rays_a), 1e-4)
+    ref = vren_ref.composite_train_multi_fw(sig, raws, deltas, ts, rays_a, 1e-4)
+    assert np.array_equal(out[0].cpu().numpy(), ref[0])
+    for a, r, name in zip(out[1:], ref[1:], ("opacity", "depth", "rend", "ws")):
+        np.testing.assert_allclose(a.cpu().numpy(), r, rtol=2e-4, atol=2e-5, err_msg=name)
+    # rows in ray order (the eager marcher's): long rays on the single-wave path, bit-identical
+    by_ray = rays_a[np.argsort(rays_a[:, 0])]
+    out2 = vren.composite_train_multi_fw(T(sig), T(raws), T(deltas), T(ts), T(by_ray), 1e-4)
+    for a, b_ in zip(out, out2):
+        assert torch.equal(a, b_)
+    _, O, D, RE, ws = ref
+    rng = np.random.default_rng(4)
+    R, S = rays_a.shape[0], sig.shape[0]
+    dO, dD = rng.normal(size=R).astype(np.float32), rng.normal(size=R).astype(np.float32)
+    dR = rng.normal(size=(R, 3)).astype(np.float32)
+    for dW in (None, rng.normal(size=S).astype(np.float32)):
+        o2 = vren.composite_train_multi_bw(T(dO), T(dD), T(dR), T(dW), T(sig), T(raws), T(ws), T(deltas), T(ts),
+                                           T(rays_a), T(O), T(D), T(RE), 1e-4)
+        r2 = vren_ref.composite_train_multi_bw(dO, dD, dR, dW, sig, raws, ws, deltas, ts, rays_a, O, D, RE, 1e-4)
+        for a, r, name in zip(o2, r2, ("dL_dsigmas", "dL_draws")):
+            np.testing.assert_allclose(a.cpu().numpy(), r, rtol=1e-3, atol=1e-4 * np.abs(r).max(), err_msg=name)
+
+
 @pytest.mark.parametrize("with_dws", [False, True])
 def test_composite_bw_parity(dev, scene, with_dws):
     """Tolerance: |Δ| <= 1e-4*max|ref| + 1e-3*|ref| (cancellation in (R - r) terms)."""

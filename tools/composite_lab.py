@@ -33,7 +33,11 @@ S = xyzs.shape[0]
 with torch.no_grad():
     out = model(xyzs, dirs)
 sig, rgb = out["sigmas"].float().contiguous(), out["rgbs"].float().contiguous()
-print("rays", R, "samples", S, "per ray", S / R, flush=True)
+Nr = rays_a[:, 2]
+print("rays", R, "samples", S, "per ray", S / R, "long(>256)", int((Nr > 256).sum()), "max", int(Nr.max()),
+      "samples in long rays", int(Nr[Nr > 256].sum()), flush=True)
+if os.environ.get("LAB_LONG_FIRST"):  # the training step's row order (long rays first)
+    rays_a = torch.cat([rays_a[Nr > 256], rays_a[Nr <= 256]]).contiguous()
 
 lab = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "lab.so"))
 lab.lab_composite_fw.restype = ctypes.c_int
