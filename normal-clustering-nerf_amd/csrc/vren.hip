@@ -948,6 +948,17 @@ __device__ __forceinline__ bool composite_fw_block(const __amdgpu_buffer_rsrc_t&
 // within the compositor's scan tolerance.
 #define CF_LONG 256
 #define CF_COOP_MAX (256 * CF_WPB)
+// The n_coop workgroups at the front of the grid walk the rows b, b + n_coop, ... and stop at the
+// first short one (N <= CF_LONG): with the long rays first, every long ray is taken whatever their
+// number.  (Rows with N > CF_COOP_MAX are passed over and stay single-wave.)  Row `row` (long) is
+// taken by a workgroup iff no row row - k * n_coop (k >= 1) is short.  Successive rows of one
+// workgroup reuse its LDS without an extra barrier: every LDS array is read between the barriers
+// of its own row, before the next row writes it behind a later barrier.
+__device__ __forceinline__ bool cf_coop_takes(const int64_t* __restrict__ rays_a, int64_t row, int n_coop) {
+    for (int64_t k = row - n_coop; k >= 0; k -= n_coop)
+        if (rays_a[3 * k + 2] <= CF_LONG) return false;
+    return true;
+}
 template <int C>
 __device__ __forceinline__ void composite_fw_coop(const float* __restrict__ sigmas, const float* __restrict__ raws,
                                                   const float* __restrict__ deltas, const float* __restrict__ ts,
@@ -1050,15 +1061,19 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_fw_kernel(
     int64_t* __restrict__ total_samples, float* __restrict__ opacity, float* __restrict__ depth,
     float* __restrict__ rend, float* __restrict__ ws, float bg, float* __restrict__ rgb_bg, int n_coop) {
     if ((int)blockIdx.x < n_coop) {
-        composite_fw_coop<C>(sigmas, raws, deltas, ts, rays_a, blockIdx.x, T_thr, total_samples, opacity, depth,
-                             rend, ws, bg, rgb_bg);
+        for (int64_t row = blockIdx.x; row < R; row += n_coop) {  // (LDS reuse: see cf_coop_takes)
+            const int N = (int)rays_a[3 * row + 2];
+            if (N <= CF_LONG) break;
+            composite_fw_coop<C>(sigmas, raws, deltas, ts, rays_a, row, T_thr, total_samples, opacity, depth, rend,
+                                 ws, bg, rgb_bg);
+        }
         return;
     }
     const int lane = threadIdx.x & 63;
     const RaySeg g = load_ray_seg(rays_a, R, (int)blockIdx.x - n_coop);
     const int N = g.N;
     const int64_t row = __builtin_amdgcn_readfirstlane((int)((blockIdx.x - n_coop) * CF_WPB + (threadIdx.x >> 6)));
-    if (row < n_coop && N > CF_LONG && N <= CF_COOP_MAX) return;  // taken by workgroup `row` (wave-uniform)
+    if (N > CF_LONG && N <= CF_COOP_MAX && cf_coop_takes(rays_a, row, n_coop)) return;  // (wave-uniform)
     const uint32_t nb = (uint32_t)N * 4u;
     const auto r_s = buf_rsrc(sigmas + g.start, nb), r_d = buf_rsrc(deltas + g.start, nb);
     const auto r_t = buf_rsrc(ts + g.start, nb), r_r = buf_rsrc(raws + g.start * C, nb * C);
@@ -1410,13 +1425,16 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_nodws(
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
     float* __restrict__ dL_draws, float bg, int n_coop) {
     if ((int)blockIdx.x < n_coop) {
-        composite_bw_coop<C, false>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a,
-                                   blockIdx.x, opacity, depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+        for (int64_t row = blockIdx.x; row < R; row += n_coop) {
+            if ((int)rays_a[3 * row + 2] <= CF_LONG) break;
+            composite_bw_coop<C, false>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts,
+                                       rays_a, row, opacity, depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+        }
         return;
     }
     const RaySeg g = load_ray_seg(rays_a, R, (int)blockIdx.x - n_coop);
     const int64_t row = __builtin_amdgcn_readfirstlane((int)((blockIdx.x - n_coop) * CF_WPB + (threadIdx.x >> 6)));
-    if (row < n_coop && g.N > CF_LONG && g.N <= CF_COOP_MAX) return;  // taken by workgroup `row`
+    if (g.N > CF_LONG && g.N <= CF_COOP_MAX && cf_coop_takes(rays_a, row, n_coop)) return;
     composite_bw_ray<C, false>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, g, opacity,
                                depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
 }
@@ -1429,13 +1447,16 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_dws(
     const float* __restrict__ depth, const float* __restrict__ rend, float T_thr, float* __restrict__ dL_dsigmas,
     float* __restrict__ dL_draws, float bg, int n_coop) {
     if ((int)blockIdx.x < n_coop) {
-        composite_bw_coop<C, true>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, rays_a,
-                                   blockIdx.x, opacity, depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+        for (int64_t row = blockIdx.x; row < R; row += n_coop) {
+            if ((int)rays_a[3 * row + 2] <= CF_LONG) break;
+            composite_bw_coop<C, true>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts,
+                                       rays_a, row, opacity, depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
+        }
         return;
     }
     const RaySeg g = load_ray_seg(rays_a, R, (int)blockIdx.x - n_coop);
     const int64_t row = __builtin_amdgcn_readfirstlane((int)((blockIdx.x - n_coop) * CF_WPB + (threadIdx.x >> 6)));
-    if (row < n_coop && g.N > CF_LONG && g.N <= CF_COOP_MAX) return;  // taken by workgroup `row`
+    if (g.N > CF_LONG && g.N <= CF_COOP_MAX && cf_coop_takes(rays_a, row, n_coop)) return;
     composite_bw_ray<C, true>(dL_dopacity, dL_ddepth, dL_drend, dL_dws, sigmas, raws, ws, deltas, ts, g, opacity,
                               depth, rend, T_thr, dL_dsigmas, dL_draws, bg);
 }
@@ -1700,8 +1721,8 @@ int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
 }
 
 // Workgroups for the long rays at the front of rays_a (the training step's rows put them first);
-// the ones whose row is short exit at once.
-static int cf_coop_blocks(int64_t n_rays) { return (int)std::min<int64_t>(n_rays, std::max<int64_t>(64, n_rays / 16)); }
+// the ones whose first row is short exit at once.
+static int cf_coop_blocks(int64_t n_rays) { return (int)std::min<int64_t>(n_rays, 256); }
 
 #define NCN_DISPATCH_C(C_RT, KERNEL, ...)                                                       \
     switch (C_RT) {                                                                            \

@@ -231,12 +231,13 @@ def test_composite_fw_edge(dev):
         np.testing.assert_allclose(a.cpu().numpy(), r, rtol=2e-4, atol=2e-5)
 
 
-def _long_first_inputs(seed):
+def _long_first_inputs(seed, extra_long=0):
     """Segments of 257..1025 samples in the rows at the front of rays_a (the training step's row
     order: the compositors take them with one workgroup each), with transmittance that stops in
     each of the 4 waves' sample ranges or never; then short rays."""
     rng = np.random.default_rng(seed)
     lens = [257, 300, 511, 512, 513, 700, 768, 769, 1000, 1024, 1025, 1024, 600, 400] + list(rng.integers(0, 256, 200))
+    lens += list(rng.integers(257, 1100, extra_long))  # more long rays than the compositors' 256 workgroups
     stop_at = [None, 100, 280, 500, None, 600, 260, 767, 900, None, 1010, 1023, None, 390]
     rows, start, sig_parts = [], 0, []
     for i, n in enumerate(lens):
@@ -245,6 +246,10 @@ def _long_first_inputs(seed):
         s = np.abs(rng.normal(0, 0.2, n)).astype(np.float32)  # T stays well above 1e-4 ...
         if i < len(stop_at) and stop_at[i] is not None and stop_at[i] < n:
             s[stop_at[i]] = 1e5  # ... until an opaque sample
+        elif i >= len(stop_at) and n > 256:  # the extra long rays: an opaque sample anywhere, or none (no borderline stops)
+            k = int(rng.integers(0, 2 * n))
+            if k < n:
+                s[k] = 1e5
         elif i >= len(stop_at):
             s = np.abs(rng.normal(0, 20, n)).astype(np.float32)
         sig_parts.append(s)
@@ -261,10 +266,12 @@ def _long_first_inputs(seed):
     return rays_a, deltas, ts, sig, raws
 
 
-def test_composite_long_rays_workgroup_path(dev):
+@pytest.mark.parametrize("extra_long", [0, 600])
+def test_composite_long_rays_workgroup_path(dev, extra_long):
     """Rays of 257..1024 samples at the front of rays_a go through the one-workgroup-per-ray path
-    (1025 stays single-wave): fw exact counts and 2e-4 values, bw at the parity tolerance."""
-    rays_a, deltas, ts, sig, raws = _long_first_inputs(3)
+    (> 1024 stays single-wave; 600 extra long rays: workgroups take several rows each): fw exact
+    counts and 2e-4 values, bw at the parity tolerance."""
+    rays_a, deltas, ts, sig, raws = _long_first_inputs(3, extra_long)
     T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = vren.composite_train_multi_fw(T(sig), T(raws), T(deltas), T(ts), T(rays_a), 1e-4)
     ref = vren_ref.composite_train_multi_fw(sig, raws, deltas, ts, rays_a, 1e-4)

@@ -1,27 +1,29 @@
 """Print one graph-replayed training step (and one grid-refresh step) from a rocprofv3 kernel trace:
-python3 tools/step_timeline.py gpurun_out/<dir>/run_kernel_trace.csv"""
+python3 tools/step_timeline.py gpurun_out/<dir>/run_kernel_trace.csv
+A step runs from one ncn_step_inputs launch to the next (with the deferred optimizer, the previous
+step's Adam runs on a side stream inside it, beside the marcher)."""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-ends = [i for i, r in enumerate(rows) if "adam_apply" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "step_inputs_kernel" in r["Kernel_Name"]]
 
 
 def show(seg, t0):
     for r in seg:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         print(f"{(s - t0) / 1000:8.1f} {(e - s) / 1000:7.1f}  {r['Kernel_Name'][:80]}")
-    print("span us", (int(seg[-1]["End_Timestamp"]) - t0) / 1000)
+    print("span us", (max(int(r["End_Timestamp"]) for r in seg) - t0) / 1000)
 
 
 done = set()
-for j in range(len(ends) - 1, 0, -1):
-    seg = rows[ends[j - 1] + 1:ends[j] + 1]
+for j in range(len(starts) - 2, 0, -1):
+    seg = rows[starts[j]:starts[j + 1]]
     kind = "refresh" if any("grid_select" in r["Kernel_Name"] for r in seg) else "step"
     if any("spin" in r["Kernel_Name"] for r in seg) or kind in done:
         continue
     print(f"--- {kind}")
-    show(seg, int(rows[ends[j - 1]]["End_Timestamp"]))
+    show(seg, int(seg[0]["Start_Timestamp"]))
     done.add(kind)
     if len(done) == 2:
         break
