@@ -44,7 +44,7 @@ table = model.flat_params()[: model._n_table]
 def fwd(lib):
     return lib.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(None), ptr(table), model._levels_ptr,
                              F32(model._xyz_min),
-                             F32(model._xyz_extent), ptr(packed), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
+                             F32(model._xyz_extent), ptr(packed), I32(0), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
 
 
 main = _lib.lib()
@@ -61,7 +61,7 @@ lmax = torch.empty(16 * 256, device=dev)
 
 def bwd(lib):
     return lib.ncn_field_bwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(None), model._levels_ptr, F32(model._xyz_min),
-                             F32(model._xyz_extent), ptr(packed), ptr(enc), ptr(dsig), ptr(drgb), ptr(None), ptr(gtab),
+                             F32(model._xyz_extent), ptr(packed), I32(0), ptr(enc), ptr(dsig), ptr(drgb), ptr(None), ptr(gtab),
                              ptr(slab),
                              ptr(dE_ws), ptr(lmax), stream())
 
