@@ -728,17 +728,21 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
     const int n_train = (plan_ok && nv > plan.cap()) ? plan.cap() : nv;
     const int niter_eff = n_train == K ? 0 : niter;
     // init picks (plan: first K of rand_perm(seed + 1)), loaded by K threads at once, then sorted
-    // with their index by thread 0 from LDS
+    // with their index by rank (thread k: its position = the picks below it, ties in index order —
+    // the order of a stable sort; one LDS pass per thread instead of a serial insertion sort, whose
+    // dependent LDS round trips cost ~5 us in one thread)
     if (clustered && tid < K) L.picki[tid] = plan_ok ? plan.init(nv, tid) : tid;
     __syncthreads();
-    if (tid == 0 && clustered) {
-        for (int k = 0; k < K; k++) {
-            const int v = L.picki[k];
-            int j = k;
-            for (; j > 0 && L.pick[j - 1] > v; j--) { L.pick[j] = L.pick[j - 1]; L.pick_ord[j] = L.pick_ord[j - 1]; }
-            L.pick[j] = v;
-            L.pick_ord[j] = k;
+    if (clustered && tid < K) {
+        const int v = L.picki[tid];
+        int rk = 0;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int u = L.picki[j];
+            rk += (u < v || (u == v && j < tid)) ? 1 : 0;
         }
+        L.pick[rk] = v;
+        L.pick_ord[rk] = tid;
     }
     for (int j = tid; j < len; j += KM_THREADS) L.pmem[j] = plan_ok ? plan.member(nv, m0 + j) : 1;
     __syncthreads();
