@@ -162,7 +162,10 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
  *   ncn_field_pack_weights(precision) from the fp32 masters.
  * enc_cache: encoding cache for the backward in the operand precision, NCN_ENC_BYTES_PER_SAMPLE
  *   bytes per sample (rounded up to 16 samples, 16-byte aligned); may be NULL for inference.
- * mode 0: full (sigmas + rgbs), mode 1: density only (sigmas; dirs/rgbs ignored).
+ * mode 0: full (sigmas + rgbs), mode 1: density only (sigmas; dirs/rgbs ignored), mode 2: density
+ *   only with the encoding split by level over the XCDs first (the grid refresh's points: each L2
+ *   then serves two levels' tables; order must be NULL): enc_cache is required, as scratch of
+ *   NCN_ENC_BYTES_PER_SAMPLE bytes per point; same sigmas as mode 1, bit for bit.
  * n_dev: NULL, or a device int32 holding the real sample count (<= n): then n is the capacity of
  *   the buffers (static-shape / graph-captured step, where the host never reads the marcher's
  *   counter); grids are sized from n, the kernels stop at *n_dev. ---- */

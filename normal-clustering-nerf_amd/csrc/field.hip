@@ -386,22 +386,27 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
         const int64_t pos = grp * 16 + r;  // processing position; s = the sample it evaluates
         const bool valid = pos < n;
         const int64_t s = valid && order ? (int64_t)order[pos] : pos;
-        float x = 0.f, y = 0.f, z = 0.f;
-        if (valid) {
-            x = (xyzs[3 * s] - xyz_min) / xyz_extent;
-            y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
-            z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
+        v8 e;
+        if (mode == 2) {  // (uniform) the encodings of encode_xcd_kernel (density only)
+            e = enc_cache[grp * 64 + lane];
+        } else {
+            float x = 0.f, y = 0.f, z = 0.f;
+            if (valid) {
+                x = (xyzs[3 * s] - xyz_min) / xyz_extent;
+                y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
+                z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
+            }
+            const float2 e00 = encode_level(table, L, 2 * g, x, y, z);
+            const float2 e01 = encode_level(table, L, 2 * g + 1, x, y, z);
+            const float2 e10 = encode_level(table, L, 8 + 2 * g, x, y, z);
+            const float2 e11 = encode_level(table, L, 9 + 2 * g, x, y, z);
+            e = v8{(T)e00.x, (T)e00.y, (T)e01.x, (T)e01.y, (T)e10.x, (T)e10.y, (T)e11.x, (T)e11.y};
+            if (enc_cache) enc_cache[grp * 64 + lane] = e;
         }
-        const float2 e00 = encode_level(table, L, 2 * g, x, y, z);
-        const float2 e01 = encode_level(table, L, 2 * g + 1, x, y, z);
-        const float2 e10 = encode_level(table, L, 8 + 2 * g, x, y, z);
-        const float2 e11 = encode_level(table, L, 9 + 2 * g, x, y, z);
-        const v8 e = v8{(T)e00.x, (T)e00.y, (T)e01.x, (T)e01.y, (T)e10.x, (T)e10.y, (T)e11.x, (T)e11.y};
-        if (enc_cache) enc_cache[grp * 64 + lane] = e;
         FwdState<T> st;
         mlp_sigma<T>(F, lane, e, st);
         if (g == 0 && valid) sigmas[s] = __expf(st.h[0]);  // TruncExp forward = exp
-        if (mode == 1) continue;
+        if (mode != 0) continue;
         float dx = 0.f, dy = 0.f, dz = 0.f;
         if (valid) {
             dx = dirs[3 * s]; dy = dirs[3 * s + 1]; dz = dirs[3 * s + 2];
@@ -415,6 +420,39 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
             rgbs[3 * s + 2] = sigmoidf_(st.out[2]);
         }
     }
+}
+
+// The hash-grid encoding of the density pass (grid refresh: ~1 M points, one per hit cell, with no
+// ray coherence) split by level over the XCDs: block b runs on XCD b % 8 (dispatch round-robin — a
+// placement hint, nothing depends on it) and XCD x encodes levels x and x + 8 of every point, so each
+// 4 MB L2 holds at most two levels' tables instead of serving all 16 (45.8 MB) from the Infinity
+// Cache (the sample-major forward on Morton-ordered grid points: 436 us; with every hashed level
+// reading one table: 206 us — tools/field_probe.py).  Output: the forward's enc_cache layout (lane
+// (g, r) of a 16-point group holds levels {2g, 2g+1 | 8+2g, 9+2g} of point r), each level's pair of
+// T values written by its own block; field_fwd_kernel mode 2 then runs sigma_net from it.  Same
+// encode_level and operand rounding as the sample-major forward: bit-identical sigmas.
+template <typename T>
+__global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                         const int32_t* __restrict__ n_dev,
+                                                         const float2* __restrict__ table, LevelTable Lt,
+                                                         float xyz_min, float xyz_extent, int nb,
+                                                         T* __restrict__ enc) {
+    __shared__ LevelTable L;
+    load_levels(L, Lt);
+    __syncthreads();
+    if (n_dev) n = min<int64_t>(n, *n_dev);
+    const int x8 = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int l = j < nb ? x8 : x8 + 8, blk = j < nb ? j : j - nb;
+    const int64_t s = (int64_t)blk * 256 + threadIdx.x;
+    if (s >= n) return;
+    const float x = (xyzs[3 * s] - xyz_min) / xyz_extent;
+    const float y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
+    const float z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
+    const float2 a = encode_level(table, L, l, x, y, z);
+    const int g = (l & 7) >> 1, half = l >> 3, sub = l & 1;
+    const int lane = g * 16 + (int)(s & 15);
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    *(t2*)(enc + ((s >> 4) * 64 + lane) * 8 + half * 4 + sub * 2) = t2{(T)a.x, (T)a.y};
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1731,12 +1769,25 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   float xyz_min, float xyz_extent, const uint16_t* weights_packed, int precision, int mode,
                   float* sigmas, float* rgbs, uint16_t* enc_cache, void* stream) {
     if (n <= 0) return 0;
-    NCN_REQUIRE(mode == 0 || mode == 1, hipErrorInvalidValue, "ncn_field_fwd: mode must be 0 or 1");
+    NCN_REQUIRE(mode >= 0 && mode <= 2, hipErrorInvalidValue, "ncn_field_fwd: mode must be 0, 1 or 2");
+    NCN_REQUIRE(mode != 2 || (enc_cache && !order), hipErrorInvalidValue,
+                "ncn_field_fwd: mode 2 needs enc_cache (scratch) and no processing order");
     NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,
                 "ncn_field_fwd: precision must be NCN_PREC_F16 or NCN_PREC_BF16");
     NCN_REQUIRE(((uintptr_t)table & 7) == 0 && ((uintptr_t)enc_cache & 15) == 0 && ((uintptr_t)weights_packed & 15) == 0,
                 hipErrorInvalidValue, "ncn_field_fwd: table 8-byte, enc_cache / weights_packed 16-byte aligned");
     const LevelTable Lt = make_table(levels);
+    if (mode == 2) {  // level-split encoding over the XCDs first (n = capacity; n_dev = the count)
+        NCN_REQUIRE(n <= (int64_t)INT32_MAX * 256 / 16, hipErrorInvalidValue, "ncn_field_fwd: n too large");
+        const int nb = (int)((n + 255) / 256);
+        if (precision == NCN_PREC_F16)
+            hipLaunchKernelGGL(encode_xcd_kernel<_Float16>, dim3(16 * nb), dim3(256), 0, (hipStream_t)stream, xyzs, n,
+                               n_dev, (const float2*)table, Lt, xyz_min, xyz_extent, nb, (_Float16*)enc_cache);
+        else
+            hipLaunchKernelGGL(encode_xcd_kernel<__bf16>, dim3(16 * nb), dim3(256), 0, (hipStream_t)stream, xyzs, n,
+                               n_dev, (const float2*)table, Lt, xyz_min, xyz_extent, nb, (__bf16*)enc_cache);
+        NCN_LAUNCH_CHECK("ncn_field_fwd (encode)");
+    }
     if (precision == NCN_PREC_F16)
         hipLaunchKernelGGL(field_fwd_kernel<_Float16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
                            n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,

@@ -374,6 +374,8 @@ class NGPMT(nn.Module):
             nbytes = int(_lib.lib().ncn_grid_work_bytes())
             ws = {"xyzs": torch.empty(N, 3, device=dev), "idx": torch.empty(N, dtype=torch.int32, device=dev),
                   "sigmas": torch.empty(N, device=dev), "scal": torch.zeros(4, dtype=torch.int32, device=dev),
+                  # the density pass's encodings (ncn_field_fwd mode 2 scratch: 64 B per point)
+                  "enc": torch.empty(((N + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev),
                   "work": torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=dev)}
             self._gws = ws
         return ws
@@ -381,7 +383,7 @@ class NGPMT(nn.Module):
     @torch.no_grad()
     def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False, seed=None):
         """ngp_mt.py:340-368 on the device (csrc/grid.hip): per cascade ncn_grid_sample -> density
-        pass (ncn_field_fwd mode 1 over the hit list, device count) -> ncn_grid_apply, then
+        pass (ncn_field_fwd mode 2 over the hit list, device count) -> ncn_grid_apply, then
         ncn_grid_packbits.  Cells hit: all of them in warmup (get_all_cells), else each cell with the
         marginal probability of the reference's M uniform + M occupied draws with replacement
         (sample_uniform_and_occupied_cells, M = G^3/4) — the documented sampling deviation of
@@ -411,9 +413,11 @@ class NGPMT(nn.Module):
                  F32(density_threshold), I64(N // 4), I32(1 if warmup else 0),
                  _lib.U64((seed + 0x9E3779B97F4A7C15 * c) % 2 ** 64), F32(decay), ptr(cc), ptr(ws["xyzs"]),
                  ptr(ws["idx"]), ptr(n_list), ptr(ws["work"]), stream())
+            # density pass, mode 2: the hash-grid encoding split by level over the XCDs into the
+            # scratch ws["enc"] (each L2 serves two levels' tables), then sigma_net from it
             call("ncn_field_fwd", ptr(ws["xyzs"]), ptr(None), I64(N), ptr(n_list), ptr(None), ptr(table), self._levels_ptr,
-                 F32(self._xyz_min), F32(self._xyz_extent), ptr(packed), I32(self._prec), I32(1), ptr(ws["sigmas"]), ptr(None),
-                 ptr(None), stream())
+                 F32(self._xyz_min), F32(self._xyz_extent), ptr(packed), I32(self._prec), I32(2), ptr(ws["sigmas"]), ptr(None),
+                 ptr(ws["enc"]), stream())
             call("ncn_grid_apply", ptr(dgc), ptr(ws["idx"]), ptr(ws["sigmas"]), ptr(n_list), I64(N), F32(decay),
                  ptr(cc), stream())
         thr_out = ws["scal"][1:2].view(torch.float32)

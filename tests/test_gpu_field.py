@@ -220,3 +220,35 @@ def test_field_morton_window_order(dev, n):
     nt = m._n_table
     for (a, b), tol in (((g0[:nt], g1[:nt]), 2e-4), ((g0[nt:], g1[nt:]), 1e-5)):
         assert float((a - b).norm() / a.norm()) < tol
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_density_level_split_mode_bitexact(dev, precision):
+    """ncn_field_fwd mode 2 (the grid refresh's density pass: encoding split by level over the
+    XCDs into a scratch, then sigma_net) == mode 1 (sample-major) bit for bit, with a device count
+    below the capacity (points past it untouched) and a count that is not a multiple of 16."""
+    from ncnerf_amd import _lib
+    from ncnerf_amd._lib import F32, I32, I64, ptr, stream
+    from ncnerf_amd import vren
+    m = NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev)
+    with torch.no_grad():
+        m.flat_params()[: m._n_table].uniform_(-0.5, 0.5, generator=torch.Generator(device=dev).manual_seed(3))
+    cap = 1 << 18
+    cells = vren.morton3D_invert(torch.arange(0, 2 * cap, 2, dtype=torch.int32, device=dev))
+    g = torch.Generator(device=dev).manual_seed(4)
+    pts = ((cells.float() + torch.rand(cells.shape, device=dev, generator=g)) / 128 - 0.5).contiguous()
+    packed = m._pack_weights()
+    table = m.flat_params()[: m._n_table]
+    for count in (cap, cap - 12345):
+        n_dev = torch.tensor([count], dtype=torch.int32, device=dev)
+        out = []
+        for mode in (1, 2):
+            sig = torch.full((cap,), -7.0, device=dev)
+            enc = torch.empty(cap * 32, dtype=torch.float16, device=dev) if mode == 2 else None
+            _lib.call("ncn_field_fwd", ptr(pts), ptr(None), I64(cap), ptr(n_dev), ptr(None), ptr(table),
+                      m._levels_ptr, F32(m._xyz_min), F32(m._xyz_extent), ptr(packed), I32(m._prec), I32(mode),
+                      ptr(sig), ptr(None), ptr(enc), stream())
+            out.append(sig)
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], out[1]), (precision, count)
+        assert bool((out[1][count:] == -7.0).all()) and bool(torch.isfinite(out[1][:count]).all())

@@ -79,6 +79,19 @@ def timeit(f, lib, reps=20):
     return np.mean([a.elapsed_time(e) for a, e in evs]) * 1e3
 
 
+# the grid refresh's density pass (mode 1): ~1 M points, one per grid cell, cells in Morton order
+cells = vren.morton3D_invert(torch.arange(0, 128 ** 3, 2, dtype=torch.int32, device=dev))
+pts = ((cells.float() + torch.rand(cells.shape, device=dev, generator=torch.Generator(device="cuda").manual_seed(1)))
+       / 128 - 0.5).contiguous()
+sig1 = torch.empty(pts.shape[0], device=dev)
+
+
+def fwd1(lib):
+    return lib.ncn_field_fwd(ptr(pts), ptr(None), I64(pts.shape[0]), ptr(None), ptr(None), ptr(table),
+                             model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(0),
+                             I32(1), ptr(sig1), ptr(None), ptr(None), stream())
+
+
 libs = [("main", main)]
 for so in sorted(glob.glob(os.path.join(ROOT, "tools", "_build", "field_*.so"))):
     L = ctypes.CDLL(so)
@@ -99,7 +112,8 @@ for name, L in libs:
         big = gref.abs() > 1e-3 * gref.abs().max()
         relb = ((g1 - gref)[big].abs() / gref[big].abs()).max().item()
         print(f"   table-grad vs main: rel-L2 {rel:.3e}, max rel on entries > 1e-3 max: {relb:.3e}")
-    print(f"{name:16s} fwd {timeit(fwd, L):8.1f} us   bwd {timeit(bwd, L):8.1f} us", flush=True)
+    print(f"{name:16s} fwd {timeit(fwd, L):8.1f} us   bwd {timeit(bwd, L):8.1f} us   "
+          f"fwd mode 1 ({pts.shape[0]} grid points) {timeit(fwd1, L):8.1f} us", flush=True)
     if hasattr(L, "ncn_diag_sc_times"):
         buf = (ctypes.c_ulonglong * (256 * 8))()
         L.ncn_diag_sc_times(buf, 1)
