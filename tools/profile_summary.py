@@ -40,16 +40,30 @@ def main(rnd):
                      "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM), WRITE_SIZE as read; Infinity-Cache hits included"}
     json.dump(out, open(os.path.join(dst, "composite_fw_traffic.json"), "w"), indent=1)
     print(json.dumps(out))
-    # the bench's roofline launches are the last 50 composite_fw dispatches of the traced run: their
-    # rocprof average must agree with bench.py's live HIP-event figure (roofline.avg_launch_us)
+    # bench.py's roofline launches are the last 135 composite_fw dispatches of the traced run (24 first
+    # calls, 48 cycling 24 input sets = HBM-cold, 48 on one set = warm, 3 first calls + 12 over the
+    # 65536-ray sets); in-step = the dispatches right behind a field forward.  The rocprof averages
+    # must agree with bench.py's live HIP-event figures (roofline.avg_launch_us / warm_us).
     traces = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_trace.csv"), recursive=True)
-    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
-         for r in csv.DictReader(open(traces[0])) if k in r["Kernel_Name"]]
-    live = {"kernel": k, "roofline_launches": 50, "rocprof_avg_us": round(statistics.mean(d[-50:]), 3),
-            "rocprof_median_us": round(statistics.median(d[-50:]), 3),
-            "all_dispatches_avg_us": round(statistics.mean(d), 3), "dispatches": len(d),
-            "method": "rocprofv3 --kernel-trace of `bench.py --steps 30`; the last 50 dispatches are bench.py's "
-                      "back-to-back roofline launches"}
+    rows = sorted(csv.DictReader(open(traces[0])), key=lambda r: int(r["Start_Timestamp"]))
+    dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0  # noqa: E731
+    d = [dur(r) for r in rows if k in r["Kernel_Name"]]
+    instep = [dur(r) for i, r in enumerate(rows) if k in r["Kernel_Name"] and i and "field_fwd" in rows[i - 1]["Kernel_Name"]]
+    rest = d[:-135]
+    live = {"kernel": k + "<3> (ncn_composite_train_fw_bg)",
+            "source": "rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 30 --no-cpu-baseline "
+                      "--no-bf16-line --no-extra-states (gpurun_out/prof_round/trace)",
+            "hbm_cold_48_launches_avg_us": round(statistics.mean(d[-111:-63]), 3),
+            "warm_48_launches_avg_us": round(statistics.mean(d[-63:-15]), 3),
+            "batch65536_12_launches_avg_us": round(statistics.mean(d[-12:]), 3),
+            "in_step_avg_us": round(statistics.mean(instep), 3), "in_step_median_us": round(statistics.median(instep), 3),
+            "in_step_dispatches": len(instep),
+            "in_step_and_eager_avg_us": round(statistics.mean(rest), 3), "in_step_and_eager_dispatches": len(rest),
+            "note": "the bench's roofline launches are the last 135 dispatches: 24 first calls, 48 cycling 24 input "
+                    "sets (HBM-cold), 48 on one set (warm), 3 first calls + 12 over the 65536-ray sets; in_step = the "
+                    "dispatches right behind a field_fwd (graph-replayed steps and the bench's in-step probe); the "
+                    "rocprof kernel durations exclude the per-launch gaps that bench.py's event pair around the "
+                    "back-to-back launches includes"}
     json.dump(live, open(os.path.join(dst, "composite_fw_rocprof_timing.json"), "w"), indent=1)
     print(json.dumps(live))
 
