@@ -50,12 +50,15 @@ class Trainer:
                                   test_time=False, random_bg=False, anneal_strategy="none", anneal_steps=0)
         self.use_graph = use_graph
         self.graph = None
-        # defer_optimizer (graph step, one process): the optimizer step of step k runs inside graph
-        # k+1 on a side stream, concurrently with step k+1's marcher (which reads no parameter), and
-        # joins before the field forward; a refresh of the occupancy grid, or flush_optimizer(),
-        # applies a pending step first.  Parameters read between steps are one step behind until
-        # flush_optimizer() is called.
-        self.defer = bool(defer_optimizer) and use_graph and self.world == 1 and model.scatter_split is None
+        # defer_optimizer (graph step): the optimizer step of step k runs inside graph k+1 on a side
+        # stream, concurrently with step k+1's marcher (which reads no parameter), and joins before
+        # the field forward; a refresh of the occupancy grid, or flush_optimizer(), applies a pending
+        # step first.  Parameters read between steps are one step behind until flush_optimizer() is
+        # called.  N > 1: the gradient all-reduce of step k (eager, after graph k) is ordered before
+        # graph k+1 on the same stream, so the deferred step reads the reduced gradient; DDP's
+        # 1/world goes in as the step's grad_scale.
+        self.defer = bool(defer_optimizer) and use_graph
+        self._grad_scale = 1.0 / self.world
         self._pending = False
         self._rng_seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # marcher jitter stream (CPU generator)
         # optional seed of each grid refresh (global_step -> int); default: drawn from torch's CPU generator
@@ -64,7 +67,7 @@ class Trainer:
     def flush_optimizer(self):
         """Apply the deferred optimizer step (defer_optimizer) now, if one is pending."""
         if self._pending:
-            self.opt.step()
+            self.opt.step(grad_scale=self._grad_scale)
             self._pending = False
 
     def _maybe_update_grid(self, global_step):
@@ -97,7 +100,7 @@ class Trainer:
             side = self._side_stream()
             side.wait_stream(cur)
             with torch.cuda.stream(side):
-                self.opt.step(gated=True)
+                self.opt.step(gated=True, grad_scale=self._grad_scale)
                 m._pack_weights()  # the MLP's fp16 fragments of the updated weights, also beside the marcher
                 m._packed_fresh = True
             kw["premarched"] = march_train_fused(m, batch["rays_o"], batch["rays_d"], kw["near_distance"],
@@ -165,11 +168,12 @@ class Trainer:
             if self.defer:
                 self.opt.gate.fill_(gate)
         self.graph.replay()
-        if not self._with_opt:
-            self.opt.step(grad_scale=distributed.reduce_gradients(self.model))
-        elif self.defer:
+        scale = distributed.reduce_gradients(self.model) if not self._with_opt else 1.0
+        if self.defer:  # (the next graph's side stream applies it, after the reduction above)
             self.opt.step_count += gate
             self._pending = True
+        elif not self._with_opt:
+            self.opt.step(grad_scale=scale)
         else:
             self.opt.step_count += 1
         return self._out

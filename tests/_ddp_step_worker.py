@@ -3,7 +3,8 @@
 `run` — under torchrun every rank trains the model through Trainer(use_graph=True) on ITS OWN
 batches (seeded by rank and step): the N>1 path — graph-captured step without the optimizer, the
 two-bucket gradient all-reduce (SUM) overlapped with the deferred coarse-level table scatter, Adam
-with grad_scale = 1/world — and rank 0 saves the parameters.
+with grad_scale = 1/world (argv[3] == "defer": inside the next step's graph, beside its marcher) —
+and rank 0 saves the parameters.
 
 `run_reference` — one process, the eager step: for every step the gradients of all ranks' batches
 are accumulated into the flat gradient (one backward per batch, no optimizer in between), then one
@@ -36,12 +37,13 @@ def _batch(scene, rank, k, device):
     return batch
 
 
-def run(steps, device, out=None, rank=0):
+def run(steps, device, out=None, rank=0, defer=False):
     from ncnerf_amd.trainer import Trainer
     scene, model = _setup(device)
-    tr = Trainer(model, use_graph=True)
+    tr = Trainer(model, use_graph=True, defer_optimizer=defer)
     for k in range(steps):
         tr.step(_batch(scene, rank, k, device), global_step=3000 + k)
+    tr.flush_optimizer()  # (defer: the last step's optimizer is still pending)
     torch.cuda.synchronize()
     flat = model.flat_params().detach().cpu().clone()
     if out:
@@ -72,6 +74,6 @@ if __name__ == "__main__":
     rank, world = distributed.init_from_env(backend=os.environ.get("DDP_BACKEND", "gloo"))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)) % torch.cuda.device_count())
     run(int(sys.argv[2]), torch.device("cuda", torch.cuda.current_device()), sys.argv[1] if rank == 0 else None,
-        rank=rank)
+        rank=rank, defer=len(sys.argv) > 3 and sys.argv[3] == "defer")
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

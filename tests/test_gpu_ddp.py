@@ -28,11 +28,16 @@ def _port():
     return p
 
 
-def test_two_rank_step_matches_single_process(dev, tmp_path):
+@pytest.mark.parametrize("defer", [False, True])
+def test_two_rank_step_matches_single_process(dev, tmp_path, defer):
+    """defer: the optimizer of step k inside graph k+1 (Trainer(defer_optimizer=True), the bench's
+    default) after the eager all-reduce of step k; 3 steps so that two deferred steps run in-graph."""
     out = str(tmp_path / "flat.pt")
-    steps = 2
+    steps = 3 if defer else 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "_ddp_step_worker.py"), out, str(steps)]
+    if defer:
+        cmd.append("defer")
     env = dict(os.environ, DDP_BACKEND="gloo", OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
