@@ -751,16 +751,18 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
 #pragma unroll
     for (int k = 0; k < K; k++) picks[k] = clustered ? __builtin_amdgcn_readfirstlane(L.pick[k]) : -1;
     CL_STAMP(56);
+    // per-lane copies for the round loop: lane r holds round r's first rank, lane k pick k (sorted),
+    // so a round's rank range is two readlanes and its picks two ballots (no LDS round trip and no
+    // K-long scalar scan per round)
+    const int wo_lane = lane < R ? L.woff[lane][0] : nv;
+    const int pk_lane = (clustered && lane < K) ? L.pick[lane] : INT_MAX;
     auto rank_round = [&](int r, const float* ar) {
         // uniform skip of the rounds that hold neither a rank of this chunk, nor an init pick, nor
         // invalid normals this workgroup labels
-        const int rlo = L.woff[r][0], rhi = r + 1 < R ? L.woff[r + 1][0] : nv;
-        int kbeg = K, kend = K;  // the (sorted) picks inside [rlo, rhi): k in [kbeg, kend)
-#pragma unroll
-        for (int k = K - 1; k >= 0; k--) {
-            if (picks[k] >= rlo) kbeg = k;
-            if (picks[k] >= rhi) kend = k;
-        }
+        const int rlo = __builtin_amdgcn_readlane(wo_lane, r);
+        const int rhi = r + 1 < R ? __builtin_amdgcn_readlane(wo_lane, r + 1) : nv;
+        // the (sorted) picks inside [rlo, rhi): k in [kbeg, kend)
+        const int kbeg = (int)__popcll(__ballot(pk_lane < rlo)), kend = (int)__popcll(__ballot(pk_lane < rhi));
         if (!(rlo < m0 + len && rhi > m0) && r % KM_BLOCKS != (int)blockIdx.x && kbeg == kend) return;
         const bool v = (flags >> r) & 1u;
         const int rank = L.woff[r][wid] + __popcll(__ballot(v) & lt);
