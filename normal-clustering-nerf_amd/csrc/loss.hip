@@ -417,19 +417,6 @@ __device__ __forceinline__ float sum_rows_tagged(const long long* __restrict__ p
     return (float)((double)a * (1.0 / KM_FXL));
 }
 
-// Centroid update from the per-workgroup partials (called by ALL threads of a workgroup): K*4
-// threads sum one (cluster, component) each in fixed workgroup order, K threads form the means, a
-// rare empty cluster is split from the largest one (faiss: +-1/1024 on alternating coordinates)
-// by thread 0, and K threads L2-normalise (spherical k-means).  C holds C_{i-1} on entry (kept
-// for an empty cluster) and C_i on return.
-template <int K>
-struct KmUpdLds {
-    float sums[K * 4];
-    float nc[K][3];
-    float cnt[K];
-    int any_empty;
-};
-
 // faiss's k-means plan (host-built by ncn_kmeans_plan_fill; the faiss restatement of
 // oracle/losses_ref.py): header words, init picks per point count, training-set membership masks
 // per point count above the subsampling cap, split_clusters' RandomGenerator(1234) floats.
@@ -464,56 +451,83 @@ __device__ __forceinline__ void faiss_renorm3(float* x) {
 // the cluster cj found by walking cj = 0, 1, ... (mod K) until RandomGenerator(1234).rand_float()
 // < (count_cj - 1) / (n_train - K), a +-1/1024 perturbation splits the two, and the counts halve
 // (float); then every centroid is L2-renormalised.  The random floats come from the plan.
+// Lanes 4k..4k+3 of waves 0-1 sum (cluster k, component c) over the workgroups' tagged rows, the
+// count and the components meet inside the quad (DPP), and the renormalised centroid goes to C
+// with ONE workgroup barrier; the same float operations as compute-then-renorm (faiss_renorm3's
+// order), so the result is bit-identical.  A rare empty cluster takes the serial split path
+// (thread 0, from the means and counts in LDS) behind two more barriers.  The thread that published
+// acc[t] last round clears it here (the next round's sums start from zero).
+template <int CTRL>
+__device__ __forceinline__ float km_dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int Q>
+__device__ __forceinline__ float km_quad_get(float v) { return km_dpp<Q | (Q << 2) | (Q << 4) | (Q << 6)>(v); }
 template <int K>
-__device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmUpdLds<K>& L, unsigned tag,
-                          unsigned* sync, const KmPlan& plan, int n_train) {
-    if (threadIdx.x < K * 4) L.sums[threadIdx.x] = sum_rows_tagged(part, K * 4, threadIdx.x, tag, sync);
-    if (threadIdx.x == 0) L.any_empty = 0;
-    __syncthreads();
-    if (threadIdx.x < K) {
-        const int k = threadIdx.x;
-        const float n = L.sums[4 * k + 3];
-        L.cnt[k] = n;
+struct KmUpdLds {
+    float nc[K][3];
+    float cnt[K];
+    int emp[2];  // per wave: an empty cluster this round (waves 0 and 1)
+};
+template <int K>
+__device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmUpdLds<K>& L,
+                          unsigned long long* __restrict__ acc, unsigned tag, unsigned* sync, const KmPlan& plan,
+                          int n_train) {
+    static_assert(K * 4 <= 128, "the sums of a round are taken by waves 0 and 1");
+    const int t = threadIdx.x;
+    if (t < K * 4) {  // (quads whole: K * 4 lanes)
+        acc[t] = 0ull;
+        const int k = t >> 2, c = t & 3;
+        const float v = sum_rows_tagged(part, K * 4, t, tag, sync);
+        const float n = km_quad_get<3>(v);
         const float inv = n > 0.f ? 1.0f / n : 0.f;
-#pragma unroll
-        for (int q = 0; q < 3; q++) L.nc[k][q] = L.sums[4 * k + q] * inv;  // (0 for an empty cluster)
-        if (n == 0.f) L.any_empty = 1;
+        const float m = v * inv;  // (0 for an empty cluster)
+        const float x0 = km_quad_get<0>(m), x1 = km_quad_get<1>(m), x2 = km_quad_get<2>(m);
+        if (c < 3) L.nc[k][c] = m;
+        else L.cnt[k] = n;
+        const uint64_t em = __ballot(c == 3 && n == 0.f);
+        if ((t & 63) == 0) L.emp[t >> 6] = em != 0;
+        const float nr = x0 * x0 + x1 * x1 + x2 * x2;  // faiss_renorm3
+        const float y = nr > 0.f ? m * (float)(1.0 / (double)sqrtf(nr)) : m;
+        if (c < 3) C[k][c] = y;
     }
     __syncthreads();
-    if (L.any_empty && threadIdx.x == 0) {
-        const float EPS = 1.0f / 1024.0f;
-        const double denom = (double)(float)(n_train - K);
-        int ri = 0;
-        const int nr = plan.n_rand();
-        for (int ci = 0; ci < K; ci++) {
-            if (L.cnt[ci] != 0.f) continue;
-            int cj = 0;
-            for (;; cj = (cj + 1) % K) {
-                const float pr = (float)(((double)L.cnt[cj] - 1.0) / denom);
-                if (ri >= nr) {  // (a split walk longer than the plan's table: flag and take cj)
-                    __hip_atomic_store(&sync[2], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
+    if (L.emp[0] | L.emp[1]) {  // (uniform, rare)
+        if (threadIdx.x == 0) {
+            const float EPS = 1.0f / 1024.0f;
+            const double denom = (double)(float)(n_train - K);
+            int ri = 0;
+            const int nr = plan.n_rand();
+            for (int ci = 0; ci < K; ci++) {
+                if (L.cnt[ci] != 0.f) continue;
+                int cj = 0;
+                for (;; cj = (cj + 1) % K) {
+                    const float pr = (float)(((double)L.cnt[cj] - 1.0) / denom);
+                    if (ri >= nr) {  // (a split walk longer than the plan's table: flag and take cj)
+                        __hip_atomic_store(&sync[2], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    if (plan.rnd(ri++) < pr) break;
                 }
-                if (plan.rnd(ri++) < pr) break;
+                for (int q = 0; q < 3; q++) {
+                    L.nc[ci][q] = L.nc[cj][q];
+                    if (q % 2 == 0) { L.nc[ci][q] *= 1 + EPS; L.nc[cj][q] *= 1 - EPS; }
+                    else { L.nc[ci][q] *= 1 - EPS; L.nc[cj][q] *= 1 + EPS; }
+                }
+                L.cnt[ci] = L.cnt[cj] / 2;
+                L.cnt[cj] -= L.cnt[ci];
             }
-            for (int q = 0; q < 3; q++) {
-                L.nc[ci][q] = L.nc[cj][q];
-                if (q % 2 == 0) { L.nc[ci][q] *= 1 + EPS; L.nc[cj][q] *= 1 - EPS; }
-                else { L.nc[ci][q] *= 1 - EPS; L.nc[cj][q] *= 1 + EPS; }
-            }
-            L.cnt[ci] = L.cnt[cj] / 2;
-            L.cnt[cj] -= L.cnt[ci];
         }
-    }
-    __syncthreads();
-    if (threadIdx.x < K) {
-        const int k = threadIdx.x;
-        float c[3] = {L.nc[k][0], L.nc[k][1], L.nc[k][2]};
-        faiss_renorm3(c);
+        __syncthreads();
+        if (threadIdx.x < K) {
+            const int k = threadIdx.x;
+            float c[3] = {L.nc[k][0], L.nc[k][1], L.nc[k][2]};
+            faiss_renorm3(c);
 #pragma unroll
-        for (int q = 0; q < 3; q++) C[k][q] = c[q];
+            for (int q = 0; q < 3; q++) C[k][q] = c[q];
+        }
+        __syncthreads();
     }
-    __syncthreads();
 }
 
 // Cluster selection of losses.py:75-166 from the final centroids and sizes -> label_map[K]
@@ -827,14 +841,17 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
         // ---- Lloyd rounds (tagged partials, no grid barrier) ----
         constexpr int NQ = K * 4;
         for (int it = 0; it <= niter_eff; it++) {
-            if (it > 0)
-                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, km_round_tag(seq, it - 1), ws.sync,
-                             plan, n_train);
+            if (it > 0) {  // (clears L.acc behind its barrier)
+                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, L.acc, km_round_tag(seq, it - 1),
+                             ws.sync, plan, n_train);
+            } else {
+                if (tid < NQ) L.acc[tid] = 0ull;
+                if (tid == 0) L.upd.emp[1] = 0;  // (K * 4 <= 64: wave 1 never writes it)
+                __syncthreads();
+            }
             CL_STAMP(2 + 2 * it);
             // assignment + per-cluster (x, y, z, count) sums of the chunk (fixed point, LDS u64 atomics):
             // training rounds over the training set, the final search (it == niter_eff) over all points
-            if (tid < NQ) L.acc[tid] = 0ull;
-            __syncthreads();
             for (int j = tid; j < len; j += KM_THREADS) {
                 const float x = L.pv[0][j], y = L.pv[1][j], z = L.pv[2][j];
                 const int a = nearest<K>(L.C, x, y, z);

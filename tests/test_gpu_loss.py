@@ -47,9 +47,21 @@ def test_normals_fwd_bwd(dev):
     assert rel < 1e-4, rel
 
 
-@pytest.mark.parametrize("n,invalid", [(6272, 0), (6272, 37), (2000, 5)])
+def _degenerate_normals(n, seed):
+    """Three exact directions (+ 50 noisy points): the 20 init picks repeat points, so Lloyd rounds
+    see empty clusters and take faiss's split path (oracle: 11 distinct final centroids)."""
+    rng = np.random.default_rng(seed)
+    axes = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1]], np.float32)
+    x = axes[rng.choice(3, n)].astype(np.float32)
+    x[:50] += rng.normal(0, 0.05, (50, 3)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    return x.astype(np.float32)
+
+
+@pytest.mark.parametrize("n,invalid", [(6272, 0), (6272, 37), (2000, 5), (6272, -1)])
 def test_cluster_loss_parity(dev, n, invalid):
-    X = _manhattan_normals(n, seed=n + invalid, invalid=invalid)
+    """invalid = -1: the degenerate set (empty clusters -> split_clusters in the Lloyd rounds)."""
+    X = _degenerate_normals(n, seed=5) if invalid < 0 else _manhattan_normals(n, seed=n + invalid, invalid=invalid)
     valid = losses_ref.valid_normals_mask(torch.from_numpy(X)).numpy()
     Xv = X[valid]
     C, a = losses_ref.spherical_kmeans(Xv, K=20, niter=20, seed=1234)
