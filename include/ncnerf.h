@@ -227,6 +227,14 @@ int ncn_photo_normals_fwd(const float* rgb, const float* rgb_gt, const float* op
                           float w_opacity, float* loss, const float* rays_o, const float* rays_d, const float* depth,
                           const int64_t* x1, const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals,
                           void* stream);
+/* The same plus the render's composited-sample count (ncn_count_samples: *count_out =
+ * sum(total_samples[0..n_count)), count_acc += {counter[0], the sum} when non-NULL) in one extra
+ * workgroup of the launch; total_samples NULL = ncn_photo_normals_fwd. */
+int ncn_photo_normals_count_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays,
+                                float w_opacity, float* loss, const float* rays_o, const float* rays_d,
+                                const float* depth, const int64_t* x1, const int64_t* x2, const int64_t* x3,
+                                int64_t n_tri, float* normals, const int64_t* total_samples, int64_t n_count,
+                                const int32_t* counter, int64_t* count_out, double* count_acc, void* stream);
 int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1,
                     const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals, void* stream);
 /* dL_ddepth += ...; if term_weights (3 device floats) is non-NULL, dL_dnormals is the (3,n_tri,3)

@@ -214,6 +214,33 @@ __device__ __forceinline__ int opaque_zero() {
 // (Placement is a performance hint only: nothing may depend on it for correctness.)
 __device__ __forceinline__ int xcd_block(int b, int G) { return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3); }
 
+// total_samples.sum() by one 1024-thread workgroup (+ optional f64 accumulators: acc[0] +=
+// counter[0] (marched), acc[1] += the sum (composited)) — ncn_count_samples, and the extra
+// workgroup of ncn_photo_normals_count_fwd.
+__device__ __forceinline__ void count_samples_wg(const int64_t* __restrict__ total, int64_t R,
+                                                 const int32_t* __restrict__ counter, int64_t* __restrict__ sum_out,
+                                                 double* __restrict__ acc) {
+    __shared__ long long part[16];
+    long long v = 0;
+    for (int64_t i = threadIdx.x; i < R; i += blockDim.x) v += total[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)v, off, 64), hi = __shfl_xor((unsigned)((unsigned long long)v >> 32), off, 64);
+        v += (long long)(((unsigned long long)hi << 32) | lo);
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += part[w];
+        *sum_out = t;
+        if (acc) {
+            acc[0] += counter ? (double)counter[0] : 0.0;
+            acc[1] += (double)t;
+        }
+    }
+}
+
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

@@ -148,16 +148,24 @@ __global__ __launch_bounds__(PH_THREADS) void photo_loss_fwd_kernel(const float*
 // The photometric/opacity reduction (workgroup 0) and the normals from depth (the other
 // workgroups, one triangle per thread) in one launch: the two independent forward parts of the
 // fused loss node.
+// With cnt_total: one more workgroup (block 1) sums the compositor's per-ray sample counts (the
+// vr_samples of the render, ncn_count_samples' work) beside them instead of in a launch of its own.
 __global__ __launch_bounds__(PH_THREADS) void photo_normals_fwd_kernel(
     const float* __restrict__ rgb, const float* __restrict__ gt, const float* __restrict__ op, int64_t R, float w_op,
     float* __restrict__ loss, const float* __restrict__ o, const float* __restrict__ d,
     const float* __restrict__ depth, const int64_t* __restrict__ x1, const int64_t* __restrict__ x2,
-    const int64_t* __restrict__ x3, int64_t T, float* __restrict__ normals) {
+    const int64_t* __restrict__ x3, int64_t T, float* __restrict__ normals, const int64_t* __restrict__ cnt_total,
+    int64_t cnt_n, const int32_t* __restrict__ cnt_counter, int64_t* __restrict__ cnt_out, double* __restrict__ cnt_acc) {
     if (blockIdx.x == 0) {
         photo_loss_fwd_wg(rgb, gt, op, R, w_op, loss);
         return;
     }
-    const int64_t t = (int64_t)(blockIdx.x - 1) * PH_THREADS + threadIdx.x;
+    const int nb0 = cnt_total ? 2 : 1;  // workgroups in front of the normals
+    if (cnt_total && blockIdx.x == 1) {
+        count_samples_wg(cnt_total, cnt_n, cnt_counter, cnt_out, cnt_acc);
+        return;
+    }
+    const int64_t t = (int64_t)(blockIdx.x - nb0) * PH_THREADS + threadIdx.x;
     if (t < T) normals_fwd_one(o, d, depth, x1, x2, x3, t, normals);
 }
 // grads scaled by the upstream gradient g[0..1] (device scalars) and zeroed for filtered terms
@@ -1110,15 +1118,27 @@ int ncn_photo_loss_bwd(const float* rgb, const float* rgb_gt, const float* opaci
     return 0;
 }
 
+int ncn_photo_normals_count_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays,
+                                float w_opacity, float* loss, const float* rays_o, const float* rays_d,
+                                const float* depth, const int64_t* x1, const int64_t* x2, const int64_t* x3,
+                                int64_t n_tri, float* normals, const int64_t* total_samples, int64_t n_count,
+                                const int32_t* counter, int64_t* count_out, double* count_acc, void* stream) {
+    NCN_REQUIRE(!total_samples || count_out, hipErrorInvalidValue, "ncn_photo_normals_count_fwd: count_out needed");
+    const int nb0 = total_samples ? 2 : 1;
+    hipLaunchKernelGGL(photo_normals_fwd_kernel, dim3(nb0 + cdiv(std::max<int64_t>(n_tri, 0), PH_THREADS)),
+                       dim3(PH_THREADS), 0, (hipStream_t)stream, rgb, rgb_gt, opacity, n_rays, w_opacity, loss, rays_o,
+                       rays_d, depth, x1, x2, x3, n_tri, normals, total_samples, n_count, counter, count_out,
+                       count_acc);
+    NCN_LAUNCH_CHECK("ncn_photo_normals_fwd");
+    return 0;
+}
+
 int ncn_photo_normals_fwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays,
                           float w_opacity, float* loss, const float* rays_o, const float* rays_d, const float* depth,
                           const int64_t* x1, const int64_t* x2, const int64_t* x3, int64_t n_tri, float* normals,
                           void* stream) {
-    hipLaunchKernelGGL(photo_normals_fwd_kernel, dim3(1 + cdiv(std::max<int64_t>(n_tri, 0), PH_THREADS)),
-                       dim3(PH_THREADS), 0, (hipStream_t)stream, rgb, rgb_gt, opacity, n_rays, w_opacity, loss, rays_o,
-                       rays_d, depth, x1, x2, x3, n_tri, normals);
-    NCN_LAUNCH_CHECK("ncn_photo_normals_fwd");
-    return 0;
+    return ncn_photo_normals_count_fwd(rgb, rgb_gt, opacity, n_rays, w_opacity, loss, rays_o, rays_d, depth, x1, x2,
+                                       x3, n_tri, normals, nullptr, 0, nullptr, nullptr, nullptr, stream);
 }
 
 int ncn_normals_fwd(const float* rays_o, const float* rays_d, const float* depth, const int64_t* x1, const int64_t* x2,

@@ -1514,26 +1514,7 @@ __global__ void morton3D_invert_kernel(const int32_t* __restrict__ idx, int64_t 
 __global__ __launch_bounds__(1024) void count_samples_kernel(const int64_t* __restrict__ total, int64_t R,
                                                              const int32_t* __restrict__ counter,
                                                              int64_t* __restrict__ sum_out, double* __restrict__ acc) {
-    __shared__ long long part[16];
-    long long v = 0;
-    for (int64_t i = threadIdx.x; i < R; i += 1024) v += total[i];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const unsigned lo = __shfl_xor((unsigned)v, off, 64), hi = __shfl_xor((unsigned)((unsigned long long)v >> 32), off, 64);
-        v += (long long)(((unsigned long long)hi << 32) | lo);
-    }
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        long long t = 0;
-#pragma unroll
-        for (int w = 0; w < 16; w++) t += part[w];
-        *sum_out = t;
-        if (acc) {
-            acc[0] += counter ? (double)counter[0] : 0.0;
-            acc[1] += (double)t;
-        }
-    }
+    count_samples_wg(total, R, counter, sum_out, acc);
 }
 
 __global__ void packbits_kernel(const float4* __restrict__ grid, int64_t n_bytes, float thr,

@@ -55,6 +55,7 @@ SIGNATURES = {
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],
     "ncn_photo_loss_fwd": [P, P, P, I64, F32, P, P],
     "ncn_photo_normals_fwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, I64, P, P],
+    "ncn_photo_normals_count_fwd": [P, P, P, I64, F32, P, P, P, P, P, P, P, I64, P, P, I64, P, P, P, P],
     "ncn_photo_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P],
     "ncn_cluster_workspace_words": [I32],
     "ncn_cluster_status_offset": [I32],

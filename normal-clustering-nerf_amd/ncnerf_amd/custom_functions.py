@@ -96,6 +96,15 @@ class VolumeRenderer(torch.autograd.Function):
         return dL_dsigmas, dL_draws, None, None, None, None
 
 
+class CountJob:
+    """The render's sample count handed to the loss node (Trainer's graph step): a plain object, not
+    a dict or tuple, so autocast's input casting of the autograd Function passes it through as is."""
+    __slots__ = ("total", "counter", "acc", "out")
+
+    def __init__(self):
+        self.total = self.counter = self.acc = self.out = None
+
+
 class VolumeRendererBg(torch.autograd.Function):
     """VolumeRenderer followed by render()'s background blend (rendering.py:232-240) as one node:
     -> (total_samples, opacity, depth, rgb = rend + bg * (1 - opacity), ws).  Same kernels with the
@@ -110,8 +119,15 @@ class VolumeRendererBg(torch.autograd.Function):
         ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
         ctx.T_threshold, ctx.bg = T_threshold, bg
         ctx.set_materialize_grads(False)
-        # count = (the marcher's device counter, a float64 (2,) accumulator) or None (ncn_count_samples)
-        cnt = vren.count_samples(total_samples, *(count if count is not None else ()))
+        # count = (the marcher's device counter, a float64 (2,) accumulator[, job]) or None
+        # (ncn_count_samples); with a job dict the count is left to the loss node's first launch
+        # (ncn_photo_normals_count_fwd): cnt is filled there, the caller must run that loss
+        if count is not None and len(count) > 2 and count[2] is not None:
+            cnt = torch.empty((), dtype=torch.int64, device=sigmas.device)
+            job = count[2]
+            job.total, job.counter, job.acc, job.out = total_samples, count[0], count[1], cnt
+        else:
+            cnt = vren.count_samples(total_samples, *(count[:2] if count is not None else ()))
         return cnt, opacity, depth, rgb, ws
 
     @staticmethod

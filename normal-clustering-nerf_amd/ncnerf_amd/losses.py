@@ -249,14 +249,18 @@ class _NeRFLossFused(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, rgb, opacity, depth, rays_o, rays_d, rgb_gt, x1, x2, x3, w_op, K, niter, seed, t_sim, w,
-                step_dev, sched):
+                step_dev, sched, count_job=None):
         R = rgb.shape[0]
         T = x1.shape[0]
         dev = rgb.device
         photo = torch.empty(4, dtype=torch.float32, device=dev)
         normals = torch.empty(T, 3, dtype=torch.float32, device=dev)
-        call("ncn_photo_normals_fwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(w_op), ptr(photo),
-             ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals), stream())
+        cj = count_job  # (custom_functions.CountJob or None)
+        tot = cj.total if cj is not None else None
+        call("ncn_photo_normals_count_fwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(w_op), ptr(photo),
+             ptr(rays_o), ptr(rays_d), ptr(depth), ptr(x1), ptr(x2), ptr(x3), I64(T), ptr(normals), ptr(tot),
+             I64(tot.shape[0] if tot is not None else 0), ptr(cj.counter if cj else None),
+             ptr(cj.out if cj else None), ptr(cj.acc if cj else None), stream())
         out = torch.empty(N_OUT, dtype=torch.float32, device=dev)
         labels = torch.empty(T, dtype=torch.int32, device=dev)
         cents = torch.empty(K, 3, dtype=torch.float32, device=dev)
@@ -286,7 +290,7 @@ class _NeRFLossFused(torch.autograd.Function):
         call("ncn_nerf_loss_bwd", ptr(rgb), ptr(rgb_gt), ptr(opacity), I64(R), F32(ctx.w_op), ptr(photo),
              ptr(rays_o), ptr(rays_d), ptr(depth), ptr(dn), ptr(up_total), ptr(up_terms), ptr(drgb), ptr(dop),
              ptr(ddepth), stream())
-        return (drgb, dop, ddepth) + (None,) * 14
+        return (drgb, dop, ddepth) + (None,) * 15
 
 
 _STD_PATCH = np.arange(64).reshape(8, 8)
@@ -403,7 +407,8 @@ class NeRFMTLoss(nn.Module):
         total, l_rgb, l_op, ort, cdot, cl1, labels, cents, raw = _NeRFLossFused.apply(
             f(pred_w_gt["rgb"]), f(pred_unsup["opacity"]), f(pred_unsup["depth"]), f(pred_unsup["rays_o"]),
             f(pred_unsup["rays_d"]), f(target_gt["rgb"]), x["x1"], x["x2"], x["x3"], float(self.opacity_w), 20, 20,
-            self.kmeans_seed, 1.0 - self.norm_CAN_tres, w, step_dev, (float(self.can_sched_start), float(self._grow)))
+            self.kmeans_seed, 1.0 - self.norm_CAN_tres, w, step_dev, (float(self.can_sched_start), float(self._grow)),
+            kwargs.get("count_job"))
         self.last_cluster = (labels, cents, raw)
         return {"rgb": l_rgb, "opacity": l_op, "norm_D_C_ort_dot": ort, "norm_D_C_centr_dot": cdot,
                 "norm_D_C_centr_L1": cl1, "total": total}
@@ -462,7 +467,11 @@ class NeRFMTLoss(nn.Module):
                 and self.depth_w == 0 and self.norm_DEpth_L1_w == 0 and self.norm_DEpth_dot_w == 0
                 and self.reg_depth_w == 0 and n_w_gt == pred_unsup["opacity"].shape[0] and n_w_gt % 64 == 0
                 and n_w_gt > 0 and _standard_patch_offsets(target_raw["patch_area"], off)):
-            return self._fused(pred_w_gt, target_gt, pred_unsup, kwargs)
+            return self._fused(pred_w_gt, target_gt, pred_unsup, dict(kwargs, count_job=pred_raw.get("_count_job")))
+        job = pred_raw.get("_count_job")
+        if job is not None:  # render left its sample count to the fused node, not used in this configuration
+            call("ncn_count_samples", ptr(job.total), I64(job.total.shape[0]), ptr(job.counter), ptr(job.out),
+                 ptr(job.acc), stream())
         fuse_normals = (clustering and self.pred_norm_depth and unsup_start == 0 and self.norm_DEpth_L1_w == 0
                         and self.norm_DEpth_dot_w == 0)
         if self.pred_norm_depth and not fuse_normals:

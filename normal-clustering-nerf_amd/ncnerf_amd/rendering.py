@@ -15,7 +15,7 @@ marches the next batch while the current one is rendered.
 import torch
 from einops import rearrange
 
-from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer, VolumeRendererBg
+from .custom_functions import CountJob, RayAABBIntersector, RayMarcher, VolumeRenderer, VolumeRendererBg
 from . import vren
 
 
@@ -158,12 +158,18 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     fuse_bg = exp_step_factor == 0 and raws.shape[1] == 3  # white background, rgb only
     renderer = VolumeRendererBg if fuse_bg else VolumeRenderer
     extra = (1.0,) if fuse_bg else ()
-    if fuse_bg and kwargs.get("count_acc") is not None:  # (extension) device-side throughput counters
+    job = CountJob() if fuse_bg and kwargs.get("count_in_loss") else None
+    if fuse_bg and (kwargs.get("count_acc") is not None or job is not None):
+        # (extension) device-side throughput counters; count_in_loss: the sample count is taken by
+        # the loss node's first launch (results["_count_job"]; the caller runs NeRFMTLoss)
         rm = results["rm_samples"]
         rm = rm if isinstance(rm, torch.Tensor) and rm.dtype == torch.int32 and rm.is_cuda else None
-        extra = (1.0, (rm, kwargs["count_acc"]))
+        acc = kwargs.get("count_acc")
+        extra = (1.0, (rm if acc is not None else None, acc, job))
     (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = renderer.apply(
         sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4), *extra)
+    if job is not None and job.out is not None:
+        results["_count_job"] = job
     i = 3
     results["rgb"] = rend if rend.shape[-1] == i else rend[..., :i]  # no slice node for rgb-only
     if model.pred_norm:

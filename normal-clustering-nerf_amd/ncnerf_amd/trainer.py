@@ -89,6 +89,7 @@ class Trainer:
     def _body(self, batch, step_dev, with_opt):
         m = self.model
         kw = dict(self.render_kwargs, global_step=0, static_shapes=True)
+        kw["count_in_loss"] = True  # vr_samples summed by the loss node's first launch (no launch of its own)
         if "march_noise" in batch:
             kw["march_noise"] = batch["march_noise"]
         else:  # jitter drawn on the device from the step counter: no torch RNG node in the graph

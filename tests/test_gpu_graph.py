@@ -130,3 +130,30 @@ def test_deferred_optimizer_matches_graph_step(dev):
     assert int((d > 1e-4).sum()) <= 5e-5 * n_t
     rel_w = float((out[1][1][n_t:] - out[0][1][n_t:]).norm() / out[0][1][n_t:].norm())
     assert rel_w < 1e-3, rel_w
+
+
+def test_graph_step_sample_counts(dev):
+    """The graph step's sample counts (the loss node's first launch sums the compositor's per-ray
+    counts; the bench's device accumulators): vr_samples of each step == the eager render's, and the
+    accumulators hold the marched and composited totals of the replayed steps."""
+    scene = SyntheticScene()
+    m = _model(dev, scene)
+    tr = Trainer(m, update_grid=False, use_graph=True)
+    acc = torch.zeros(2, dtype=torch.float64, device=dev)
+    tr.render_kwargs["count_acc"] = acc
+    want_rm, want_vr = 0, 0
+    for k in range(3):
+        b = scene.torch_batch(2048, seed=70 + k, device=dev)
+        b["march_noise"] = torch.rand(2048, device=dev, generator=torch.Generator(device=dev).manual_seed(k))
+        if k == 1:
+            acc.zero_()  # (step 0 captured the graph: its warm-up bodies counted too)
+        with torch.no_grad():
+            r = render(m, b["rays_o"], b["rays_d"], near_distance=0.01, max_samples=1024,
+                       march_noise=b["march_noise"], static_shapes=True)
+        out, _ = tr.step(b, global_step=1000 + k)
+        torch.cuda.synchronize()
+        assert int(out["vr_samples"]) == int(r["vr_samples"]) > 0
+        if k >= 1:
+            want_rm += int(r["rm_samples"])
+            want_vr += int(r["vr_samples"])
+    assert int(acc[0]) == want_rm and int(acc[1]) == want_vr, (acc.tolist(), want_rm, want_vr)
