@@ -49,9 +49,25 @@ def spawn_ranks(n, argv):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
+    # poll every rank: the first non-zero exit ends the others (a crashed rank would otherwise leave
+    # its peers blocked in a collective and this parent waiting on them forever)
+    import time
     rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            break
+        time.sleep(0.2)
     for p in procs:
-        p.wait()
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
         rc = rc or p.returncode
     return rc
 
@@ -266,6 +282,11 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s)", file=sys.stderr)
         sys.exit(3)
     if args.dist_selftest:
+        if os.environ.get("NCN_SELFTEST_CRASH_RANK") == str(rank):  # (launch test: a rank that dies early)
+            sys.exit(7)
+        if os.environ.get("NCN_SELFTEST_HANG_RANK") == str(rank):  # (launch test: a rank that never returns)
+            import time
+            time.sleep(3600)
         t = torch.tensor([float(rank)])
         if world > 1:
             dist.all_reduce(t)

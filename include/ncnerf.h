@@ -191,7 +191,13 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * loss_scale: NULL, or a device float S (a power of two): the AMP loss scale of the reference's
  * precision=16 run (torch GradScaler, train_nerf.py:954) — the MLP chain runs on the upstream
  * gradients times S (no fp16 underflow) and the outputs leave divided by S (ncn_adam_step's
- * amp_state keeps S and its growth/backoff).
+ * amp_state keeps S and its growth/backoff).  With precision NCN_PREC_F16 the chain also carries
+ * tcnn's own module loss scale NCN_TCNN_LOSS_SCALE (tinycudann/modules.py: fp16 modules multiply
+ * dL/doutput by 128 and divide the input and parameter gradients by 128, on top of the caller's
+ * GradScaler): the factor is S * 128 in, 1 / (S * 128) out.  An "external" AMP caller (the
+ * upstream gradient already carries its GradScaler's scale, as tcnn sees it under PL precision=16)
+ * passes a device 1.0f: the chain then runs at the upstream scale * 128, the outputs keep the
+ * upstream scale.
  * n_blocks is returned by ncn_field_bwd_blocks(n).  dE_ws is a device workspace of
  * ncn_field_bwd_dE_floats(n) floats (the level-major encoding gradient between the MLP pass and the
  * LDS-aggregating table scatter pass). */
@@ -333,6 +339,7 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
  * after NCN_AMP_GROWTH_INTERVAL finite steps in a row the scale doubles (torch.cuda.amp.GradScaler
  * defaults: init 2^16, factors 2 / 0.5, interval 2000). */
 #define NCN_AMP_INIT_SCALE 65536.0f
+#define NCN_TCNN_LOSS_SCALE 128.0f /* tcnn fp16 module loss scale (ncn_field_bwd) */
 #define NCN_AMP_GROWTH_INTERVAL 2000
 int64_t ncn_adam_step_work_floats(void);
 

@@ -31,6 +31,7 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 // MFMA operand traits: T = _Float16 or __bf16; v4 = one K=16 / half a K=32 fragment, v8 = K=32.
 template <typename T> struct Mfma;
 template <> struct Mfma<_Float16> {
+    static constexpr bool f16 = true;
     typedef _Float16 v4 __attribute__((ext_vector_type(4)));
     typedef _Float16 v8 __attribute__((ext_vector_type(8)));
     static __device__ __forceinline__ float4_t k32(v8 a, v8 b, float4_t c) {
@@ -41,6 +42,7 @@ template <> struct Mfma<_Float16> {
     }
 };
 template <> struct Mfma<__bf16> {
+    static constexpr bool f16 = false;
     typedef __bf16 v4 __attribute__((ext_vector_type(4)));
     typedef __bf16 v8 __attribute__((ext_vector_type(8)));
     static __device__ __forceinline__ float4_t k32(v8 a, v8 b, float4_t c) {
@@ -697,9 +699,10 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dL_drgb, const float* __restrict__ loss_scale, float* __restrict__ dE_out,
     float* __restrict__ slab, float* __restrict__ level_max, const int32_t* __restrict__ order) {
     typedef typename Mfma<T>::v4 v4;
-    // AMP loss scale (GradScaler of the reference's precision=16 run): the fp16 chain sees the
-    // upstream gradients times S (a power of two), dE and dW leave it divided by S
-    const float S = loss_scale ? *loss_scale : 1.f, inv_S = 1.f / S;
+    // AMP loss scale (GradScaler of the reference's precision=16 run) times tcnn's fp16 module loss
+    // scale (128): the fp16 chain sees the upstream gradients times S (a power of two), dE and dW
+    // leave it divided by S.  bf16 (fp32's exponent range) runs unscaled, as tcnn's non-fp16 modules.
+    const float S = loss_scale ? *loss_scale * (Mfma<T>::f16 ? NCN_TCNN_LOSS_SCALE : 1.f) : 1.f, inv_S = 1.f / S;
     typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     if (n_dev) n = min<int64_t>(n, *n_dev);

@@ -63,7 +63,7 @@ def reduce_gradients(model):
     Single process: runs the deferred scatter, returns 1."""
     split = getattr(model, "scatter_split", None)
     if not is_distributed():
-        if split is not None and model._deferred is not None:
+        if split is not None and model._deferred:
             model.run_deferred_scatter()
         return 1.0
     if split is None:

@@ -8,8 +8,12 @@ The clustering block runs on the GPU end to end: `_extract_normals_from_ray_batc
 + the three cluster losses + their gradient are ONE persistent launch (`ncn_cluster_loss`), so the
 step no longer copies normals to the host (losses.py:434) or syncs on `.item()`s.
 
-The k-means is a deterministic spherical Lloyd k-means (stratified seeded init, faiss-style
-empty-cluster split); faiss itself is not available and unpinned, see DESIGN.md.
+The k-means restates faiss's published `Clustering::train` as losses.py:86-89 calls it
+(faiss.Kmeans(3, 20, niter=20, spherical=True)): the training set subsampled to 256*K points by
+rand_perm(seed 1234) when larger, the initial centroids the first K of rand_perm(seed 1235), Lloyd
+rounds with spherical renormalisation and faiss's split_clusters for empty clusters (its
+RandomGenerator walk from a host-built std::mt19937 plan), then a final search over all points.
+faiss itself is not available here: parity unpinned w.r.t. faiss, see DESIGN.md §3.
 
 Not provided (weight 0 in every reference config, hyperparameters.py:33-49): semantic,
 Manhattan-NeRF and the canonical-direction terms (raise if enabled).

@@ -123,22 +123,29 @@ class _FieldFunction(torch.autograd.Function):
         if split is None:
             call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), ptr(order), model._levels_ptr, F32(model._xyz_min),
                  F32(model._xyz_extent), ptr(packed), I32(model._prec), ptr(enc), ptr(dsig), ptr(drgb),
-                 ptr(model.amp_state), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
+                 ptr(model._bwd_loss_scale()), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
         else:
             # data-parallel step: the levels [split, 16) are scattered now, [0, split) later by
             # run_deferred_scatter() while the all-reduce of the first bucket is in flight
             lmax = model._level_max()
             call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(model._prec), ptr(enc),
-                 ptr(dsig), ptr(drgb), ptr(model.amp_state),
+                 ptr(dsig), ptr(drgb), ptr(model._bwd_loss_scale()),
                  ptr(slab), ptr(dE_ws), ptr(lmax), stream())
             call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), model._levels_ptr, F32(model._xyz_min),
                  F32(model._xyz_extent), ptr(dE_ws), ptr(lmax), I32(split), I32(16), I32(0), ptr(g_table), stream())
-            model._deferred = (x, n, n_dev, order, dE_ws, lmax, g_table)
+            # (a list: a step with two field backwards — e.g. density() with grad and forward() —
+            # leaves two pending coarse-level scatters, both run by run_deferred_scatter)
+            model._deferred.append((x, n, n_dev, order, dE_ws, lmax, g_table))
         call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
         return None, None, None, None, None, None, None, None
 
 
 class NGPMT(nn.Module):
+    def _bwd_loss_scale(self):
+        """The field backward's loss_scale operand (ncn_field_bwd): the internal GradScaler's scale,
+        a device 1.0 under external AMP, None for bf16."""
+        return self.amp_state if self.amp_state is not None else self._amp_unit
+
     def _level_max(self):
         """ncn_field_bwd's per-level max |dE| workspace: 16 floats per MLP-pass workgroup (<= 256)."""
         dev = self._flat.device
@@ -147,12 +154,22 @@ class NGPMT(nn.Module):
         return self._lmax
 
     def __init__(self, scale, grid_size, rgb_act="Sigmoid", pred_sem=False, pred_norm=False, seed=1337,
-                 precision="fp16", **kwargs):
+                 precision="fp16", amp="internal", **kwargs):
         """precision: MFMA operand type of the MLPs, "fp16" (tcnn's FullyFusedMLP, the reference's AMP
-        run) or "bf16" (config #3); parameters, table and accumulation stay fp32."""
+        run) or "bf16" (config #3); parameters, table and accumulation stay fp32.
+        amp (fp16 only): "internal" — the model keeps its own GradScaler state (`amp_state`, updated by
+        FlatAdam / ncn_adam_step) and the field backward applies it at the MLP's boundary, so the
+        caller's loss is unscaled (the Trainer path); "external" — the caller runs AMP itself
+        (train_nerf.py's PL precision=16 + GradScaler, or torch.cuda.amp.GradScaler): the upstream
+        gradient arrives already scaled, the backward applies only tcnn's own fp16 module scale
+        (x128 in, /128 out, NCN_TCNN_LOSS_SCALE) and the gradients leave in the caller's scale, as
+        tcnn's do; any optimizer (torch.optim.Adam(W), apex FusedAdam) then steps them."""
         super().__init__()
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        if amp not in ("internal", "external"):
+            raise ValueError("amp must be 'internal' or 'external'")
+        self.amp = amp
         self.precision = precision
         self._prec = PRECISIONS[precision]
         if rgb_act != "Sigmoid":
@@ -196,14 +213,17 @@ class NGPMT(nn.Module):
         # underflowing): the field backward multiplies its upstream gradients by the scale and
         # divides its outputs by it; ncn_adam_step skips non-finite steps and grows / backs off the
         # scale.  bf16 operands (fp32's exponent range) run unscaled, as PL's bf16 mode does.
-        self.register_buffer("amp_state", torch.tensor([_lib.AMP_INIT_SCALE, 0.0]) if precision == "fp16" else None)
+        f16 = precision == "fp16"
+        self.register_buffer("amp_state", torch.tensor([_lib.AMP_INIT_SCALE, 0.0]) if f16 and amp == "internal" else None)
+        # external AMP: the backward's loss-scale operand is a constant 1 (only tcnn's x128 remains)
+        self.register_buffer("_amp_unit", torch.ones(1) if f16 and amp == "external" else None, persistent=False)
         # None: the backward scatters every level.  An int L (data-parallel step): levels [L, 16)
         # are scattered in the backward, [0, L) by run_deferred_scatter() (grad_buckets(L)).
         self.scatter_split = None
         # Morton-window processing order (ncn_field_sort_windows) for training batches: off by default
         # (measured: forward 88 -> 72 us, but sort 40 us + MLP backward +6 us + scatter +9 us)
         self.sort_samples = False
-        self._deferred = None
+        self._deferred = []  # pending coarse-level scatters of the split data-parallel step
 
     # -- flat buffers --------------------------------------------------------------------------
     def _apply(self, fn, recurse=True):
@@ -255,12 +275,13 @@ class NGPMT(nn.Module):
     def run_deferred_scatter(self, max_blocks=0):
         """Scatter of the levels [0, scatter_split) left by the last backward (same tensors; inside a
         captured step they are the graph's static buffers, refilled by every replay)."""
-        if self._deferred is None:
+        if not self._deferred:
             raise RuntimeError("run_deferred_scatter: no deferred scatter (scatter_split unset or no backward yet)")
-        x, n, n_dev, order, dE_ws, lmax, g_table = self._deferred
-        call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
-             F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(0), I32(self.scatter_split), I32(max_blocks),
-             ptr(g_table), stream())
+        for x, n, n_dev, order, dE_ws, lmax, g_table in self._deferred:
+            call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
+                 F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(0), I32(self.scatter_split), I32(max_blocks),
+                 ptr(g_table), stream())
+        self._deferred = []
 
     def prepare_weights(self):
         """Pack the MLP weights now (after the optimizer step) so the next forward reuses them."""

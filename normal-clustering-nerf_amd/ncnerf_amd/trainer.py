@@ -5,7 +5,8 @@ refresh every 16 steps (train_nerf.py:314-320) when `update_grid` is on, and the
 learning rate (CosineAnnealingLR(T_max=num_epochs), train_nerf.py:286-288; an epoch is the
 training set's 1000 items, base.py:78-81, split over the ranks by DDP's DistributedSampler).
 
-Hyper-parameters default to the Hypersim config (experiments/hypersim/hyperparameters.py)."""
+Hyper-parameters default to the Hypersim config (experiments/hypersim/hyperparameters.py);
+preset="scannet_manhattan" selects config #5's (experiments/scannet_man/hyperparameters.py)."""
 import math
 
 import torch
@@ -24,6 +25,20 @@ HYPERSIM_HPARAMS = dict(
     loss_norm_can_end=-1, loss_norm_can_grow=2500, lr=1e-2, num_epochs=30, batch_size=8192,
     ray_sampling_strategy="all_images_triang_patch", grad_clip=0.05, pred_norm_depth=True)
 
+# config #5 (experiments/scannet_man/hyperparameters.py): the Hypersim settings with the three
+# normal-clustering weights at 1e-2 (:45-47); scale, grid, samples, lr, batch and clip are equal (:21-24)
+SCANNET_HPARAMS = dict(HYPERSIM_HPARAMS, loss_norm_D_C_ort_dot_w=1e-2, loss_norm_D_C_centr_dot_w=1e-2,
+                       loss_norm_D_C_centr_L1_w=1e-2)
+
+PRESETS = {"hypersim": HYPERSIM_HPARAMS, "scannet_manhattan": SCANNET_HPARAMS}
+
+
+def hparams_for(preset):
+    """The hyper-parameter dict of a dataset preset (train_nerf.py --dataset_name)."""
+    if preset not in PRESETS:
+        raise ValueError(f"unknown preset {preset!r}; one of {sorted(PRESETS)}")
+    return dict(PRESETS[preset])
+
 
 class Trainer:
     warmup_steps = 256
@@ -32,8 +47,10 @@ class Trainer:
     epoch_items = 1000  # base.py:78-81 (training "epoch" = 1000 batches)
 
     def __init__(self, model, hparams=None, update_grid=False, use_graph=False, scatter_split=None,
-                 defer_optimizer=False):
-        self.h = dict(HYPERSIM_HPARAMS, **(hparams or {}))
+                 defer_optimizer=False, preset="hypersim"):
+        """hparams: overrides of the preset's hyper-parameters (PRESETS: "hypersim" = configs #1-#4,
+        "scannet_manhattan" = config #5)."""
+        self.h = dict(hparams_for(preset), **(hparams or {}))
         self.model = model
         self.loss = NeRFMTLoss(self.h)
         # the Adam pass zeroes the gradient it consumed: no zero_grad fill in the step
@@ -186,7 +203,10 @@ class Trainer:
         if global_step % self.status_interval == 0:
             check_cluster_status(m.flat_params().device)  # (raises if an earlier launch timed out)
         self._maybe_update_grid(global_step)
-        self.opt.set_epoch(global_step // self.steps_per_epoch)
+        epoch = global_step // self.steps_per_epoch
+        if epoch != self.opt.epoch:
+            self.flush_optimizer()  # (a pending step belongs to the previous epoch's learning rate)
+        self.opt.set_epoch(epoch)
         if self.use_graph:
             return self._graph_step(batch, global_step)
         kw = dict(self.render_kwargs, global_step=global_step)

@@ -102,6 +102,76 @@ def hash_encode(x01, table, levels):
     return (wts * g).sum(2).reshape(n, L * F_PER_LEVEL)
 
 
+_HG = None
+
+
+def _hg_lib():
+    """oracle/_build/libhashgrid_ref.so (oracle/hashgrid_ref.c), built on first use."""
+    global _HG
+    if _HG is None:
+        import ctypes
+        import os
+        import subprocess
+        here = os.path.dirname(os.path.abspath(__file__))
+        so = os.path.join(here, "_build", "libhashgrid_ref.so")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(os.path.join(here, "hashgrid_ref.c")):
+            subprocess.check_call(["make", "-s", "-C", here])
+        _HG = ctypes.CDLL(so)
+    return _HG
+
+
+def _level_arrays(levels):
+    key = id(levels)
+    cache = getattr(_level_arrays, "cache", {})
+    if key not in cache:
+        cache[key] = (levels,
+                      np.array([lv["scale"] for lv in levels], np.float32),
+                      np.array([lv["res"] for lv in levels], np.int64),
+                      np.array([lv["params"] for lv in levels], np.int64),
+                      np.array([lv["offset"] for lv in levels], np.int64))
+        _level_arrays.cache = cache
+    return cache[key][1:]
+
+
+class _HashEncodeC(torch.autograd.Function):
+    """hash_encode through oracle/hashgrid_ref.c (same algorithm; fw gather, serial bw scatter)."""
+
+    @staticmethod
+    def forward(ctx, x01, table, levels):
+        import ctypes
+        L = _hg_lib()
+        x = x01.detach().contiguous().float()
+        tab = table.detach().contiguous()
+        n = x.shape[0]
+        enc = torch.empty(n, 2 * len(levels), dtype=torch.float32)
+        arrs = _level_arrays(levels)
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        A = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        L.hashgrid_fwd(P(x), ctypes.c_int64(n), P(tab), *[A(a) for a in arrs], P(enc))
+        ctx.save_for_backward(x)
+        ctx.levels, ctx.n_table = levels, table.shape
+        return enc
+
+    @staticmethod
+    def backward(ctx, g):
+        import ctypes
+        (x,) = ctx.saved_tensors
+        g = g.contiguous().float()
+        dt = torch.zeros(ctx.n_table, dtype=torch.float32)
+        arrs = _level_arrays(ctx.levels)
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        A = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _hg_lib().hashgrid_bwd(P(x), ctypes.c_int64(x.shape[0]), P(g), *[A(a) for a in arrs], P(dt))
+        return None, dt, None
+
+
+def encode(x01, table, levels, impl="torch"):
+    """hash_encode (impl "torch") or its C restatement (impl "c", oracle/hashgrid_ref.c)."""
+    if impl == "c":
+        return _HashEncodeC.apply(x01, table, levels)
+    return hash_encode(x01, table, levels)
+
+
 class _RoundST(torch.autograd.Function):
     """Round to fp16/bf16 in the forward, straight-through (fp32, unrounded) in the backward: the
     oracle's backward models the kernel's loss-scaled chain (no fp16 underflow), not an autograd
@@ -155,13 +225,13 @@ def field_forward(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=N
     return sig, rgb, h
 
 
-def density(xyzs, P, levels, scale=0.5, chunk=1 << 18):
+def density(xyzs, P, levels, scale=0.5, chunk=1 << 18, impl="torch"):
     """NGPMT.density (ngp_mt.py:157-171): exp(sigma_net(enc(x))[:, 0]), fp32, in chunks (no grad)."""
     out = []
     with torch.no_grad():
         for i in range(0, xyzs.shape[0], chunk):
             x01 = (xyzs[i:i + chunk] - (-scale)) / (2 * scale)
-            h = torch.relu(hash_encode(x01, P.table, levels) @ P.W1.t()) @ P.W2.t()
+            h = torch.relu(encode(x01, P.table, levels, impl) @ P.W1.t()) @ P.W2.t()
             out.append(torch.exp(h[:, 0]))
     return torch.cat(out) if out else torch.zeros(0)
 
@@ -180,13 +250,14 @@ class _TruncExp(torch.autograd.Function):
         return g * torch.exp(x.clamp(-15, 15))
 
 
-def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=None):
+def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=None, impl="torch"):
     """Same as field_forward with TruncExp's clamped backward, differentiable w.r.t. P.  With
     emulation the forward operands are rounded where the HIP kernel rounds them (the rounding is
-    straight-through in the backward), so ReLU masks match the kernel's."""
+    straight-through in the backward), so ReLU masks match the kernel's.  impl: the encoding's
+    statement ("torch" or "c", see encode())."""
     q = _rounder(emulate_f16, emulate)
     x01 = (xyzs - (-scale)) / (2 * scale)
-    enc = hash_encode(x01, P.table, levels)
+    enc = encode(x01, P.table, levels, impl)
     h = q(torch.relu(q(enc) @ q(P.W1).t())) @ q(P.W2).t()
     sig = _TruncExp.apply(h[:, 0])
     d = dirs / torch.norm(dirs, dim=1, keepdim=True)

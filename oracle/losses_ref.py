@@ -91,6 +91,35 @@ class Mt19937:
         y ^= y >> 18
         return y & 0xFFFFFFFF
 
+    @staticmethod
+    def _twist_np(mt):
+        """The same twist, vectorised in the four ranges whose inputs are all old or all new."""
+        mt = mt.copy()
+
+        def f(i0, i1):
+            i = np.arange(i0, i1)
+            y = (mt[i] & 0x80000000) | (mt[(i + 1) % 624] & 0x7FFFFFFF)
+            mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ np.where(y & 1, np.uint64(0x9908B0DF), np.uint64(0))
+        for a, b in ((0, 227), (227, 454), (454, 623), (623, 624)):
+            f(a, b)
+        return mt
+
+    def draws(self, count):
+        """The next `count` outputs as a uint64 array (same sequence as `count` calls)."""
+        out = []
+        while count > 0:
+            if self.i >= 624:
+                self.mt, self.i = self._twist_np(self.mt), 0
+            y = self.mt[self.i:self.i + count].copy()
+            self.i += y.size
+            count -= y.size
+            y ^= y >> np.uint64(11)
+            y ^= (y << np.uint64(7)) & np.uint64(0x9D2C5680)
+            y ^= (y << np.uint64(15)) & np.uint64(0xEFC60000)
+            y ^= y >> np.uint64(18)
+            out.append(y & np.uint64(0xFFFFFFFF))
+        return np.concatenate(out) if out else np.zeros(0, np.uint64)
+
 
 def rand_perm_prefix(n, seed, m):
     """faiss rand_perm(perm, n, seed) (utils/random.cpp): Fisher-Yates with
@@ -106,8 +135,7 @@ def rand_perm_prefix(n, seed, m):
 
 def rand_floats(seed, count):
     """RandomGenerator::rand_float() = mt() / float(mt.max()) in f32."""
-    rng = Mt19937(seed)
-    return np.array([np.float32(np.float32(rng()) / np.float32(4294967295.0)) for _ in range(count)], np.float32)
+    return (Mt19937(seed).draws(count).astype(np.float32) / np.float32(4294967295.0)).astype(np.float32)
 
 
 MAX_POINTS_PER_CENTROID = 256  # faiss ClusteringParameters default

@@ -43,16 +43,29 @@ INIT_SEED = 4
 THRESHOLD = 0.01 * 1024 / 3 ** 0.5  # train_nerf.py:316 (density_tresh_decay 1)
 
 
-def batch_seed(k):
-    return 10_000 + k
+# Ensemble members (VERDICT r2 "do this" 1): member m draws its own initial parameters, batches,
+# marcher noise and refresh seeds; m = None is the legacy single trajectory of round 2.
+MEMBER_STRIDE = 1_000_000
 
 
-def noise_of(k, n=N_RAYS):
-    return torch.rand(n, generator=torch.Generator().manual_seed(20_000 + k))
+def init_seed(member=None):
+    return INIT_SEED if member is None else 100 + member
 
 
-def grid_seed(k):
-    return 30_000 + k
+def _base(member):
+    return 0 if member is None else MEMBER_STRIDE * (member + 1)
+
+
+def batch_seed(k, member=None):
+    return _base(member) + 10_000 + k
+
+
+def noise_of(k, n=N_RAYS, member=None):
+    return torch.rand(n, generator=torch.Generator().manual_seed(_base(member) + 20_000 + k))
+
+
+def grid_seed(k, member=None):
+    return _base(member) + 30_000 + k
 
 
 def camera_K():
@@ -65,38 +78,38 @@ def _psnr(se, n):
     return -10.0 * math.log10(max(se / n, 1e-12))
 
 
-def run_ref(steps, every, threads, log, out=None):
+def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, impl="torch"):
     from oracle import field_ref, grid_ref
     from oracle.train_ref import CPUTrainer, render_train_ref
     from ncnerf_amd import synthetic
     from ncnerf_amd.synthetic import SyntheticScene
     torch.set_num_threads(threads)
     scene = SyntheticScene()
-    cpu = CPUTrainer(scene.bitfield, seed=INIT_SEED, num_epochs=30, epoch_steps=1000)
+    cpu = CPUTrainer(scene.bitfield, seed=init_seed(member), num_epochs=30, epoch_steps=1000, encode_impl=impl)
     grid, _ = grid_ref.mark_invisible_cells(camera_K(), scene.poses, (synthetic.IMG_W, synthetic.IMG_H), 0.01, 128,
                                             0.5)
     ev = [scene.batch(N_RAYS, seed=s, gt=GT) for s in EVAL_SEEDS]
     curve, t0 = [], time.time()
     for k in range(steps):
         if k % 16 == 0:
-            dens = lambda x: field_ref.density(torch.from_numpy(x), cpu.P, cpu.levels).numpy()  # noqa: E731
-            grid, thr, bf = grid_ref.grid_refresh(grid, dens, THRESHOLD, k < 256, grid_seed(k), 128, 0.5)
+            dens = lambda x: field_ref.density(torch.from_numpy(x), cpu.P, cpu.levels, impl=impl).numpy()  # noqa: E731
+            grid, thr, bf = grid_ref.grid_refresh(grid, dens, THRESHOLD, k < 256, grid_seed(k, member), 128, 0.5)
             cpu.bitfield = np.ascontiguousarray(bf, np.uint8)
-        b = scene.batch(N_RAYS, seed=batch_seed(k), gt=GT)
-        loss, S = cpu.step(b, global_step=k, noise=noise_of(k).numpy())
+        b = scene.batch(n_rays, seed=batch_seed(k, member), gt=GT)
+        loss, S = cpu.step(b, global_step=k, noise=noise_of(k, n_rays, member).numpy())
         if (k + 1) % every == 0 or k + 1 == steps:
             se, n = 0.0, 0
             with torch.no_grad():
                 for e in ev:
                     r = render_train_ref(cpu.P, cpu.levels, e["rays_o"], e["rays_d"], cpu.bitfield,
-                                         np.zeros(N_RAYS, np.float32))
+                                         np.zeros(N_RAYS, np.float32), impl=impl)
                     se += float(((r["rgb"].clamp(0, 1) - torch.from_numpy(e["rgb"])) ** 2).sum())
                     n += e["rgb"].size
             curve.append({"step": k + 1, "psnr": _psnr(se, n), "loss": loss, "samples": S,
                           "occupied_frac": float(np.unpackbits(cpu.bitfield).mean()), "t_s": round(time.time() - t0, 1)})
             log(json.dumps(curve[-1]))
-            res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": N_RAYS, "gt": GT,
-                   "init_seed": INIT_SEED, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
+            res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": n_rays, "gt": GT,
+                   "member": member, "init_seed": init_seed(member), "encode_impl": impl, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
                    "curve": curve}
             if out:  # the trajectory so far (a partial run is usable up to its last checkpoint)
                 with open(out, "w") as f:
@@ -104,7 +117,7 @@ def run_ref(steps, every, threads, log, out=None):
     return res
 
 
-def run_hip(steps, every, log, cross_check=False):
+def run_hip(steps, every, log, cross_check=False, member=None, n_rays=N_RAYS, trainer_kw=None):
     from ncnerf_amd import synthetic
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.rendering import render
@@ -113,7 +126,7 @@ def run_hip(steps, every, log, cross_check=False):
     from oracle import field_ref
     dev = torch.device("cuda:0")
     scene = SyntheticScene()
-    P, _ = field_ref.init_params(seed=INIT_SEED)
+    P, _ = field_ref.init_params(seed=init_seed(member))
     ev = [scene.torch_batch(N_RAYS, seed=s, device=dev, gt=GT) for s in EVAL_SEEDS]
     m = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
     flat, off = m.flat_params(), 0
@@ -123,12 +136,12 @@ def run_hip(steps, every, log, cross_check=False):
             off += W.numel()
     m.mark_invisible_cells(torch.from_numpy(camera_K()), dev, torch.from_numpy(scene.poses).to(dev),
                            (synthetic.IMG_W, synthetic.IMG_H), 0.01)
-    tr = Trainer(m, update_grid=True, use_graph=True)
-    tr.grid_seed = grid_seed
+    tr = Trainer(m, update_grid=True, use_graph=True, **(trainer_kw or {}))
+    tr.grid_seed = lambda k: grid_seed(k, member)
     curve, t0 = [], time.time()
     for k in range(steps):
-        b = scene.torch_batch(N_RAYS, seed=batch_seed(k), device=dev, gt=GT)
-        b["march_noise"] = noise_of(k).to(dev)
+        b = scene.torch_batch(n_rays, seed=batch_seed(k, member), device=dev, gt=GT)
+        b["march_noise"] = noise_of(k, n_rays, member).to(dev)
         _, ld = tr.step(b, global_step=k)
         if (k + 1) % every == 0 or k + 1 == steps:
             se, se_tr, se_or, n = 0.0, 0.0, 0.0, 0
@@ -136,7 +149,7 @@ def run_hip(steps, every, log, cross_check=False):
             if cross_check:  # the same parameters and bitfield through the oracle's renderer (CPU)
                 from oracle.train_ref import render_train_ref
                 flat = m.flat_params().detach().cpu()
-                Pc, levels = field_ref.init_params(seed=INIT_SEED)
+                Pc, levels = field_ref.init_params(seed=init_seed(member))
                 off, ts_ = 0, []
                 for W in Pc.tensors():
                     ts_.append(flat[off:off + W.numel()].view_as(W).clone())
@@ -159,7 +172,7 @@ def run_hip(steps, every, log, cross_check=False):
                           "occupied_frac": float((m.density_bitfield.cpu().numpy()[:, None] >> np.arange(8) & 1).mean()),
                           "t_s": round(time.time() - t0, 1)})
             log(json.dumps(curve[-1]))
-    return {"side": "HIP", "curve": curve}
+    return {"side": "HIP", "member": member, "rays_per_step": n_rays, "curve": curve}
 
 
 def main():
@@ -171,17 +184,21 @@ def main():
     ap.add_argument("--ref", default=None, help="(hip) the oracle trajectory JSON")
     ap.add_argument("--repeats", type=int, default=2, help="(hip) identical-input HIP runs")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--member", type=int, default=None, help="ensemble member (seeds); default: legacy seeds")
+    ap.add_argument("--rays", type=int, default=N_RAYS, help="rays per training step")
+    ap.add_argument("--impl", default="torch", choices=("torch", "c"), help="(ref) the oracle's hash-grid statement")
     ap.add_argument("--cross-check", action="store_true",
                     help="(hip) also render the HIP parameters with the train-path renderer and the oracle's")
     a = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     if a.side == "ref":
-        res = run_ref(a.steps, a.every, a.threads, log, a.out)
+        res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl)
     else:
         ref = json.load(open(a.ref)) if a.ref else None
         steps = ref["steps"] if ref else a.steps
-        runs = [run_hip(steps, a.every, log, cross_check=(i == 0 and a.cross_check)) for i in range(a.repeats)]
-        res = {"steps": steps, "rays_per_step": N_RAYS, "gt": GT, "hip_runs": runs}
+        runs = [run_hip(steps, a.every, log, cross_check=(i == 0 and a.cross_check), member=a.member, n_rays=a.rays)
+                for i in range(a.repeats)]
+        res = {"steps": steps, "rays_per_step": a.rays, "gt": GT, "hip_runs": runs}
         last = [r["curve"][-1]["psnr"] for r in runs]
         res["psnr_hip"] = last
         res["hip_run_to_run_db"] = max(last) - min(last)

@@ -39,3 +39,15 @@ def test_world_mismatch_fails():
                        text=True, timeout=120)
     assert r.returncode == 3, (r.returncode, r.stdout, r.stderr[-2000:])
     assert "--gpus 2" in r.stderr
+
+
+def test_crashed_rank_ends_the_launch():
+    """A rank that exits non-zero ends the others (blocked in the all-reduce) and the parent returns
+    its status instead of hanging (spawn_ranks polls every rank)."""
+    import time
+    t = time.time()
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-selftest"],
+                       env=_env(NCN_SELFTEST_CRASH_RANK="0", NCN_SELFTEST_HANG_RANK="1"), capture_output=True,
+                       text=True, timeout=200)
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    assert time.time() - t < 150
