@@ -224,6 +224,7 @@ class NGPMT(nn.Module):
         # (measured: forward 88 -> 72 us, but sort 40 us + MLP backward +6 us + scatter +9 us)
         self.sort_samples = False
         self._deferred = []  # pending coarse-level scatters of the split data-parallel step
+        self._deferred_static = False  # True once a captured step owns the list (Trainer._capture)
 
     # -- flat buffers --------------------------------------------------------------------------
     def _apply(self, fn, recurse=True):
@@ -281,7 +282,8 @@ class NGPMT(nn.Module):
             call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
                  F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(0), I32(self.scatter_split), I32(max_blocks),
                  ptr(g_table), stream())
-        self._deferred = []
+        if not self._deferred_static:  # (a captured step's entries name its static buffers: kept for every replay)
+            self._deferred = []
 
     def prepare_weights(self):
         """Pack the MLP weights now (after the optimizer step) so the next forward reuses them."""

@@ -157,9 +157,13 @@ class Trainer:
             for _ in range(2):
                 self._body(self._static, self._step_dev, self._with_opt)
         torch.cuda.current_stream(dev).wait_stream(side)
+        self.model._deferred = []  # (the warm-ups' deferred scatters are dropped with their gradients)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._out = self._body(self._static, self._step_dev, self._with_opt)
+        # the captured backward's deferred scatter names the graph's static buffers: every replay's
+        # reduce_gradients runs that same entry
+        self.model._deferred_static = bool(self.model._deferred)
         for t, v in zip(state, saved):
             t.copy_(v)
         self.opt.step_count = saved_count

@@ -191,10 +191,12 @@ def _fixed_sum(X):
     return (q.astype(np.float64) * (1.0 / KM_FXL)).astype(np.float32)
 
 
-def spherical_kmeans(X, K=KM_K, niter=KM_NITER, seed=1234):
+def spherical_kmeans(X, K=KM_K, niter=KM_NITER, seed=1234, trace=None):
     """faiss.Kmeans(3, K, niter, spherical=True).train(X) + index.search(X, 1) (losses.py:86-89),
     restated (module doc) with the HIP kernel's arithmetic (_dots, _fixed_sum), so the device
-    result is reproduced bit for bit.  Returns (centroids (K,3) f32, assign (n,) i64)."""
+    result is reproduced bit for bit.  Returns (centroids (K,3) f32, assign (n,) i64).
+    trace (a list): appends the first training round whose assignment equals the previous round's
+    (from there on the rounds are a fixed point), or niter if none does."""
     X = np.ascontiguousarray(X, dtype=np.float32)
     n = X.shape[0]
     sub, picks = faiss_training_set(n, K, seed)
@@ -205,8 +207,12 @@ def spherical_kmeans(X, K=KM_K, niter=KM_NITER, seed=1234):
         return C, np.argmax(_dots(X, C), axis=1).astype(np.int64)
     C = _renorm(X[picks])
     EPS = 1.0 / 1024.0
-    for _ in range(niter):
+    prev, fixed = None, None
+    for it in range(niter):
         a = np.argmax(_dots(Xt, C), axis=1)  # IndexFlatIP search, ties -> lowest index
+        if fixed is None and prev is not None and np.array_equal(a, prev):
+            fixed = it
+        prev = a
         cnt = np.bincount(a, minlength=K).astype(np.float32)  # hassign
         newC = np.zeros((K, 3), np.float32)
         for k in range(K):
@@ -233,6 +239,8 @@ def spherical_kmeans(X, K=KM_K, niter=KM_NITER, seed=1234):
                 cnt[cj] -= cnt[ci]
         C = _renorm(newC)
     a = np.argmax(_dots(X, C), axis=1).astype(np.int64)  # kmeans.index.search(normals_np, 1)
+    if trace is not None:
+        trace.append(niter if fixed is None else fixed)
     return C, a
 
 

@@ -9,11 +9,9 @@ Checked against the internal path (Trainer: the model's own GradScaler state at 
 FlatAdam) on the same initial parameters, batches and marcher noise:
   * one backward: the external gradients / S equal the internal gradients (the loss scale is an
     exact power of two everywhere; only the f32 atomic order of the table flush differs);
-  * three optimizer steps: parameters agree to the optimizer test's torch-AdamW tolerance
-    (2e-6 relative + 5e-7, tests/test_gpu_optim.py), except entries whose gradient is at the
-    rounding level of that atomic order (Adam with eps 1e-15 turns ANY non-zero gradient into a
-    ~lr step, so a gradient of 1e-12 vs -1e-12 moves the entry by 2 lr): those are counted and
-    bounded, and excluded by the relative size of their gradient, not by a looser tolerance."""
+  * three optimizer steps in lockstep (each from the same parameters and moments): parameters
+    agree to the optimizer test's torch-AdamW tolerance (2e-6 relative + 5e-7,
+    tests/test_gpu_optim.py)."""
 import pytest
 import torch
 
@@ -70,37 +68,48 @@ def test_external_amp_gradient_equals_internal(dev):
     torch.testing.assert_close(ge[n_t:], gi[n_t:], rtol=1e-5, atol=1e-6 * float(gi[n_t:].abs().max()))
 
 
-def test_external_amp_trains_like_internal(dev):
+def test_external_amp_steps_like_internal(dev):
+    """Three training steps in lockstep: before every step the external model takes the internal
+    one's parameters and torch.optim.AdamW takes FlatAdam's moments and step count, so each step
+    is compared from the SAME state (free-running, the two trainings drift apart chaotically: a
+    1e-7 parameter difference from the optimizers' different f32 arithmetic moves the next
+    gradients by ~1e-4 relative through the k-means assignment and the marcher's thresholds, and
+    Adam with eps 1e-15 turns that into lr-sized steps; that drift is what the PSNR ensembles
+    measure).  Per step: the internal path = Trainer (its GradScaler state at the MLP boundary +
+    FlatAdam); the external path = torch.amp.GradScaler + clip_grad_norm_(0.05) + AdamW on
+    amp="external"; the updated parameters must agree to the optimizer test's torch-AdamW
+    tolerance (2e-6 relative + 5e-7), all but order-level sign changes of near-zero gradients
+    (at most 1e-6 of the entries)."""
     steps = 3
     scene, mi = _setup(dev, "internal")
     _, me = _setup(dev, "external")
     tr = Trainer(mi)
     loss_fn = NeRFMTLoss(dict(HYPERSIM_HPARAMS))
-    groups = [{"params": [me.xyz_encoder.params], "weight_decay": 0.0},
-              {"params": [me.sigma_net.params, me.rgb_net.params], "weight_decay": 1e-6}]
+    params = [me.xyz_encoder.params, me.sigma_net.params, me.rgb_net.params]
+    groups = [{"params": params[:1], "weight_decay": 0.0}, {"params": params[1:], "weight_decay": 1e-6}]
     opt = torch.optim.AdamW(groups, lr=1e-2, betas=(0.9, 0.999), eps=1e-15, foreach=False)
     scaler = torch.amp.GradScaler("cuda")  # init_scale 2^16, as PL precision=16
-    last_gi = None
+    n_t = mi._n_table
+    cuts = (0, n_t, n_t + me.sigma_net.params.numel(), mi.flat_params().numel())
+    n = mi.flat_params().numel()
     for k in range(steps):
+        with torch.no_grad():
+            me.flat_params().copy_(mi.flat_params())
+        if k > 0:  # FlatAdam's state -> AdamW's
+            for j, p in enumerate(params):
+                a, b = cuts[j], cuts[j + 1]
+                opt.state[p] = {"step": torch.tensor(float(tr.opt.step_count)), "exp_avg": tr.opt.m[a:b].clone(),
+                                "exp_avg_sq": tr.opt.v[a:b].clone()}
         b = _batch(scene, k, dev)
         tr.step(b, global_step=STEP0 + k)
         opt.zero_grad(set_to_none=False)
         scaler.scale(_loss(me, b, k, loss_fn)).backward()
         scaler.unscale_(opt)
-        if k == steps - 1:
-            last_gi = me.flat_grad().clone()
-        torch.nn.utils.clip_grad_norm_(list(me.parameters()), 0.05)
+        torch.nn.utils.clip_grad_norm_(params, 0.05)
         scaler.step(opt)
         scaler.update()
+        pi, pe = mi.flat_params(), me.flat_params()
+        bad = (pi - pe).abs() > 2e-6 * pe.abs() + 5e-7
+        print(f"step {k}: beyond tolerance {int(bad.sum())} of {n}, max err {float((pi - pe).abs().max()):.3g}")
+        assert int(bad.sum()) <= 1e-6 * n, int(bad.sum())
     assert scaler.get_scale() == 65536.0 and float(mi.amp_state[0]) == 65536.0  # no overflow skips
-    pi, pe = mi.flat_params(), me.flat_params()
-    err = (pi - pe).abs()
-    bad = err > 2e-6 * pe.abs() + 5e-7
-    # entries off by an Adam sign flip: their last gradient sits at the atomic-order rounding level
-    tiny = last_gi.abs() < 1e-6 * float(last_gi.abs().max())
-    print("params beyond tolerance:", int(bad.sum()), "of", pe.numel(), "of which tiny-gradient:", int((bad & tiny).sum()),
-          "max err", float(err.max()))
-    assert int((bad & ~tiny).sum()) <= 1e-5 * pe.numel(), int((bad & ~tiny).sum())
-    assert int(bad.sum()) <= 1e-4 * pe.numel(), int(bad.sum())
-    n_t = mi._n_table
-    torch.testing.assert_close(pe[n_t:], pi[n_t:], rtol=2e-6, atol=5e-7)

@@ -1,0 +1,46 @@
+"""The split data-parallel backward (NGPMT.scatter_split): the table levels [0, split) of every
+field backward are left for run_deferred_scatter (distributed.reduce_gradients runs it while the
+first bucket's all-reduce is in flight).  A step with TWO field backwards must scatter both — the
+pending scatters are a list, not one slot that the second backward overwrites."""
+import pytest
+import torch
+
+from ncnerf_amd.ngp_mt import NGPMT
+
+pytestmark = pytest.mark.gpu
+
+
+def _loss(m, x, d, x2, w):
+    out = m(x, d)
+    s2 = m(x2, d)["sigmas"]
+    return (out["sigmas"] * w[0]).sum() + (out["rgbs"] * w[1]).sum() + (s2 * w[2]).sum()
+
+
+def test_two_backwards_both_deferred_scatters_run(dev):
+    g = torch.Generator(device=dev).manual_seed(3)
+    n = 5000
+    x = (torch.rand(n, 3, device=dev, generator=g) - 0.5) * 0.98
+    x2 = (torch.rand(n, 3, device=dev, generator=g) - 0.5) * 0.98
+    d = torch.nn.functional.normalize(torch.randn(n, 3, device=dev, generator=g), dim=1)
+    w = [torch.randn(n, device=dev, generator=g) * 1e-2, torch.randn(n, 3, device=dev, generator=g) * 1e-2,
+         torch.randn(n, device=dev, generator=g) * 1e-2]
+    grads = []
+    for split in (None, 10):
+        torch.manual_seed(0)
+        m = NGPMT(scale=0.5, grid_size=128).to(dev)
+        with torch.no_grad():
+            m.flat_params()[: m._n_table].uniform_(-0.3, 0.3, generator=torch.Generator(device=dev).manual_seed(5))
+        m.scatter_split = split
+        # two separate backwards in one step (e.g. a density() term and the render's forward())
+        _loss(m, x, d, x2, w).backward()
+        (m(x2, d)["rgbs"] * w[1]).sum().backward()
+        if split is not None:
+            assert len(m._deferred) == 3  # three field backwards, three pending coarse-level scatters
+            m.run_deferred_scatter()
+            assert m._deferred == []
+        torch.cuda.synchronize()
+        grads.append(m.flat_grad().clone())
+    ref, got = grads
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 1e-6, rel
+    assert int(((got == 0) != (ref == 0)).sum()) == 0
