@@ -200,9 +200,13 @@ def box_exit_depth(o, d):
     return t.min(axis=1).astype(np.float32)
 
 
-def make_render_fixture(rendering, ngp_mt):
+def make_render_fixture(rendering, ngp_mt, n_rays=256, name="render_train.npz", seed=0, table_subset=None):
+    """render() + backward of the reference glue on n_rays rays.  table_subset: store the table
+    gradient on that many of its non-zero entries (a seeded random subset; the full set at 8192
+    rays would be ~30 MB) and drop the per-sample arrays (the marcher is pinned bit-exact elsewhere;
+    their f64 sums are kept as checksums)."""
     scene = SyntheticScene()
-    b = scene.batch(256, seed=0)
+    b = scene.batch(n_rays, seed=seed)
     model = ngp_mt.NGPMT(scale=0.5, grid_size=128)
     model.density_bitfield.copy_(torch.from_numpy(scene.bitfield))
     o, d = torch.from_numpy(b["rays_o"]), torch.from_numpy(b["rays_d"])
@@ -210,11 +214,15 @@ def make_render_fixture(rendering, ngp_mt):
     res = rendering.render(model, o, d, near_distance=0.01, max_samples=1024, test_time=False, random_bg=False,
                            anneal_strategy="none", anneal_steps=0)
     g = torch.Generator().manual_seed(2)
-    wr, wd, wo = torch.randn(256, 3, generator=g), torch.randn(256, generator=g), torch.randn(256, generator=g)
+    wr, wd, wo = torch.randn(n_rays, 3, generator=g), torch.randn(n_rays, generator=g), torch.randn(n_rays, generator=g)
     loss = (res["rgb"] * wr).sum() + (res["depth"] * wd).sum() + (res["opacity"] * wo).sum()
     loss.backward()
     gt = model.xyz_encoder.params.grad.view(-1, 2)
     nz = torch.nonzero(gt.abs().sum(1) > 0)[:, 0]
+    n_nz = int(nz.numel())
+    if table_subset is not None and n_nz > table_subset:
+        pick = np.sort(np.random.default_rng(4).choice(n_nz, table_subset, replace=False))
+        nz = nz[torch.from_numpy(pick)]
     out = dict(rays_o=b["rays_o"], rays_d=b["rays_d"], noise=RECORD["noise"], bitfield_seed=0,
                param_seed=PARAM_SEED, table_init=TABLE_INIT, loss_wr=wr.numpy(), loss_wd=wd.numpy(), loss_wo=wo.numpy(),
                rgb=res["rgb"].detach().numpy(), depth=res["depth"].detach().numpy(),
@@ -223,9 +231,14 @@ def make_render_fixture(rendering, ngp_mt):
                rm_samples=np.array(int(res["rm_samples"])), vr_samples=np.array(int(res["vr_samples"])),
                rays_o_out=res["rays_o"].numpy(), grad_sigma_net=model.sigma_net.params.grad.numpy(),
                grad_rgb_net=model.rgb_net.params.grad.numpy(), grad_table_nz_idx=nz.numpy(),
-               grad_table_nz=gt[nz].numpy(), grad_table_norm=np.array(float(gt.norm())))
-    np.savez_compressed(os.path.join(HERE, "render_train.npz"), **out)
-    print("render_train.npz: S=%d vr=%d" % (int(res["rm_samples"]), int(res["vr_samples"])))
+               grad_table_nz=gt[nz].numpy(), grad_table_norm=np.array(float(gt.norm())),
+               grad_table_norm64=np.array(float(gt.double().norm())),
+               grad_table_nnz=np.array(n_nz), batch_seed=np.array(seed))
+    if table_subset is not None:
+        for k in ("ws", "deltas", "ts"):
+            out[k + "_sum"] = np.array(float(np.asarray(out.pop(k), np.float64).sum()))
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print("%s: S=%d vr=%d table nnz=%d" % (name, int(res["rm_samples"]), int(res["vr_samples"]), n_nz))
 
 
 def make_loss_fixture(losses, n_rays=2048, seed=3, name="loss_cluster.npz", step=3000):
@@ -334,9 +347,14 @@ def main():
     only = sys.argv[1:]
     if not only or "render" in only:
         make_render_fixture(rendering, ngp_mt)
+    if not only or "render8192" in only:  # config #2's batch ("do this" 2)
+        make_render_fixture(rendering, ngp_mt, n_rays=8192, name="render_train_8192.npz", seed=21,
+                            table_subset=65536)
     if not only or "loss" in only:
         make_loss_fixture(losses)
         make_loss_fixture(losses, n_rays=1024, seed=5, name="loss_cluster_ramp.npz", step=1200)
+    if not only or "loss8192" in only:  # 6 272 normals: faiss's 256*K subsample path (losses.py:86)
+        make_loss_fixture(losses, n_rays=8192, seed=9, name="loss_cluster_8192.npz", step=3000)
     if not only or "select" in only:
         make_select_fixture(losses)
     if not only or "invisible" in only:

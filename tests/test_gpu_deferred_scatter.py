@@ -30,6 +30,7 @@ def test_two_backwards_both_deferred_scatters_run(dev):
         m = NGPMT(scale=0.5, grid_size=128).to(dev)
         with torch.no_grad():
             m.flat_params()[: m._n_table].uniform_(-0.3, 0.3, generator=torch.Generator(device=dev).manual_seed(5))
+        m.amp_state[0] = 1.0  # (order-1e-2 upstream gradients: no loss scale needed)
         m.scatter_split = split
         # two separate backwards in one step (e.g. a density() term and the render's forward())
         _loss(m, x, d, x2, w).backward()

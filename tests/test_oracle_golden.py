@@ -19,8 +19,11 @@ def _load(name):
     return dict(np.load(os.path.join(G, name), allow_pickle=False))
 
 
-def test_render_train_glue():
-    f = _load("render_train.npz")
+@pytest.mark.parametrize("name", ["render_train.npz", "render_train_8192.npz"])
+def test_render_train_glue(name):
+    """256 rays (every per-sample array, the full table-gradient row set) and config #2's 8192 rays
+    (per-sample arrays as f64 checksums, the table gradient on a seeded 65 536-row subset)."""
+    f = _load(name)
     scene = SyntheticScene()
     P, levels = field_ref.init_params(seed=int(f["param_seed"]), table_init=float(f["table_init"]))
     P = field_ref.FieldParams(*[t.requires_grad_(True) for t in P.tensors()])
@@ -28,8 +31,15 @@ def test_render_train_glue():
     assert res["rm_samples"] == int(f["rm_samples"]) and res["vr_samples"] == int(f["vr_samples"])
     # the reference's rays_a order is the (sequential) stub's order = ray order here
     assert np.array_equal(res["rays_a"], f["rays_a"])
-    assert np.array_equal(res["deltas"], f["deltas"]) and np.array_equal(res["ts"], f["ts"])
-    for k in ("rgb", "depth", "opacity", "ws"):
+    if "ts" in f:
+        assert np.array_equal(res["deltas"], f["deltas"]) and np.array_equal(res["ts"], f["ts"])
+        per_ray = ("rgb", "depth", "opacity", "ws")
+    else:
+        assert float(np.asarray(res["deltas"], np.float64).sum()) == float(f["deltas_sum"])
+        assert float(np.asarray(res["ts"], np.float64).sum()) == float(f["ts_sum"])
+        np.testing.assert_allclose(float(res["ws"].detach().double().sum()), float(f["ws_sum"]), rtol=1e-6)
+        per_ray = ("rgb", "depth", "opacity")
+    for k in per_ray:
         np.testing.assert_allclose(res[k].detach().numpy(), f[k], atol=1e-5, err_msg=k)
     assert np.array_equal(f["rays_o_out"], f["rays_d"])  # quirk q1 is in the fixture
     loss = (res["rgb"] * torch.from_numpy(f["loss_wr"])).sum() + (res["depth"] * torch.from_numpy(f["loss_wd"])).sum() \
@@ -40,11 +50,16 @@ def test_render_train_glue():
     for got, ref in ((gs, f["grad_sigma_net"]), (gr, f["grad_rgb_net"])):
         assert np.linalg.norm(got - ref) <= 1e-4 * np.linalg.norm(ref)
     gt = P.table.grad.numpy()
-    np.testing.assert_allclose(np.linalg.norm(gt), f["grad_table_norm"], rtol=1e-4)
+    if "grad_table_norm64" in f:  # (an f32 norm over ~1.7 M entries is itself off by ~3e-4)
+        np.testing.assert_allclose(np.linalg.norm(gt.astype(np.float64)), f["grad_table_norm64"], rtol=1e-4)
+    else:
+        np.testing.assert_allclose(np.linalg.norm(gt), f["grad_table_norm"], rtol=1e-4)
     np.testing.assert_allclose(gt[f["grad_table_nz_idx"]], f["grad_table_nz"], rtol=1e-3, atol=1e-9)
+    if "grad_table_nnz" in f:
+        assert int((np.abs(gt).sum(1) > 0).sum()) == int(f["grad_table_nnz"])
 
 
-@pytest.mark.parametrize("name", ["loss_cluster.npz", "loss_cluster_ramp.npz"])
+@pytest.mark.parametrize("name", ["loss_cluster.npz", "loss_cluster_ramp.npz", "loss_cluster_8192.npz"])
 def test_loss_and_clustering(name):
     f = _load(name)
     R = f["depth"].shape[0]
