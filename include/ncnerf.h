@@ -342,6 +342,14 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 #define NCN_TCNN_LOSS_SCALE 128.0f /* tcnn fp16 module loss scale (ncn_field_bwd) */
 #define NCN_AMP_GROWTH_INTERVAL 2000
 int64_t ncn_adam_step_work_floats(void);
+/* Data-parallel gradient wire format (replaces DDP's fp16 gradient buckets, train_nerf.py:944-952:
+ * the reference's tcnn parameters and gradients are fp16 at the GradScaler's scale).
+ * pack: wire[i] = fp16(grad[i] * scale[0]) (round to nearest even; overflow -> inf, a step the
+ * GradScaler of ncn_adam_step then skips); unpack: grad[i] = float(wire[i]) / scale[0] (overwrites).
+ * scale: NULL (1) or a device float, the AMP scale S (amp_state[0], a power of two).  n elements,
+ * grad and wire 16-byte aligned. */
+int ncn_grad_pack_f16(const float* grad, int64_t n, const float* scale, uint16_t* wire, void* stream);
+int ncn_grad_unpack_f16(const uint16_t* wire, int64_t n, const float* scale, float* grad, void* stream);
 
 #ifdef __cplusplus
 }

@@ -248,11 +248,67 @@ __global__ __launch_bounds__(256) void step_inputs_kernel(StepCopies c, int nb, 
     }
 }
 
+// DDP gradient wire format (the data-parallel step's all-reduce): the reference's gradients are
+// tcnn's fp16 parameter gradients at the GradScaler's scale S (tcnn modules keep fp16 params, and PL
+// precision=16 scales the loss; train_nerf.py:944-955), so DDP all-reduces fp16 values S * g.  Here
+// the gradient is kept unscaled in fp32; pack writes fp16(S * g) (round to nearest even, overflow ->
+// inf, which the GradScaler step then skips), unpack writes float(w) / S back.  S is a power of two,
+// so only the fp16 rounding of S * g is lossy — the reference's own rounding.  8 elements per thread
+// (two float4 loads, one 16-B store), a scalar tail.
+__global__ __launch_bounds__(256) void grad_pack_f16_kernel(const float* __restrict__ g, int64_t n,
+                                                            const float* __restrict__ scale,
+                                                            _Float16* __restrict__ w) {
+    const float s = scale ? *scale : 1.f;
+    const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+        const float4 a = ((const float4*)g)[2 * i], b = ((const float4*)g)[2 * i + 1];
+        typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+        const h8 o = {(_Float16)(a.x * s), (_Float16)(a.y * s), (_Float16)(a.z * s), (_Float16)(a.w * s),
+                      (_Float16)(b.x * s), (_Float16)(b.y * s), (_Float16)(b.z * s), (_Float16)(b.w * s)};
+        ((h8*)w)[i] = o;
+    }
+    for (int64_t i = 8 * n8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) w[i] = (_Float16)(g[i] * s);
+}
+__global__ __launch_bounds__(256) void grad_unpack_f16_kernel(const _Float16* __restrict__ w, int64_t n,
+                                                              const float* __restrict__ scale, float* __restrict__ g) {
+    const float inv = scale ? 1.f / *scale : 1.f;
+    const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * 256;
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+        const h8 v = ((const h8*)w)[i];
+        ((float4*)g)[2 * i] = make_float4((float)v[0] * inv, (float)v[1] * inv, (float)v[2] * inv, (float)v[3] * inv);
+        ((float4*)g)[2 * i + 1] = make_float4((float)v[4] * inv, (float)v[5] * inv, (float)v[6] * inv, (float)v[7] * inv);
+    }
+    for (int64_t i = 8 * n8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) g[i] = (float)w[i] * inv;
+}
+
 }  // namespace ncn
 
 using namespace ncn;
 
 extern "C" {
+
+int ncn_grad_pack_f16(const float* grad, int64_t n, const float* scale, uint16_t* wire, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(((((uintptr_t)grad) & 15) | (((uintptr_t)wire) & 15)) == 0, hipErrorInvalidValue,
+                "ncn_grad_pack_f16: grad and wire must be 16-byte aligned");
+    const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 4096);
+    hipLaunchKernelGGL(grad_pack_f16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, grad, n, scale,
+                       (_Float16*)wire);
+    NCN_LAUNCH_CHECK("ncn_grad_pack_f16");
+    return 0;
+}
+
+int ncn_grad_unpack_f16(const uint16_t* wire, int64_t n, const float* scale, float* grad, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(((((uintptr_t)grad) & 15) | (((uintptr_t)wire) & 15)) == 0, hipErrorInvalidValue,
+                "ncn_grad_unpack_f16: grad and wire must be 16-byte aligned");
+    const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 4096);
+    hipLaunchKernelGGL(grad_unpack_f16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)wire,
+                       n, scale, grad);
+    NCN_LAUNCH_CHECK("ncn_grad_unpack_f16");
+    return 0;
+}
 
 int ncn_step_inputs(int n_bufs, const void* const* src, void* const* dst, const int64_t* n_bytes, int64_t* step_dst,
                     int64_t step, int32_t* flag_dst, int32_t flag, void* stream) {

@@ -2,8 +2,10 @@
 
 One process per GPU; backend "nccl" is RCCL on ROCm (xGMI).  Every rank draws its own ray batch
 (weak scaling, 8192 rays per rank as in the reference, base.py:94-171); the only data-path exchange
-is the all-reduce (SUM) of the flat gradient buffer (hash table + MLPs, ~45.8 MB fp32) per step,
-the 1/world of DDP's average folded into the optimizer.  `reduce_gradients` issues it as two
+is the all-reduce (SUM) of the flat gradient buffer (hash table + MLPs, 11.5 M values) per step —
+as fp16 values S * g (22.9 MB: the reference's own DDP wire, tcnn's fp16 gradients at the
+GradScaler's scale) when the model runs the fp16 AMP, else fp32 (45.8 MB) — the 1/world of DDP's
+average folded into the optimizer.  `reduce_gradients` issues it as two
 buckets so that most of it overlaps the table scatter: the backward scatters the fine table levels
 [split, 16) first; their bucket (plus the MLP weights, contiguous behind them) is all-reduced
 asynchronously while the coarse levels [0, split) are scattered, then the coarse bucket follows.
@@ -55,26 +57,77 @@ def allreduce_grads(flat_grad, average=True):
     return 1.0
 
 
+# Gradient wire format of the all-reduce.  "auto": fp16 values S * g when the model runs the fp16
+# AMP (it has the GradScaler state amp_state) — what the reference's DDP moves: tcnn keeps fp16
+# parameters, so its gradient buckets are fp16 at PL's loss scale S — half the bytes of fp32 on
+# xGMI; "fp32": the unscaled fp32 gradient (the bf16 / fp32 models always use it: no scale).
+DP_WIRE = os.environ.get("NCN_DP_WIRE", "auto")
+
+
+def wire_of(model):
+    """"fp16" or "fp32": the format reduce_gradients moves the model's gradient in."""
+    if DP_WIRE == "fp32" or getattr(model, "amp_state", None) is None:
+        return "fp32"
+    return "fp16"
+
+
+class _Bucket:
+    """One all-reduce bucket: a view of the flat gradient, moved as is (fp32) or packed to the fp16
+    wire (ncn_grad_pack_f16, x S) and unpacked (/ S) into the same view after the collective."""
+
+    def __init__(self, model, view):
+        self.view = view
+        self.scale = None
+        self.wire = None
+        if wire_of(model) == "fp16":
+            fg = model.flat_grad()
+            if getattr(model, "_wire_buf", None) is None or model._wire_buf.numel() != fg.numel() \
+                    or model._wire_buf.device != fg.device:
+                model._wire_buf = torch.empty(fg.numel(), dtype=torch.float16, device=fg.device)
+            off = (view.data_ptr() - fg.data_ptr()) // 4
+            self.wire = model._wire_buf[off:off + view.numel()]
+            self.scale = model.amp_state
+
+    def start(self):
+        from . import _lib
+        t = self.view
+        if self.wire is not None:
+            _lib.call("ncn_grad_pack_f16", _lib.ptr(self.view), _lib.I64(self.view.numel()), _lib.ptr(self.scale),
+                      _lib.ptr(self.wire), _lib.stream())
+            t = self.wire
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+
+    def finish(self, work):
+        from . import _lib
+        work.wait()
+        if self.wire is not None:
+            _lib.call("ncn_grad_unpack_f16", _lib.ptr(self.wire), _lib.I64(self.view.numel()), _lib.ptr(self.scale),
+                      _lib.ptr(self.view), _lib.stream())
+
+
 def reduce_gradients(model):
     """DDP's gradient all-reduce of one step (sum over ranks; returns the 1/world scale for the
-    optimizer).  With model.scatter_split set, the backward left the coarse table levels unscattered:
-    bucket A (fine levels + MLP weights) is reduced asynchronously while the deferred scatter runs on
-    the current stream, then bucket B; both are waited on (current stream) before returning.
-    Single process: runs the deferred scatter, returns 1."""
+    optimizer), in the format wire_of(model) names.  With model.scatter_split set, the backward left
+    the coarse table levels unscattered: bucket A (fine levels + MLP weights) is reduced
+    asynchronously while the deferred scatter runs on the current stream, then bucket B; both are
+    waited on (current stream) before returning.  Single process: runs the deferred scatter,
+    returns 1."""
     split = getattr(model, "scatter_split", None)
     if not is_distributed():
         if split is not None and model._deferred:
             model.run_deferred_scatter()
         return 1.0
     if split is None:
-        dist.all_reduce(model.flat_grad(), op=dist.ReduceOp.SUM)
+        bk = _Bucket(model, model.flat_grad())
+        bk.finish(bk.start())
     else:
         a, b = model.grad_buckets(split)
-        wa = dist.all_reduce(a, op=dist.ReduceOp.SUM, async_op=True)
+        ba, bb = _Bucket(model, a), _Bucket(model, b)
+        wa = ba.start()
         model.run_deferred_scatter(max_blocks=DP_SCATTER_BLOCKS)
-        wb = dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True)
-        wa.wait()
-        wb.wait()
+        wb = bb.start()
+        ba.finish(wa)
+        bb.finish(wb)
     return 1.0 / dist.get_world_size()
 
 

@@ -8,7 +8,9 @@ and rank 0 saves the parameters.
 
 `run_reference` — one process, the eager step: for every step the gradients of all ranks' batches
 are accumulated into the flat gradient (one backward per batch, no optimizer in between), then one
-Adam step with grad_scale = 1/world, i.e. DDP's average computed without any collective."""
+Adam step with grad_scale = 1/world, i.e. DDP's average computed without any collective.  With the
+fp16 gradient wire (distributed.wire_of: the fp16 AMP model) the per-rank gradients are rounded to
+fp16(S g) and summed as the collective sums them."""
 import os
 import sys
 
@@ -56,14 +58,24 @@ def run_reference(steps, device, world):
     from ncnerf_amd.trainer import Trainer
     scene, model = _setup(device)
     tr = Trainer(model, use_graph=False)
+    from ncnerf_amd import distributed
+    fp16_wire = distributed.wire_of(model) == "fp16"
     for k in range(steps):
         tr.opt.set_epoch((3000 + k) // -(-tr.epoch_items // world))  # the ranks' epoch (DistributedSampler)
+        per_rank = []
         for r in range(world):
             batch = _batch(scene, r, k, device)
             # the graph step's kernels (fused marcher, sample-order compositor) on the eager path
             kw = dict(tr.render_kwargs, global_step=3000 + k, march_noise=batch["march_noise"], static_shapes=True)
             results = render(model, batch["rays_o"], batch["rays_d"], **kw)
             tr.loss(results, batch, global_step=3000 + k)["total"].backward()
+            if fp16_wire:  # each rank's gradient on its own (the wire rounds them separately)
+                per_rank.append(model.flat_grad().clone())
+                model.flat_grad().zero_()
+        if fp16_wire:  # the fp16 wire: fp16(S g_r) per rank, summed (2 ranks: one correctly rounded add), / S
+            S = float(model.amp_state[0])
+            tot = sum((g * S).half().float() for g in per_rank).half().float() / S
+            model.flat_grad().copy_(tot)
         tr.opt.step(grad_scale=1.0 / world)
     torch.cuda.synchronize()
     return model.flat_params().detach().cpu().clone()

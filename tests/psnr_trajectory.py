@@ -117,7 +117,14 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
     return res
 
 
-def run_hip(steps, every, log, cross_check=False, member=None, n_rays=N_RAYS, trainer_kw=None):
+def host_batches(steps, n_rays, member=None):
+    """The training batches of a trajectory (host arrays), to reuse across repeated HIP runs."""
+    from ncnerf_amd.synthetic import SyntheticScene
+    scene = SyntheticScene()
+    return [scene.batch(n_rays, seed=batch_seed(k, member), gt=GT) for k in range(steps)]
+
+
+def run_hip(steps, every, log, cross_check=False, member=None, n_rays=N_RAYS, trainer_kw=None, batches=None):
     from ncnerf_amd import synthetic
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.rendering import render
@@ -140,7 +147,11 @@ def run_hip(steps, every, log, cross_check=False, member=None, n_rays=N_RAYS, tr
     tr.grid_seed = lambda k: grid_seed(k, member)
     curve, t0 = [], time.time()
     for k in range(steps):
-        b = scene.torch_batch(n_rays, seed=batch_seed(k, member), device=dev, gt=GT)
+        if batches is not None:
+            b = {kk: (torch.from_numpy(v).to(dev) if isinstance(v, np.ndarray) and not kk.endswith("_offsets_local")
+                      else v) for kk, v in batches[k].items()}
+        else:
+            b = scene.torch_batch(n_rays, seed=batch_seed(k, member), device=dev, gt=GT)
         b["march_noise"] = noise_of(k, n_rays, member).to(dev)
         _, ld = tr.step(b, global_step=k)
         if (k + 1) % every == 0 or k + 1 == steps:
