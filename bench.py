@@ -285,8 +285,7 @@ def main():
         if os.environ.get("NCN_SELFTEST_CRASH_RANK") == str(rank):  # (launch test: a rank that dies early)
             sys.exit(7)
         if os.environ.get("NCN_SELFTEST_HANG_RANK") == str(rank):  # (launch test: a rank that never returns)
-            import time
-            time.sleep(3600)
+            __import__("time").sleep(3600)
         t = torch.tensor([float(rank)])
         if world > 1:
             dist.all_reduce(t)

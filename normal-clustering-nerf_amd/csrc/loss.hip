@@ -256,6 +256,13 @@ constexpr int NCN_MAX_NQ = 80;       // K * 4 at K = 20
 constexpr int KM_THREADS = KM_THREADS_CFG;  // threads per workgroup of the clustering kernel
 constexpr int KM_BLOCKS = KM_BLOCKS_CFG;    // co-resident workgroups (grid barriers)
 constexpr int KM_CHUNK_MAX = CL_MAX_TRI / KM_BLOCKS;
+// Copies of a Lloyd round's per-cluster LDS accumulators: lane l adds into copy l % KM_ACC_COPIES,
+// so the lanes of one wave that picked the same cluster (same-address u64 atomics serialise) are
+// spread over the copies; the publishing thread sums its word's copies (exact integers: the result
+// does not depend on the split).
+#ifndef KM_ACC_COPIES
+#define KM_ACC_COPIES 4
+#endif
 
 
 __device__ __forceinline__ bool valid_normal(float a, float b, float c) {
@@ -484,7 +491,8 @@ __device__ void km_update(const long long* __restrict__ part, float (*C)[3], KmU
     static_assert(K * 4 <= 128, "the sums of a round are taken by waves 0 and 1");
     const int t = threadIdx.x;
     if (t < K * 4) {  // (quads whole: K * 4 lanes)
-        acc[t] = 0ull;
+#pragma unroll
+        for (int c = 0; c < KM_ACC_COPIES; c++) acc[c * NCN_MAX_NQ + t] = 0ull;
         const int k = t >> 2, c = t & 3;
         const float v = sum_rows_tagged(part, K * 4, t, tag, sync);
         const float n = km_quad_get<3>(v);
@@ -641,6 +649,7 @@ struct ClusterLds {
     int pk[KM_CHUNK_MAX];       // k-means assignment, then selected cluster 0..2 (-1 unselected)
     int plab[KM_CHUNK_MAX];     // selected label +-1..3 / 0
     unsigned long long acc[NCN_MAX_NQ];  // this workgroup's fixed-point sums of the phase
+    unsigned long long accr[KM_ACC_COPIES][NCN_MAX_NQ];  // the Lloyd rounds' sums (per-lane copies)
     float C[K][3];
     float cnt[K];
     int label_map[K];
@@ -850,10 +859,13 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
         constexpr int NQ = K * 4;
         for (int it = 0; it <= niter_eff; it++) {
             if (it > 0) {  // (clears L.acc behind its barrier)
-                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, L.acc, km_round_tag(seq, it - 1),
+                km_update<K>(ws.part + ((it - 1) & 1) * KM_BLOCKS * NQ, L.C, L.upd, &L.accr[0][0], km_round_tag(seq, it - 1),
                              ws.sync, plan, n_train);
             } else {
-                if (tid < NQ) L.acc[tid] = 0ull;
+                if (tid < NQ) {
+#pragma unroll
+                    for (int c = 0; c < KM_ACC_COPIES; c++) L.accr[c][tid] = 0ull;
+                }
                 if (tid == 0) L.upd.emp[1] = 0;  // (K * 4 <= 64: wave 1 never writes it)
                 __syncthreads();
             }
@@ -865,15 +877,20 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
                 const int a = nearest<K>(L.C, x, y, z);
                 L.pk[j] = a;
                 if (it < niter_eff && !L.pmem[j]) continue;
-                atomicAdd(&L.acc[4 * a], km_fixl(x));
-                atomicAdd(&L.acc[4 * a + 1], km_fixl(y));
-                atomicAdd(&L.acc[4 * a + 2], km_fixl(z));
-                atomicAdd(&L.acc[4 * a + 3], (unsigned long long)KM_FXL);
+                unsigned long long* ac = L.accr[lane % KM_ACC_COPIES];
+                atomicAdd(&ac[4 * a], km_fixl(x));
+                atomicAdd(&ac[4 * a + 1], km_fixl(y));
+                atomicAdd(&ac[4 * a + 2], km_fixl(z));
+                atomicAdd(&ac[4 * a + 3], (unsigned long long)KM_FXL);
             }
             __syncthreads();
-            if (tid < NQ)
+            if (tid < NQ) {
+                unsigned long long sum = 0ull;
+#pragma unroll
+                for (int c = 0; c < KM_ACC_COPIES; c++) sum += L.accr[c][tid];
                 st_c(ws.part + (it & 1) * KM_BLOCKS * NQ + blockIdx.x * NQ + tid,
-                     km_tagged(km_round_tag(seq, it), (long long)L.acc[tid]));
+                     km_tagged(km_round_tag(seq, it), (long long)sum));
+            }
             CL_STAMP(3 + 2 * it);
         }
         // ---- select: final cluster sizes = count column of the final-search partials ----

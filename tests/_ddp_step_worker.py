@@ -32,19 +32,39 @@ def _setup(device):
     return scene, model
 
 
-def _batch(scene, rank, k, device):
+# GLOBAL: config #4's layout — ONE global batch per step (65 536 rays), each rank taking its
+# shard_patches slice (8192 rays of whole 8x8 patches); otherwise every rank draws its own batch
+GLOBAL = os.environ.get("DDP_GLOBAL_RAYS")
+
+
+def _batch(scene, rank, k, device, world=1):
+    if GLOBAL:
+        from ncnerf_amd import distributed
+        n = int(GLOBAL)
+        full = scene.batch(n, seed=50_000 + k)
+        lo, hi = distributed.shard_patches(n // 64, rank, world)
+        g = torch.Generator().manual_seed(60_000 + k)
+        noise = torch.rand(n, generator=g)[lo * 64:hi * 64]
+        batch = {}
+        for kk, v in full.items():
+            if hasattr(v, "shape") and not kk.endswith("_offsets_local") and v.shape[:1] == (n,):
+                batch[kk] = torch.from_numpy(v[lo * 64:hi * 64].copy()).to(device)
+            else:
+                batch[kk] = v
+        batch["march_noise"] = noise.to(device)
+        return batch
     batch = scene.torch_batch(N_RAYS, seed=1000 * rank + 10 + k, device=device)
     g = torch.Generator().manual_seed(1000 * rank + k)
     batch["march_noise"] = torch.rand(N_RAYS, generator=g).to(device)
     return batch
 
 
-def run(steps, device, out=None, rank=0, defer=False):
+def run(steps, device, out=None, rank=0, defer=False, world=1):
     from ncnerf_amd.trainer import Trainer
     scene, model = _setup(device)
     tr = Trainer(model, use_graph=True, defer_optimizer=defer)
     for k in range(steps):
-        tr.step(_batch(scene, rank, k, device), global_step=3000 + k)
+        tr.step(_batch(scene, rank, k, device, world), global_step=3000 + k)
     tr.flush_optimizer()  # (defer: the last step's optimizer is still pending)
     torch.cuda.synchronize()
     flat = model.flat_params().detach().cpu().clone()
@@ -64,7 +84,7 @@ def run_reference(steps, device, world):
         tr.opt.set_epoch((3000 + k) // -(-tr.epoch_items // world))  # the ranks' epoch (DistributedSampler)
         per_rank = []
         for r in range(world):
-            batch = _batch(scene, r, k, device)
+            batch = _batch(scene, r, k, device, world)
             # the graph step's kernels (fused marcher, sample-order compositor) on the eager path
             kw = dict(tr.render_kwargs, global_step=3000 + k, march_noise=batch["march_noise"], static_shapes=True)
             results = render(model, batch["rays_o"], batch["rays_d"], **kw)
@@ -72,9 +92,12 @@ def run_reference(steps, device, world):
             if fp16_wire:  # each rank's gradient on its own (the wire rounds them separately)
                 per_rank.append(model.flat_grad().clone())
                 model.flat_grad().zero_()
-        if fp16_wire:  # the fp16 wire: fp16(S g_r) per rank, summed (2 ranks: one correctly rounded add), / S
+        if fp16_wire:  # the fp16 wire: fp16(S g_r) per rank, summed in rank order with fp16 rounding, / S
             S = float(model.amp_state[0])
-            tot = sum((g * S).half().float() for g in per_rank).half().float() / S
+            tot = (per_rank[0] * S).half()
+            for g in per_rank[1:]:
+                tot = (tot.float() + (g * S).half().float()).half()
+            tot = tot.float() / S
             model.flat_grad().copy_(tot)
         tr.opt.step(grad_scale=1.0 / world)
     torch.cuda.synchronize()
@@ -86,6 +109,6 @@ if __name__ == "__main__":
     rank, world = distributed.init_from_env(backend=os.environ.get("DDP_BACKEND", "gloo"))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)) % torch.cuda.device_count())
     run(int(sys.argv[2]), torch.device("cuda", torch.cuda.current_device()), sys.argv[1] if rank == 0 else None,
-        rank=rank, defer=len(sys.argv) > 3 and sys.argv[3] == "defer")
+        rank=rank, defer=len(sys.argv) > 3 and sys.argv[3] == "defer", world=world)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

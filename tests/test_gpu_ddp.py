@@ -51,3 +51,35 @@ def test_two_rank_step_matches_single_process(dev, tmp_path, defer):
     d = (dist_flat - single).abs()
     assert int((d > 1e-4).sum()) <= 3 * floor + 1e-6 * d.numel(), (int((d > 1e-4).sum()), floor)
     assert float((d > 1e-6).float().mean()) <= 1e-3
+
+
+def test_config4_sharded_global_batch_8_ranks(dev, tmp_path, monkeypatch):
+    """Config #4's workload: ONE 65 536-ray global batch per step, sharded over 8 ranks by
+    shard_patches (8192 rays of whole 8x8 patches each), the data-parallel Trainer step (graph,
+    two-bucket all-reduce overlapped with the coarse scatter, deferred optimizer) on 8 gloo ranks
+    sharing this GPU, against one process that accumulates the 8 shards' gradients and steps with
+    1/8.  fp32 wire here (an 8-way fp16 sum's rounding depends on the collective's summation
+    order; the fp16 wire is pinned exactly by the 2-rank test above)."""
+    from ncnerf_amd import distributed
+    monkeypatch.setattr(distributed, "DP_WIRE", "fp32")
+    out = str(tmp_path / "flat8.pt")
+    steps, world = 2, 8
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "_ddp_step_worker.py"), out, str(steps),
+           "defer"]
+    env = dict(os.environ, DDP_BACKEND="gloo", OMP_NUM_THREADS="2", DDP_GLOBAL_RAYS="65536", NCN_DP_WIRE="fp32")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    dist_flat = torch.load(out, weights_only=True)
+    sys.path.insert(0, HERE)
+    import _ddp_step_worker as w
+    monkeypatch.setattr(w, "GLOBAL", "65536")
+    single = w.run_reference(steps, dev, world=world)
+    single2 = w.run_reference(steps, dev, world=world)
+    assert torch.isfinite(single).all()
+    floor = int(((single2 - single).abs() > 1e-4).sum())
+    d = (dist_flat - single).abs()
+    print(f"8 ranks vs single process: {int((d > 1e-4).sum())} entries off by > 1e-4 (floor {floor}), "
+          f"{float((d > 1e-6).float().mean()):.2e} off by > 1e-6")
+    assert int((d > 1e-4).sum()) <= 3 * floor + 1e-6 * d.numel(), (int((d > 1e-4).sum()), floor)
+    assert float((d > 1e-6).float().mean()) <= 1e-3

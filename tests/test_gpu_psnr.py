@@ -1,15 +1,33 @@
-"""PSNR parity of the HIP training step against the oracle CPU step after equal steps (same
-init, batches and marcher noise; tests/psnr_parity.py).  A short run: 40 steps of 1024 rays.
-Tolerance 0.1 dB here (north_star: 0.05 dB; the longer committed runs are in profiles/round2/):
-the two trainings differ by fp16 MLP operands and summation order, nothing else, and the HIP side
-alone moves by ~0.03 dB run to run at 40 steps (float-atomic order of the table-gradient flush):
-four runs of this test measured -0.031, -0.034, -0.039 and -0.058 dB, so a 0.05 dB bound would
-fail on run-to-run noise, not on a systematic difference."""
+"""PSNR parity of the HIP training step against the oracle CPU step (north_star: "PSNR within
++-0.05 dB of reference after equal steps").
+
+Why an ensemble: on this synthetic room a single trajectory is chaotic — the fp16 MLP operands of
+the HIP field and the oracle's fp32 ones start two trajectories apart at the 1e-3 level, and after
+~100 steps two trainings from the SAME inputs differ by ~0.2 dB at step 125 and by dB later (two
+HIP runs on identical inputs, which differ only by float-atomic order, stay within ~0.01 dB at
+step 125 and then split too).  So parity is a statement about the mean over seeds, read against
+the standard error of the paired difference (tests/psnr_ensemble.py):
+
+* test_psnr_ensemble_vs_oracle: 4 members of the committed oracle ensemble
+  (tests/golden/psnr_oracle_ensemble.json: 12 seeds, 2048-ray batches, grid refresh on, 1000
+  steps) re-trained on the HIP path for 250 steps; the mean paired difference HIP - oracle at
+  steps 125 and 250 must lie within 3 standard errors, the SE from the paired-difference spread
+  measured on the full 12-member ensemble (tests/golden/psnr_hip_ensemble.json: 3 HIP runs per
+  member, committed from a GPU run of `tests/psnr_ensemble.py hip`) — a bias of that size
+  (0.3-0.5 dB) is what the round-1 fp16-underflow bug produced (+3 dB at 250 steps);
+* test_psnr_parity_short: one pair (same init, batches, noise; 1024-ray batches, 40 steps) within
+  0.1 dB, and the HIP test renderer vs the oracle renderer on the SAME parameters within 0.05 dB
+  (the renderers themselves agree to ~1e-3 dB)."""
+import json
+import math
+import os
+
 import pytest
 
 from psnr_parity import run
 
 pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def test_psnr_parity_short():
@@ -19,3 +37,19 @@ def test_psnr_parity_short():
     assert abs(r["delta_db"]) <= 0.1, r
     # the HIP test renderer and the oracle renderer agree on the same parameters
     assert abs(r["psnr_ref_hip_render_same_rays"] - r["psnr_ref_oracle_render"]) <= 0.05, r
+
+
+def test_psnr_ensemble_vs_oracle():
+    import psnr_ensemble as pe
+    oracle = json.load(open(os.path.join(G, "psnr_oracle_ensemble.json")))
+    ref_stats = {s["step"]: s for s in json.load(open(os.path.join(G, "psnr_hip_ensemble.json")))["stats"]}
+    members = [m["member"] for m in oracle["members"]][:4]
+    runs = pe.run_hip_ensemble(members, 1, 250, 125, oracle["members"][0]["rays_per_step"], print)
+    st = pe.stats(oracle, runs)
+    assert [s["step"] for s in st] == [125, 250]
+    for s in st:
+        sd = ref_stats[s["step"]]["paired_delta_sd"]  # paired-difference spread of the full ensemble
+        bound = 3.0 * sd / math.sqrt(s["members"])
+        print(f"step {s['step']}: mean paired delta {s['paired_delta_mean']:+.3f} dB over {s['members']} members, "
+              f"bound +-{bound:.3f} (3 SE, sd {sd:.3f} from the committed 12-member ensemble)")
+        assert abs(s["paired_delta_mean"]) <= bound, s
