@@ -307,7 +307,7 @@ def main():
 
     GT = "surface_bright"  # synthetic target colours (ncnerf_amd.synthetic)
 
-    def measure(precision, steps, kernel_table, pretrain, state="procedural"):
+    def measure(precision, steps, kernel_table, pretrain, state="procedural", preset="hypersim"):
         """Build the model in `precision`, pretrain it `pretrain` untimed steps, warm up, time `steps`
         graph-replayed training steps (barrier + synchronize on both sides), max over ranks.
         state "procedural": the procedural occupancy grid (BASELINE.md §2), fixed while pretraining;
@@ -316,7 +316,7 @@ def main():
         scene = SyntheticScene()
         model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
         trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph,
-                          defer_optimizer=not args.no_defer)
+                          defer_optimizer=not args.no_defer, preset=preset)
         # marched / composited sample counts accumulated on the device by the step itself
         # (ncn_count_samples: no per-step copies in the timed region)
         count_acc = torch.zeros(2, dtype=torch.float64, device=dev)
@@ -431,6 +431,13 @@ def main():
                           "rm_samples_per_ray": round(float(r3["tot"][0].item()) / n_r, 2),
                           "pretrain_steps": pre, "state": what}
             del r3
+        # config #5's preset (ScanNet-Manhattan hyper-parameters: cluster weights 1e-2) on the same inputs
+        r5 = measure(args.precision, args.steps, False, args.pretrain, "procedural", "scannet_manhattan")
+        extra["other_config"] = {"preset": "scannet_manhattan", "value": round(args.rays * world * args.steps / r5["el"], 1),
+                                 "unit": "rays/s", "ms_per_step": round(1e3 * r5["el"] / args.steps, 3),
+                                 "workload": "configs[4]'s hyper-parameters (experiments/scannet_man/hyperparameters.py:"
+                                             " loss_norm_D_C_* = 1e-2) on the synthetic Hypersim-shaped inputs"}
+        del r5
     achieved = cf_bytes_per_launch / (cf_us * 1e-6) / 1e9
     if rank != 0:
         if world > 1:
@@ -462,6 +469,8 @@ def main():
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
+                   "grad_wire": ("fp16 (S*g, the reference's DDP wire)" if args.precision == "fp16" and
+                                 distributed.DP_WIRE != "fp32" else "fp32") if world > 1 else None,
                    "step": "eager" if args.no_graph else "hip_graph" + (
                        "" if args.no_defer else " (optimizer of step k beside the marcher of step k+1)")},
         "samples_per_s": round(float(tot[0].item()) / el, 1),

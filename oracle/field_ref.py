@@ -225,13 +225,15 @@ def field_forward(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=N
     return sig, rgb, h
 
 
-def density(xyzs, P, levels, scale=0.5, chunk=1 << 18, impl="torch"):
-    """NGPMT.density (ngp_mt.py:157-171): exp(sigma_net(enc(x))[:, 0]), fp32, in chunks (no grad)."""
+def density(xyzs, P, levels, scale=0.5, chunk=1 << 18, impl="torch", emulate=None):
+    """NGPMT.density (ngp_mt.py:157-171): exp(sigma_net(enc(x))[:, 0]), fp32, in chunks (no grad);
+    emulate ("fp16"/"bf16"): the MLP operands rounded as in field_forward."""
+    q = _rounder(False, emulate)
     out = []
     with torch.no_grad():
         for i in range(0, xyzs.shape[0], chunk):
             x01 = (xyzs[i:i + chunk] - (-scale)) / (2 * scale)
-            h = torch.relu(encode(x01, P.table, levels, impl) @ P.W1.t()) @ P.W2.t()
+            h = q(torch.relu(q(encode(x01, P.table, levels, impl)) @ q(P.W1).t())) @ q(P.W2).t()
             out.append(torch.exp(h[:, 0]))
     return torch.cat(out) if out else torch.zeros(0)
 

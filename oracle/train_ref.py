@@ -34,7 +34,7 @@ class _Composite(torch.autograd.Function):
 
 
 def render_train_ref(P, levels, rays_o, rays_d, bitfield, noise, near=0.01, max_samples=1024, T_thr=1e-4,
-                     impl="torch"):
+                     impl="torch", emulate=None):
     """rendering.py:9-42 + 152-242 (train path, exp_step_factor 0) on the oracle: returns the
     differentiable rgb (with white background), depth, opacity and the marcher/compositor outputs."""
     o, d = np.ascontiguousarray(rays_o, np.float32), np.ascontiguousarray(rays_d, np.float32)
@@ -45,7 +45,7 @@ def render_train_ref(P, levels, rays_o, rays_d, bitfield, noise, near=0.01, max_
     rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, bitfield, 1, 0.5, 0.0, noise, 128,
                                                                          max_samples)
     sig, rgb, _ = field_ref.field_forward_autograd(torch.from_numpy(xyzs), torch.from_numpy(dirs), P, levels,
-                                                   impl=impl)
+                                                   impl=impl, emulate=emulate)
     vr, opacity, depth, rend, ws = _Composite.apply(sig, rgb, torch.from_numpy(deltas), torch.from_numpy(ts),
                                                     torch.from_numpy(rays_a), T_thr)
     return dict(rgb=rend + 1.0 * (1 - opacity)[:, None], depth=depth, opacity=opacity, ws=ws, rays_a=rays_a,
@@ -56,11 +56,12 @@ class CPUTrainer:
     """Hypersim config: scale 0.5, G 128, max_samples 1024, near 0.01, loss weights as the trainer."""
 
     def __init__(self, bitfield, seed=0, lr=1e-2, w_cluster=2e-3, opacity_w=1e-3, num_epochs=None, epoch_steps=1000,
-                 encode_impl="torch"):
+                 encode_impl="torch", emulate=None):
         """encode_impl: "torch" (field_ref.hash_encode, the pure-PyTorch path of config #1) or "c"
         (its C restatement, oracle/hashgrid_ref.c: the same algorithm ~10x faster, for the PSNR
         seed ensembles)."""
         self.encode_impl = encode_impl
+        self.emulate = emulate  # "fp16": the MLP operands rounded as tcnn's / the HIP kernel's (field_ref)
         P, self.levels = field_ref.init_params(seed=seed)
         self.params = [t.requires_grad_(True) for t in P.tensors()]
         self.P = field_ref.FieldParams(*self.params)
@@ -94,7 +95,7 @@ class CPUTrainer:
                                                                              noise, 128, 1024)
         self.opt.zero_grad()
         sig, rgb, _ = field_ref.field_forward_autograd(torch.from_numpy(xyzs), torch.from_numpy(dirs), self.P,
-                                                       self.levels, impl=self.encode_impl)
+                                                       self.levels, impl=self.encode_impl, emulate=self.emulate)
         _, opacity, depth, rend, _ = _Composite.apply(sig, rgb, torch.from_numpy(deltas), torch.from_numpy(ts),
                                                       torch.from_numpy(rays_a), 1e-4)
         out_rgb = rend + 1.0 * (1 - opacity)[:, None]

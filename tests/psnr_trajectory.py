@@ -78,21 +78,23 @@ def _psnr(se, n):
     return -10.0 * math.log10(max(se / n, 1e-12))
 
 
-def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, impl="torch"):
+def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, impl="torch", emulate=None):
     from oracle import field_ref, grid_ref
     from oracle.train_ref import CPUTrainer, render_train_ref
     from ncnerf_amd import synthetic
     from ncnerf_amd.synthetic import SyntheticScene
     torch.set_num_threads(threads)
     scene = SyntheticScene()
-    cpu = CPUTrainer(scene.bitfield, seed=init_seed(member), num_epochs=30, epoch_steps=1000, encode_impl=impl)
+    cpu = CPUTrainer(scene.bitfield, seed=init_seed(member), num_epochs=30, epoch_steps=1000, encode_impl=impl,
+                     emulate=emulate)
     grid, _ = grid_ref.mark_invisible_cells(camera_K(), scene.poses, (synthetic.IMG_W, synthetic.IMG_H), 0.01, 128,
                                             0.5)
     ev = [scene.batch(N_RAYS, seed=s, gt=GT) for s in EVAL_SEEDS]
     curve, t0 = [], time.time()
     for k in range(steps):
         if k % 16 == 0:
-            dens = lambda x: field_ref.density(torch.from_numpy(x), cpu.P, cpu.levels, impl=impl).numpy()  # noqa: E731
+            dens = lambda x: field_ref.density(torch.from_numpy(x), cpu.P, cpu.levels, impl=impl,  # noqa: E731
+                                               emulate=emulate).numpy()
             grid, thr, bf = grid_ref.grid_refresh(grid, dens, THRESHOLD, k < 256, grid_seed(k, member), 128, 0.5)
             cpu.bitfield = np.ascontiguousarray(bf, np.uint8)
         b = scene.batch(n_rays, seed=batch_seed(k, member), gt=GT)
@@ -102,14 +104,14 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
             with torch.no_grad():
                 for e in ev:
                     r = render_train_ref(cpu.P, cpu.levels, e["rays_o"], e["rays_d"], cpu.bitfield,
-                                         np.zeros(N_RAYS, np.float32), impl=impl)
+                                         np.zeros(N_RAYS, np.float32), impl=impl, emulate=emulate)
                     se += float(((r["rgb"].clamp(0, 1) - torch.from_numpy(e["rgb"])) ** 2).sum())
                     n += e["rgb"].size
             curve.append({"step": k + 1, "psnr": _psnr(se, n), "loss": loss, "samples": S,
                           "occupied_frac": float(np.unpackbits(cpu.bitfield).mean()), "t_s": round(time.time() - t0, 1)})
             log(json.dumps(curve[-1]))
             res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": n_rays, "gt": GT,
-                   "member": member, "init_seed": init_seed(member), "encode_impl": impl, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
+                   "member": member, "init_seed": init_seed(member), "encode_impl": impl, "emulate": emulate, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
                    "curve": curve}
             if out:  # the trajectory so far (a partial run is usable up to its last checkpoint)
                 with open(out, "w") as f:
@@ -198,12 +200,14 @@ def main():
     ap.add_argument("--member", type=int, default=None, help="ensemble member (seeds); default: legacy seeds")
     ap.add_argument("--rays", type=int, default=N_RAYS, help="rays per training step")
     ap.add_argument("--impl", default="torch", choices=("torch", "c"), help="(ref) the oracle's hash-grid statement")
+    ap.add_argument("--emulate", default=None, choices=("fp16", "bf16"),
+                    help="(ref) round the MLP operands as tcnn's fp16 FullyFusedMLP / the HIP kernel do")
     ap.add_argument("--cross-check", action="store_true",
                     help="(hip) also render the HIP parameters with the train-path renderer and the oracle's")
     a = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     if a.side == "ref":
-        res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl)
+        res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl, emulate=a.emulate)
     else:
         ref = json.load(open(a.ref)) if a.ref else None
         steps = ref["steps"] if ref else a.steps
