@@ -148,3 +148,38 @@ def test_composite_bw_matches_finite_differences(with_dws):
             rp[i, c] += 1e-2; rm[i, c] -= 1e-2
             fd = (L(sig, rp) - L(sig, rm)) / 2e-2
             assert abs(fd - dr[i, c]) <= 1e-3 * max(1e-3, abs(fd)) + 1e-5
+
+
+def test_hashgrid_c_statement_matches_torch():
+    """oracle/hashgrid_ref.c (the PSNR-ensemble trainer's encoding) vs field_ref.hash_encode (the
+    primary torch statement): forward to f32 rounding of the 8-corner sum order, backward scatter
+    with the identical non-zero set (box corners, the centre and random points at table init 0.5)."""
+    import torch
+    from oracle import field_ref as F
+    P, levels = F.init_params(seed=3, table_init=0.5)
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(20000, 3, generator=g) * 0.98 - 0.49
+    x[:5] = torch.tensor([[-0.5, -0.5, -0.5], [0.5, 0.5, 0.5], [0, 0, 0], [0.4999, -0.25, 0.125], [-0.3, 0.3, 0.0]])
+    x01 = x + 0.5
+    t1 = P.table.clone().requires_grad_(True)
+    t2 = P.table.clone().requires_grad_(True)
+    a = F.hash_encode(x01, t1, levels)
+    b = F.encode(x01, t2, levels, "c")
+    assert float((a - b).abs().max()) <= 2e-7 * max(1.0, float(a.abs().max()))
+    gup = torch.randn(a.shape, generator=g)
+    a.backward(gup)
+    b.backward(gup)
+    assert torch.equal(t1.grad != 0, t2.grad != 0)
+    assert float((t1.grad - t2.grad).abs().max()) <= 1e-6 * float(t1.grad.abs().max())
+
+
+def test_mt19937_vectorised_draws():
+    """losses_ref.Mt19937.draws (vectorised twist + tempering) == the scalar generator, and the
+    C++ standard's known answer (the 10 000th output of default-seeded mt19937 is 4123659995)."""
+    from oracle.losses_ref import Mt19937
+    for seed in (0, 1234, 2 ** 31 + 7):
+        a, b = Mt19937(seed), Mt19937(seed)
+        x = np.array([a() for _ in range(1500)], np.uint64)
+        y = np.concatenate([b.draws(700), b.draws(1), b.draws(799)])
+        assert np.array_equal(x, y)
+    assert int(Mt19937(5489).draws(10000)[-1]) == 4123659995
