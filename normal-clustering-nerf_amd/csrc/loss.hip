@@ -271,14 +271,22 @@ __device__ __forceinline__ bool valid_normal(float a, float b, float c) {
     return !(zero || bad);
 }
 
+// argmax_k <x, C_k> with ((x0 c0 + x1 c1) + x2 c2) in f32, no FMA (contract(off) above); ties ->
+// lowest k.  Two clusters per packed-f32 instruction (v_pk_mul_f32 / v_pk_add_f32: the same IEEE
+// products and sums per half), then the compares in k order.
 template <int K>
 __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, float z) {
+    static_assert(K % 2 == 0, "clusters in pairs");
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 X = {x, x}, Y = {y, y}, Z = {z, z};
     int best = 0;
-    float bv = x * C[0][0] + y * C[0][1] + z * C[0][2];
+    float bv = -INFINITY;
 #pragma unroll
-    for (int k = 1; k < K; k++) {
-        const float v = x * C[k][0] + y * C[k][1] + z * C[k][2];
-        if (v > bv) { bv = v; best = k; }
+    for (int k = 0; k < K; k += 2) {
+        const f2 c0 = {C[k][0], C[k + 1][0]}, c1 = {C[k][1], C[k + 1][1]}, c2 = {C[k][2], C[k + 1][2]};
+        const f2 v = (X * c0 + Y * c1) + Z * c2;
+        if (k == 0 || v.x > bv) { bv = v.x; best = k; }
+        if (v.y > bv) { bv = v.y; best = k + 1; }
     }
     return best;
 }
@@ -578,32 +586,23 @@ __device__ void select_clusters(const float (*C)[3], const float* cnt, float t_s
         L.cargmin[j] = mi;
     }
     __syncthreads();
-    if (tid < 64) {  // one wave: c2 = first argmin of cmin (lanes < K), its c3, then per-cluster labels
-        const float mv = tid < K ? L.cmin[tid] : INFINITY;
-        float best = mv;
-        int bi = tid < K ? tid : K;
+    if (tid < 64) {  // one wave: c2 = first argmin of cmin, its c3, then per-cluster labels
+        // (wave-uniform serial scans over the K LDS values: independent broadcast loads and a short
+        // compare chain, instead of 6 dependent cross-lane shuffles per argmin)
+        auto first_argmin = [&](const float* v) {  // ties -> lowest index
+            float b = v[0];
+            int bi = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {  // (value, index) min, ties -> lowest index
-            const float ov = __shfl_xor(best, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            if (ov < best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-        }
-        const int c2 = bi, c3 = L.cargmin[c2];
+            for (int k = 1; k < K; k++)
+                if (v[k] < b) { b = v[k]; bi = k; }
+            return bi;
+        };
+        const int c2 = first_argmin(L.cmin), c3 = L.cargmin[c2];
         const int cs[3] = {c1, c2, c3};
         // opposite of each main cluster: first argmin of sim[cs[q]][*]
         int co[3];
 #pragma unroll
-        for (int q = 0; q < 3; q++) {
-            float b2 = tid < K ? L.sim[cs[q]][tid] : INFINITY;
-            int i2 = tid < K ? tid : K;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const float ov = __shfl_xor(b2, o, 64);
-                const int oi = __shfl_xor(i2, o, 64);
-                if (ov < b2 || (ov == b2 && oi < i2)) { b2 = ov; i2 = oi; }
-            }
-            co[q] = i2;
-        }
+        for (int q = 0; q < 3; q++) co[q] = first_argmin(L.sim[cs[q]]);
         if (tid < K) {  // the sequential overwrite order of losses.py: main clusters, then opposites
             const int k = tid;
             int lab = 0;
