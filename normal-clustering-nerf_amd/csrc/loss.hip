@@ -274,8 +274,21 @@ __device__ __forceinline__ bool valid_normal(float a, float b, float c) {
 // argmax_k <x, C_k> with ((x0 c0 + x1 c1) + x2 c2) in f32, no FMA (contract(off) above); ties ->
 // lowest k.  Two clusters per packed-f32 instruction (v_pk_mul_f32 / v_pk_add_f32: the same IEEE
 // products and sums per half), then the compares in k order.
+#ifndef KM_PACKED_DOT
+#define KM_PACKED_DOT 1
+#endif
 template <int K>
 __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, float z) {
+    if constexpr (!KM_PACKED_DOT) {  // (A/B switch) one cluster at a time
+        int best = 0;
+        float bv = x * C[0][0] + y * C[0][1] + z * C[0][2];
+#pragma unroll
+        for (int k = 1; k < K; k++) {
+            const float v = x * C[k][0] + y * C[k][1] + z * C[k][2];
+            if (v > bv) { bv = v; best = k; }
+        }
+        return best;
+    }
     static_assert(K % 2 == 0, "clusters in pairs");
     typedef float f2 __attribute__((ext_vector_type(2)));
     const f2 X = {x, x}, Y = {y, y}, Z = {z, z};
