@@ -275,7 +275,7 @@ __device__ __forceinline__ bool valid_normal(float a, float b, float c) {
 // lowest k.  Two clusters per packed-f32 instruction (v_pk_mul_f32 / v_pk_add_f32: the same IEEE
 // products and sums per half), then the compares in k order.
 #ifndef KM_PACKED_DOT
-#define KM_PACKED_DOT 1
+#define KM_PACKED_DOT 0  // packed: 87 vs 82 us for the whole kernel (the pair building costs more than it saves)
 #endif
 template <int K>
 __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, float z) {
