@@ -267,7 +267,8 @@ int64_t ncn_kmeans_plan_words(int n_tri, int K);
 int ncn_kmeans_plan_fill(int n_tri, int K, uint32_t seed, uint32_t* host_out);
 /* Validity filter, spherical k-means (K in {10,20}, niter Lloyd iterations), cluster selection,
  * the three cluster losses and their gradient w.r.t. the normals, scaled by w_ort / w_dot / w_l1,
- * in ONE launch of 32 co-resident workgroups (grid barriers between the phases).  n_tri <= 16384.
+ * in ONE launch of 16 co-resident workgroups (KM_BLOCKS in csrc/loss.hip; tagged partial words between
+ * the Lloyd rounds, grid barriers between the later phases).  n_tri <= 16384.
  * kmeans_plan: device copy of ncn_kmeans_plan_fill(n_tri, K, seed) (a mismatched plan sets the
  * status word, ncn_cluster_status_offset).
  * out_losses (11 floats): [0..2] = unweighted (ort, centr_dot, centr_L1) after the validity filter;

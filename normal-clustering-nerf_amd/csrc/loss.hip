@@ -1,7 +1,7 @@
 // Normal-clustering loss path for gfx950:
 //  * normals from rendered depth over pixel triangles  (datasets/hypersim_src/utils.py:504-541)
 //  * spherical k-means + Manhattan cluster selection + cluster losses and their analytic gradient
-//    (losses.py:47-166, 420-478), all inside ONE persistent launch of 32 workgroups (Lloyd partials
+//    (losses.py:47-166, 420-478), all inside ONE persistent launch of KM_BLOCKS = 16 workgroups (Lloyd partials
 //    exchanged as tagged words), so the per-step clustering needs no device->host round trip (the
 //    reference copies the normals to the host for faiss, losses.py:434).
 #pragma clang fp contract(off)

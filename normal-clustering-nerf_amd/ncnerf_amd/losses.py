@@ -72,7 +72,7 @@ def check_cluster_status(dev=None):
         off = int(_lib.lib().ncn_cluster_status_offset(I32(K)))
         if int(ws.view(torch.int32)[off].item()) != 0:
             raise _lib.NcnError(f"ncn_cluster_loss on {d} (K={K}): a grid barrier / Lloyd hand-off timed out "
-                                f"(co-residency of its {32} workgroups failed); cluster losses are invalid")
+                                f"(its workgroups were not co-resident); cluster losses are invalid")
 
 
 class _Normals(torch.autograd.Function):
