@@ -90,7 +90,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
-         "ncn_field_bwd", "ncn_cluster_loss")
+         "ncn_field_bwd", "ncn_field_bwd_mlp_part", "ncn_field_scatter", "ncn_cluster_loss")
 
 
 def pmc_traffic():
@@ -257,6 +257,9 @@ def main():
     ap.add_argument("--no-defer", action="store_true",
                     help="keep each step's optimizer at the end of its own graph (default: it runs in the next "
                          "step's graph beside the marcher, Trainer(defer_optimizer=True))")
+    ap.add_argument("--no-split", action="store_true",
+                    help="the autograd backward after the whole loss node (default: Trainer(split_backward=True), "
+                         "the photometric backward beside the normal clustering)")
     ap.add_argument("--precision", choices=("fp16", "bf16"), default="fp16",
                     help="MFMA operand type of the field MLP (fp16 = tcnn's FullyFusedMLP, the reference's AMP run)")
     ap.add_argument("--no-bf16-line", action="store_true",
@@ -316,7 +319,7 @@ def main():
         scene = SyntheticScene()
         model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
         trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph,
-                          defer_optimizer=not args.no_defer, preset=preset)
+                          defer_optimizer=not args.no_defer, preset=preset, split_backward=not args.no_split)
         # marched / composited sample counts accumulated on the device by the step itself
         # (ncn_count_samples: no per-step copies in the timed region)
         count_acc = torch.zeros(2, dtype=torch.float64, device=dev)
@@ -472,7 +475,8 @@ def main():
                    "grad_wire": ("fp16 (S*g, the reference's DDP wire)" if args.precision == "fp16" and
                                  distributed.DP_WIRE != "fp32" else "fp32") if world > 1 else None,
                    "step": "eager" if args.no_graph else "hip_graph" + (
-                       "" if args.no_defer else " (optimizer of step k beside the marcher of step k+1)")},
+                       "" if args.no_defer else " (optimizer of step k beside the marcher of step k+1)") + (
+                       "" if args.no_split else " (photometric backward beside the normal clustering)")},
         "samples_per_s": round(float(tot[0].item()) / el, 1),
         "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),

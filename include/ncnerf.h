@@ -219,6 +219,21 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
                       const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
                       const float* loss_scale, float* slab, float* dE_ws, float* level_max, void* stream);
+/* The MLP pass split by the gradient's source (the fused training step runs the rgb part while
+ * the normal clustering computes the depth gradient): part 1 (rgb) = the rgb_net path from
+ * dL_drgbs alone — slab tiles of W3..W5 and the rgb part of dL/dh into dh_stash
+ * (ncn_field_bwd_stash_floats(n) floats, 16-byte aligned); part 2 (sigma) = dL/dh = stash +
+ * TruncExp'(h0) * (dL_dsigmas + dL_dsigmas2) (either may be NULL), then sigma_net: slab tiles of
+ * W1, W2, dE_ws, level_max; part 3 = ncn_field_bwd_mlp (plus the second dsigma term).  Parts 1
+ * and 2 of one step take the same n_blocks (> 0 caps the grid, leaving CUs to a concurrent kernel;
+ * 0 = ncn_field_bwd_blocks(n)); ncn_field_reduce_wgrad then sums that many slab rows.  Together
+ * they produce ncn_field_bwd_mlp's outputs (dL/dsigma summed from its two terms in f32). */
+int64_t ncn_field_bwd_stash_floats(int64_t n);
+int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                           const uint16_t* weights_packed, int precision, const uint16_t* enc_cache,
+                           const float* dL_dsigmas, const float* dL_dsigmas2, const float* dL_drgbs,
+                           const float* loss_scale, int part, int n_blocks, float* slab, float* dE_ws,
+                           float* level_max, float* dh_stash, void* stream);
 int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
@@ -300,7 +315,10 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, cons
  * ncn_cluster_loss).  One thread per ray: dL_drgb (R,3) and dL_dopacity (R) of the photometric
  * terms, and dL_ddepth (R) GATHERED from the ray's triangle roles (written, not accumulated: no
  * zero-fill, no atomics).  up_total: NULL or the device gradient of `total`; up_terms: NULL or 5
- * device floats (gradients of the rgb, opacity, ort, centr_dot, centr_L1 outputs), added to it. */
+ * device floats (gradients of the rgb, opacity, ort, centr_dot, centr_L1 outputs), added to it.
+ * The two output groups can be taken apart: dL_drgb = dL_dopacity = NULL skips the photometric
+ * part, dL_ddepth = NULL the clustering part (dL_dnormals is then not read), so the photometric
+ * gradient can flow back while ncn_cluster_loss still runs. */
 int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacity, int64_t n_rays, float w_opacity,
                       const float* photo_loss, const float* rays_o, const float* rays_d, const float* depth,
                       const float* dL_dnormals, const float* up_total, const float* up_terms, float* dL_drgb,

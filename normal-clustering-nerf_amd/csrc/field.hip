@@ -495,25 +495,38 @@ __device__ __forceinline__ V x_get(const uint16_t* tile, int lane) {
 }
 
 // Per-group inputs of the backward (prefetched one step ahead).
+// Backward parts (the split MLP pass of the training step, ncn_field_bwd_mlp_part): BWD_RGB = the
+// rgb_net path alone (needs only dL/drgb: it can run while the clustering still computes the depth
+// gradient) — dW3..dW5 and the rgb part of dL/dh, stashed; BWD_SIGMA = the rest: dL/dh = stash +
+// TruncExp'(h0) dL/dsigma, then sigma_net and the encoding gradient, dW1, dW2.  BWD_ALL = both.
+enum { BWD_RGB = 1, BWD_SIGMA = 2, BWD_ALL = 3 };
 template <typename T>
 struct BwdIn {
     typename Mfma<T>::v8 e;
     float dx, dy, dz, dsig, dr0, dr1, dr2;
+    float4_t dhr;  // (BWD_SIGMA) the stashed rgb part of dL/dh of this lane's tile
 };
-template <typename T>
+template <typename T, int PART>
 __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, int lane,
                                          const typename Mfma<T>::v8* __restrict__ enc, const float* __restrict__ dirs,
-                                         const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
+                                         const float* __restrict__ dL_dsig, const float* __restrict__ dL_dsig2,
+                                         const float* __restrict__ dL_drgb, const float4_t* __restrict__ stash,
                                          const int32_t* __restrict__ order, float S) {
     const int64_t pos = grp * 16 + (lane & 15);  // processing position (enc_cache / dE order)
     const bool valid = pos < n;
     in.e = enc[grp * 64 + lane];
     in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
+    if constexpr (PART == BWD_SIGMA) in.dhr = stash[grp * 64 + lane];
     if (valid) {
         const int64_t s = order ? (int64_t)order[pos] : pos;
-        in.dx = dirs[3 * s]; in.dy = dirs[3 * s + 1]; in.dz = dirs[3 * s + 2];
-        in.dsig = dL_dsig ? dL_dsig[s] * S : 0.f;
-        if (dL_drgb) { in.dr0 = dL_drgb[3 * s] * S; in.dr1 = dL_drgb[3 * s + 1] * S; in.dr2 = dL_drgb[3 * s + 2] * S; }
+        if constexpr ((PART & BWD_RGB) != 0) {
+            in.dx = dirs[3 * s]; in.dy = dirs[3 * s + 1]; in.dz = dirs[3 * s + 2];
+            if (dL_drgb) { in.dr0 = dL_drgb[3 * s] * S; in.dr1 = dL_drgb[3 * s + 1] * S; in.dr2 = dL_drgb[3 * s + 2] * S; }
+        }
+        if constexpr ((PART & BWD_SIGMA) != 0) {
+            const float ds = (dL_dsig ? dL_dsig[s] : 0.f) + (dL_dsig2 ? dL_dsig2[s] : 0.f);
+            in.dsig = ds * S;
+        }
     }
 }
 
@@ -521,23 +534,25 @@ __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, i
 __device__ __forceinline__ float lmax_upd(float m, float a, float b) {  // non-finite -> INF
     return (isfinite(a) && isfinite(b)) ? fmaxf(m, fmaxf(fabsf(a), fabsf(b))) : INFINITY;
 }
-template <typename T>
+template <typename T, int PART>
 __device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const BwdIn<T>& cur, int64_t grp,
                                           int64_t n, int64_t n_stride, int lane, float* __restrict__ dE_out,
-                                          float (&lm)[4], float inv_S) {
+                                          float (&lm)[4], float inv_S, float4_t* __restrict__ stash) {
     typedef Mfma<T> M;
     typedef typename M::v4 v4;
     typedef typename M::v8 v8;
     const int g = lane >> 4, r = lane & 15;
     const int64_t s = grp * 16 + r;
     const bool valid = s < n;
+    FwdState<T> st;
+    mlp_sigma<T>(F, lane, cur.e, st);
+    float4_t dh;
+    if constexpr ((PART & BWD_RGB) != 0) {
     float dx = cur.dx, dy = cur.dy, dz = cur.dz;
     if (valid) {
         const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
         dx /= nrm; dy /= nrm; dz /= nrm;
     }
-    FwdState<T> st;
-    mlp_sigma<T>(F, lane, cur.e, st);
     mlp_rgb<T>(F, lane, dx, dy, dz, st);
     // dY5: d(pre-sigmoid) = drgb * s(1-s), rows 0..2 on g==0 (the padded output rows get zero)
     float4_t dy5 = zero4();
@@ -572,8 +587,15 @@ __device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const
     x_put(Xw + XB3D * 256, lane, st.x3d);
     x_put(Xw + XB3H * 256, lane, st.x3h);
     // L3 backward -> dh (rgb path) ; + TruncExp backward on h[0]
-    float4_t dh = M::k32(F.a32(B_L3, lane), cat8<v8>(dD3[0], dD3[1]), zero4());
+    dh = M::k32(F.a32(B_L3, lane), cat8<v8>(dD3[0], dD3[1]), zero4());
     dh = M::k32(F.a32(B_L3 + 1, lane), cat8<v8>(dD3[2], dD3[3]), dh);
+    if constexpr (PART == BWD_RGB) {  // the sigma part follows in its own pass (BWD_SIGMA)
+        stash[grp * 64 + lane] = dh;
+        return;
+    }
+    } else {
+        dh = cur.dhr;  // (BWD_SIGMA) the rgb path's dL/dh, from the stash
+    }
     if (g == 0) dh[0] += cur.dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
     const v4 dhh = cvt4<T>(dh);
     x_put(Xw + XA2 * 256, lane, dhh);
@@ -624,34 +646,66 @@ __device__ __forceinline__ typename Mfma<T>::v8 x_pair(const uint16_t* X, int q,
     const v4 b = q + 1 < ng ? x_get<v4>(X + ((q + 1) * N_XFRAG + tile) * 256, lane) : v4{0, 0, 0, 0};
     return cat8<typename Mfma<T>::v8>(a, b);
 }
-template <typename T>
+template <typename T, int PART>
 __device__ __forceinline__ void bwd_dw(const uint16_t* X, int ng, int wid, int lane, float4_t (&acc)[5]) {
     typedef Mfma<T> M;
     typedef typename M::v8 v8;
+    constexpr bool RGB = (PART & BWD_RGB) != 0, SIG = (PART & BWD_SIGMA) != 0;
+    if constexpr (PART == BWD_SIGMA) {  // 12 tiles: W1 (4 row x 2 col blocks) one per wave, W2 on waves 0-3
+        for (int q = 0; q < ng; q += 2) {
+            acc[0] = M::k32(x_pair<T>(X, q, ng, XA1 + (wid >> 1), lane), x_pair<T>(X, q, ng, XB1 + (wid & 1), lane),
+                            acc[0]);
+            if (wid < 4)
+                acc[1] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid, lane), acc[1]);
+        }
+        return;
+    }
+    if constexpr (PART == BWD_RGB) {  // 28 tiles: W4 on waves 0-3 (4 each), W3 row block + W5 on waves 4-7
+        for (int q = 0; q < ng; q += 2) {
+            if (wid < 4) {
+                const v8 A4 = x_pair<T>(X, q, ng, XA4 + wid, lane);
+#pragma unroll
+                for (int b = 0; b < 4; b++) acc[b] = M::k32(A4, x_pair<T>(X, q, ng, XB4 + b, lane), acc[b]);
+            } else {
+                const v8 A3 = x_pair<T>(X, q, ng, XA3 + wid - 4, lane);
+                acc[0] = M::k32(A3, x_pair<T>(X, q, ng, XB3D, lane), acc[0]);
+                acc[1] = M::k32(A3, x_pair<T>(X, q, ng, XB3H, lane), acc[1]);
+                acc[4] = M::k32(x_pair<T>(X, q, ng, XA5, lane), x_pair<T>(X, q, ng, XB5 + wid - 4, lane), acc[4]);
+            }
+        }
+        return;
+    }
     for (int q = 0; q < ng; q += 2) {
         if (wid < 4) {
-            const v8 A4 = x_pair<T>(X, q, ng, XA4 + wid, lane);
+            if constexpr (RGB) {
+                const v8 A4 = x_pair<T>(X, q, ng, XA4 + wid, lane);
 #pragma unroll
-            for (int b = 0; b < 4; b++) acc[b] = M::k32(A4, x_pair<T>(X, q, ng, XB4 + b, lane), acc[b]);
-            acc[4] = M::k32(x_pair<T>(X, q, ng, XA5, lane), x_pair<T>(X, q, ng, XB5 + wid, lane), acc[4]);
+                for (int b = 0; b < 4; b++) acc[b] = M::k32(A4, x_pair<T>(X, q, ng, XB4 + b, lane), acc[b]);
+                acc[4] = M::k32(x_pair<T>(X, q, ng, XA5, lane), x_pair<T>(X, q, ng, XB5 + wid, lane), acc[4]);
+            }
         } else if (wid < 6) {
-            const v8 Bd = x_pair<T>(X, q, ng, XB3D, lane), Bh = x_pair<T>(X, q, ng, XB3H, lane);
+            if constexpr (RGB) {
+                const v8 Bd = x_pair<T>(X, q, ng, XB3D, lane), Bh = x_pair<T>(X, q, ng, XB3H, lane);
 #pragma unroll
-            for (int aa = 0; aa < 2; aa++) {
-                const v8 A3 = x_pair<T>(X, q, ng, XA3 + 2 * (wid - 4) + aa, lane);
-                acc[2 * aa] = M::k32(A3, Bd, acc[2 * aa]);
-                acc[2 * aa + 1] = M::k32(A3, Bh, acc[2 * aa + 1]);
+                for (int aa = 0; aa < 2; aa++) {
+                    const v8 A3 = x_pair<T>(X, q, ng, XA3 + 2 * (wid - 4) + aa, lane);
+                    acc[2 * aa] = M::k32(A3, Bd, acc[2 * aa]);
+                    acc[2 * aa + 1] = M::k32(A3, Bh, acc[2 * aa + 1]);
+                }
             }
-            acc[4] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid - 4, lane), acc[4]);
+            if constexpr (SIG)
+                acc[4] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid - 4, lane), acc[4]);
         } else {
-            const v8 B0 = x_pair<T>(X, q, ng, XB1, lane), B1 = x_pair<T>(X, q, ng, XB1 + 1, lane);
+            if constexpr (SIG) {
+                const v8 B0 = x_pair<T>(X, q, ng, XB1, lane), B1 = x_pair<T>(X, q, ng, XB1 + 1, lane);
 #pragma unroll
-            for (int aa = 0; aa < 2; aa++) {
-                const v8 A1 = x_pair<T>(X, q, ng, XA1 + 2 * (wid - 6) + aa, lane);
-                acc[2 * aa] = M::k32(A1, B0, acc[2 * aa]);
-                acc[2 * aa + 1] = M::k32(A1, B1, acc[2 * aa + 1]);
+                for (int aa = 0; aa < 2; aa++) {
+                    const v8 A1 = x_pair<T>(X, q, ng, XA1 + 2 * (wid - 6) + aa, lane);
+                    acc[2 * aa] = M::k32(A1, B0, acc[2 * aa]);
+                    acc[2 * aa + 1] = M::k32(A1, B1, acc[2 * aa + 1]);
+                }
+                acc[4] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid - 4, lane), acc[4]);
             }
-            acc[4] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid - 4, lane), acc[4]);
         }
     }
 }
@@ -659,45 +713,87 @@ __device__ __forceinline__ void bwd_dw(const uint16_t* X, int ng, int wid, int l
 // The owned tiles (C layout: lane (g,r) = rows 4g+i, column r) into the workgroup's slab row.
 // W3 columns: the h tile's column r is input 3+r; the [d, pad] tile's column q is input q (d) or
 // 16+q (the 13 constant-1 padding inputs, whose gradient is the plain sum of dY).
+// (A split pass stores only its own tiles: the other pass writes the rest of the same slab row.)
+template <int PART>
 __device__ __forceinline__ void bwd_store_dw(float* __restrict__ out, int wid, int lane, float4_t (&acc)[5], float inv_S) {
+    constexpr bool RGB = (PART & BWD_RGB) != 0, SIG = (PART & BWD_SIGMA) != 0;
     const int g = lane >> 4, r = lane & 15;
 #pragma unroll
     for (int t = 0; t < 5; t++)
 #pragma unroll
         for (int i = 0; i < 4; i++) acc[t][i] *= inv_S;
+    if constexpr (PART == BWD_SIGMA) {  // (bwd_dw's split-pass tile ownership)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 4 * g + i;
+            out[W1_OFF + (16 * (wid >> 1) + row) * 32 + 16 * (wid & 1) + r] = acc[0][i];
+            if (wid < 4) out[W2_OFF + row * 64 + 16 * wid + r] = acc[1][i];
+        }
+        return;
+    }
+    if constexpr (PART == BWD_RGB) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = 4 * g + i;
+            if (wid < 4) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) out[W4_OFF + (16 * wid + row) * 64 + 16 * b + r] = acc[b][i];
+            } else {
+                const int orow = 16 * (wid - 4) + row;
+                out[W3_OFF + orow * 32 + (r < 3 ? r : 16 + r)] = acc[0][i];
+                out[W3_OFF + orow * 32 + 3 + r] = acc[1][i];
+                out[W5_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int row = 4 * g + i;
         if (wid < 4) {
+            if constexpr (RGB) {
 #pragma unroll
-            for (int b = 0; b < 4; b++) out[W4_OFF + (16 * wid + row) * 64 + 16 * b + r] = acc[b][i];
-            out[W5_OFF + row * 64 + 16 * wid + r] = acc[4][i];
+                for (int b = 0; b < 4; b++) out[W4_OFF + (16 * wid + row) * 64 + 16 * b + r] = acc[b][i];
+                out[W5_OFF + row * 64 + 16 * wid + r] = acc[4][i];
+            }
         } else if (wid < 6) {
+            if constexpr (RGB) {
 #pragma unroll
-            for (int aa = 0; aa < 2; aa++) {
-                const int orow = 16 * (2 * (wid - 4) + aa) + row;
-                out[W3_OFF + orow * 32 + (r < 3 ? r : 16 + r)] = acc[2 * aa][i];
-                out[W3_OFF + orow * 32 + 3 + r] = acc[2 * aa + 1][i];
+                for (int aa = 0; aa < 2; aa++) {
+                    const int orow = 16 * (2 * (wid - 4) + aa) + row;
+                    out[W3_OFF + orow * 32 + (r < 3 ? r : 16 + r)] = acc[2 * aa][i];
+                    out[W3_OFF + orow * 32 + 3 + r] = acc[2 * aa + 1][i];
+                }
             }
-            out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
+            if constexpr (SIG) out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
         } else {
+            if constexpr (SIG) {
 #pragma unroll
-            for (int aa = 0; aa < 2; aa++) {
-                const int orow = 16 * (2 * (wid - 6) + aa) + row;
-                out[W1_OFF + orow * 32 + r] = acc[2 * aa][i];
-                out[W1_OFF + orow * 32 + 16 + r] = acc[2 * aa + 1][i];
+                for (int aa = 0; aa < 2; aa++) {
+                    const int orow = 16 * (2 * (wid - 6) + aa) + row;
+                    out[W1_OFF + orow * 32 + r] = acc[2 * aa][i];
+                    out[W1_OFF + orow * 32 + 16 + r] = acc[2 * aa + 1][i];
+                }
+                out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
             }
-            out[W2_OFF + row * 64 + 16 * (wid - 4) + r] = acc[4][i];
         }
     }
 }
 
-template <typename T>
+// one 8-wave workgroup per CU on 256 CUs; at least ~4 steps of 8 groups each
+__host__ __device__ inline int bwd_blocks_of(int64_t n) {
+    const int64_t groups = (n + 15) / 16;
+    const int64_t b = (groups + 31) / 32;
+    return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
+template <typename T, int PART = BWD_ALL>
 __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* __restrict__ dirs, int64_t n, const int32_t* __restrict__ n_dev, const uint16_t* __restrict__ wpacked,
     const typename Mfma<T>::v8* __restrict__ enc_cache, const float* __restrict__ dL_dsig,
     const float* __restrict__ dL_drgb, const float* __restrict__ loss_scale, float* __restrict__ dE_out,
-    float* __restrict__ slab, float* __restrict__ level_max, const int32_t* __restrict__ order) {
+    float* __restrict__ slab, float* __restrict__ level_max, const int32_t* __restrict__ order,
+    const float* __restrict__ dL_dsig2 = nullptr, float4_t* __restrict__ stash = nullptr) {
     typedef typename Mfma<T>::v4 v4;
     // AMP loss scale (GradScaler of the reference's precision=16 run) times tcnn's fp16 module loss
     // scale (128): the fp16 chain sees the upstream gradients times S (a power of two), dE and dW
@@ -705,6 +801,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float S = loss_scale ? *loss_scale * (Mfma<T>::f16 ? NCN_TCNN_LOSS_SCALE : 1.f) : 1.f, inv_S = 1.f / S;
     typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
+    const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
     if (n_dev) n = min<int64_t>(n, *n_dev);
     __shared__ v8 F32s[N_FRAG32 * 64];                                              // 34 KB
     __shared__ v4 F16s[N_FRAG16 * 64];                                              // 4 KB
@@ -725,25 +822,27 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t stride = (int64_t)gridDim.x * BWD_WAVES;
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
     BwdIn<T> nxt;
-    if (base + wid < n_groups) bwd_load<T>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order, S);
+    if (base + wid < n_groups)
+        bwd_load<T, PART>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stash, order, S);
     for (; base < n_groups; base += stride) {
         const int64_t grp = base + wid;
         const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
         const BwdIn<T> cur = nxt;
         if (grp + stride < n_groups)
-            bwd_load<T>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_drgb, order, S);
+            bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stash, order, S);
         if (grp < n_groups) {
             Frags<T> F;
             const int z = opaque_zero();
             F.f32 = F32s + z;
             F.f16 = F16s + z;
-            bwd_group<T>(F, X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S);
+            bwd_group<T, PART>(F, X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S, stash);
         }
         lds_barrier();  // (the dE stores and the next step's loads stay in flight)
-        bwd_dw<T>(X, ng, wid, lane, acc);
+        bwd_dw<T, PART>(X, ng, wid, lane, acc);
         lds_barrier();
     }
-    bwd_store_dw(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc, inv_S);
+    bwd_store_dw<PART>(slab + (int64_t)blockIdx.x * NCN_FIELD_NW, wid, lane, acc, inv_S);
+    if constexpr (PART == BWD_RGB) return;  // (no encoding gradient in the rgb pass)
     // level maxima: the 16 lanes of a row (same g) share their 4 levels; the row leaders of the 8
     // waves meet in LDS and the workgroup writes its row of level_max [blocks][16] (no atomics: the
     // scatter reduces the rows)
@@ -771,6 +870,9 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         for (int w = 0; w < BWD_WAVES; w++) m = fmaxf(m, lmw[w][threadIdx.x]);
         level_max[blockIdx.x * 16 + threadIdx.x] = m;
     }
+    // a capped grid (ncn_field_bwd_mlp_part's n_blocks) leaves the scatter's remaining rows neutral
+    if (blockIdx.x == 0)
+        for (int i = (int)gridDim.x * 16 + threadIdx.x; i < lm_rows * 16; i += BWD_THREADS) level_max[i] = 0.f;
 }
 
 // Sum of the per-workgroup dW slabs: blockIdx.y takes a chunk of slabs (coalesced 1 KB rows),
@@ -1740,6 +1842,21 @@ static int fwd_grid(int64_t n) {
 
 using namespace ncn;
 
+template <int PART>
+static void launch_bwd_part(int precision, int nb, hipStream_t st, const float* dirs, int64_t n, const int32_t* n_dev,
+                            const uint16_t* wp, const uint16_t* enc, const float* dsig, const float* drgb,
+                            const float* loss_scale, float* dE_ws, float* slab, float* level_max,
+                            const int32_t* order, const float* dsig2, float* stash) {
+    if (precision == NCN_PREC_F16)
+        hipLaunchKernelGGL((field_bwd_kernel<_Float16, PART>), dim3(nb), dim3(BWD_THREADS), 0, st, dirs, n, n_dev, wp,
+                           (const Mfma<_Float16>::v8*)enc, dsig, drgb, loss_scale, dE_ws, slab, level_max, order, dsig2,
+                           (float4_t*)stash);
+    else
+        hipLaunchKernelGGL((field_bwd_kernel<__bf16, PART>), dim3(nb), dim3(BWD_THREADS), 0, st, dirs, n, n_dev, wp,
+                           (const Mfma<__bf16>::v8*)enc, dsig, drgb, loss_scale, dE_ws, slab, level_max, order, dsig2,
+                           (float4_t*)stash);
+}
+
 extern "C" {
 
 int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int precision, void* stream) {
@@ -1805,11 +1922,7 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
     return 0;
 }
 
-int ncn_field_bwd_blocks(int64_t n) {
-    const int64_t groups = (n + 15) / 16;
-    // one 8-wave workgroup per CU on 256 CUs; at least ~4 steps of 8 groups each
-    return (int)std::max<int64_t>(1, std::min<int64_t>(256, (groups + 31) / 32));
-}
+int ncn_field_bwd_blocks(int64_t n) { return bwd_blocks_of(n); }
 
 int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(int64_t)3) : 0; }
 
@@ -1832,6 +1945,38 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
                            (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<__bf16>::v8*)enc_cache,
                            dL_dsigmas, dL_drgbs, loss_scale, dE_ws, slab, level_max, order);
     NCN_LAUNCH_CHECK("ncn_field_bwd_mlp");
+    return 0;
+}
+
+int64_t ncn_field_bwd_stash_floats(int64_t n) { return n > 0 ? 256 * ((n + 15) / 16) : 0; }
+
+int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                           const uint16_t* weights_packed, int precision, const uint16_t* enc_cache,
+                           const float* dL_dsigmas, const float* dL_dsigmas2, const float* dL_drgbs,
+                           const float* loss_scale, int part, int n_blocks, float* slab, float* dE_ws,
+                           float* level_max, float* dh_stash, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,
+                "ncn_field_bwd_mlp_part: precision must be NCN_PREC_F16 or NCN_PREC_BF16");
+    NCN_REQUIRE(part == 1 || part == 2 || part == 3, hipErrorInvalidValue,
+                "ncn_field_bwd_mlp_part: part must be 1 (rgb), 2 (sigma) or 3 (both)");
+    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)enc_cache & 15) == 0 &&
+                    ((uintptr_t)weights_packed & 15) == 0 && ((uintptr_t)dh_stash & 15) == 0,
+                hipErrorInvalidValue, "ncn_field_bwd_mlp_part: dE_ws / enc_cache / weights_packed / dh_stash must be 16-byte aligned");
+    NCN_REQUIRE(part != 2 || level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp_part: level_max workspace required");
+    NCN_REQUIRE(part == 3 || dh_stash != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp_part: dh_stash required for a split pass");
+    const int nb = n_blocks > 0 ? std::min(n_blocks, ncn_field_bwd_blocks(n)) : ncn_field_bwd_blocks(n);
+    const hipStream_t st = (hipStream_t)stream;
+    if (part == 1)
+        launch_bwd_part<1>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
+                           loss_scale, dE_ws, slab, level_max, order, dL_dsigmas2, dh_stash);
+    else if (part == 2)
+        launch_bwd_part<2>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
+                           loss_scale, dE_ws, slab, level_max, order, dL_dsigmas2, dh_stash);
+    else
+        launch_bwd_part<3>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
+                           loss_scale, dE_ws, slab, level_max, order, dL_dsigmas2, dh_stash);
+    NCN_LAUNCH_CHECK("ncn_field_bwd_mlp_part");
     return 0;
 }
 

@@ -205,12 +205,15 @@ __global__ void nerf_loss_bwd_kernel(const float* __restrict__ rgb, const float*
 #pragma unroll
     for (int q = 0; q < 5; q++) u[q] = ut + (up_terms ? up_terms[q] : 0.f);
     // photometric (photo_loss_bwd_kernel)
-    const float ga = u[0] * photo[2], gb = u[1] * photo[3];
-    const float sa = 2.f / (float)(3 * R);
+    if (drgb) {
+        const float ga = u[0] * photo[2], gb = u[1] * photo[3];
+        const float sa = 2.f / (float)(3 * R);
 #pragma unroll
-    for (int c = 0; c < 3; c++) drgb[3 * ray + c] = ga == 0.f ? 0.f : ga * sa * (rgb[3 * ray + c] - gt[3 * ray + c]);
-    const float oo = op[ray] + 1e-10f;
-    dop[ray] = gb == 0.f ? 0.f : gb * w_op * (-(logf(oo) + 1.f)) / (float)R;
+        for (int c = 0; c < 3; c++) drgb[3 * ray + c] = ga == 0.f ? 0.f : ga * sa * (rgb[3 * ray + c] - gt[3 * ray + c]);
+        const float oo = op[ray] + 1e-10f;
+        dop[ray] = gb == 0.f ? 0.f : gb * w_op * (-(logf(oo) + 1.f)) / (float)R;
+    }
+    if (!ddepth) return;
     // normals -> depth, gathered over this ray's triangle roles
     const int64_t T = (R / 64) * 49;
     const float tw[3] = {u[2], u[3], u[4]};
@@ -1195,6 +1198,8 @@ int ncn_nerf_loss_bwd(const float* rgb, const float* rgb_gt, const float* opacit
                       float* dL_dopacity, float* dL_ddepth, void* stream) {
     NCN_REQUIRE(n_rays % 64 == 0, hipErrorInvalidValue, "ncn_nerf_loss_bwd: n_rays=%lld is not whole 8x8 patches",
                 (long long)n_rays);
+    NCN_REQUIRE((dL_drgb == nullptr) == (dL_dopacity == nullptr), hipErrorInvalidValue,
+                "ncn_nerf_loss_bwd: dL_drgb and dL_dopacity are written together (both or neither)");
     if (n_rays <= 0) return 0;
     hipLaunchKernelGGL(nerf_loss_bwd_kernel, dim3(cdiv(n_rays, 256)), dim3(256), 0, (hipStream_t)stream, rgb, rgb_gt,
                        opacity, n_rays, w_opacity, photo_loss, rays_o, rays_d, depth, dL_dnormals, up_total, up_terms,

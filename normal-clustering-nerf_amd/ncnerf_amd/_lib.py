@@ -51,6 +51,8 @@ SIGNATURES = {
     "ncn_field_bwd_dE_floats": [I64],
     "ncn_field_bwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P, P],
     "ncn_field_bwd_mlp": [P, I64, P, P, P, I32, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd_stash_floats": [I64],
+    "ncn_field_bwd_mlp_part": [P, I64, P, P, P, I32, P, P, P, P, P, I32, I32, P, P, P, P, P],
     "ncn_field_scatter": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
@@ -108,6 +110,7 @@ def lib():
         L.ncn_cluster_status_offset.restype = ctypes.c_int64
         L.ncn_kmeans_plan_words.restype = ctypes.c_int64
         L.ncn_field_bwd_dE_floats.restype = ctypes.c_int64
+        L.ncn_field_bwd_stash_floats.restype = ctypes.c_int64
         L.ncn_adam_step_work_floats.restype = ctypes.c_int64
         L.ncn_grid_work_bytes.restype = ctypes.c_int64
         L.ncn_march_train_fused_work_bytes.restype = ctypes.c_int64

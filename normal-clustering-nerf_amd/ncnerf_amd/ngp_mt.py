@@ -80,26 +80,8 @@ class _FieldFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, d, table, w_sigma, w_rgb, model, mode, n_dev=None):
-        n = x.shape[0]  # capacity when n_dev (device int32 count) is given
-        dev = x.device
         need_grad = any(ctx.needs_input_grad[2:5])  # grad mode is off inside Function.forward
-        sigmas = torch.empty(n, dtype=torch.float32, device=dev)
-        rgbs = torch.empty(n, 3, dtype=torch.float32, device=dev) if mode == 0 else sigmas.new_empty(0, 3)
-        enc = None
-        if need_grad:
-            enc = torch.empty(((n + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev)
-        packed = model._take_packed()
-        order = None
-        if need_grad and model.sort_samples and n >= SORT_MIN_SAMPLES:
-            # processing order: Morton-sorted windows of 4096 samples (ncn_field_sort_windows); the
-            # encoding cache and the backward's dE are kept in it, the outputs stay in sample order
-            order = torch.empty(n, dtype=torch.int32, device=dev)
-            call("ncn_field_sort_windows", ptr(x), I64(n), ptr(n_dev), F32(model._xyz_min), F32(model._xyz_extent),
-                 ptr(order), stream())
-        call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(n_dev), ptr(order), ptr(table),
-             model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(model._prec), I32(mode),
-             ptr(sigmas),
-             ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
+        sigmas, rgbs, enc, packed, order = model._field_fwd(x, d, n_dev, mode, need_grad)
         if need_grad:
             ctx.save_for_backward(x, d, enc, packed, n_dev, order)
             ctx.model = model
@@ -119,23 +101,16 @@ class _FieldFunction(torch.autograd.Function):
         dE_ws = torch.empty(int(_lib.lib().ncn_field_bwd_dE_floats(I64(n))), dtype=torch.float32, device=x.device)
         c = lambda t: None if t is None else t.contiguous().float()
         dsig, drgb = c(dL_dsigmas), c(dL_drgbs)
-        split = model.scatter_split
-        if split is None:
+        if model.scatter_split is None:
             call("ncn_field_bwd", ptr(x), ptr(d), I64(n), ptr(n_dev), ptr(order), model._levels_ptr, F32(model._xyz_min),
                  F32(model._xyz_extent), ptr(packed), I32(model._prec), ptr(enc), ptr(dsig), ptr(drgb),
                  ptr(model._bwd_loss_scale()), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
         else:
-            # data-parallel step: the levels [split, 16) are scattered now, [0, split) later by
-            # run_deferred_scatter() while the all-reduce of the first bucket is in flight
             lmax = model._level_max()
             call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(model._prec), ptr(enc),
                  ptr(dsig), ptr(drgb), ptr(model._bwd_loss_scale()),
                  ptr(slab), ptr(dE_ws), ptr(lmax), stream())
-            call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), model._levels_ptr, F32(model._xyz_min),
-                 F32(model._xyz_extent), ptr(dE_ws), ptr(lmax), I32(split), I32(16), I32(0), ptr(g_table), stream())
-            # (a list: a step with two field backwards — e.g. density() with grad and forward() —
-            # leaves two pending coarse-level scatters, both run by run_deferred_scatter)
-            model._deferred.append((x, n, n_dev, order, dE_ws, lmax, g_table))
+            model._scatter(x, n, n_dev, order, dE_ws, lmax, g_table)
         call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
         return None, None, None, None, None, None, None, None
 
@@ -303,6 +278,43 @@ class NGPMT(nn.Module):
         return self._packed
 
     # -- field -----------------------------------------------------------------------------------
+    def _field_fwd(self, x, d, n_dev, mode, need_grad):
+        """ncn_field_fwd on x (N,3) / d (N,3) fp32 contiguous (capacity N when n_dev, a device int32
+        count, is given) -> (sigmas, rgbs, enc_cache, packed weights, order); enc_cache and order
+        (None unless sort_samples) are the backward's inputs, None without need_grad."""
+        n = x.shape[0]
+        dev = x.device
+        sigmas = torch.empty(n, dtype=torch.float32, device=dev)
+        rgbs = torch.empty(n, 3, dtype=torch.float32, device=dev) if mode == 0 else sigmas.new_empty(0, 3)
+        enc = None
+        if need_grad:
+            enc = torch.empty(((n + 15) // 16) * 16 * ENC_BYTES // 2, dtype=torch.float16, device=dev)
+        packed = self._take_packed()
+        order = None
+        if need_grad and self.sort_samples and n >= SORT_MIN_SAMPLES:
+            # processing order: Morton-sorted windows of 4096 samples (ncn_field_sort_windows); the
+            # encoding cache and the backward's dE are kept in it, the outputs stay in sample order
+            order = torch.empty(n, dtype=torch.int32, device=dev)
+            call("ncn_field_sort_windows", ptr(x), I64(n), ptr(n_dev), F32(self._xyz_min), F32(self._xyz_extent),
+                 ptr(order), stream())
+        call("ncn_field_fwd", ptr(x), ptr(d) if mode == 0 else ptr(None), I64(n), ptr(n_dev), ptr(order),
+             ptr(self.xyz_encoder.params), self._levels_ptr, F32(self._xyz_min), F32(self._xyz_extent), ptr(packed), I32(self._prec), I32(mode),
+             ptr(sigmas), ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
+        return sigmas, rgbs, enc, packed, order
+
+    def _scatter(self, x, n, n_dev, order, dE_ws, lmax, g_table):
+        """Table scatter after the MLP pass: every level (scatter_split None), else the levels
+        [scatter_split, 16) now and [0, scatter_split) queued for run_deferred_scatter() — the
+        data-parallel step scatters them while the all-reduce of the first bucket is in flight."""
+        split = self.scatter_split
+        lo = 0 if split is None else split
+        call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
+             F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(lo), I32(16), I32(0), ptr(g_table), stream())
+        if split is not None:
+            # (a list: a step with two field backwards — e.g. density() with grad and forward() —
+            # leaves two pending coarse-level scatters, both run by run_deferred_scatter)
+            self._deferred.append((x, n, n_dev, order, dE_ws, lmax, g_table))
+
     def density(self, x, return_feat=False):
         """ngp_mt.py:157-171 (density-only kernel mode)."""
         if return_feat:

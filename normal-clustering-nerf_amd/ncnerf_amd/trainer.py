@@ -47,9 +47,11 @@ class Trainer:
     epoch_items = 1000  # base.py:78-81 (training "epoch" = 1000 batches)
 
     def __init__(self, model, hparams=None, update_grid=False, use_graph=False, scatter_split=None,
-                 defer_optimizer=False, preset="hypersim"):
+                 defer_optimizer=False, preset="hypersim", split_backward=False):
         """hparams: overrides of the preset's hyper-parameters (PRESETS: "hypersim" = configs #1-#4,
-        "scannet_manhattan" = config #5)."""
+        "scannet_manhattan" = config #5).  split_backward (graph step, reference loss configuration):
+        the step runs as split_step.SplitStep — the photometric backward overlaps the normal
+        clustering — instead of render -> loss -> autograd backward."""
         self.h = dict(hparams_for(preset), **(hparams or {}))
         self.model = model
         self.loss = NeRFMTLoss(self.h)
@@ -66,6 +68,8 @@ class Trainer:
         self.render_kwargs = dict(near_distance=self.h["rend_near_dist"], max_samples=self.h["rend_max_samples"],
                                   test_time=False, random_bg=False, anneal_strategy="none", anneal_steps=0)
         self.use_graph = use_graph
+        self.split_backward = bool(split_backward) and use_graph
+        self._split = None  # the SplitStep of the captured graph (split_backward and split_eligible)
         self.graph = None
         # defer_optimizer (graph step): the optimizer step of step k runs inside graph k+1 on a side
         # stream, concurrently with step k+1's marcher (which reads no parameter), and joins before
@@ -124,15 +128,22 @@ class Trainer:
             kw["premarched"] = march_train_fused(m, batch["rays_o"], batch["rays_d"], kw["near_distance"],
                                                  kw["max_samples"], kw.get("march_noise"), kw.get("march_rng"))
             cur.wait_stream(side)
-        results = render(m, batch["rays_o"], batch["rays_d"], **kw)
-        loss_d = self.loss(results, batch, global_step=step_dev)
-        total = loss_d["total"]
-        if getattr(self, "_one", None) is None or self._one.device != total.device:
-            self._one = torch.ones((), dtype=total.dtype, device=total.device)
-        torch.autograd.backward(total, grad_tensors=self._one)  # (no ones_like fill node per step)
+        if self._split is not None:
+            results, loss_d = self._split.run(batch, step_dev, premarched=kw.get("premarched"))
+        else:
+            results = render(m, batch["rays_o"], batch["rays_d"], **kw)
+            loss_d = self.loss(results, batch, global_step=step_dev)
+            # (a constant upstream gradient: no ones_like fill node per step)
+            torch.autograd.backward(loss_d["total"], grad_tensors=self._unit(loss_d["total"].device))
         if with_opt and not self.defer:
             self.opt.step()
         return results, loss_d
+
+    def _unit(self, dev):
+        """A device fp32 1.0: the upstream gradient of the total loss."""
+        if getattr(self, "_one", None) is None or self._one.device != dev:
+            self._one = torch.ones((), dtype=torch.float32, device=dev)
+        return self._one
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
@@ -145,6 +156,8 @@ class Trainer:
         if self.render_kwargs.get("anneal_steps", 0) > 0:
             raise NotImplementedError("ray-range annealing is step-dependent host control flow")
         self._static = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in batch.items()}
+        from .split_step import SplitStep, split_eligible
+        self._split = SplitStep(self) if self.split_backward and split_eligible(self, self._static) else None
         self._step_dev = torch.zeros((), dtype=torch.int64, device=dev)
         # the optimizer is in the graph unless the gradient is reduced (or its scatter finished) outside
         self._with_opt = not distributed.is_distributed() and self.model.scatter_split is None

@@ -59,10 +59,10 @@ def _batch(scene, rank, k, device, world=1):
     return batch
 
 
-def run(steps, device, out=None, rank=0, defer=False, world=1):
+def run(steps, device, out=None, rank=0, defer=False, world=1, split=False):
     from ncnerf_amd.trainer import Trainer
     scene, model = _setup(device)
-    tr = Trainer(model, use_graph=True, defer_optimizer=defer)
+    tr = Trainer(model, use_graph=True, defer_optimizer=defer, split_backward=split)
     for k in range(steps):
         tr.step(_batch(scene, rank, k, device, world), global_step=3000 + k)
     tr.flush_optimizer()  # (defer: the last step's optimizer is still pending)
@@ -109,6 +109,6 @@ if __name__ == "__main__":
     rank, world = distributed.init_from_env(backend=os.environ.get("DDP_BACKEND", "gloo"))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)) % torch.cuda.device_count())
     run(int(sys.argv[2]), torch.device("cuda", torch.cuda.current_device()), sys.argv[1] if rank == 0 else None,
-        rank=rank, defer=len(sys.argv) > 3 and sys.argv[3] == "defer", world=world)
+        rank=rank, defer="defer" in sys.argv[3:], world=world, split="split" in sys.argv[3:])
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

@@ -28,16 +28,20 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("defer", [False, True])
-def test_two_rank_step_matches_single_process(dev, tmp_path, defer):
+@pytest.mark.parametrize("defer,split", [(False, False), (True, False), (True, True)])
+def test_two_rank_step_matches_single_process(dev, tmp_path, defer, split):
     """defer: the optimizer of step k inside graph k+1 (Trainer(defer_optimizer=True), the bench's
-    default) after the eager all-reduce of step k; 3 steps so that two deferred steps run in-graph."""
+    default) after the eager all-reduce of step k; 3 steps so that two deferred steps run in-graph.
+    split: the bench's split backward (Trainer(split_backward=True)), whose deferred coarse-level
+    scatter the all-reduce overlaps as the autograd step's."""
     out = str(tmp_path / "flat.pt")
     steps = 3 if defer else 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(HERE, "_ddp_step_worker.py"), out, str(steps)]
     if defer:
         cmd.append("defer")
+    if split:
+        cmd.append("split")
     env = dict(os.environ, DDP_BACKEND="gloo", OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
