@@ -221,19 +221,26 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
                       const float* loss_scale, float* slab, float* dE_ws, float* level_max, void* stream);
 /* The MLP pass split by the gradient's source (the fused training step runs the rgb part while
  * the normal clustering computes the depth gradient): part 1 (rgb) = the rgb_net path from
- * dL_drgbs alone — slab tiles of W3..W5 and the rgb part of dL/dh into dh_stash
- * (ncn_field_bwd_stash_floats(n) floats, 16-byte aligned); part 2 (sigma) = dL/dh = stash +
- * TruncExp'(h0) * (dL_dsigmas + dL_dsigmas2) (either may be NULL), then sigma_net: slab tiles of
- * W1, W2, dE_ws, level_max; part 3 = ncn_field_bwd_mlp (plus the second dsigma term).  Parts 1
- * and 2 of one step take the same n_blocks (> 0 caps the grid, leaving CUs to a concurrent kernel;
- * 0 = ncn_field_bwd_blocks(n)); ncn_field_reduce_wgrad then sums that many slab rows.  Together
- * they produce ncn_field_bwd_mlp's outputs (dL/dsigma summed from its two terms in f32). */
+ * dL_drgbs alone — slab tiles of W3..W5 (rows [0, its grid)) and the rgb part of dL/dh into
+ * dh_stash (ncn_field_bwd_stash_floats(n) floats, 16-byte aligned); it also zeroes level_max.
+ * Part 2 (sigma) = dL/dh = stash + TruncExp'(h0) * (dL_dsigmas + dL_dsigmas2) (either may be
+ * NULL), then sigma_net: slab tiles of W1, W2 (rows [0, its grid)), dE_ws, level_max (max-reduced
+ * into the 16 * ncn_field_bwd_blocks(n) floats the scatter reads).  Part 3 = ncn_field_bwd_mlp
+ * (plus the second dsigma term).  Each part's grid is n_blocks when > 0 (capped at
+ * ncn_field_bwd_part_blocks(n, part); a cap leaves CUs to a concurrent kernel), else
+ * ncn_field_bwd_part_blocks(n, part) — part 2 keeps less LDS and runs twice the workgroups.
+ * The slab holds max(grid 1, grid 2) rows; ncn_field_reduce_wgrad_parts(slab, grid 2, grid 1)
+ * then sums each net's rows.  Parts 1 + 2 on equal grids give ncn_field_bwd_mlp's outputs bit for
+ * bit (one dsigma term). */
 int64_t ncn_field_bwd_stash_floats(int64_t n);
+int ncn_field_bwd_part_blocks(int64_t n, int part);
 int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                            const uint16_t* weights_packed, int precision, const uint16_t* enc_cache,
                            const float* dL_dsigmas, const float* dL_dsigmas2, const float* dL_drgbs,
                            const float* loss_scale, int part, int n_blocks, float* slab, float* dE_ws,
                            float* level_max, float* dh_stash, void* stream);
+int ncn_field_reduce_wgrad_parts(const float* slab, int n_blocks_sigma, int n_blocks_rgb, float* grad_w,
+                                 void* stream);
 int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,

@@ -19,6 +19,7 @@
 // Operand precision is a template parameter: fp16 (tcnn's FullyFusedMLP precision) or bf16
 // (config #3); fp32 hash table + fp32 trilinear interpolation, fp32 accumulation either way.
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include "common.h"
 #include "../../include/ncnerf.h"
@@ -245,6 +246,18 @@ struct Frags {
     __device__ __forceinline__ v8 a32(int f, int lane) const { return f32[f * 64 + lane]; }
     __device__ __forceinline__ v4 a16(int f, int lane) const { return f16[f * 64 + lane]; }
 };
+// The sigma_net fragments alone (the split backward's sigma pass, compact LDS): F_L1, F_L2 at
+// their indices, B_L1 packed right behind them; B_L2 as the only fp16 fragments.
+template <typename T>
+struct FragsSigma : Frags<T> {
+    __device__ __forceinline__ typename Mfma<T>::v8 a32(int f, int lane) const {
+        return this->f32[(f >= B_L1 ? f - (B_L1 - F_L3) : f) * 64 + lane];
+    }
+    __device__ __forceinline__ typename Mfma<T>::v4 a16(int f, int lane) const {
+        return this->f16[(f - B_L2) * 64 + lane];
+    }
+};
+constexpr int N_SIG32 = F_L3 + 4, N_SIG16 = 4;  // F_L1, F_L2, B_L1 / B_L2
 
 // Shared per-group forward (16 samples).  Produces every intermediate the backward needs.
 template <typename T>
@@ -258,8 +271,8 @@ struct FwdState {
     float4_t out;   // rgb pre-activation tile (rows 0..2 valid on g==0)
 };
 
-template <typename T>
-__device__ __forceinline__ void mlp_sigma(const Frags<T>& F, int lane, typename Mfma<T>::v8 e, FwdState<T>& st) {
+template <typename T, typename FR>
+__device__ __forceinline__ void mlp_sigma(const FR& F, int lane, typename Mfma<T>::v8 e, FwdState<T>& st) {
     typedef Mfma<T> M;
     typedef typename M::v8 v8;
 #pragma unroll
@@ -534,8 +547,12 @@ __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, i
 __device__ __forceinline__ float lmax_upd(float m, float a, float b) {  // non-finite -> INF
     return (isfinite(a) && isfinite(b)) ? fmaxf(m, fmaxf(fabsf(a), fabsf(b))) : INFINITY;
 }
-template <typename T, int PART>
-__device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const BwdIn<T>& cur, int64_t grp,
+// exchange tiles a pass keeps per group: the sigma pass only XA2..XB1+1 (compact layout, origin XA2)
+template <int PART> constexpr int x_count() { return PART == BWD_SIGMA ? N_XFRAG - XA2 : N_XFRAG; }
+template <int PART> constexpr int x_origin() { return PART == BWD_SIGMA ? XA2 : 0; }
+
+template <typename T, int PART, typename FR>
+__device__ __forceinline__ void bwd_group(const FR& F, uint16_t* Xw, const BwdIn<T>& cur, int64_t grp,
                                           int64_t n, int64_t n_stride, int lane, float* __restrict__ dE_out,
                                           float (&lm)[4], float inv_S, float4_t* __restrict__ stash) {
     typedef Mfma<T> M;
@@ -598,18 +615,19 @@ __device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const
     }
     if (g == 0) dh[0] += cur.dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
     const v4 dhh = cvt4<T>(dh);
-    x_put(Xw + XA2 * 256, lane, dhh);
+    constexpr int XO = x_origin<PART>();
+    x_put(Xw + (XA2 - XO) * 256, lane, dhh);
 #pragma unroll
-    for (int b = 0; b < 4; b++) x_put(Xw + (XB2 + b) * 256, lane, st.x2[b]);
+    for (int b = 0; b < 4; b++) x_put(Xw + (XB2 - XO + b) * 256, lane, st.x2[b]);
     // L2 backward -> dH1, ReLU(x2) mask -> dD1
     v4 dD1[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) dD1[t] = relu_mask4<T>(M::k16(F.a16(B_L2 + t, lane), dhh, zero4()), st.x2[t]);
 #pragma unroll
-    for (int t = 0; t < 4; t++) x_put(Xw + (XA1 + t) * 256, lane, dD1[t]);
+    for (int t = 0; t < 4; t++) x_put(Xw + (XA1 - XO + t) * 256, lane, dD1[t]);
     const v4 e0 = v4{cur.e[0], cur.e[1], cur.e[2], cur.e[3]}, e1 = v4{cur.e[4], cur.e[5], cur.e[6], cur.e[7]};
-    x_put(Xw + XB1 * 256, lane, e0);
-    x_put(Xw + (XB1 + 1) * 256, lane, e1);
+    x_put(Xw + (XB1 - XO) * 256, lane, e0);
+    x_put(Xw + (XB1 - XO + 1) * 256, lane, e1);
     // L1 backward -> dE (tile t holds levels 8t+2g, 8t+2g+1)
     const v8 d1a = cat8<v8>(dD1[0], dD1[1]), d1b = cat8<v8>(dD1[2], dD1[3]);
     float4_t dE[2];
@@ -639,11 +657,11 @@ __device__ __forceinline__ void bwd_group(const Frags<T>& F, uint16_t* Xw, const
 // waves 0-3: W4 row-block a = wid (4 tiles) + W5 column block wid; waves 4-5: W3 row-blocks
 // 2(wid-4), +1 (d/pad and h tiles) + W2 block wid-4; waves 6-7: W1 row-blocks 2(wid-6), +1 (two K
 // tiles) + W2 block wid-4.
-template <typename T>
+template <typename T, int NX = N_XFRAG, int XO = 0>
 __device__ __forceinline__ typename Mfma<T>::v8 x_pair(const uint16_t* X, int q, int ng, int tile, int lane) {
     typedef typename Mfma<T>::v4 v4;
-    const v4 a = x_get<v4>(X + (q * N_XFRAG + tile) * 256, lane);
-    const v4 b = q + 1 < ng ? x_get<v4>(X + ((q + 1) * N_XFRAG + tile) * 256, lane) : v4{0, 0, 0, 0};
+    const v4 a = x_get<v4>(X + (q * NX + tile - XO) * 256, lane);
+    const v4 b = q + 1 < ng ? x_get<v4>(X + ((q + 1) * NX + tile - XO) * 256, lane) : v4{0, 0, 0, 0};
     return cat8<typename Mfma<T>::v8>(a, b);
 }
 template <typename T, int PART>
@@ -652,11 +670,13 @@ __device__ __forceinline__ void bwd_dw(const uint16_t* X, int ng, int wid, int l
     typedef typename M::v8 v8;
     constexpr bool RGB = (PART & BWD_RGB) != 0, SIG = (PART & BWD_SIGMA) != 0;
     if constexpr (PART == BWD_SIGMA) {  // 12 tiles: W1 (4 row x 2 col blocks) one per wave, W2 on waves 0-3
+        constexpr int NX = x_count<PART>(), XO = x_origin<PART>();
         for (int q = 0; q < ng; q += 2) {
-            acc[0] = M::k32(x_pair<T>(X, q, ng, XA1 + (wid >> 1), lane), x_pair<T>(X, q, ng, XB1 + (wid & 1), lane),
-                            acc[0]);
+            acc[0] = M::k32(x_pair<T, NX, XO>(X, q, ng, XA1 + (wid >> 1), lane),
+                            x_pair<T, NX, XO>(X, q, ng, XB1 + (wid & 1), lane), acc[0]);
             if (wid < 4)
-                acc[1] = M::k32(x_pair<T>(X, q, ng, XA2, lane), x_pair<T>(X, q, ng, XB2 + wid, lane), acc[1]);
+                acc[1] = M::k32(x_pair<T, NX, XO>(X, q, ng, XA2, lane), x_pair<T, NX, XO>(X, q, ng, XB2 + wid, lane),
+                                acc[1]);
         }
         return;
     }
@@ -803,14 +823,25 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
     if (n_dev) n = min<int64_t>(n, *n_dev);
-    __shared__ v8 F32s[N_FRAG32 * 64];                                              // 34 KB
-    __shared__ v4 F16s[N_FRAG16 * 64];                                              // 4 KB
-    __shared__ __attribute__((aligned(16))) uint16_t X[BWD_WAVES * N_XFRAG * 256];  // 120 KB dW operand images
+    // the sigma pass keeps only the sigma_net fragments and its 11 exchange tiles per group (57 KB:
+    // two workgroups per CU); the others all 34 + 8 fragments and 30 tiles (158 KB)
+    constexpr bool SIGONLY = PART == BWD_SIGMA;
+    constexpr int NF32 = SIGONLY ? N_SIG32 : N_FRAG32, NF16 = SIGONLY ? N_SIG16 : N_FRAG16, NX = x_count<PART>();
+    __shared__ v8 F32s[NF32 * 64];
+    __shared__ v4 F16s[NF16 * 64];
+    __shared__ __attribute__((aligned(16))) uint16_t X[BWD_WAVES * NX * 256];  // dW operand images
     {
         const v8* w32 = (const v8*)wpacked;
         const v4* w16 = (const v4*)(wpacked + N_FRAG32 * 512);
-        for (int i = threadIdx.x; i < N_FRAG32 * 64; i += BWD_THREADS) F32s[i] = w32[i];
-        for (int i = threadIdx.x; i < N_FRAG16 * 64; i += BWD_THREADS) F16s[i] = w16[i];
+        for (int i = threadIdx.x; i < NF32 * 64; i += BWD_THREADS) {
+            const int f = i >> 6;  // (sigma pass: B_L1 packed behind F_L2)
+            F32s[i] = w32[(SIGONLY && f >= F_L3 ? f + (B_L1 - F_L3) : f) * 64 + (i & 63)];
+        }
+        for (int i = threadIdx.x; i < NF16 * 64; i += BWD_THREADS) F16s[i] = w16[(SIGONLY ? B_L2 * 64 : 0) + i];
+    }
+    if constexpr (PART == BWD_RGB) {  // the sigma pass max-reduces into the level_max rows: zero them
+        if (blockIdx.x == 0 && level_max)
+            for (int i = threadIdx.x; i < lm_rows * 16; i += BWD_THREADS) level_max[i] = 0.f;
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -831,11 +862,11 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         if (grp + stride < n_groups)
             bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stash, order, S);
         if (grp < n_groups) {
-            Frags<T> F;
+            typename std::conditional<SIGONLY, FragsSigma<T>, Frags<T>>::type F;
             const int z = opaque_zero();
             F.f32 = F32s + z;
             F.f16 = F16s + z;
-            bwd_group<T, PART>(F, X + wid * N_XFRAG * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S, stash);
+            bwd_group<T, PART>(F, X + wid * NX * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S, stash);
         }
         lds_barrier();  // (the dE stores and the next step's loads stay in flight)
         bwd_dw<T, PART>(X, ng, wid, lane, acc);
@@ -868,20 +899,28 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         float m = 0.f;
 #pragma unroll
         for (int w = 0; w < BWD_WAVES; w++) m = fmaxf(m, lmw[w][threadIdx.x]);
-        level_max[blockIdx.x * 16 + threadIdx.x] = m;
+        if constexpr (PART == BWD_SIGMA)  // (any grid size: rows zeroed by the rgb pass; m >= 0, so the
+            // IEEE order is the unsigned order of the bits)
+            atomicMax((unsigned*)&level_max[(blockIdx.x % lm_rows) * 16 + threadIdx.x], __float_as_uint(m));
+        else
+            level_max[blockIdx.x * 16 + threadIdx.x] = m;
     }
     // a capped grid (ncn_field_bwd_mlp_part's n_blocks) leaves the scatter's remaining rows neutral
-    if (blockIdx.x == 0)
+    if (PART == BWD_ALL && blockIdx.x == 0)
         for (int i = (int)gridDim.x * 16 + threadIdx.x; i < lm_rows * 16; i += BWD_THREADS) level_max[i] = 0.f;
 }
 
 // Sum of the per-workgroup dW slabs: blockIdx.y takes a chunk of slabs (coalesced 1 KB rows),
 // chunk partials are added with f32 atomics (gw accumulates, like every .grad).
 constexpr int WRED_CHUNK = 16;
-__global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb, float* __restrict__ gw) {
+// (nb_sigma rows of the sigma_net weights W1, W2 and nb_rgb rows of the rgb_net's: the split
+// backward's two passes run on grids of their own)
+__global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb_sigma, int nb_rgb, float* __restrict__ gw) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= NCN_FIELD_NW) return;
+    const int nb = i < W3_OFF ? nb_sigma : nb_rgb;
     const int b0 = blockIdx.y * WRED_CHUNK, b1 = min(nb, b0 + WRED_CHUNK);
+    if (b0 >= b1) return;
     float s = 0.f;
     for (int b = b0; b < b1; b++) s += slab[(int64_t)b * NCN_FIELD_NW + i];
     atomicAdd(gw + i, s);
@@ -1950,6 +1989,12 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
 
 int64_t ncn_field_bwd_stash_floats(int64_t n) { return n > 0 ? 256 * ((n + 15) / 16) : 0; }
 
+// the sigma pass fits two workgroups per CU (compact LDS): twice the one-pass grid, at most 512
+int ncn_field_bwd_part_blocks(int64_t n, int part) {
+    const int nb = ncn_field_bwd_blocks(n);
+    return part == 2 ? std::min(512, 2 * nb) : nb;
+}
+
 int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                            const uint16_t* weights_packed, int precision, const uint16_t* enc_cache,
                            const float* dL_dsigmas, const float* dL_dsigmas2, const float* dL_drgbs,
@@ -1963,9 +2008,10 @@ int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, c
     NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)enc_cache & 15) == 0 &&
                     ((uintptr_t)weights_packed & 15) == 0 && ((uintptr_t)dh_stash & 15) == 0,
                 hipErrorInvalidValue, "ncn_field_bwd_mlp_part: dE_ws / enc_cache / weights_packed / dh_stash must be 16-byte aligned");
-    NCN_REQUIRE(part != 2 || level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp_part: level_max workspace required");
+    NCN_REQUIRE(level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp_part: level_max workspace required");
     NCN_REQUIRE(part == 3 || dh_stash != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp_part: dh_stash required for a split pass");
-    const int nb = n_blocks > 0 ? std::min(n_blocks, ncn_field_bwd_blocks(n)) : ncn_field_bwd_blocks(n);
+    const int nb = n_blocks > 0 ? std::min(n_blocks, ncn_field_bwd_part_blocks(n, part))
+                                : ncn_field_bwd_part_blocks(n, part);
     const hipStream_t st = (hipStream_t)stream;
     if (part == 1)
         launch_bwd_part<1>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
@@ -2025,8 +2071,18 @@ int ncn_diag_sc_times(unsigned long long* host, int reset) {
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream) {
     if (n_blocks <= 0) return 0;
     hipLaunchKernelGGL(reduce_wgrad_kernel, dim3(cdiv(NCN_FIELD_NW, 256), cdiv(n_blocks, WRED_CHUNK)), dim3(256), 0,
-                       (hipStream_t)stream, slab, n_blocks, grad_w);
+                       (hipStream_t)stream, slab, n_blocks, n_blocks, grad_w);
     NCN_LAUNCH_CHECK("ncn_field_reduce_wgrad");
+    return 0;
+}
+
+int ncn_field_reduce_wgrad_parts(const float* slab, int n_blocks_sigma, int n_blocks_rgb, float* grad_w,
+                                 void* stream) {
+    const int nb = std::max(n_blocks_sigma, n_blocks_rgb);
+    if (nb <= 0) return 0;
+    hipLaunchKernelGGL(reduce_wgrad_kernel, dim3(cdiv(NCN_FIELD_NW, 256), cdiv(nb, WRED_CHUNK)), dim3(256), 0,
+                       (hipStream_t)stream, slab, n_blocks_sigma, n_blocks_rgb, grad_w);
+    NCN_LAUNCH_CHECK("ncn_field_reduce_wgrad_parts");
     return 0;
 }
 

@@ -23,9 +23,10 @@ terms and comes from the second (joint) composite backward after the clustering.
 ncn_field_bwd_mlp_part's rgb pass takes the rgb_net weight gradients and the rgb part of dL/dh
 (stashed in fp32); the sigma pass adds TruncExp'(h0) dL/dsigma and finishes the sigma_net and
 encoding gradients.  Every per-sample value is therefore bit-identical to the autograd step's;
-only the float-atomic flush order of the table gradient differs, as between any two runs.  Both passes use at most SPLIT_BLOCKS workgroups so the
-clustering's 16 co-resident workgroups keep CUs of their own (a field-backward workgroup takes a
-whole CU's LDS).  Only the fused-loss configuration takes this path (split_eligible); any other
+only the float-atomic flush order of the table gradient differs, as between any two runs.  The rgb
+pass uses at most SPLIT_BLOCKS workgroups so the clustering's 16 co-resident workgroups keep CUs
+of their own (an rgb-pass workgroup takes a whole CU's LDS); the sigma pass keeps only the
+sigma_net's fragments and exchange tiles in LDS and runs two workgroups per CU.  Only the fused-loss configuration takes this path (split_eligible); any other
 falls back to the autograd step."""
 import torch
 
@@ -114,9 +115,10 @@ class SplitStep:
         w = (L.norm_D_C_ort_dot_w, L.norm_D_C_centr_dot_w, L.norm_D_C_centr_L1_w)
         one = tr._unit(dev)
         lib = _lib.lib()
-        nb = min(SPLIT_BLOCKS, int(lib.ncn_field_bwd_blocks(I64(n))))
+        nb = (min(SPLIT_BLOCKS, int(lib.ncn_field_bwd_part_blocks(I64(n), I32(1)))),
+              int(lib.ncn_field_bwd_part_blocks(I64(n), I32(2))))  # (the sigma pass: two workgroups per CU)
         drgb, dop, ddepth = torch.empty_like(rgb), torch.empty_like(opacity), torch.empty_like(depth)
-        slab = torch.empty(nb * N_W, dtype=torch.float32, device=dev)
+        slab = torch.empty(max(nb) * N_W, dtype=torch.float32, device=dev)
         dE_ws = torch.empty(int(lib.ncn_field_bwd_dE_floats(I64(n))), dtype=torch.float32, device=dev)
         stash = torch.empty(int(lib.ncn_field_bwd_stash_floats(I64(n))), dtype=torch.float32, device=dev)
         lmax = m._level_max()
@@ -125,7 +127,8 @@ class SplitStep:
 
         def mlp_part(part, dsig, drw):
             call("ncn_field_bwd_mlp_part", ptr(dirs), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec),
-                 ptr(enc), ptr(dsig), ptr(None), ptr(drw), ptr(scale), I32(part), I32(nb), ptr(slab), ptr(dE_ws),
+                 ptr(enc), ptr(dsig), ptr(None), ptr(drw), ptr(scale), I32(part), I32(nb[part - 1]), ptr(slab),
+                 ptr(dE_ws),
                  ptr(lmax), ptr(stash), stream())
 
         # the photometric backward on a side stream (its first launch waits for the fork; the
@@ -156,7 +159,7 @@ class SplitStep:
                                                 opacity, depth, rend, T_thr, bg=1.0)
         mlp_part(2, dsig, None)
         m._scatter(xyzs, n, n_dev, order, dE_ws, lmax, g_table)
-        call("ncn_field_reduce_wgrad", ptr(slab), I32(nb), ptr(g_w), stream())
+        call("ncn_field_reduce_wgrad_parts", ptr(slab), I32(nb[1]), I32(nb[0]), ptr(g_w), stream())
         L.last_cluster = (labels, cents, out)
         results = {"rays_a": rays_a, "deltas": deltas, "ts": ts, "rm_samples": n_dev, "vr_samples": cnt,
                    "opacity": opacity, "depth": depth, "ws": ws, "rgb": rgb, "rays_d": rays_d, "rays_o": rays_d,
