@@ -47,11 +47,12 @@ class Trainer:
     epoch_items = 1000  # base.py:78-81 (training "epoch" = 1000 batches)
 
     def __init__(self, model, hparams=None, update_grid=False, use_graph=False, scatter_split=None,
-                 defer_optimizer=False, preset="hypersim", split_backward=False):
+                 defer_optimizer=False, preset="hypersim", split_backward=True):
         """hparams: overrides of the preset's hyper-parameters (PRESETS: "hypersim" = configs #1-#4,
-        "scannet_manhattan" = config #5).  split_backward (graph step, reference loss configuration):
-        the step runs as split_step.SplitStep — the photometric backward overlaps the normal
-        clustering — instead of render -> loss -> autograd backward."""
+        "scannet_manhattan" = config #5).  split_backward (graph step; taken when the loss is the
+        reference configuration, split_step.split_eligible): the step runs as split_step.SplitStep —
+        the photometric backward overlaps the normal clustering, every per-sample value as the
+        autograd backward computes it — instead of render -> loss -> autograd backward."""
         self.h = dict(hparams_for(preset), **(hparams or {}))
         self.model = model
         self.loss = NeRFMTLoss(self.h)
