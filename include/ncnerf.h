@@ -246,6 +246,14 @@ int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const 
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
                       int max_blocks, float* grad_table, void* stream);
 int ncn_field_reduce_wgrad(const float* slab, int n_blocks, float* grad_w, void* stream);
+/* ncn_field_scatter with ncn_field_reduce_wgrad_parts(slab, n_blocks_sigma, n_blocks_rgb, grad_w)
+ * folded into the same launch (its workgroups sum slices of the slab rows before their table units:
+ * one kernel boundary and launch ramp less on the split backward's critical path).  slab NULL =
+ * ncn_field_scatter. */
+int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                            const uint32_t* levels, float xyz_min, float xyz_extent, const float* dE_ws,
+                            const float* level_max, int level_lo, int level_hi, int max_blocks, float* grad_table,
+                            const float* slab, int n_blocks_sigma, int n_blocks_rgb, float* grad_w, void* stream);
 
 /* ---- normal clustering loss path: replaces _extract_normals_from_ray_batch
  *      (hypersim_src/utils.py:504-541) and the faiss + torch cluster block of NeRFMTLoss

@@ -1738,7 +1738,10 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    float* __restrict__ grad,
                                                                    const float* __restrict__ level_max, int lm_rows,
                                                                    int level_lo, int level_hi,
-                                                                   const int32_t* __restrict__ order) {
+                                                                   const int32_t* __restrict__ order,
+                                                                   const float* __restrict__ wslab = nullptr,
+                                                                   int nb_sigma = 0, int nb_rgb = 0,
+                                                                   float* __restrict__ gw = nullptr) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
     __shared__ float wmax[SC_WAVES];
     __shared__ int fill[2];  // claimed-slot counts, alternating per unit (reset one unit ahead)
@@ -1749,6 +1752,22 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     __syncthreads();
     for (int i = threadIdx.x; i < lm_rows * 16; i += SC_THREADS)  // one load per thread, LDS max
         atomicMax((unsigned*)&lmax_s[i & 15], __float_as_uint(level_max[i]));  // (non-negative floats)
+    if (wslab) {
+        // (ncn_field_scatter_wgrad) the MLP weight-gradient slab rows summed into gw first: each
+        // workgroup a contiguous slice of the weights, its threads (weight, 16-row chunk) pairs with
+        // the weight varying fastest (coalesced rows); one f32 atomic per pair, as reduce_wgrad_kernel
+        const int per = (NCN_FIELD_NW + (int)gridDim.x - 1) / (int)gridDim.x;
+        const int w0 = (int)blockIdx.x * per, nw = min(NCN_FIELD_NW, w0 + per) - w0;
+        const int chunks = (max(nb_sigma, nb_rgb) + WRED_CHUNK - 1) / WRED_CHUNK;
+        for (int idx = threadIdx.x; idx < nw * chunks; idx += SC_THREADS) {
+            const int w = w0 + idx % nw, c = idx / nw;
+            const int nb = w < W3_OFF ? nb_sigma : nb_rgb;
+            const int b1 = min(nb, (c + 1) * WRED_CHUNK);
+            float acc = 0.f;
+            for (int b = c * WRED_CHUNK; b < b1; b++) acc += wslab[(int64_t)b * NCN_FIELD_NW + w];
+            if (c * WRED_CHUNK < nb) atomicAdd(gw + w, acc);
+        }
+    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
     const int64_t e_stride = (n_stride + 3) & ~(int64_t)3;  // dE row stride (as written by field_bwd)
@@ -2026,22 +2045,32 @@ int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, c
     return 0;
 }
 
-int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
-                      const uint32_t* levels, float xyz_min,
-                      float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
-                      int max_blocks, float* grad_table, void* stream) {
-    if (n <= 0 || level_hi <= level_lo) return 0;
+int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                            const uint32_t* levels, float xyz_min, float xyz_extent, const float* dE_ws,
+                            const float* level_max, int level_lo, int level_hi, int max_blocks, float* grad_table,
+                            const float* slab, int n_blocks_sigma, int n_blocks_rgb, float* grad_w, void* stream) {
+    if (n <= 0 || level_hi <= level_lo) return slab ? ncn_field_reduce_wgrad_parts(slab, n_blocks_sigma, n_blocks_rgb,
+                                                                                   grad_w, stream) : 0;
     NCN_REQUIRE(0 <= level_lo && level_hi <= 16, hipErrorInvalidValue, "ncn_field_scatter: levels must lie in [0, 16)");
     NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
                 "ncn_field_scatter: dE_ws and xyzs must be 16-byte aligned");
+    NCN_REQUIRE(!slab || grad_w, hipErrorInvalidValue, "ncn_field_scatter_wgrad: grad_w required with a slab");
     const LevelTable Lt = make_table(levels);
     int grid = scatter_grid(n);
     if (max_blocks > 0) grid = std::min(grid, max_blocks);
     hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
                        xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
-                       level_lo, level_hi, order);
+                       level_lo, level_hi, order, slab, n_blocks_sigma, n_blocks_rgb, grad_w);
     NCN_LAUNCH_CHECK("ncn_field_scatter");
     return 0;
+}
+
+int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
+                      const uint32_t* levels, float xyz_min,
+                      float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
+                      int max_blocks, float* grad_table, void* stream) {
+    return ncn_field_scatter_wgrad(xyzs, n, n_dev, order, levels, xyz_min, xyz_extent, dE_ws, level_max, level_lo,
+                                   level_hi, max_blocks, grad_table, nullptr, 0, 0, nullptr, stream);
 }
 
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,

@@ -56,6 +56,7 @@ SIGNATURES = {
     "ncn_field_reduce_wgrad_parts": [P, I32, I32, P, P],
     "ncn_field_bwd_mlp_part": [P, I64, P, P, P, I32, P, P, P, P, P, I32, I32, P, P, P, P, P],
     "ncn_field_scatter": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P],
+    "ncn_field_scatter_wgrad": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P, I32, I32, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],
     "ncn_normals_fwd": [P, P, P, P, P, P, I64, P, P],
     "ncn_normals_bwd": [P, P, P, P, P, P, I64, P, P, P, P],

@@ -302,14 +302,18 @@ class NGPMT(nn.Module):
              ptr(sigmas), ptr(rgbs) if mode == 0 else ptr(None), ptr(enc), stream())
         return sigmas, rgbs, enc, packed, order
 
-    def _scatter(self, x, n, n_dev, order, dE_ws, lmax, g_table):
+    def _scatter(self, x, n, n_dev, order, dE_ws, lmax, g_table, wgrad=None):
         """Table scatter after the MLP pass: every level (scatter_split None), else the levels
         [scatter_split, 16) now and [0, scatter_split) queued for run_deferred_scatter() — the
-        data-parallel step scatters them while the all-reduce of the first bucket is in flight."""
+        data-parallel step scatters them while the all-reduce of the first bucket is in flight.
+        wgrad = (slab, sigma-pass rows, rgb-pass rows, grad_w): the split backward's weight-gradient
+        reduction, folded into this launch (ncn_field_scatter_wgrad)."""
         split = self.scatter_split
         lo = 0 if split is None else split
-        call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
-             F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(lo), I32(16), I32(0), ptr(g_table), stream())
+        slab, nb_s, nb_r, g_w = wgrad if wgrad is not None else (None, 0, 0, None)
+        call("ncn_field_scatter_wgrad", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
+             F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(lo), I32(16), I32(0), ptr(g_table), ptr(slab),
+             I32(nb_s), I32(nb_r), ptr(g_w), stream())
         if split is not None:
             # (a list: a step with two field backwards — e.g. density() with grad and forward() —
             # leaves two pending coarse-level scatters, both run by run_deferred_scatter)

@@ -15,7 +15,7 @@ back-propagated on a side stream while the clustering runs:
                                                                        -> composite bw (rgb)
                                                                        -> field MLP bwd, rgb part
   main (after the join): composite bw (all terms) -> field MLP bwd, sigma part -> table scatter
-                         -> dW reduction
+                         (+ the dW slab reduction in the same launch)
 
 The rgb_net's input gradient dL/draws = w * dL/drgb needs only the photometric term, so the first
 composite backward yields it exactly as the joint one would; dL/dsigma mixes all three upstream
@@ -158,8 +158,7 @@ class SplitStep:
         dsig, _ = vren.composite_train_multi_bw(dop, ddepth, drgb, None, sigmas, rgbs, ws, deltas, ts, rays_a,
                                                 opacity, depth, rend, T_thr, bg=1.0)
         mlp_part(2, dsig, None)
-        m._scatter(xyzs, n, n_dev, order, dE_ws, lmax, g_table)
-        call("ncn_field_reduce_wgrad_parts", ptr(slab), I32(nb[1]), I32(nb[0]), ptr(g_w), stream())
+        m._scatter(xyzs, n, n_dev, order, dE_ws, lmax, g_table, wgrad=(slab, nb[1], nb[0], g_w))
         L.last_cluster = (labels, cents, out)
         results = {"rays_a": rays_a, "deltas": deltas, "ts": ts, "rm_samples": n_dev, "vr_samples": cnt,
                    "opacity": opacity, "depth": depth, "ws": ws, "rgb": rgb, "rays_d": rays_d, "rays_o": rays_d,
