@@ -48,9 +48,11 @@ def merge(files, out=FIXTURE):
                         "steps": r["steps"], "curve": [{"step": c["step"], "psnr": round(c["psnr"], 5),
                                                         "loss": round(c["loss"], 7)} for c in r["curve"]]})
     members.sort(key=lambda m: m["member"])
+    preset = json.load(open(files[0])).get("preset", "hypersim")
     res = {"side": "oracle CPU (fp32), oracle/train_ref.py with the C hash-grid statement", "gt": "surface_bright",
-           "eval_rays": 16384, "members": members,
-           "generator": "python tests/psnr_trajectory.py ref --member m --rays 2048 --steps 1000 --every 125 --impl c"}
+           "eval_rays": 16384, "members": members, "preset": preset,
+           "generator": "python tests/psnr_trajectory.py ref --member m --rays 2048 --steps 1000 --every 125 --impl c"
+                        + ("" if preset == "hypersim" else f" --preset {preset}")}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(f"{out}: {len(members)} members")
@@ -82,7 +84,7 @@ def stats(oracle, hip_runs):
     return out
 
 
-def run_hip_ensemble(members, repeats, steps, every, n_rays, log):
+def run_hip_ensemble(members, repeats, steps, every, n_rays, log, preset="hypersim"):
     import psnr_trajectory as pt
     runs = {}
     for m in members:
@@ -90,7 +92,8 @@ def run_hip_ensemble(members, repeats, steps, every, n_rays, log):
         runs[m] = []
         for r in range(repeats):
             t0 = time.time()
-            res = pt.run_hip(steps, every, lambda s: None, member=m, n_rays=n_rays, batches=batches)
+            res = pt.run_hip(steps, every, lambda s: None, member=m, n_rays=n_rays, batches=batches,
+                             trainer_kw={"preset": preset})
             runs[m].append(res["curve"])
             log(f"member {m} run {r}: " + " ".join(f"{c['step']}:{c['psnr']:.3f}" for c in res["curve"])
                 + f" ({time.time() - t0:.1f} s)")
@@ -105,17 +108,18 @@ def main():
     ap.add_argument("--members", type=int, default=None, help="(hip) first M members of the fixture")
     ap.add_argument("--steps", type=int, default=None, help="(hip) default: the fixture's")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fixture", default=FIXTURE, help="the oracle ensemble (merge: output; hip: input)")
     a = ap.parse_args()
     if a.mode == "merge":
-        merge(a.files, a.out or FIXTURE)
+        merge(a.files, a.out or a.fixture)
         return
     log = lambda s: print(s, flush=True)  # noqa: E731
-    oracle = json.load(open(FIXTURE))
+    oracle = json.load(open(a.fixture))
     mems = [m["member"] for m in oracle["members"]][: a.members]
     steps = a.steps or oracle["members"][0]["steps"]
     n_rays = oracle["members"][0]["rays_per_step"]
     every = oracle["members"][0]["curve"][0]["step"]
-    runs = run_hip_ensemble(mems, a.repeats, steps, every, n_rays, log)
+    runs = run_hip_ensemble(mems, a.repeats, steps, every, n_rays, log, oracle.get("preset", "hypersim"))
     st = stats(oracle, runs)
     for s in st:
         log(json.dumps(s))

@@ -78,7 +78,12 @@ def _psnr(se, n):
     return -10.0 * math.log10(max(se / n, 1e-12))
 
 
-def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, impl="torch", emulate=None):
+# normal-clustering weights per preset (the three loss_norm_D_C_* terms; ncnerf_amd.trainer.PRESETS)
+PRESET_CLUSTER_W = {"hypersim": 2e-3, "scannet_manhattan": 1e-2}
+
+
+def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, impl="torch", emulate=None,
+            preset="hypersim"):
     from oracle import field_ref, grid_ref
     from oracle.train_ref import CPUTrainer, render_train_ref
     from ncnerf_amd import synthetic
@@ -86,7 +91,7 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
     torch.set_num_threads(threads)
     scene = SyntheticScene()
     cpu = CPUTrainer(scene.bitfield, seed=init_seed(member), num_epochs=30, epoch_steps=1000, encode_impl=impl,
-                     emulate=emulate)
+                     emulate=emulate, w_cluster=PRESET_CLUSTER_W[preset])
     grid, _ = grid_ref.mark_invisible_cells(camera_K(), scene.poses, (synthetic.IMG_W, synthetic.IMG_H), 0.01, 128,
                                             0.5)
     ev = [scene.batch(N_RAYS, seed=s, gt=GT) for s in EVAL_SEEDS]
@@ -111,7 +116,8 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
                           "occupied_frac": float(np.unpackbits(cpu.bitfield).mean()), "t_s": round(time.time() - t0, 1)})
             log(json.dumps(curve[-1]))
             res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": n_rays, "gt": GT,
-                   "member": member, "init_seed": init_seed(member), "encode_impl": impl, "emulate": emulate, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
+                   "member": member, "init_seed": init_seed(member), "encode_impl": impl, "emulate": emulate,
+                   "preset": preset, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
                    "curve": curve}
             if out:  # the trajectory so far (a partial run is usable up to its last checkpoint)
                 with open(out, "w") as f:
@@ -199,6 +205,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--member", type=int, default=None, help="ensemble member (seeds); default: legacy seeds")
     ap.add_argument("--rays", type=int, default=N_RAYS, help="rays per training step")
+    ap.add_argument("--preset", default="hypersim", choices=sorted(PRESET_CLUSTER_W),
+                    help="hyper-parameter preset (the normal-clustering weights)")
     ap.add_argument("--impl", default="torch", choices=("torch", "c"), help="(ref) the oracle's hash-grid statement")
     ap.add_argument("--emulate", default=None, choices=("fp16", "bf16"),
                     help="(ref) round the MLP operands as tcnn's fp16 FullyFusedMLP / the HIP kernel do")
@@ -207,7 +215,8 @@ def main():
     a = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     if a.side == "ref":
-        res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl, emulate=a.emulate)
+        res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl,
+                      emulate=a.emulate, preset=a.preset)
     else:
         ref = json.load(open(a.ref)) if a.ref else None
         steps = ref["steps"] if ref else a.steps

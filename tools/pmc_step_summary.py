@@ -17,6 +17,9 @@ for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
         if k is None:
             continue
+        if k == "field_bwd_kernel":  # the split backward's passes (template PART 1 / 2; 3 = one pass)
+            part = next((p for p in ("1", "2", "3") if f"Li{p}E" in r["Kernel_Name"]), "3")
+            k += {"1": " (rgb pass)", "2": " (sigma pass)", "3": " (one pass)"}[part]
         key = (f, r["Dispatch_Id"])
         vals[k][r["Counter_Name"]][key] = vals[k][r["Counter_Name"]].get(key, 0.0) + float(r["Counter_Value"])
 out = {}
