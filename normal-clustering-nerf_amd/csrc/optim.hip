@@ -218,7 +218,10 @@ __global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, 
         ((float4*)p)[i] = P;
         ((float4*)m)[i] = M;
         ((float4*)v)[i] = V;
-        if (ZERO) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        // (the table gradient is sparse — most hash entries get no contribution in a step — so only
+        // the non-zero float4s are written back as zeros: less HBM write traffic, same contents)
+        if (ZERO && (G.x != 0.f || G.y != 0.f || G.z != 0.f || G.w != 0.f))
+            ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     for (int64_t i = 4 * n4 + tid; i < n; i += nth) {
         upd(p[i], g[i], m[i], v[i], i < n0 ? wd0 : wd1);
