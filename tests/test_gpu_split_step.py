@@ -36,10 +36,12 @@ def _model(dev, scene, seed=7, precision="fp16"):
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("n", [1000, 70001, 600000])
-def test_mlp_parts_equal_one_pass(dev, precision, n):
+@pytest.mark.parametrize("n,sort", [(1000, False), (70001, False), (70001, True), (600000, False)])
+def test_mlp_parts_equal_one_pass(dev, precision, n, sort):
+    """sort: the Morton-window processing order (NGPMT.sort_samples) through both passes."""
     g = torch.Generator(device=dev).manual_seed(n)
     m = NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev)
+    m.sort_samples = sort
     with torch.no_grad():
         m.flat_params()[: m._n_table].uniform_(-0.3, 0.3, generator=g)
     if m.amp_state is not None:
@@ -49,6 +51,7 @@ def test_mlp_parts_equal_one_pass(dev, precision, n):
     n_dev = torch.tensor([n - 7], dtype=torch.int32, device=dev)  # (a device count below capacity)
     with torch.no_grad():
         _, _, enc, packed, order = m._field_fwd(x, d, n_dev, 0, True)
+    assert (order is not None) == sort
     dsig = torch.randn(n, device=dev, generator=g) * 1e-2
     drgb = torch.randn(n, 3, device=dev, generator=g) * 1e-2
     L = _lib.lib()
@@ -103,7 +106,8 @@ def _batch(scene, dev, R, seed):
     return b
 
 
-def test_split_step_matches_autograd(dev):
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_split_step_matches_autograd(dev, precision):
     """One step, no optimizer: SplitStep.run vs render -> NeRFMTLoss -> backward (the Trainer's
     graph body without the split), both on the static-shape path with the same march noise."""
     scene = SyntheticScene()
@@ -111,7 +115,7 @@ def test_split_step_matches_autograd(dev):
     step_dev = torch.tensor(1500, dtype=torch.int64, device=dev)  # inside the clustering ramp
     out = []
     for split in (False, True):
-        m = _model(dev, scene)
+        m = _model(dev, scene, precision=precision)
         tr = Trainer(m, update_grid=False, use_graph=False)
         assert split_eligible(tr, b)
         m.flat_grad().zero_()
