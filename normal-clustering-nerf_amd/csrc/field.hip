@@ -1533,6 +1533,40 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
     }
 }
 
+// (Experiment, off) Wave-level merge of the finished runs that share a cell: up to SC_CELL_MERGE
+// groups of lanes with equal keys summed by one wave reduction each (wave_sum_multi) into the
+// group's first lane before the LDS adds.  Measured (tools/scatter_probe.py, bench batch, levels
+// alone / all): 3 groups 63 -> 69 us on level 0, 191 -> 227 us all levels; 8 groups worse still —
+// the reductions (and the spills they cause at 128 VGPRs) cost more than the same-slot LDS atomics
+// they remove.
+#ifndef SC_CELL_MERGE
+#define SC_CELL_MERGE 0
+#endif
+__device__ __forceinline__ void sc_merge_cells(int lane, bool& act, uint32_t px, uint32_t py, uint32_t pz,
+                                               float (&v)[16]) {
+    uint64_t rem = __ballot(act);
+#pragma unroll 1
+    for (int it = 0; it < SC_CELL_MERGE && rem; it++) {
+        const int leader = (int)__builtin_ctzll(rem);
+        const uint32_t kx = __builtin_amdgcn_readlane(px, leader), ky = __builtin_amdgcn_readlane(py, leader),
+                       kz = __builtin_amdgcn_readlane(pz, leader);
+        const bool mine = act && px == kx && py == ky && pz == kz;
+        const uint64_t grp = __ballot(mine);
+        if (__popcll(grp) < 2) break;  // (uniform) a lone record: leave it and the rest to the per-lane adds
+        float s[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) s[j] = mine ? v[j] : 0.f;
+        wave_sum_multi<16>(s);
+        if (lane == leader) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = s[j];
+        } else if (mine) {
+            act = false;
+        }
+        rem &= ~grp;
+    }
+}
+
 // A lane's C consecutive samples: consecutive samples in the same cell are summed in registers and
 // a finished run goes to sc_add_cell (called by the whole wave when some lane has one).
 template <int C>
@@ -1552,7 +1586,11 @@ __device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C
             q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
             emit = q.px != p.px || q.py != p.py || q.pz != p.pz;
         }
-        if (__ballot(emit && any)) sc_add_cell(sh, lane, emit && any, p.px, p.py, p.pz, v, L, grad);  // uniform
+        if (__ballot(emit && any)) {  // uniform
+            bool act = emit && any;
+            if (SC_CELL_MERGE > 0 && !L.direct) sc_merge_cells(lane, act, p.px, p.py, p.pz, v);
+            sc_add_cell(sh, lane, act, p.px, p.py, p.pz, v, L, grad);
+        }
         if (i < C) {
 #pragma unroll
             for (int j = 0; j < 16; j++) v[j] = emit ? 0.f : v[j];
@@ -1606,6 +1644,11 @@ __device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: 
 #define SC_TNOW(v)
 #define SC_TADD(i, a, b)
 #endif
+// (Experiment, off) levels >= SC_DIRECT_FROM without the LDS table, every run's corners added with
+// global f32 atomics: measured (tools/scatter_probe.py) 190 -> 627 us from level 15, 1079 us from 14.
+#ifndef SC_DIRECT_FROM
+#define SC_DIRECT_FROM 16
+#endif
 template <int C, bool RUNS>
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const float2* __restrict__ dEl,
@@ -1623,7 +1666,8 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     L.params = Lt.params[l];
     L.off = Lt.offset[l];
     L.dense = (uint64_t)L.res * L.res * L.res <= L.params;  // tcnn: stride stays <= params
-    L.direct = !isfinite(m);
+    // levels >= SC_DIRECT_FROM: every run's corners straight to global f32 atomics (no LDS table)
+    L.direct = !isfinite(m) || l >= SC_DIRECT_FROM;
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
     // An entry's sum over the unit is at most (unit samples) * m (a sample's 8 corner weights sum
@@ -1696,6 +1740,9 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
 #endif
 __device__ __forceinline__ int sc_cell_rounds(int l) { return l < 6 ? SC_CELL_ROUNDS_A : l < 10 ? SC_CELL_ROUNDS_B : 1; }
 
+#ifndef SC_CELL_CONTIG
+#define SC_CELL_CONTIG 0
+#endif
 template <int C>
 __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1, int rounds,
                                              const float* __restrict__ xyzs, const float2* __restrict__ dEl,
@@ -1714,7 +1761,10 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
     L.k = (SC_PACK ? 30 : 61) - lg_unit - e2;
     ScChunk<C> ch;
-    const int64_t lane_off = (int64_t)(lane * SC_WAVES + wid) * C;
+    // lane t of wave w takes chunk t * SC_WAVES + w (neighbouring chunks in different waves); (off)
+    // SC_CELL_CONTIG: wave w covers the contiguous chunks 64w .. 64w+63 — measured: levels 6-9 alone
+    // 37 -> 31 us, all levels 191 -> 193 us (no gain inside the full launch)
+    const int64_t lane_off = (SC_CELL_CONTIG ? (int64_t)wid * 64 + lane : (int64_t)lane * SC_WAVES + wid) * C;
     sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, nrm, order);
     for (int r = 0; r < rounds; r++) {
         ScChunk<C> nx;

@@ -114,6 +114,8 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
         coarse = timeit(L, lo=0, hi=10)
         fine = timeit(L, lo=10, hi=16)
         print(f"  {name:24s} all {t:7.1f} us  levels0-9 {coarse:7.1f}  levels10-15 {fine:7.1f}  {msg}", flush=True)
+        if os.environ.get("SCATTER_PROBE_PER_LEVEL"):
+            print("   per level:", " ".join(f"{l}:{timeit(L, lo=l, hi=l + 1):.1f}" for l in range(16)), flush=True)
         if hasattr(L, "ncn_diag_sc_times"):
             buf = (ctypes.c_ulonglong * (256 * 10))()
             L.ncn_diag_sc_times(buf, 1)
