@@ -222,7 +222,9 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
 /* The MLP pass split by the gradient's source (the fused training step runs the rgb part while
  * the normal clustering computes the depth gradient): part 1 (rgb) = the rgb_net path from
  * dL_drgbs alone — slab tiles of W3..W5 (rows [0, its grid)) and the rgb part of dL/dh into
- * dh_stash (ncn_field_bwd_stash_floats(n) floats, 16-byte aligned); it also zeroes level_max.
+ * dh_stash (ncn_field_bwd_stash_floats(n) floats, 16-byte aligned: the MLP-operand-rounded values
+ * the sigma pass consumes, plus the fp32 element the TruncExp term is added to — 36 B per sample);
+ * it also zeroes level_max.
  * Part 2 (sigma) = dL/dh = stash + TruncExp'(h0) * (dL_dsigmas + dL_dsigmas2) (either may be
  * NULL), then sigma_net: slab tiles of W1, W2 (rows [0, its grid)), dE_ws, level_max (max-reduced
  * into the 16 * ncn_field_bwd_blocks(n) floats the scatter reads).  Part 3 = ncn_field_bwd_mlp

@@ -517,19 +517,24 @@ template <typename T>
 struct BwdIn {
     typename Mfma<T>::v8 e;
     float dx, dy, dz, dsig, dr0, dr1, dr2;
-    float4_t dhr;  // (BWD_SIGMA) the stashed rgb part of dL/dh of this lane's tile
+    typename Mfma<T>::v4 dq;  // (BWD_SIGMA) the stashed rgb part of dL/dh of this lane's tile, as operands
+    float h0;                 // (BWD_SIGMA, g = 0) its row-0 element in fp32 (TruncExp's term is added to it)
 };
 template <typename T, int PART>
 __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, int lane,
                                          const typename Mfma<T>::v8* __restrict__ enc, const float* __restrict__ dirs,
                                          const float* __restrict__ dL_dsig, const float* __restrict__ dL_dsig2,
-                                         const float* __restrict__ dL_drgb, const float4_t* __restrict__ stash,
+                                         const float* __restrict__ dL_drgb,
+                                         const typename Mfma<T>::v4* __restrict__ stq, const float* __restrict__ sth0,
                                          const int32_t* __restrict__ order, float S) {
     const int64_t pos = grp * 16 + (lane & 15);  // processing position (enc_cache / dE order)
     const bool valid = pos < n;
     in.e = enc[grp * 64 + lane];
     in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
-    if constexpr (PART == BWD_SIGMA) in.dhr = stash[grp * 64 + lane];
+    if constexpr (PART == BWD_SIGMA) {
+        in.dq = stq[grp * 64 + lane];
+        in.h0 = (lane >> 4) == 0 ? sth0[grp * 16 + (lane & 15)] : 0.f;
+    }
     if (valid) {
         const int64_t s = order ? (int64_t)order[pos] : pos;
         if constexpr ((PART & BWD_RGB) != 0) {
@@ -554,7 +559,8 @@ template <int PART> constexpr int x_origin() { return PART == BWD_SIGMA ? XA2 : 
 template <typename T, int PART, typename FR>
 __device__ __forceinline__ void bwd_group(const FR& F, uint16_t* Xw, const BwdIn<T>& cur, int64_t grp,
                                           int64_t n, int64_t n_stride, int lane, float* __restrict__ dE_out,
-                                          float (&lm)[4], float inv_S, float4_t* __restrict__ stash) {
+                                          float (&lm)[4], float inv_S, typename Mfma<T>::v4* __restrict__ stq,
+                                          float* __restrict__ sth0) {
     typedef Mfma<T> M;
     typedef typename M::v4 v4;
     typedef typename M::v8 v8;
@@ -607,14 +613,23 @@ __device__ __forceinline__ void bwd_group(const FR& F, uint16_t* Xw, const BwdIn
     dh = M::k32(F.a32(B_L3, lane), cat8<v8>(dD3[0], dD3[1]), zero4());
     dh = M::k32(F.a32(B_L3 + 1, lane), cat8<v8>(dD3[2], dD3[3]), dh);
     if constexpr (PART == BWD_RGB) {  // the sigma part follows in its own pass (BWD_SIGMA)
-        stash[grp * 64 + lane] = dh;
+        // stash: the operand-rounded tile (what the sigma pass converts it to anyway) and, for the
+        // row-0 element that TruncExp's term is added to first, its fp32 value: 36 B per sample
+        stq[grp * 64 + lane] = cvt4<T>(dh);
+        if (g == 0) sth0[grp * 16 + r] = dh[0];
         return;
     }
-    } else {
-        dh = cur.dhr;  // (BWD_SIGMA) the rgb path's dL/dh, from the stash
     }
-    if (g == 0) dh[0] += cur.dsig * __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
-    const v4 dhh = cvt4<T>(dh);
+    v4 dhh;
+    const float tex = __expf(fminf(fmaxf(st.h[0], -15.f), 15.f));
+    if constexpr (PART == BWD_SIGMA) {  // (the same explicit fma and rounding as below: bit-identical)
+        dhh = cur.dq;
+        if (g == 0) dhh[0] = (T)fmaf(cur.dsig, tex, cur.h0);
+    } else {  // (the split passes' order: the whole tile rounded as the rgb pass stashes it, then the
+              // row-0 element recomputed with the TruncExp term — keeps the two forms bit-identical)
+        dhh = cvt4<T>(dh);
+        if (g == 0) dhh[0] = (T)fmaf(cur.dsig, tex, dh[0]);
+    }
     constexpr int XO = x_origin<PART>();
     x_put(Xw + (XA2 - XO) * 256, lane, dhh);
 #pragma unroll
@@ -813,7 +828,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const typename Mfma<T>::v8* __restrict__ enc_cache, const float* __restrict__ dL_dsig,
     const float* __restrict__ dL_drgb, const float* __restrict__ loss_scale, float* __restrict__ dE_out,
     float* __restrict__ slab, float* __restrict__ level_max, const int32_t* __restrict__ order,
-    const float* __restrict__ dL_dsig2 = nullptr, float4_t* __restrict__ stash = nullptr) {
+    const float* __restrict__ dL_dsig2 = nullptr, float* __restrict__ stash = nullptr) {
     typedef typename Mfma<T>::v4 v4;
     // AMP loss scale (GradScaler of the reference's precision=16 run) times tcnn's fp16 module loss
     // scale (128): the fp16 chain sees the upstream gradients times S (a power of two), dE and dW
@@ -822,6 +837,10 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
+    // split passes' stash (ncn_field_bwd_stash_floats): [groups][64] operand tiles, then [groups][16]
+    // fp32 row-0 elements (capacity groups: the layout does not depend on the device count)
+    v4* stq = (v4*)stash;
+    float* sth0 = stash ? stash + ((n + 15) / 16) * 128 : nullptr;
     if (n_dev) n = min<int64_t>(n, *n_dev);
     // the sigma pass keeps only the sigma_net fragments and its 11 exchange tiles per group (57 KB:
     // two workgroups per CU); the others all 34 + 8 fragments and 30 tiles (158 KB)
@@ -854,19 +873,20 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
     BwdIn<T> nxt;
     if (base + wid < n_groups)
-        bwd_load<T, PART>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stash, order, S);
+        bwd_load<T, PART>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order, S);
     for (; base < n_groups; base += stride) {
         const int64_t grp = base + wid;
         const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
         const BwdIn<T> cur = nxt;
         if (grp + stride < n_groups)
-            bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stash, order, S);
+            bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order,
+                              S);
         if (grp < n_groups) {
             typename std::conditional<SIGONLY, FragsSigma<T>, Frags<T>>::type F;
             const int z = opaque_zero();
             F.f32 = F32s + z;
             F.f16 = F16s + z;
-            bwd_group<T, PART>(F, X + wid * NX * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S, stash);
+            bwd_group<T, PART>(F, X + wid * NX * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S, stq, sth0);
         }
         lds_barrier();  // (the dE stores and the next step's loads stay in flight)
         bwd_dw<T, PART>(X, ng, wid, lane, acc);
@@ -1958,11 +1978,11 @@ static void launch_bwd_part(int precision, int nb, hipStream_t st, const float* 
     if (precision == NCN_PREC_F16)
         hipLaunchKernelGGL((field_bwd_kernel<_Float16, PART>), dim3(nb), dim3(BWD_THREADS), 0, st, dirs, n, n_dev, wp,
                            (const Mfma<_Float16>::v8*)enc, dsig, drgb, loss_scale, dE_ws, slab, level_max, order, dsig2,
-                           (float4_t*)stash);
+                           stash);
     else
         hipLaunchKernelGGL((field_bwd_kernel<__bf16, PART>), dim3(nb), dim3(BWD_THREADS), 0, st, dirs, n, n_dev, wp,
                            (const Mfma<__bf16>::v8*)enc, dsig, drgb, loss_scale, dE_ws, slab, level_max, order, dsig2,
-                           (float4_t*)stash);
+                           stash);
 }
 
 extern "C" {
@@ -2056,7 +2076,8 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
     return 0;
 }
 
-int64_t ncn_field_bwd_stash_floats(int64_t n) { return n > 0 ? 256 * ((n + 15) / 16) : 0; }
+// per 16-sample group: 64 lanes x 4 operand values (2 B) + 16 fp32 row-0 elements = 144 floats
+int64_t ncn_field_bwd_stash_floats(int64_t n) { return n > 0 ? 144 * ((n + 15) / 16) : 0; }
 
 // the sigma pass fits two workgroups per CU (compact LDS): twice the one-pass grid, at most 512
 int ncn_field_bwd_part_blocks(int64_t n, int part) {
