@@ -1960,9 +1960,12 @@ static LevelTable make_table(const uint32_t* levels) {
     return t;
 }
 
+#ifndef NCN_FWD_MAX_BLOCKS
+#define NCN_FWD_MAX_BLOCKS 4096
+#endif
 static int fwd_grid(int64_t n) {
     const int64_t groups = (n + 15) / 16;
-    const int64_t g = std::min<int64_t>(std::max<int64_t>((groups + 3) / 4, 1), 4096);
+    const int64_t g = std::min<int64_t>(std::max<int64_t>((groups + 3) / 4, 1), NCN_FWD_MAX_BLOCKS);
     return (int)((g + 7) & ~(int64_t)7);  // a multiple of 8 (xcd_block)
 }
 

@@ -93,9 +93,15 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 // adam_prep runs ONE 1024-thread workgroup per CU (256 on MI355X): every arrival is an atomic on
 // the same counter word, and same-address atomics serialise at the memory side (MI355X_MICROARCH.md
 // "Global float atomics", contention row), so 2048 arrivals cost ~15-20 us where 256 cost ~2.
-constexpr int ADAM_BLOCKS = 256;     // workgroups of adam_prep (partials)
+#ifndef NCN_ADAM_BLOCKS
+#define NCN_ADAM_BLOCKS 256
+#endif
+#ifndef NCN_ADAM_UNROLL
+#define NCN_ADAM_UNROLL 12
+#endif
+constexpr int ADAM_BLOCKS = NCN_ADAM_BLOCKS;  // workgroups of adam_prep (partials)
 constexpr int ADAM_THREADS = 1024;
-constexpr int ADAM_UNROLL = 12;      // float4 loads in flight per thread (45.8 MB: 11 per thread)
+constexpr int ADAM_UNROLL = NCN_ADAM_UNROLL;  // float4 loads in flight per thread (45.8 MB: 11 per thread)
 __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __restrict__ g, int64_t n, float gscale,
                                                                float max_norm, double b1, double b2, float lr,
                                                                const float* __restrict__ lr_dev,

@@ -89,6 +89,8 @@ for so in [] if os.environ.get("SCATTER_PROBE_MAIN_ONLY") else sorted(glob.glob(
     L = ctypes.CDLL(so)
     L.ncn_field_scatter.argtypes = _lib.SIGNATURES["ncn_field_scatter"]
     L.ncn_field_scatter.restype = ctypes.c_int
+    L.ncn_field_fwd.argtypes = _lib.SIGNATURES["ncn_field_fwd"]
+    L.ncn_field_fwd.restype = ctypes.c_int
     libs.append((os.path.basename(so)[6:-3], L))
 gref = None
 for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.environ.get("SCATTER_PROBE_IDENTITY") else (False, True):
@@ -110,6 +112,12 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
         else:
             rel = ((g1 - gref).norm() / gref.norm()).item()
             msg = f"rel-L2 vs first {rel:.2e}"
+        if os.environ.get("SCATTER_PROBE_FWD"):  # (the forward of each library, same inputs)
+            fw = lambda: L.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(ORDER[0]), ptr(table),  # noqa: E731
+                                         model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed),
+                                         I32(0), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
+            print(f"  {name:24s} field_fwd {ev_time(fw):7.1f} us", flush=True)
+            continue
         t = timeit(L)
         coarse = timeit(L, lo=0, hi=10)
         fine = timeit(L, lo=10, hi=16)
