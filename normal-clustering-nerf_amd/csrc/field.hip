@@ -1801,6 +1801,94 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     lds_barrier();
 }
 
+// Unit queues of field_scatter_kernel (SC_DYN), one per first level of a launch (a launch over
+// [level_lo, level_hi) uses queue level_lo; launches with the same level_lo are stream-ordered).
+// Zero between launches: each launch's last ticket resets its queue.
+#ifndef SC_DYN
+#define SC_DYN 0  // measured: 191 vs 196 us, then 194 vs 190 (static): no gain beyond noise
+#endif
+__device__ unsigned sc_queue[16];
+
+// One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
+__device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n_run, int64_t n_dir4, int64_t ud,
+                                            int64_t ud2, int64_t ur, int64_t n, int cell_lo, int run_lo, int dir_lo,
+                                            int dir_mid, int& layout, int& par, ScShared& sh, char* arena,
+                                            float* wmax, int* fill, const float* lmax_s, int wid, int lane,
+                                            const float* __restrict__ xyzs, const float2* __restrict__ dE,
+                                            int64_t e_stride, const ScNorm& nrm, const LevelTable& Lt,
+                                            float* __restrict__ grad, const int32_t* __restrict__ order) {
+    constexpr int C_RUN = SC_C_RUN, C_DIR = SC_C_DIR, C_CELL = SC_C_CELL;
+    const int mode = u < n_cell ? SC_MODE_CELL : u < n_cell + n_run ? SC_MODE_RUN : SC_MODE_DIR;
+    if (mode != layout) {  // (re)initialise the table of the new layout
+        lds_barrier();
+        sh = sc_layout(arena, wmax, fill, mode);
+        const int nv = mode == SC_MODE_CELL ? SC_CELL_VALS * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
+        for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
+        for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
+        if (threadIdx.x == 0) fill[0] = fill[1] = 0;
+        lds_barrier();
+        layout = mode;
+        par = 0;
+    }
+    int l, rounds = 1;
+    int64_t s0, s1;
+    if (mode == SC_MODE_CELL) {
+        int64_t v = u;
+        l = cell_lo;
+        for (;; l++) {  // (uniform, at most SC_CELL_HI steps)
+            rounds = sc_cell_rounds(l);
+            const int64_t span = (int64_t)SC_THREADS * C_CELL * rounds;
+            const int64_t nu = (n + span - 1) / span;
+            if (v < nu) {
+                s0 = v * span;
+                s1 = min(n, s0 + span);
+                break;
+            }
+            v -= nu;
+        }
+    } else if (mode == SC_MODE_RUN) {
+        const int64_t v = u - n_cell;
+        const int li = (int)(v / ur);
+        l = run_lo + li;
+        s0 = (v - li * ur) * (SC_THREADS * C_RUN);
+        s1 = min(n, s0 + SC_THREADS * C_RUN);
+    } else {
+        int64_t v = u - n_cell - n_run;
+        if (v < n_dir4) {
+            const int li = (int)(v / ud);
+            l = dir_lo + li;
+            s0 = (v - li * ud) * (SC_THREADS * C_DIR);
+            s1 = min(n, s0 + SC_THREADS * C_DIR);
+        } else {
+            v -= n_dir4;
+            const int li = (int)(v / ud2);
+            l = dir_mid + li;
+            s0 = (v - li * ud2) * (SC_THREADS * 2);
+            s1 = min(n, s0 + SC_THREADS * 2);
+            rounds = 2;  // (marks the C = 2 form below)
+        }
+    }
+    float m = lmax_s[l];
+#ifdef NCN_DIAG_SC_LEVELS_MASK
+    if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
+#endif
+    if (m == 0.f) return;  // uniform: nothing to add on this level (no barrier, parity kept)
+    // the unit claims into fill[par]; fill[par ^ 1] (read by every lane before the previous
+    // unit's closing barrier) is reset here for the next unit
+    sh.fill = fill + par;
+    if (threadIdx.x == 0) fill[par ^ 1] = 0;
+    par ^= 1;
+    const float2* dEl = dE + (int64_t)l * e_stride;
+    if (mode == SC_MODE_CELL)
+        sc_cell_unit<C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
+    else if (mode == SC_MODE_RUN)
+        sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+    else if (rounds == 2)
+        sc_unit<2, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+    else
+        sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+}
+
 __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
@@ -1868,80 +1956,35 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     const int64_t n_dir4 = dir_mid > dir_lo ? (int64_t)(dir_mid - dir_lo) * ud : 0;
     const int64_t n_dir2 = dir_hi > dir_mid ? (int64_t)(dir_hi - dir_mid) * ud2 : 0;
     const int64_t n_units = n_cell + n_run + n_dir4 + n_dir2;
-    // (grid-stride: a workgroup takes its cell units first, then run, then direct: at most two
-    // layout switches)
-    int layout = -1, par = 0;
+    // Units are ordered heaviest first (the coarse cell levels' long units, then the finer levels).
+    // Workgroup b takes unit b; with SC_DYN every later unit is drawn from a device queue (ticket
+    // t -> unit gridDim.x + t), so a workgroup that finishes early takes the next unit instead of a
+    // fixed stride (the units' costs differ ~10x across levels).  The ticket for the next unit is
+    // drawn at the start of the current one (its latency hides behind the unit) and handed to the
+    // workgroup through LDS at the unit's end.  Tickets are monotone, so a workgroup's units still
+    // go cell -> run -> direct (at most two layout switches).  The holder of the launch's last ticket
+    // (every workgroup's last draw fails, so it is the last access to the counter) resets it.
+    int layout = -1, par = 0, qb = 0;
     ScShared sh;
-    for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-        const int mode = u < n_cell ? SC_MODE_CELL : u < n_cell + n_run ? SC_MODE_RUN : SC_MODE_DIR;
-        if (mode != layout) {  // (re)initialise the table of the new layout
-            lds_barrier();
-            sh = sc_layout(arena, wmax, fill, mode);
-            const int nv = mode == SC_MODE_CELL ? SC_CELL_VALS * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
-            for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
-            for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
-            if (threadIdx.x == 0) fill[0] = fill[1] = 0;
-            lds_barrier();
-            layout = mode;
-            par = 0;
-        }
-        int l, rounds = 1;
-        int64_t s0, s1;
-        if (mode == SC_MODE_CELL) {
-            int64_t v = u;
-            l = cell_lo;
-            for (;; l++) {  // (uniform, at most SC_CELL_HI steps)
-                rounds = sc_cell_rounds(l);
-                const int64_t span = (int64_t)SC_THREADS * C_CELL * rounds;
-                const int64_t nu = (n + span - 1) / span;
-                if (v < nu) {
-                    s0 = v * span;
-                    s1 = min(n, s0 + span);
-                    break;
-                }
-                v -= nu;
+    __shared__ unsigned qnext[2];
+    unsigned* const queue = sc_queue + level_lo;
+    const int64_t n_tickets = max<int64_t>(0, n_units - gridDim.x) + min<int64_t>(gridDim.x, n_units);
+    for (int64_t u = blockIdx.x; u < n_units;) {
+        unsigned tk = 0;
+        if (SC_DYN && threadIdx.x == 0) tk = atomicAdd(queue, 1u);
+        sc_one_unit(u, n_cell, n_run, n_dir4, ud, ud2, ur, n, cell_lo, run_lo, dir_lo, dir_mid, layout, par, sh,
+                    arena, wmax, fill, lmax_s, wid, lane, xyzs, dE, e_stride, nrm, Lt, grad, order);
+        if (SC_DYN) {
+            if (threadIdx.x == 0) {
+                qnext[qb] = tk;
+                if ((int64_t)tk == n_tickets - 1) atomicExch(queue, 0u);  // (the launch's last draw)
             }
-        } else if (mode == SC_MODE_RUN) {
-            const int64_t v = u - n_cell;
-            const int li = (int)(v / ur);
-            l = run_lo + li;
-            s0 = (v - li * ur) * (SC_THREADS * C_RUN);
-            s1 = min(n, s0 + SC_THREADS * C_RUN);
+            __syncthreads();
+            u = (int64_t)gridDim.x + qnext[qb];
+            qb ^= 1;
         } else {
-            int64_t v = u - n_cell - n_run;
-            if (v < n_dir4) {
-                const int li = (int)(v / ud);
-                l = dir_lo + li;
-                s0 = (v - li * ud) * (SC_THREADS * C_DIR);
-                s1 = min(n, s0 + SC_THREADS * C_DIR);
-            } else {
-                v -= n_dir4;
-                const int li = (int)(v / ud2);
-                l = dir_mid + li;
-                s0 = (v - li * ud2) * (SC_THREADS * 2);
-                s1 = min(n, s0 + SC_THREADS * 2);
-                rounds = 2;  // (marks the C = 2 form below)
-            }
+            u += gridDim.x;
         }
-        float m = lmax_s[l];
-#ifdef NCN_DIAG_SC_LEVELS_MASK
-        if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
-#endif
-        if (m == 0.f) continue;  // uniform: nothing to add on this level (no barrier, parity kept)
-        // the unit claims into fill[par]; fill[par ^ 1] (read by every lane before the previous
-        // unit's closing barrier) is reset here for the next unit
-        sh.fill = fill + par;
-        if (threadIdx.x == 0) fill[par ^ 1] = 0;
-        par ^= 1;
-        const float2* dEl = dE + (int64_t)l * e_stride;
-        if (mode == SC_MODE_CELL)
-            sc_cell_unit<C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
-        else if (mode == SC_MODE_RUN)
-            sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
-        else if (rounds == 2)
-            sc_unit<2, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
-        else
-            sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
     }
 }
 

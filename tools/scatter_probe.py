@@ -116,7 +116,12 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
             fw = lambda: L.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(ORDER[0]), ptr(table),  # noqa: E731
                                          model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed),
                                          I32(0), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
-            print(f"  {name:24s} field_fwd {ev_time(fw):7.1f} us", flush=True)
+            t_fw = ev_time(fw)
+            out = (sig.clone(), rgb.clone(), enc.clone())
+            if name == "main":
+                FWD_REF = out
+            same = all(torch.equal(a, b) for a, b in zip(out, FWD_REF))
+            print(f"  {name:24s} field_fwd {t_fw:7.1f} us  bit-identical to main: {same}", flush=True)
             continue
         t = timeit(L)
         coarse = timeit(L, lo=0, hi=10)
