@@ -1055,6 +1055,9 @@ __device__ __forceinline__ void sc_unpack(long long q, int& xs, int& ys) {
 #ifndef SC_C_DIR
 #define SC_C_DIR 4  // samples per lane on the direct levels (unit = one sort window)
 #endif
+#ifndef SC_DIR_DYN
+#define SC_DIR_DYN 2  // direct units of C = 4 in dynamic grabs of 64 x 2 (sc_unit): 2 = grab after the adds (191 us all levels vs 195 static); 1 = grab one ahead (194: 9 VGPRs spilled); 0 = static
+#endif
 #ifndef SC_DIR_HALF
 #define SC_DIR_HALF 15  // direct levels from here on: 2 samples per lane (units of 2048; 13: 198, 14: 202, 15: 190, none: 202 us)
 #endif
@@ -1074,6 +1077,7 @@ struct ScShared {
     int slots;
     float* wmax;
     int* fill;
+    int* grab;  // (SC_DIR_DYN) the unit's grab counter
 };
 enum { SC_MODE_DIR = 0, SC_MODE_RUN = 1, SC_MODE_CELL = 2 };
 __device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fill, int mode) {
@@ -1679,7 +1683,8 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     // chunk of lane t of wave w: t * SC_WAVES + w — the 64 lanes of one wave-instruction hold chunks
     // SC_WAVES * C positions apart, so in the Morton processing order (where neighbouring positions
     // share cells) they rarely address the same LDS slot at once (same-address LDS atomics serialise)
-    sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, nrm, order);
+    constexpr bool DYN = SC_DIR_DYN && !RUNS && C == 4;
+    if (!DYN) sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, nrm, order);
     ScLevel L;
     L.scale = Lt.scale[l];
     L.res = Lt.res[l];
@@ -1701,7 +1706,38 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
         sc_phase_a<C>(sh, wid, lane, ch, L, grad, staged);
         if (staged) sc_phase_b(sh, wid, lane, staged, L, grad);
     } else {
-        sc_direct<C>(sh, lane, ch, L, grad);
+        if constexpr (DYN) {
+            // The unit's samples in grabs of 64 lanes x 2: grab k gives lane t the samples
+            // s0 + (t * NG + k) * 2 (lanes NG * 2 = 64 positions apart, as the static mapping).
+            // Wave w takes grab w, then draws grabs from the unit's LDS counter one grab ahead
+            // (its chunk loads overlap the current grab), so a wave slowed by claims / set-full
+            // fallbacks takes fewer grabs and the waves reach the unit's barrier together.
+            constexpr int NG = SC_THREADS * C / 128;
+            int k = wid;
+            ScChunk<2> cg;
+            sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, nrm, order);
+            while (k < NG) {  // (wave-uniform)
+                if constexpr (SC_DIR_DYN == 2) {  // (variant) no prefetch: grab after the grab's adds
+                    sc_direct<2>(sh, lane, cg, L, grad);
+                    int kn = 0;
+                    if (lane == 0) kn = atomicAdd(sh.grab, 1);
+                    kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
+                    if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, nrm, order);
+                    k = kn;
+                } else {
+                    int kn = 0;
+                    if (lane == 0) kn = atomicAdd(sh.grab, 1);
+                    kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
+                    ScChunk<2> nx;
+                    if (kn < NG) sc_load_chunk<2>(nx, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, nrm, order);
+                    sc_direct<2>(sh, lane, cg, L, grad);
+                    if (kn < NG) cg = nx;
+                    k = kn;
+                }
+            }
+        } else {
+            sc_direct<C>(sh, lane, ch, L, grad);
+        }
     }
     SC_TNOW(t2);
 #ifdef NCN_DIAG_SC_TIMES
@@ -1825,7 +1861,7 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
         const int nv = mode == SC_MODE_CELL ? SC_CELL_VALS * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
         for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
         for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
-        if (threadIdx.x == 0) fill[0] = fill[1] = 0;
+        if (threadIdx.x == 0) fill[0] = fill[1] = fill[2] = fill[3] = 0;
         lds_barrier();
         layout = mode;
         par = 0;
@@ -1876,7 +1912,8 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
     // the unit claims into fill[par]; fill[par ^ 1] (read by every lane before the previous
     // unit's closing barrier) is reset here for the next unit
     sh.fill = fill + par;
-    if (threadIdx.x == 0) fill[par ^ 1] = 0;
+    sh.grab = fill + 2 + par;  // (the grab counters behind the claim counts, alternating alike)
+    if (threadIdx.x == 0) { fill[par ^ 1] = 0; fill[2 + (par ^ 1)] = 0; }
     par ^= 1;
     const float2* dEl = dE + (int64_t)l * e_stride;
     if (mode == SC_MODE_CELL)
@@ -1902,7 +1939,7 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
                                                                    float* __restrict__ gw = nullptr) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
     __shared__ float wmax[SC_WAVES];
-    __shared__ int fill[2];  // claimed-slot counts, alternating per unit (reset one unit ahead)
+    __shared__ int fill[4];  // claimed-slot counts [0, 2) and grab counters [2, 4), alternating per unit (reset one unit ahead)
     // per-level max |dE| over the MLP pass's workgroup rows (the fixed-point scale of each level);
     // visible to every thread at the first layout barrier
     __shared__ float lmax_s[16];
