@@ -148,6 +148,9 @@ __global__ void pack_weights_kernel(const float* __restrict__ W, T* __restrict__
 }
 
 // ---- hash grid ----
+#ifndef NCN_ENC_LEVEL_MAJOR
+#define NCN_ENC_LEVEL_MAJOR 1  // density pass scratch level-major (encode_xcd_kernel / field_fwd mode 2)
+#endif
 struct LevelTable {
     float scale[16];
     uint32_t res[16], params[16], offset[16];
@@ -384,6 +387,7 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
     typedef typename Mfma<T>::v8 v8;
     __shared__ v8 Fs[N_FWD32 * 64];
     __shared__ LevelTable L;
+    const int64_t n16 = (n + 15) & ~(int64_t)15;  // (mode 2, level-major scratch) per-level stride
     if (n_dev) n = min<int64_t>(n, *n_dev);  // device-resident count (static-capacity buffers)
     for (int i = threadIdx.x; i < N_FWD32 * 64; i += 256) Fs[i] = wpacked[i];
     load_levels(L, Lt);
@@ -403,7 +407,15 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
         const int64_t s = valid && order ? (int64_t)order[pos] : pos;
         v8 e;
         if (mode == 2) {  // (uniform) the encodings of encode_xcd_kernel (density only)
+#if NCN_ENC_LEVEL_MAJOR
+            typedef T t2 __attribute__((ext_vector_type(2)));
+            const t2* el = (const t2*)enc_cache + pos;  // levels 2g, 2g+1 | 8+2g, 9+2g of sample pos
+            const t2 a0 = el[(2 * g) * n16], a1 = el[(2 * g + 1) * n16];
+            const t2 b0 = el[(8 + 2 * g) * n16], b1 = el[(9 + 2 * g) * n16];
+            e = v8{a0[0], a0[1], a1[0], a1[1], b0[0], b0[1], b1[0], b1[1]};
+#else
             e = enc_cache[grp * 64 + lane];
+#endif
         } else {
             float x = 0.f, y = 0.f, z = 0.f;
             if (valid) {
@@ -442,9 +454,10 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
 // placement hint, nothing depends on it) and XCD x encodes levels x and x + 8 of every point, so each
 // 4 MB L2 holds at most two levels' tables instead of serving all 16 (45.8 MB) from the Infinity
 // Cache (the sample-major forward on Morton-ordered grid points: 436 us; with every hashed level
-// reading one table: 206 us — tools/field_probe.py).  Output: the forward's enc_cache layout (lane
-// (g, r) of a 16-point group holds levels {2g, 2g+1 | 8+2g, 9+2g} of point r), each level's pair of
-// T values written by its own block; field_fwd_kernel mode 2 then runs sigma_net from it.  Same
+// reading one table: 206 us — tools/field_probe.py).  Output: a level-major scratch [16][n16] of T
+// pairs (NCN_ENC_LEVEL_MAJOR; 172 vs 179 us for the pass with the forward's fragment-order layout,
+// tools/density_probe.py), each level's pairs written by its own block; field_fwd_kernel mode 2
+// gathers lane (g, r)'s levels {2g, 2g+1 | 8+2g, 9+2g} from it and runs sigma_net.  Same
 // encode_level and operand rounding as the sample-major forward: bit-identical sigmas.
 template <typename T>
 __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict__ xyzs, int64_t n,
@@ -455,6 +468,7 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
     __shared__ LevelTable L;
     load_levels(L, Lt);
     __syncthreads();
+    const int64_t n16 = (n + 15) & ~(int64_t)15;  // per-level stride of the level-major scratch
     if (n_dev) n = min<int64_t>(n, *n_dev);
     const int x8 = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int l = j < nb ? x8 : x8 + 8, blk = j < nb ? j : j - nb;
@@ -464,10 +478,17 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
     const float y = (xyzs[3 * s + 1] - xyz_min) / xyz_extent;
     const float z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
     const float2 a = encode_level(table, L, l, x, y, z);
+    typedef T t2 __attribute__((ext_vector_type(2)));
+#if NCN_ENC_LEVEL_MAJOR
+    // level-major scratch [16][n16] of T pairs: a workgroup's 256 points of one level are one
+    // contiguous 1 KB store (the fragment-order layout below scattered 4-byte pieces of 64-byte
+    // records over 16 workgroups on 8 XCDs)
+    ((t2*)enc)[(int64_t)l * n16 + s] = t2{(T)a.x, (T)a.y};
+#else
     const int g = (l & 7) >> 1, half = l >> 3, sub = l & 1;
     const int lane = g * 16 + (int)(s & 15);
-    typedef T t2 __attribute__((ext_vector_type(2)));
     *(t2*)(enc + ((s >> 4) * 64 + lane) * 8 + half * 4 + sub * 2) = t2{(T)a.x, (T)a.y};
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
