@@ -375,8 +375,20 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_windows_kernel(const float*
 
 // ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
+// Waves per SIMD the field forward is compiled for (0: the compiler's choice, 128 VGPRs + 8 AGPRs
+// = 3 waves/SIMD).  Measured (tools/scatter_probe.py, same box): 4 (116 VGPRs, no spill) 101.1 us,
+// default 101.5, 5 (17 VGPRs spilled) 124.6, 6 (34 spilled) 147.7 — more waves in flight do not
+// speed the gathers up, so the default stays.
+#ifndef NCN_FWD_WPE
+#define NCN_FWD_WPE 0
+#endif
+#if NCN_FWD_WPE > 0
+#define NCN_FWD_ATTR __attribute__((amdgpu_waves_per_eu(NCN_FWD_WPE)))
+#else
+#define NCN_FWD_ATTR
+#endif
 template <typename T>
-__global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
+__global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                         int64_t n, const int32_t* __restrict__ n_dev,
                                                         const float2* __restrict__ table, LevelTable Lt,
                                                         float xyz_min, float xyz_extent,
