@@ -93,8 +93,8 @@ def test_padded_rgb_input_is_a_bias(dev):
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-def test_field_backward(dev, precision):
-    n = 3000
+@pytest.mark.parametrize("n", [3000, 4097, 12289])  # (scatter units of 4096 / 2048: partial last units, dynamic grabs)
+def test_field_backward(dev, precision, n):
     P, levels = field_ref.init_params(seed=5, table_init=0.5)
     m = _model_from_oracle(P, dev, precision)
     x, d = _inputs(n, 2)
