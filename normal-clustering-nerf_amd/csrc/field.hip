@@ -387,7 +387,10 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_windows_kernel(const float*
 #else
 #define NCN_FWD_ATTR
 #endif
-template <typename T>
+// DENSITY: the grid refresh's mode 2 (encodings from encode_xcd_kernel's scratch, sigma only) as its
+// own instantiation — the training forward's loop then carries no trace of it (with the scratch read
+// inside the shared loop the training kernel took 136 registers, 3 waves/SIMD, and ran ~10 % slower).
+template <typename T, bool DENSITY>
 __global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                         int64_t n, const int32_t* __restrict__ n_dev,
                                                         const float2* __restrict__ table, LevelTable Lt,
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float
         const bool valid = pos < n;
         const int64_t s = valid && order ? (int64_t)order[pos] : pos;
         v8 e;
-        if (mode == 2) {  // (uniform) the encodings of encode_xcd_kernel (density only)
+        if constexpr (DENSITY) {  // the encodings of encode_xcd_kernel (mode 2: density only)
 #if NCN_ENC_LEVEL_MAJOR
             typedef T t2 __attribute__((ext_vector_type(2)));
             const t2* el = (const t2*)enc_cache + pos;  // levels 2g, 2g+1 | 8+2g, 9+2g of sample pos
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float
         FwdState<T> st;
         mlp_sigma<T>(F, lane, e, st);
         if (g == 0 && valid) sigmas[s] = __expf(st.h[0]);  // TruncExp forward = exp
-        if (mode != 0) continue;
+        if (DENSITY || mode != 0) continue;
         float dx = 0.f, dy = 0.f, dz = 0.f;
         if (valid) {
             dx = dirs[3 * s]; dy = dirs[3 * s + 1]; dz = dirs[3 * s + 2];
@@ -2153,12 +2156,14 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
         NCN_LAUNCH_CHECK("ncn_field_fwd (encode)");
     }
     if (precision == NCN_PREC_F16)
-        hipLaunchKernelGGL(field_fwd_kernel<_Float16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
+        hipLaunchKernelGGL((mode == 2 ? field_fwd_kernel<_Float16, true> : field_fwd_kernel<_Float16, false>),
+                           dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
                            n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,
                            (const Mfma<_Float16>::v8*)weights_packed, mode, sigmas, rgbs,
                            (Mfma<_Float16>::v8*)enc_cache, order);
     else
-        hipLaunchKernelGGL(field_fwd_kernel<__bf16>, dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
+        hipLaunchKernelGGL((mode == 2 ? field_fwd_kernel<__bf16, true> : field_fwd_kernel<__bf16, false>),
+                           dim3(fwd_grid(n)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
                            n, n_dev, (const float2*)table, Lt, xyz_min, xyz_extent,
                            (const Mfma<__bf16>::v8*)weights_packed, mode, sigmas, rgbs, (Mfma<__bf16>::v8*)enc_cache,
                            order);
