@@ -190,8 +190,19 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
         }
     }
 }
+// Waves per SIMD adam_apply is compiled for (0: the compiler's choice, 83 VGPRs = 5 waves/SIMD).
+// Measured (tools/adam_probe.py, prep + apply over 11.45 M parameters): default 74.2 / 72.9 us,
+// 6 waves 72.7 / 73.1, 8 waves 75.0 / 75.7 — HBM-bound, so the default stays.
+#ifndef NCN_ADAM_WPE
+#define NCN_ADAM_WPE 0
+#endif
+#if NCN_ADAM_WPE > 0
+#define NCN_ADAM_ATTR __attribute__((amdgpu_waves_per_eu(NCN_ADAM_WPE)))
+#else
+#define NCN_ADAM_ATTR
+#endif
 template <bool ZERO>
-__global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, float* __restrict__ g,
+__global__ __launch_bounds__(256) NCN_ADAM_ATTR void adam_apply_kernel(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                          int64_t n0, float b1, float b2, float eps, float wd0,
                                                          float wd1, const float* __restrict__ sc) {
