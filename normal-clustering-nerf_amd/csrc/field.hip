@@ -375,10 +375,10 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_windows_kernel(const float*
 
 // ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
-// Waves per SIMD the field forward is compiled for (0: the compiler's choice, 128 VGPRs + 8 AGPRs
-// = 3 waves/SIMD).  Measured (tools/scatter_probe.py, same box): 4 (116 VGPRs, no spill) 101.1 us,
-// default 101.5, 5 (17 VGPRs spilled) 124.6, 6 (34 spilled) 147.7 — more waves in flight do not
-// speed the gathers up, so the default stays.
+// Waves per SIMD the field forward is compiled for (0: the compiler's choice — the training
+// instantiation takes 120 VGPRs + 8 AGPRs, 4 waves/SIMD).  Measured on a build whose training loop
+// still carried the density read (128 + 8, 3 waves/SIMD; tools/scatter_probe.py, same box): 4 waves
+// 101.1 us, default 101.5, 5 (17 VGPRs spilled) 124.6, 6 (34 spilled) 147.7 — not occupancy-bound.
 #ifndef NCN_FWD_WPE
 #define NCN_FWD_WPE 0
 #endif
