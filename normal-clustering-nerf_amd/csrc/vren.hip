@@ -1416,8 +1416,18 @@ __device__ __forceinline__ void composite_bw_coop(
     }
 }
 
+// Waves per SIMD composite_bw_kernel_nodws is compiled for (0: the compiler's choice, 80 VGPRs at
+// C = 3 = 6 waves/SIMD: the 8192-ray launch's ~9 K waves then need two rounds of residency).
+#ifndef NCN_CBW_WPE
+#define NCN_CBW_WPE 0
+#endif
+#if NCN_CBW_WPE > 0
+#define NCN_CBW_ATTR __attribute__((amdgpu_waves_per_eu(NCN_CBW_WPE)))
+#else
+#define NCN_CBW_ATTR
+#endif
 template <int C>
-__global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_nodws(
+__global__ __launch_bounds__(64 * CF_WPB) NCN_CBW_ATTR void composite_bw_kernel_nodws(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
