@@ -1417,7 +1417,8 @@ __device__ __forceinline__ void composite_bw_coop(
 }
 
 // Waves per SIMD composite_bw_kernel_nodws is compiled for (0: the compiler's choice, 80 VGPRs at
-// C = 3 = 6 waves/SIMD: the 8192-ray launch's ~9 K waves then need two rounds of residency).
+// C = 3 = 6 waves/SIMD).  Measured (tools/composite_bw_probe.py, 8192 marched rays): default 9.6 us,
+// 7 waves (2 VGPRs spilled) 9.9-10.0, 8 waves (6 spilled) 10.3-10.5 — the default stays.
 #ifndef NCN_CBW_WPE
 #define NCN_CBW_WPE 0
 #endif
