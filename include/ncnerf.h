@@ -225,6 +225,10 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
  * dh_stash (ncn_field_bwd_stash_floats(n) floats, 16-byte aligned: the MLP-operand-rounded values
  * the sigma pass consumes, plus the fp32 element the TruncExp term is added to — 36 B per sample);
  * it also zeroes level_max.
+ * ORDERING: part 2 reads the stash and max-reduces (atomicMax) into the level_max rows part 1
+ * zeroed, so part 2 must be stream-ordered after a COMPLETED part 1 on the same stash and level_max
+ * (when part 1 runs on another stream, join that stream first, e.g. cur.wait_stream(side)); part 2
+ * on its own would read a stale stash and the previous step's maxima.
  * Part 2 (sigma) = dL/dh = stash + TruncExp'(h0) * (dL_dsigmas + dL_dsigmas2) (either may be
  * NULL), then sigma_net: slab tiles of W1, W2 (rows [0, its grid)), dE_ws, level_max (max-reduced
  * into the 16 * ncn_field_bwd_blocks(n) floats the scatter reads).  Part 3 = ncn_field_bwd_mlp
@@ -318,8 +322,11 @@ int ncn_kmeans_plan_fill(int n_tri, int K, uint32_t seed, uint32_t* host_out);
  *   one workspace per stream (two concurrent calls must not share one). */
 int64_t ncn_cluster_workspace_words(int K);
 /* Index (in 32-bit words) of the workspace's sticky error word: non-zero once a grid barrier or a
- * Lloyd hand-off of any call on this workspace timed out (its results are then wrong).  The
- * caller reads it outside the hot loop (the training step: every few steps) and fails. */
+ * Lloyd hand-off of any call on this workspace timed out (its partial sums may be incomplete).
+ * While it is set, every call drops its cluster terms as the reference's validity filter drops an
+ * invalid term (losses.py:246-262): out_losses[0..2] and [4..6] are 0, dn is 0, out_losses[10] is
+ * the photometric part only — so no gradient of a timed-out clustering is ever applied.  The
+ * caller reads the word outside the hot loop (the training step: every few steps) and fails. */
 int64_t ncn_cluster_status_offset(int K);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, const uint32_t* kmeans_plan,
                      float t_similar,
@@ -379,12 +386,16 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 #define NCN_AMP_GROWTH_INTERVAL 2000
 int64_t ncn_adam_step_work_floats(void);
 /* Data-parallel gradient wire format (replaces DDP's fp16 gradient buckets, train_nerf.py:944-952:
- * the reference's tcnn parameters and gradients are fp16 at the GradScaler's scale).
- * pack: wire[i] = fp16(grad[i] * scale[0]) (round to nearest even; overflow -> inf, a step the
- * GradScaler of ncn_adam_step then skips); unpack: grad[i] = float(wire[i]) / scale[0] (overwrites).
- * scale: NULL (1) or a device float, the AMP scale S (amp_state[0], a power of two).  n elements,
- * grad and wire 16-byte aligned. */
-int ncn_grad_pack_f16(const float* grad, int64_t n, const float* scale, uint16_t* wire, void* stream);
+ * the reference's tcnn parameters and gradients are fp16 at the GradScaler's scale, and torch DDP's
+ * default hook divides each bucket by the world size before the all-reduce SUM,
+ * ddp_comm_hooks/default_hooks.py _allreduce_fut).
+ * pack: wire[i] = fp16(float(fp16(grad[i] * scale[0])) / world) — the bucket's rounding, then DDP's
+ * div_(world) rounding (round to nearest even; overflow -> inf, a step the GradScaler of
+ * ncn_adam_step then skips); unpack: grad[i] = float(wire[i]) / scale[0] (overwrites): after the
+ * SUM this is already the average over the ranks.
+ * scale: NULL (1) or a device float, the AMP scale S (amp_state[0], a power of two).  world >= 1.
+ * n elements, grad and wire 16-byte aligned. */
+int ncn_grad_pack_f16(const float* grad, int64_t n, const float* scale, int world, uint16_t* wire, void* stream);
 int ncn_grad_unpack_f16(const uint16_t* wire, int64_t n, const float* scale, float* grad, void* stream);
 
 #ifdef __cplusplus

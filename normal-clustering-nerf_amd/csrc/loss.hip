@@ -350,8 +350,9 @@ __device__ __forceinline__ void st_c(long long* p, long long v) {
 }
 // Grid barrier number `phase` (1, 2, ...) over the KM_BLOCKS co-resident workgroups.  The spin is
 // bounded: a barrier that does not complete within ~2^22 polls sets the error word (sync[2],
-// sticky; ncn_cluster_status_offset) and lets the workgroup run on (wrong numbers, never a hang);
-// the training step reads the word every few steps and raises (losses.check_cluster_status).
+// sticky; ncn_cluster_status_offset) and lets the workgroup run on (never a hang); the launch then
+// drops its cluster terms (zero losses and gradients, the grad stage below), and the training step
+// reads the word every few steps and raises (losses.check_cluster_status).
 // NCN_KM_SPIN_LIMIT / NCN_KM_POLL_LIMIT: diagnostic builds force the flag with a limit of 1.
 #ifndef NCN_KM_SPIN_LIMIT
 #define NCN_KM_SPIN_LIMIT (1u << 22)
@@ -676,6 +677,7 @@ struct ClusterLds {
     float pickv[K][3];  // the init picks' normals (register-resident compaction)
     unsigned char pmem[KM_CHUNK_MAX];  // training-set membership of the chunk's points (faiss subsampling)
     int total;
+    int timed_out;  // the sticky error word, read once after the last grid barrier
     KmUpdLds<K> upd;
     SelLds<K> sel;
     ClStats S;
@@ -974,7 +976,16 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
         w_dot = fmaxf(0.f, fminf(w_dot, ds * (w_dot / sched_grow)));
         w_l1 = fmaxf(0.f, fminf(w_l1, ds * (w_l1 / sched_grow)));
     }
-    const bool ok = clustered && L.S.ok;
+    // A barrier / hand-off timeout (this launch's or an earlier one's: the word is sticky until the
+    // host clears it) means the partial sums may be incomplete.  The cluster terms are then dropped
+    // as the reference's validity filter drops an invalid term (losses.py:246-262): losses 0, no
+    // gradient, so no corrupt gradient is ever applied while the host's periodic status read
+    // (losses.check_cluster_status) is pending.  Read after the last grid barrier: every flag store
+    // is drained (vmcnt(0)) by the storing wave before its workgroup's next arrival, so a workgroup
+    // whose data depends on a timed-out one sees the word.
+    if (tid == 0) L.timed_out = (int)__hip_atomic_load(&ws.sync[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool ok = clustered && L.S.ok && L.timed_out == 0;
     if (blockIdx.x == 0 && tid < K * 3) out_centroids[tid] = clustered ? (&L.C[0][0])[tid] : 0.f;
     if (tid == 0) {
         float ort = 0.f, cdot = 0.f, cl1 = 0.f;

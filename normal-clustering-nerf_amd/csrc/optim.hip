@@ -270,24 +270,29 @@ __global__ __launch_bounds__(256) void step_inputs_kernel(StepCopies c, int nb, 
 
 // DDP gradient wire format (the data-parallel step's all-reduce): the reference's gradients are
 // tcnn's fp16 parameter gradients at the GradScaler's scale S (tcnn modules keep fp16 params, and PL
-// precision=16 scales the loss; train_nerf.py:944-955), so DDP all-reduces fp16 values S * g.  Here
-// the gradient is kept unscaled in fp32; pack writes fp16(S * g) (round to nearest even, overflow ->
-// inf, which the GradScaler step then skips), unpack writes float(w) / S back.  S is a power of two,
-// so only the fp16 rounding of S * g is lossy — the reference's own rounding.  8 elements per thread
-// (two float4 loads, one 16-B store), a scalar tail.
+// precision=16 scales the loss; train_nerf.py:944-955), and torch DDP's default communication hook
+// divides every bucket by the world size BEFORE the all-reduce SUM ("Apply the division first to
+// avoid overflow, especially for FP16": torch/distributed/algorithms/ddp_comm_hooks/default_hooks.py,
+// _allreduce_fut).  So the wire carries fp16(fp16(S * g) / world): pack performs both roundings as
+// DDP does (the bucket holds fp16(S * g); div_ rounds the quotient to fp16 again), the collective
+// sums, and unpack writes float(w) / S — the world's average, so the optimizer takes no 1/world.
+// Overflow -> inf, which the GradScaler step then skips on every rank alike, at the reference's
+// magnitudes (a per-rank value near the fp16 maximum no longer overflows the 8-way sum).  8 elements
+// per thread (two float4 loads, one 16-B store), a scalar tail.
 __global__ __launch_bounds__(256) void grad_pack_f16_kernel(const float* __restrict__ g, int64_t n,
-                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ scale, int world,
                                                             _Float16* __restrict__ w) {
-    const float s = scale ? *scale : 1.f;
+    const float s = scale ? *scale : 1.f, wf = (float)world;
+    // DDP's two roundings: the bucket's fp16(S g), then its in-place div_(world) (fp16 result)
+    auto wire = [&](float x) { return (_Float16)((float)(_Float16)(x * s) / wf); };
     const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * 256;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
         const float4 a = ((const float4*)g)[2 * i], b = ((const float4*)g)[2 * i + 1];
         typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-        const h8 o = {(_Float16)(a.x * s), (_Float16)(a.y * s), (_Float16)(a.z * s), (_Float16)(a.w * s),
-                      (_Float16)(b.x * s), (_Float16)(b.y * s), (_Float16)(b.z * s), (_Float16)(b.w * s)};
+        const h8 o = {wire(a.x), wire(a.y), wire(a.z), wire(a.w), wire(b.x), wire(b.y), wire(b.z), wire(b.w)};
         ((h8*)w)[i] = o;
     }
-    for (int64_t i = 8 * n8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) w[i] = (_Float16)(g[i] * s);
+    for (int64_t i = 8 * n8 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) w[i] = wire(g[i]);
 }
 __global__ __launch_bounds__(256) void grad_unpack_f16_kernel(const _Float16* __restrict__ w, int64_t n,
                                                               const float* __restrict__ scale, float* __restrict__ g) {
@@ -308,13 +313,14 @@ using namespace ncn;
 
 extern "C" {
 
-int ncn_grad_pack_f16(const float* grad, int64_t n, const float* scale, uint16_t* wire, void* stream) {
+int ncn_grad_pack_f16(const float* grad, int64_t n, const float* scale, int world, uint16_t* wire, void* stream) {
     if (n <= 0) return 0;
+    NCN_REQUIRE(world >= 1, hipErrorInvalidValue, "ncn_grad_pack_f16: world must be >= 1");
     NCN_REQUIRE(((((uintptr_t)grad) & 15) | (((uintptr_t)wire) & 15)) == 0, hipErrorInvalidValue,
                 "ncn_grad_pack_f16: grad and wire must be 16-byte aligned");
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 4096);
     hipLaunchKernelGGL(grad_pack_f16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, grad, n, scale,
-                       (_Float16*)wire);
+                       world, (_Float16*)wire);
     NCN_LAUNCH_CHECK("ncn_grad_pack_f16");
     return 0;
 }

@@ -23,7 +23,7 @@ U64 = ctypes.c_uint64
 
 # name -> argtypes (stream last); every function returns int (hipError_t)
 SIGNATURES = {
-    "ncn_grad_pack_f16": [P, I64, P, P, P],
+    "ncn_grad_pack_f16": [P, I64, P, I32, P, P],
     "ncn_grad_unpack_f16": [P, I64, P, P, P],
     "ncn_morton3D": [P, I64, P, P],
     "ncn_morton3D_invert": [P, I64, P, P],

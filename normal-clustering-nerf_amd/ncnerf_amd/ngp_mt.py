@@ -122,8 +122,14 @@ class NGPMT(nn.Module):
         return self.amp_state if self.amp_state is not None else self._amp_unit
 
     def _level_max(self):
-        """ncn_field_bwd's per-level max |dE| workspace: 16 floats per MLP-pass workgroup (<= 256)."""
+        """ncn_field_bwd's per-level max |dE| workspace: 16 floats per MLP-pass workgroup (<= 256).
+        The scatter reads it as each level's fixed-point scale, so with scatter_split set (a backward
+        whose coarse levels are scattered later, run_deferred_scatter) every backward gets its own:
+        a shared buffer would hand the earlier pending scatters the LAST backward's maxima
+        (overflowing 64-bit sums, or a level dropped when its maximum there is 0)."""
         dev = self._flat.device
+        if self.scatter_split is not None:
+            return torch.empty(16 * 256, dtype=torch.float32, device=dev)
         if getattr(self, "_lmax", None) is None or self._lmax.device != dev:
             self._lmax = torch.empty(16 * 256, dtype=torch.float32, device=dev)
         return self._lmax
@@ -198,8 +204,8 @@ class NGPMT(nn.Module):
         # Morton-window processing order (ncn_field_sort_windows) for training batches: off by default
         # (measured: forward 88 -> 72 us, but sort 40 us + MLP backward +6 us + scatter +9 us)
         self.sort_samples = False
-        self._deferred = []  # pending coarse-level scatters of the split data-parallel step
-        self._deferred_static = False  # True once a captured step owns the list (Trainer._capture)
+        self._deferred = []  # pending coarse-level scatters of the split data-parallel step (eager backwards)
+        self._deferred_graph = []  # the captured step's coarse-level scatters (Trainer._capture), every replay
 
     # -- flat buffers --------------------------------------------------------------------------
     def _apply(self, fn, recurse=True):
@@ -248,16 +254,19 @@ class NGPMT(nn.Module):
         cut = 2 * self.levels[split]["offset"]
         return fg[cut:], fg[:cut]
 
-    def run_deferred_scatter(self, max_blocks=0):
-        """Scatter of the levels [0, scatter_split) left by the last backward (same tensors; inside a
-        captured step they are the graph's static buffers, refilled by every replay)."""
-        if not self._deferred:
+    def run_deferred_scatter(self, max_blocks=0, graph=False):
+        """Scatter of the levels [0, scatter_split) left by the field backwards: graph=False — the
+        eager backwards since the last call (then cleared); graph=True — the captured step's entries
+        (Trainer._capture moves them to _deferred_graph: they name the graph's static buffers, refilled
+        by every replay, and are run after each replay)."""
+        entries = self._deferred_graph if graph else self._deferred
+        if not entries:
             raise RuntimeError("run_deferred_scatter: no deferred scatter (scatter_split unset or no backward yet)")
-        for x, n, n_dev, order, dE_ws, lmax, g_table in self._deferred:
+        for x, n, n_dev, order, dE_ws, lmax, g_table in entries:
             call("ncn_field_scatter", ptr(x), I64(n), ptr(n_dev), ptr(order), self._levels_ptr, F32(self._xyz_min),
                  F32(self._xyz_extent), ptr(dE_ws), ptr(lmax), I32(0), I32(self.scatter_split), I32(max_blocks),
                  ptr(g_table), stream())
-        if not self._deferred_static:  # (a captured step's entries name its static buffers: kept for every replay)
+        if not graph:
             self._deferred = []
 
     def prepare_weights(self):

@@ -78,9 +78,10 @@ class Trainer:
         # step first.  Parameters read between steps are one step behind until flush_optimizer() is
         # called.  N > 1: the gradient all-reduce of step k (eager, after graph k) is ordered before
         # graph k+1 on the same stream, so the deferred step reads the reduced gradient; DDP's
-        # 1/world goes in as the step's grad_scale.
+        # 1/world goes in as the step's grad_scale on the fp32 wire (the fp16 wire divides before
+        # the sum, as DDP does: grad_scale 1).
         self.defer = bool(defer_optimizer) and use_graph
-        self._grad_scale = 1.0 / self.world
+        self._grad_scale = distributed.grad_scale_after_reduce(model, self.world)
         self._pending = False
         self._rng_seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # marcher jitter stream (CPU generator)
         # optional seed of each grid refresh (global_step -> int); default: drawn from torch's CPU generator
@@ -176,8 +177,9 @@ class Trainer:
         with torch.cuda.graph(self.graph):
             self._out = self._body(self._static, self._step_dev, self._with_opt)
         # the captured backward's deferred scatter names the graph's static buffers: every replay's
-        # reduce_gradients runs that same entry
-        self.model._deferred_static = bool(self.model._deferred)
+        # reduce_gradients(graph=True) runs that same entry; eager backwards keep their own list
+        self.model._deferred_graph = self.model._deferred
+        self.model._deferred = []
         for t, v in zip(state, saved):
             t.copy_(v)
         self.opt.step_count = saved_count
@@ -204,7 +206,7 @@ class Trainer:
             if self.defer:
                 self.opt.gate.fill_(gate)
         self.graph.replay()
-        scale = distributed.reduce_gradients(self.model) if not self._with_opt else 1.0
+        scale = distributed.reduce_gradients(self.model, graph=True) if not self._with_opt else 1.0
         if self.defer:  # (the next graph's side stream applies it, after the reduction above)
             self.opt.step_count += gate
             self._pending = True

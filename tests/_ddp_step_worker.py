@@ -9,8 +9,10 @@ and rank 0 saves the parameters.
 `run_reference` — one process, the eager step: for every step the gradients of all ranks' batches
 are accumulated into the flat gradient (one backward per batch, no optimizer in between), then one
 Adam step with grad_scale = 1/world, i.e. DDP's average computed without any collective.  With the
-fp16 gradient wire (distributed.wire_of: the fp16 AMP model) the per-rank gradients are rounded to
-fp16(S g) and summed as the collective sums them."""
+fp16 gradient wire (distributed.wire_of: the fp16 AMP model) each rank's gradient is rounded as
+DDP's bucket holds it and divides it — fp16(fp16(S g) / world) — the ranks' values are summed in
+rank order with fp16 rounding (the collective's own order may differ: `wire_sum` below), / S, and
+Adam takes grad_scale 1."""
 import os
 import sys
 
@@ -73,7 +75,24 @@ def run(steps, device, out=None, rank=0, defer=False, world=1, split=False):
     return flat
 
 
+def wire_value(g, S, world):
+    """One rank's fp16 wire value: DDP's bucket fp16(S g), divided in place by the world (fp16)."""
+    return ((g * S).half().float() / world).half()
+
+
+def wire_sum(per_rank, S, world):
+    """The fp16 wire's all-reduce SUM in rank order with fp16 rounding of every partial sum (float)."""
+    tot = wire_value(per_rank[0], S, world)
+    for g in per_rank[1:]:
+        tot = (tot.float() + wire_value(g, S, world).float()).half()
+    return tot.float()
+
+
+AMBIGUOUS = [None]  # run_reference, fp16 wire: union over the steps of the order-ambiguous entries
+
+
 def run_reference(steps, device, world):
+    AMBIGUOUS[0] = None
     from ncnerf_amd.rendering import render
     from ncnerf_amd.trainer import Trainer
     scene, model = _setup(device)
@@ -92,14 +111,16 @@ def run_reference(steps, device, world):
             if fp16_wire:  # each rank's gradient on its own (the wire rounds them separately)
                 per_rank.append(model.flat_grad().clone())
                 model.flat_grad().zero_()
-        if fp16_wire:  # the fp16 wire: fp16(S g_r) per rank, summed in rank order with fp16 rounding, / S
+        if fp16_wire:
             S = float(model.amp_state[0])
-            tot = (per_rank[0] * S).half()
-            for g in per_rank[1:]:
-                tot = (tot.float() + (g * S).half().float()).half()
-            tot = tot.float() / S
-            model.flat_grad().copy_(tot)
-        tr.opt.step(grad_scale=1.0 / world)
+            model.flat_grad().copy_(wire_sum(per_rank, S, world) / S)
+            # entries whose reduced sum may round to another side of zero (or to zero) in another
+            # summation order: |exact sum| within the order-independent bound of an fp16 sum
+            h = torch.stack([wire_value(g, S, world).double() for g in per_rank])
+            bound = (world - 1) * (2.0 ** -11 * h.abs().sum(0) + 2.0 ** -25)
+            amb = ((h.sum(0).abs() <= bound) & (h != 0).any(0)).cpu()  # (all-zero terms: exactly 0 in any order)
+            AMBIGUOUS[0] = amb if AMBIGUOUS[0] is None else (AMBIGUOUS[0] | amb)
+        tr.opt.step(grad_scale=distributed.grad_scale_after_reduce(model, world))
     torch.cuda.synchronize()
     return model.flat_params().detach().cpu().clone()
 

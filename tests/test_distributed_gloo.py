@@ -41,9 +41,13 @@ class _SplitModel:
         cut = 2 * split  # (2 floats per level in this stand-in)
         return self.g[cut:], self.g[:cut]
 
-    def run_deferred_scatter(self, max_blocks=0):
+    def run_deferred_scatter(self, max_blocks=0, graph=False):
         self.calls.append(max_blocks)
         self.g[: 2 * self.scatter_split] += 1000.0
+
+
+class _AmpStandIn:
+    amp_state = object()
 
 
 def _worker(rank, world, port, q):
@@ -58,6 +62,9 @@ def _worker(rank, world, port, q):
     assert scale == 0.5 and g2.tolist() == [3.0] * 4
     sm = _SplitModel(rank)
     assert distributed.reduce_gradients(sm) == 0.5
+    # DDP's average: the fp16 wire (an AMP model) divides before the sum, the fp32 wire after it
+    assert distributed.grad_scale_after_reduce(_AmpStandIn()) == 1.0
+    assert distributed.grad_scale_after_reduce(sm) == 0.5
     assert sm.calls == [distributed.DP_SCATTER_BLOCKS]
     base = torch.arange(12, dtype=torch.float32) * 2 + 100  # sum over ranks 0, 1 of arange + 100 r
     want_split = base.clone()

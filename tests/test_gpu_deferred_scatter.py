@@ -1,7 +1,9 @@
 """The split data-parallel backward (NGPMT.scatter_split): the table levels [0, split) of every
 field backward are left for run_deferred_scatter (distributed.reduce_gradients runs it while the
 first bucket's all-reduce is in flight).  A step with TWO field backwards must scatter both — the
-pending scatters are a list, not one slot that the second backward overwrites."""
+pending scatters are a list, not one slot that the second backward overwrites — and each pending
+scatter keeps its own per-level maxima (the fixed-point scale of its sums): a later backward with a
+much smaller, or zero, upstream gradient must not rescale or drop an earlier one's."""
 import pytest
 import torch
 
@@ -16,7 +18,8 @@ def _loss(m, x, d, x2, w):
     return (out["sigmas"] * w[0]).sum() + (out["rgbs"] * w[1]).sum() + (s2 * w[2]).sum()
 
 
-def test_two_backwards_both_deferred_scatters_run(dev):
+@pytest.mark.parametrize("later", [1.0, 1e-3, 0.0])
+def test_two_backwards_both_deferred_scatters_run(dev, later):
     g = torch.Generator(device=dev).manual_seed(3)
     n = 5000
     x = (torch.rand(n, 3, device=dev, generator=g) - 0.5) * 0.98
@@ -34,7 +37,7 @@ def test_two_backwards_both_deferred_scatters_run(dev):
         m.scatter_split = split
         # two separate backwards in one step (e.g. a density() term and the render's forward())
         _loss(m, x, d, x2, w).backward()
-        (m(x2, d)["rgbs"] * w[1]).sum().backward()
+        (m(x2, d)["rgbs"] * (w[1] * later)).sum().backward()
         if split is not None:
             assert len(m._deferred) == 3  # three field backwards, three pending coarse-level scatters
             m.run_deferred_scatter()
@@ -42,6 +45,7 @@ def test_two_backwards_both_deferred_scatters_run(dev):
         torch.cuda.synchronize()
         grads.append(m.flat_grad().clone())
     ref, got = grads
+    assert torch.isfinite(got).all()
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 1e-6, rel
     assert int(((got == 0) != (ref == 0)).sum()) == 0

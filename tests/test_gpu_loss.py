@@ -247,3 +247,81 @@ def test_cluster_status_word(dev):
         L.check_cluster_status(dev)
     ws.view(torch.int32)[off] = 0
     L.check_cluster_status(dev)
+
+
+_DROP_CHILD = r"""
+import os, sys
+sys.path[:0] = [os.path.join(sys.argv[1], "normal-clustering-nerf_amd"), sys.argv[1]]
+import torch
+from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
+from ncnerf_amd.synthetic import SyntheticScene
+from ncnerf_amd.rendering import render
+from ncnerf_amd.trainer import Trainer
+from ncnerf_amd import losses as L, _lib
+dev = torch.device("cuda", 0)
+scene = SyntheticScene()
+torch.manual_seed(0)
+model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+with torch.no_grad():  # a non-trivial field so that the depth (and the normals) carry gradient
+    model.flat_params()[: model._n_table].uniform_(-0.5, 0.5, generator=torch.Generator(device=dev).manual_seed(5))
+batch = scene.torch_batch(2048, seed=11, device=dev)
+noise = torch.rand(2048, generator=torch.Generator().manual_seed(12)).to(dev)
+tr = Trainer(model, use_graph=False)
+out = {}
+for step in [int(s) for s in sys.argv[3].split(",")]:
+    model.flat_grad().zero_()
+    kw = dict(tr.render_kwargs, global_step=step, march_noise=noise)
+    res = render(model, batch["rays_o"], batch["rays_d"], **kw)
+    loss_d = tr.loss(res, batch, global_step=step)
+    loss_d["total"].backward()
+    torch.cuda.synchronize()
+    out[step] = {"grad": model.flat_grad().cpu().clone(),
+                 "losses": {k: float(v) for k, v in loss_d.items() if torch.is_tensor(v) and v.numel() == 1}}
+try:
+    L.check_cluster_status()
+    out["status"] = 0
+except _lib.NcnError:
+    out["status"] = 1
+torch.save(out, sys.argv[2])
+"""
+
+
+def test_cluster_timeout_drops_cluster_terms(dev, tmp_path):
+    """A clustering launch whose grid barrier / hand-off timed out must not train on its partial
+    sums: the kernel drops the cluster terms (losses 0, no normal gradient) as the reference's
+    validity filter drops an invalid term (losses.py:246-262).  The diagnostic library (spin limits
+    1: every barrier times out) at a step past the weight ramp (3000) must give the gradient of the
+    photometric terms alone — the product library's gradient at step 400, where the ramp holds the
+    cluster weights at 0 (losses.py:217) — while the product library's own gradient at step 3000
+    differs from that (the cluster terms do contribute there)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    diag = os.path.join(root, "normal-clustering-nerf_amd", "ncnerf_amd", "libncnerf_diag_kmspin.so")
+    assert os.path.exists(diag), "build the diagnostic library (make -C normal-clustering-nerf_amd)"
+    runs = {}
+    for name, lib, steps in (("prod", None, "400,3000"), ("diag", diag, "3000")):
+        o = str(tmp_path / f"{name}.pt")
+        env = dict(os.environ)
+        if lib:
+            env["NCN_LIB_PATH"] = lib
+        r = subprocess.run([sys.executable, "-c", _DROP_CHILD, root, o, steps], env=env, capture_output=True,
+                           text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        runs[name] = torch.load(o, weights_only=True)
+    prod, diag_r = runs["prod"], runs["diag"]
+    assert prod["status"] == 0 and diag_r["status"] == 1
+    photo, full, dropped = prod[400]["grad"], prod[3000]["grad"], diag_r[3000]["grad"]
+    lo = diag_r[3000]["losses"]
+    for k in ("norm_D_C_ort_dot", "norm_D_C_centr_dot", "norm_D_C_centr_L1"):
+        assert lo[k] == 0.0, (k, lo[k])
+    assert lo["total"] == float(np.float32(lo["rgb"]) + np.float32(lo["opacity"]))  # (the kernel's f32 sum)
+    assert prod[3000]["losses"]["norm_D_C_centr_L1"] > 0
+    assert torch.isfinite(dropped).all()
+    rel = lambda a, b: float((a - b).norm() / b.norm())
+    print(f"timed-out step vs photometric-only gradient: rel-L2 {rel(dropped, photo):.2e}; "
+          f"full step vs photometric-only: {rel(full, photo):.2e}")
+    assert rel(dropped, photo) < 1e-5
+    assert rel(full, photo) > 1e-3
