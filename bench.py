@@ -89,7 +89,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
-TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
+TIMED = ("ncn_composite_train_fw_sm", "ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
          "ncn_field_bwd", "ncn_field_bwd_mlp_part", "ncn_field_scatter", "ncn_cluster_loss")
 
 
@@ -106,37 +106,52 @@ def pmc_traffic():
 
 def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
     """Live HIP-event measurement of the roofline kernel, the training step's compositor
-    (ncn_composite_train_fw_bg over the fused marcher's rays_a, long rays first).  `n_sets` input
-    sets (the bench batches marched with different jitter and run through the field as in the step,
-    ~16.5 MB each: n_sets x that > the 256 MiB Infinity Cache) are prepared; then
+    (ncn_composite_train_fw_bg over the fused marcher's rays_a, long rays first; the sample-major
+    ncn_composite_train_fw_sm timed beside it on the same sets).  `n_sets` input sets (the bench
+    batches marched with different jitter and run through the field as in the step, ~16.5 MB each:
+    n_sets x that > the 256 MiB Infinity Cache) are prepared; then
       hbm:     `reps` back-to-back launches cycling through the sets behind a GPU spin: every launch
                reads inputs the launches between evicted from the caches (HBM-bound), the average
                launch duration -> `achieved` / `frac`;
       warm:    `reps` back-to-back launches on ONE set (its inputs cache-resident);
       in_step: one launch right behind the field forward that wrote its inputs, bracketed by its own
                event pair (includes the launch ramp and the event overhead), mean over the batches.
-    Returns (algorithmic bytes per launch (mean over the sets), {hbm, warm, in_step} us)."""
+    Returns (algorithmic bytes per launch (mean over the sets), {hbm, warm, in_step, ...} us)."""
     from ncnerf_amd import _lib
     from ncnerf_amd._lib import F32, I32, I64, ptr, stream
     from ncnerf_amd import vren
-    from ncnerf_amd.rendering import march_train_fused
-    fn = _lib.lib().ncn_composite_train_fw_bg
+    from ncnerf_amd.rendering import march_buffers, march_train_fused
+    fn = _lib.lib().ncn_composite_train_fw_bg  # the step's compositor (ray-major)
+    fn_sm = _lib.lib().ncn_composite_train_fw_sm  # the sample-major alternative, timed beside it
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+
+    def sm_args(k, R, S, n_dev=None, grid=None):
+        return [ptr(k["sig"]), ptr(k["rgb"]), ptr(k["dl"]), ptr(k["ts"]), ptr(k["codes"]), ptr(k["ra"]), I64(R),
+                I64(S), ptr(n_dev), I64(grid or S), I32(3), F32(1e-4)] + [ptr(t) for t in k["res"][:5]] + [
+                    F32(1.0), ptr(k["res"][5]), stream()]
+
+    def rm_args(k, R, S):
+        return [ptr(k["sig"]), ptr(k["rgb"]), ptr(k["dl"]), ptr(k["ts"]), ptr(k["ra"]), I64(R), I64(S), I32(3),
+                F32(1e-4)] + [ptr(t) for t in k["res"][:5]] + [F32(1.0), ptr(k["res"][5]), stream()]
+
     sets, t_in = [], []
     with torch.no_grad():
         for j in range(n_sets):
             batch = batches[j % len(batches)]
             o, d = batch["rays_o"].contiguous(), batch["rays_d"].contiguous()
             R = o.shape[0]
-            mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(R, device=dev))
+            mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(R, device=dev),
+                                   out=march_buffers(R, 1024, dev, codes=True))
             S = int(mk["counter"][0].item())
             out = model(mk["xyzs"], mk["dirs"], n_samples_dev=mk["counter"])
             res = [torch.empty(R, dtype=torch.int64, device=dev), torch.empty(R, device=dev), torch.empty(R, device=dev),
                    torch.empty(R, 3, device=dev), torch.empty(S, device=dev), torch.empty(R, 3, device=dev)]
-            if j < len(batches):  # in-step: right behind the field forward that produced the inputs
-                args = [ptr(out["sigmas"]), ptr(out["rgbs"]), ptr(mk["deltas"]), ptr(mk["ts"]), ptr(mk["rays_a"]),
-                        I64(R), I64(S), I32(3), F32(1e-4)] + [ptr(t) for t in res[:5]] + [F32(1.0), ptr(res[5]),
-                                                                                          stream()]
+            if j < len(batches):  # in-step: right behind the field forward that produced the inputs, as
+                # the step launches it (capacity-sized arrays)
+                full = {"sig": out["sigmas"], "rgb": out["rgbs"], "dl": mk["deltas"], "ts": mk["ts"],
+                        "codes": mk["sample_ray"], "ra": mk["rays_a"],
+                        "res": res[:4] + [torch.empty(mk["ts"].shape[0], device=dev), res[5]]}
+                args = rm_args(full, R, mk["ts"].shape[0])
                 for rep in range(2):  # (rep 0 warms up)
                     if rep:
                         out = model(mk["xyzs"], mk["dirs"], n_samples_dev=mk["counter"])
@@ -146,33 +161,37 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
                     b.record()
                     torch.cuda.synchronize()
                 t_in.append(a.elapsed_time(b) * 1e3)
+                del full
             # compact copies (S rows) so the sets are disjoint, cache-sized data
             keep = {"sig": out["sigmas"][:S].clone(), "rgb": out["rgbs"][:S].clone(), "dl": mk["deltas"][:S].clone(),
-                    "ts": mk["ts"][:S].clone(), "ra": mk["rays_a"].clone(), "res": res}
-            keep["args"] = [ptr(keep["sig"]), ptr(keep["rgb"]), ptr(keep["dl"]), ptr(keep["ts"]), ptr(keep["ra"]),
-                            I64(R), I64(S), I32(3), F32(1e-4)] + [ptr(t) for t in res[:5]] + [F32(1.0),
-                                                                                          ptr(res[5]), stream()]
+                    "ts": mk["ts"][:S].clone(), "ra": mk["rays_a"].clone(), "codes": mk["sample_ray"][:S].clone(),
+                    "res": res}
+            keep["args"] = rm_args(keep, R, S)
+            keep["args_sm"] = sm_args(keep, R, S)
             sets.append(keep)
             del out, mk
         for k in sets:  # (first-call costs, and the algorithmic bytes of each set)
+            assert fn_sm(*k["args_sm"]) == 0
             assert fn(*k["args"]) == 0
         torch.cuda.synchronize()
         nbytes = [24.0 * float(k["res"][0].sum().item()) + 4.0 * k["sig"].shape[0] + 52.0 * k["ra"].shape[0]
                   for k in sets]
 
-        def b2b(arg_list, n=reps):
+        def b2b(f, arg_list, n=reps):
             torch.cuda.synchronize()
             a, b = ev(), ev()
             torch.cuda._sleep(2_000_000)  # ~1 ms: every launch below is queued before the first runs
             a.record()
             for i in range(n):
-                fn(*arg_list[i % len(arg_list)])
+                f(*arg_list[i % len(arg_list)])
             b.record()
             torch.cuda.synchronize()
             return a.elapsed_time(b) * 1e3 / n
 
-        t_hbm = b2b([k["args"] for k in sets])
-        t_warm = b2b([sets[0]["args"]])
+        t_hbm = b2b(fn, [k["args"] for k in sets])
+        t_warm = b2b(fn, [sets[0]["args"]])
+        t_hbm_sm = b2b(fn_sm, [k["args_sm"] for k in sets])
+        t_warm_sm = b2b(fn_sm, [sets[0]["args_sm"]])
         # the same kernel on config #4's global batch (65536 rays, one launch): 3 sets of ~140 MB
         # cycled (> the Infinity Cache), so each launch reads from HBM
         big = []
@@ -189,43 +208,31 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
             # 256 samples first, the rest in ray order (sample segments unchanged)
             long_ = ra[:, 2] > 256
             ra = torch.cat([ra[long_], ra[~long_]]).contiguous()
-            mk = {"rays_a": ra, "deltas": deltas, "ts": ts}
             out = model(xyzs, dirs)
             R = 65536
             res = [torch.empty(R, dtype=torch.int64, device=dev), torch.empty(R, device=dev), torch.empty(R, device=dev),
                    torch.empty(R, 3, device=dev), torch.empty(S, device=dev), torch.empty(R, 3, device=dev)]
-            k = {"sig": out["sigmas"][:S].clone(), "rgb": out["rgbs"][:S].clone(), "dl": mk["deltas"][:S].clone(),
-                 "ts": mk["ts"][:S].clone(), "ra": mk["rays_a"].clone(), "res": res}
-            k["args"] = [ptr(k["sig"]), ptr(k["rgb"]), ptr(k["dl"]), ptr(k["ts"]), ptr(k["ra"]), I64(R), I64(S), I32(3),
-                         F32(1e-4)] + [ptr(t) for t in res[:5]] + [F32(1.0), ptr(res[5]), stream()]
-            del out, mk
+            k = {"sig": out["sigmas"][:S].clone(), "rgb": out["rgbs"][:S].clone(), "dl": deltas[:S].clone(),
+                 "ts": ts[:S].clone(), "ra": ra.clone(), "res": res}
+            k["args"] = rm_args(k, R, S)
+            del out
             big.append(k)
         for k in big:
             assert fn(*k["args"]) == 0
         torch.cuda.synchronize()
         big_bytes = [24.0 * float(k["res"][0].sum().item()) + 4.0 * k["sig"].shape[0] + 52.0 * k["ra"].shape[0]
                      for k in big]
-        t_big = b2b([k["args"] for k in big], n=12)
+        t_big = b2b(fn, [k["args"] for k in big], n=12)
         del big
     mean_bytes = float(np.mean([nbytes[i % len(sets)] for i in range(reps)]))
-    return mean_bytes, {"hbm": t_hbm, "warm": t_warm, "in_step": float(np.mean(t_in)),
-                        "warm_bytes": nbytes[0], "big_us": t_big, "big_bytes": float(np.mean(big_bytes))}
+    return mean_bytes, {"hbm": t_hbm, "warm": t_warm, "in_step": float(np.mean(t_in)), "hbm_sm": t_hbm_sm,
+                        "warm_sm": t_warm_sm, "warm_bytes": nbytes[0], "big_us": t_big,
+                        "big_bytes": float(np.mean(big_bytes))}
 
 
-def cpu_baseline(n_rays=2048, steps=20, warmup=3):
-    """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on the host cores),
-    timed as BASELINE.md §2 asks: median wall time of 20 steps after 3 warm-up steps.  Threads: all
-    cores this process may run on (its affinity mask), capped by OMP_NUM_THREADS when the box sets
-    it (the GPU box's CPU share); both counts are reported."""
+def _cpu_leg(threads, n_rays, steps, warmup):
     from oracle.train_ref import CPUTrainer
     from ncnerf_amd.synthetic import SyntheticScene
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except AttributeError:
-        affinity = os.cpu_count() or 1
-    threads = affinity
-    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
-        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(threads)
     scene = SyntheticScene()
     tr = CPUTrainer(scene.bitfield)
@@ -237,12 +244,94 @@ def cpu_baseline(n_rays=2048, steps=20, warmup=3):
         t0 = time.perf_counter()
         tr.step(b)
         times.append(time.perf_counter() - t0)
-    med = float(np.median(times))
-    return {"value": round(n_rays / med, 1), "unit": "rays/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+    return float(np.median(times)), float(sum(times))
+
+
+def distill_opaque(model, trainer, scene, dev, steps=300, n_points=1 << 16, sigma_in=3000.0, sigma_out=1e-2):
+    """The opaque state of a converged NeRF, reached directly: the field's density is fitted to the
+    procedural room's occupancy (log sigma -> log sigma_in inside occupied voxels, log sigma_out
+    elsewhere; random points and directions, MSE on log sigma through the field backward and the
+    trainer's own Adam), so that rays terminate at the first surface as they do once a scene's
+    surfaces have converged (the photometric + opacity losses alone take far longer than the bench
+    can spend to push T below 1e-4 on this room).  Returns the fit's last loss."""
+    occ = torch.from_numpy(scene.occ).to(dev)
+    G = occ.shape[0]
+    g = torch.Generator(device=dev).manual_seed(77)
+    lo, hi = math.log(sigma_out), math.log(sigma_in)
+    loss = None
+    for _ in range(steps):
+        x = (torch.rand(n_points, 3, device=dev, generator=g) - 0.5) * 0.999
+        v = ((x + 0.5) * G).long().clamp_(0, G - 1)
+        target = torch.where(occ[v[:, 0], v[:, 1], v[:, 2]], hi, lo)
+        d = torch.nn.functional.normalize(torch.randn(n_points, 3, device=dev, generator=g), dim=1)
+        loss = ((torch.log(model(x, d)["sigmas"]) - target) ** 2).mean()
+        loss.backward()
+        trainer.opt.step()
+    torch.cuda.synchronize()
+    return round(float(loss), 4)
+
+
+def cpu_baseline(n_rays=2048, steps=20, warmup=3):
+    """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on the host cores),
+    timed as BASELINE.md §2 asks: median wall time of 20 steps after 3 warm-up steps, twice: on every
+    CPU of this process's affinity mask, and capped by OMP_NUM_THREADS when the box sets it (the GPU
+    box's CPU share).  `value` is the faster of the two (the stronger baseline); both are reported."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    legs = {"affinity": affinity}
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) < affinity:
+        legs["omp_num_threads"] = int(omp)
+    runs = {}
+    for name, threads in legs.items():
+        med, tot = _cpu_leg(threads, n_rays, steps, warmup)
+        runs[name] = {"threads": threads, "rays_per_s": round(n_rays / med, 1), "ms_per_step": round(med * 1e3, 1),
+                      "timed_s": round(tot, 1)}
+    best = max(runs, key=lambda k: runs[k]["rays_per_s"])
+    torch.set_num_threads(legs.get("omp_num_threads", affinity))
+    return {"value": runs[best]["rays_per_s"], "unit": "rays/s", "cores": runs[best]["threads"], "kind": "port",
+            "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "legs": runs,
             "sample": f"median of {steps} full training steps of {n_rays} rays (config #1) after {warmup} warm-up "
                       f"steps on the oracle CPU path (oracle/train_ref.py: C marcher/compositor + torch fp32 "
-                      f"field/losses), {med * 1e3:.0f} ms/step, {sum(times):.1f} s timed"}
+                      f"field/losses), once on all {affinity} CPUs of the affinity mask"
+                      + (f" and once on OMP_NUM_THREADS={legs['omp_num_threads']}" if "omp_num_threads" in legs else "")
+                      + f"; value = the faster ({best})"}
+
+
+def eval_render(model, scene, dev, n_images=3):
+    """The test-time render of full 1024x768 images (786 432 rays each) through render(...,
+    test_time=True): the reference's host-driven loop of rendering.py:45-149 (march N_samples per
+    alive ray, field on the valid samples, incremental composite, alive compaction) with `model`.
+    Wall time per image (synchronize on both sides), loop iterations, marched samples, and the host
+    time blocked at the loop's per-iteration syncs (valid_mask.sum(), the alive compaction)."""
+    from ncnerf_amd.rendering import render
+    kw = dict(near_distance=0.01, max_samples=1024, test_time=True)
+    res = []
+    with torch.no_grad():
+        o, d = scene.image_rays(0, dev)
+        render(model, o, d, **kw)  # (first-call costs)
+        for cam in range(1, n_images + 1):
+            o, d = scene.image_rays(cam, dev)
+            st = {}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = render(model, o, d, loop_stats=st, **kw)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            res.append((t1 - t0, st, float(out["opacity"].mean())))
+    wall = float(np.median([r[0] for r in res]))
+    its = [r[1].get("iterations", 0) for r in res]
+    blocked = [r[1].get("blocked_s", 0.0) / r[0] for r in res]
+    return {"ms_per_image": round(wall * 1e3, 2), "rays_per_image": int(o.shape[0]),
+            "rays_per_s": round(o.shape[0] / wall, 1), "images": n_images,
+            "loop_iterations": its, "samples_marched_per_image": [int(r[1].get("samples_marched", 0)) for r in res],
+            "host_blocked_share": round(float(np.median(blocked)), 3), "mean_opacity": [round(r[2], 3) for r in res],
+            "method": "render(model, rays of one synthetic camera's full image, test_time=True): rendering.py:45-149's "
+                      "loop on ncn_march_test / the field / ncn_composite_test_fw; median wall time of "
+                      f"{n_images} images after one warm-up image; host_blocked_share = host time inside the "
+                      "loop's syncing statements / wall time"}
 
 
 def main():
@@ -272,6 +361,8 @@ def main():
                     help="skip the extra measurements of trained states: 500 steps pretrained on the procedural "
                          "grid (rays terminate early), and the grid train_nerf.py maintains itself "
                          "(mark_invisible_cells + grid refresh from step 0)")
+    ap.add_argument("--no-eval-render", action="store_true",
+                    help="skip the test-time render of full 1024x768 images (eval_render line)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="launch/rendezvous check only (no GPU work): every rank all-reduces its rank, rank 0 "
                          "prints {world, backend, sum}")
@@ -426,6 +517,9 @@ def main():
             if pre == args.pretrain and st == "procedural":
                 continue  # (the headline measurement)
             r3 = measure(args.precision, args.steps, False, pre, st)
+            if key == "pretrained_state" and world == 1 and not args.no_eval_render:
+                extra["eval_render"] = dict(eval_render(r3["model"], SyntheticScene(), dev),
+                                            model="the pretrained_state model")
             n_r = args.rays * world * args.steps
             extra[key] = {"value": round(n_r / r3["el"], 1), "unit": "rays/s",
                           "ms_per_step": round(1e3 * r3["el"] / args.steps, 3),
@@ -489,6 +583,12 @@ def main():
                      "warm_us": round(cf_t["warm"], 2),
                      "frac_warm": round(cf_t["warm_bytes"] / (cf_t["warm"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                      "in_step_us": round(cf_t["in_step"], 2),
+                     "sample_major": {"kernel": "ncn_composite_train_fw_sm (per-sample ray codes, no rays_a "
+                                                "dependency; opt-in: NCN_COMPOSITE=sm)",
+                                      "avg_launch_us": round(cf_t["hbm_sm"], 2),
+                                      "frac": round(cf_bytes_per_launch / (cf_t["hbm_sm"] * 1e-6) / 1e9 /
+                                                    HBM_PEAK_GBS, 4),
+                                      "warm_us": round(cf_t["warm_sm"], 2)},
                      "batch65536": {"avg_launch_us": round(cf_t["big_us"], 2),
                                     "algorithmic_bytes_per_launch": round(cf_t["big_bytes"]),
                                     "frac": round(cf_t["big_bytes"] / (cf_t["big_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),

@@ -112,10 +112,13 @@ class VolumeRendererBg(torch.autograd.Function):
 
     @staticmethod
     @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg, count=None):
+    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg, count=None, sm=None):
+        """sm: None, or (per-sample ray codes, device sample counter, grid samples) of the fused
+        training marcher: the sample-major compositor (ncn_composite_train_fw_sm)."""
         sigmas = sigmas.contiguous(); raws = raws.contiguous()
+        kw = {} if sm is None else dict(sample_ray=sm[0], n_samples_dev=sm[1], grid_samples=sm[2])
         total_samples, opacity, depth, rend, ws, rgb = vren.composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a,
-                                                                                       T_threshold, bg=bg)
+                                                                                       T_threshold, bg=bg, **kw)
         ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
         ctx.T_threshold, ctx.bg = T_threshold, bg
         ctx.set_materialize_grads(False)
@@ -138,7 +141,7 @@ class VolumeRendererBg(torch.autograd.Function):
         dL_dsigmas, dL_draws = vren.composite_train_multi_bw(c(dL_dopacity), c(dL_ddepth), c(dL_drgb), c(dL_dws),
                                                              sigmas, raws, ws, deltas, ts, rays_a, opacity, depth,
                                                              rend, ctx.T_threshold, bg=ctx.bg)
-        return dL_dsigmas, dL_draws, None, None, None, None, None, None
+        return dL_dsigmas, dL_draws, None, None, None, None, None, None, None
 
 
 class TruncExp(torch.autograd.Function):

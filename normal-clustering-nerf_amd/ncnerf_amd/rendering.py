@@ -12,6 +12,9 @@ read of the counter), which is what lets Trainer capture the whole step in one H
 kwargs['premarched'] (a march_train_static() result) skips intersect + march: the pipelined step
 marches the next batch while the current one is rendered.
 """
+import os
+import time
+
 import torch
 from einops import rearrange
 
@@ -61,6 +64,7 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
     alive_indices = torch.arange(N_rays, device=device)
     min_samples = 1 if exp_step_factor == 0 else 4
     hits_t0 = hits_t[:, 0].contiguous()
+    stats = kwargs.get("loop_stats")  # (extension) iteration count and host time blocked at the syncs
     while samples < max_samples:
         N_alive = len(alive_indices)
         if N_alive == 0:
@@ -74,9 +78,15 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
         xyzs = rearrange(xyzs, "n1 n2 c -> (n1 n2) c")
         dirs = rearrange(dirs, "n1 n2 c -> (n1 n2) c")
         valid_mask = ~torch.all(dirs == 0, dim=1)
-        if valid_mask.sum() == 0:
+        if stats is not None:
+            t0 = time.perf_counter()
+        if valid_mask.sum() == 0:  # (host sync)
             break
-        output = model(xyzs[valid_mask], dirs[valid_mask], **kwargs)
+        if stats is not None:
+            stats["blocked_s"] = stats.get("blocked_s", 0.0) + time.perf_counter() - t0
+            stats["iterations"] = stats.get("iterations", 0) + 1
+            stats["samples_marched"] = stats.get("samples_marched", 0) + N_alive * N_samples
+        output = model(xyzs[valid_mask], dirs[valid_mask], **{k: v for k, v in kwargs.items() if k != "loop_stats"})
         sigmas = torch.zeros(len(xyzs), device=device)
         sigmas[valid_mask] = output["sigmas"].float()
         sigmas = rearrange(sigmas, "(n1 n2) -> n1 n2", n2=N_samples)
@@ -89,7 +99,11 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
             raws = torch.cat((raws, rearrange(extra, "(n1 n2) c -> n1 n2 c", n2=N_samples)), dim=-1)
         vren.composite_test_multi_fw(sigmas.contiguous(), raws.contiguous(), deltas, ts, hits_t0, alive_indices,
                                      kwargs.get("T_threshold", 1e-4), N_eff_samples, opacity, depth, rend)
-        alive_indices = alive_indices[alive_indices >= 0]
+        if stats is not None:
+            t0 = time.perf_counter()
+        alive_indices = alive_indices[alive_indices >= 0]  # (host sync: the compaction's size)
+        if stats is not None:
+            stats["blocked_s"] += time.perf_counter() - t0
     hits_t[:, 0] = hits_t0
     results["opacity"] = opacity
     results["depth"] = depth
@@ -158,6 +172,9 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     fuse_bg = exp_step_factor == 0 and raws.shape[1] == 3  # white background, rgb only
     renderer = VolumeRendererBg if fuse_bg else VolumeRenderer
     extra = (1.0,) if fuse_bg else ()
+    sm = None  # the fused marcher's per-sample ray codes: the sample-major compositor
+    if fuse_bg and pm is not None and pm.get("sample_ray") is not None:
+        sm = (pm["sample_ray"], pm["counter"], rays_a.shape[0] * SM_GRID_SAMPLES_PER_RAY)
     job = CountJob() if fuse_bg and kwargs.get("count_in_loss") else None
     if fuse_bg and (kwargs.get("count_acc") is not None or job is not None):
         # (extension) device-side throughput counters; count_in_loss: the sample count is taken by
@@ -166,6 +183,8 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
         rm = rm if isinstance(rm, torch.Tensor) and rm.dtype == torch.int32 and rm.is_cuda else None
         acc = kwargs.get("count_acc")
         extra = (1.0, (rm if acc is not None else None, acc, job))
+    if sm is not None:
+        extra = (extra + (None,))[:2] + (sm,)
     (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = renderer.apply(
         sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4), *extra)
     if job is not None and job.out is not None:
@@ -217,6 +236,18 @@ def _fused_march_ok(model, kw, n_rays):
                         if k not in ("march_noise", "march_rng", "count_acc")))
 
 
+SM_MAX_SAMPLES = 1024  # the sample-major compositor's longest ray (its long-ray workgroups)
+# The training step's compositor: "ray" (ray-major ncn_composite_train_fw_bg, the default) or "sm"
+# (sample-major ncn_composite_train_fw_sm over the fused marcher's per-sample ray codes).  Measured
+# (DESIGN section 5): the sample-major form removes the rays_a -> sample load dependency but its
+# cross-lane segment work and the continuation of range-crossing rays cost more than that saves
+# (9.7 vs 6.6 us HBM-cold, 7.3 vs 4.4 warm on the bench's 8192-ray sets), so it is opt-in.
+SM_COMPOSITE = os.environ.get("NCN_COMPOSITE", "ray") == "sm"
+# samples per ray the sample-major compositor's grid covers in one pass when the count is on the
+# device (graph-captured step; its waves loop over any beyond)
+SM_GRID_SAMPLES_PER_RAY = int(os.environ.get("NCN_SM_SPR", "96"))
+
+
 @torch.no_grad()
 def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=None, rng=None, out=None):
     """ncn_march_train_fused: RayAABBIntersector + near clamp (rendering.py:24-28) + RayMarcher
@@ -250,13 +281,15 @@ def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=N
          F32(h[1]), F32(h[2]), F32(near_distance), ptr(noise), U64(int(seed) % 2 ** 64), ptr(ctr),
          ptr(model.density_bitfield), I32(int(model.cascades)), F32(float(model.scale)), I32(int(model.grid_size)),
          I32(ms), ptr(slab_xyz), ptr(slab_t), ptr(slab_dt), ptr(ws), ptr(out["rays_a"]), ptr(out["xyzs"]),
-         ptr(out["dirs"]), ptr(out["deltas"]), ptr(out["ts"]), ptr(out["counter"]), stream())
+         ptr(out["dirs"]), ptr(out["deltas"]), ptr(out["ts"]), ptr(out["counter"]), ptr(out.get("sample_ray")),
+         stream())
     return out
 
 
-def march_buffers(R, max_samples, device, share_scratch=None):
+def march_buffers(R, max_samples, device, share_scratch=None, codes=None):
     """Output + scratch buffers of march_train_fused for R rays (capacity R*max_samples samples);
-    share_scratch: another march_buffers() whose scratch (slabs, work) is reused (never concurrently)."""
+    share_scratch: another march_buffers() whose scratch (slabs, work) is reused (never concurrently);
+    codes: also the per-sample ray codes of the sample-major compositor (default: SM_COMPOSITE)."""
     from ._lib import I64, lib
     cap = R * int(max_samples)
     f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=device)
@@ -266,9 +299,13 @@ def march_buffers(R, max_samples, device, share_scratch=None):
         ws = torch.empty((int(lib().ncn_march_train_fused_work_bytes(I64(R))) + 3) // 4, dtype=torch.int32,
                          device=device)
         scratch = (f(cap * 3), f(cap), f(cap), ws)
-    return {"rays_a": torch.empty(R, 3, dtype=torch.int64, device=device), "xyzs": f(cap, 3), "dirs": f(cap, 3),
-            "deltas": f(cap), "ts": f(cap), "counter": torch.empty(2, dtype=torch.int32, device=device),
-            "_slab": scratch}
+    out = {"rays_a": torch.empty(R, 3, dtype=torch.int64, device=device), "xyzs": f(cap, 3), "dirs": f(cap, 3),
+           "deltas": f(cap), "ts": f(cap), "counter": torch.empty(2, dtype=torch.int32, device=device),
+           "_slab": scratch}
+    if (SM_COMPOSITE if codes is None else codes) and int(max_samples) <= SM_MAX_SAMPLES:
+        # per-sample ray codes: the sample-major compositor's input
+        out["sample_ray"] = torch.empty(cap, dtype=torch.int32, device=device)
+    return out
 
 
 

@@ -34,7 +34,7 @@ from . import _lib, vren
 from ._lib import F32, I32, I64, call, ptr, stream
 from .losses import N_OUT, _cluster_workspace, _standard_patch_offsets, kmeans_plan
 from .ngp_mt import N_W
-from .rendering import march_train_fused
+from .rendering import SM_GRID_SAMPLES_PER_RAY, march_train_fused
 
 SPLIT_BLOCKS = 240  # MLP-backward workgroups of each split pass: 256 CUs - the clustering's 16
 K_CLUSTERS, K_ITERS = 20, 20  # NeRFMTLoss._fused (losses.py:86-89: faiss.Kmeans(3, 20, niter=20))
@@ -92,8 +92,10 @@ class SplitStep:
         n_dev = pm["counter"][0]
         n = xyzs.shape[0]
         sigmas, rgbs, enc, packed, order = m._field_fwd(xyzs, dirs, n_dev, 0, True)
+        sm = {} if pm.get("sample_ray") is None else dict(
+            sample_ray=pm["sample_ray"], n_samples_dev=pm["counter"], grid_samples=R * SM_GRID_SAMPLES_PER_RAY)
         total_s, opacity, depth, rend, ws, rgb = vren.composite_train_multi_fw(sigmas, rgbs, deltas, ts, rays_a,
-                                                                              T_thr, bg=1.0)
+                                                                              T_thr, bg=1.0, **sm)
         # ---- NeRFMTLoss forward (_NeRFLossFused.forward) ----
         x1, x2, x3 = self._triangles(R, dev)
         T = x1.shape[0]

@@ -183,6 +183,16 @@ class SyntheticScene:
         return {"rays_o": rays_o, "rays_d": rays_d, "rgb": rgb, "patch_area": PATCH * PATCH,
                 "x1_offsets_local": self.x1_off, "x2_offsets_local": self.x2_off, "x3_offsets_local": self.x3_off}
 
+    def image_rays(self, cam, device=None):
+        """Every pixel of camera `cam`'s 1024x768 image (get_rays, ray_utils.py:45-71): the rays of
+        the reference's test-time render of one image (validation_step, train_nerf.py:381)."""
+        P = self.poses[cam]
+        rays_d = (self.dirs @ P[:, :3].T).astype(np.float32)
+        rays_o = np.broadcast_to(P[:, 3].astype(np.float32), rays_d.shape).copy()
+        if device is None:
+            return rays_o, rays_d
+        return (torch.from_numpy(rays_o).to(device), torch.from_numpy(np.ascontiguousarray(rays_d)).to(device))
+
     def torch_batch(self, n_rays, seed, device, gt="surface"):
         """batch() with the per-ray arrays on `device`; the patch offsets stay host arrays (constant
         metadata of the sampling strategy, as the reference's base.py:53-58 keeps them)."""

@@ -186,6 +186,29 @@ class _RoundST(torch.autograd.Function):
         return g, None
 
 
+class _RoundGrad(torch.autograd.Function):
+    """Identity in the forward; in the backward the incoming gradient is rounded as the HIP field
+    backward rounds it (ncn_field_bwd, csrc/field.hip bwd_group): carried at the scale K = 128 * S
+    (tcnn's fp16 module loss scale x the GradScaler's S), converted to the MLP operand type (fp16
+    overflow -> inf, underflow -> subnormal / 0), and handed on unscaled: fp16(g K) / K."""
+
+    @staticmethod
+    def forward(ctx, t, dt, K):
+        ctx.dt, ctx.K = dt, K
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g * ctx.K).to(ctx.dt).float() / ctx.K, None, None
+
+
+def _grad_rounder(emulate, bwd_scale):
+    if emulate is None or bwd_scale is None:
+        return lambda t: t
+    dt = {"fp16": torch.float16, "bf16": torch.bfloat16}[emulate]
+    return lambda t: _RoundGrad.apply(t, dt, float(bwd_scale))
+
+
 def _rounder(emulate_f16=False, emulate=None):
     mode = emulate or ("fp16" if emulate_f16 else None)
     if mode is None:
@@ -252,20 +275,27 @@ class _TruncExp(torch.autograd.Function):
         return g * torch.exp(x.clamp(-15, 15))
 
 
-def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=None, impl="torch"):
+def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, emulate=None, impl="torch",
+                           bwd_scale=None):
     """Same as field_forward with TruncExp's clamped backward, differentiable w.r.t. P.  With
     emulation the forward operands are rounded where the HIP kernel rounds them (the rounding is
     straight-through in the backward), so ReLU masks match the kernel's.  impl: the encoding's
-    statement ("torch" or "c", see encode())."""
+    statement ("torch" or "c", see encode()).
+    bwd_scale (with emulate): the backward's gradients are rounded where csrc/field.hip's bwd_group
+    rounds them, at that scale (128 x the GradScaler's scale): the pre-sigmoid output gradient
+    (dY5), the pre-ReLU gradients of layers 4, 3 and 1 (dD4, dD3, dD1), and dL/dh after the rgb path
+    and TruncExp's term are added (dhh); dL/denc and the weight gradients are fp32 products of those
+    rounded operands, as the kernel's MFMA accumulates them."""
     q = _rounder(emulate_f16, emulate)
+    rg = _grad_rounder(emulate or ("fp16" if emulate_f16 else None), bwd_scale)
     x01 = (xyzs - (-scale)) / (2 * scale)
     enc = encode(x01, P.table, levels, impl)
-    h = q(torch.relu(q(enc) @ q(P.W1).t())) @ q(P.W2).t()
+    h = rg(q(torch.relu(rg(q(enc) @ q(P.W1).t()))) @ q(P.W2).t())
     sig = _TruncExp.apply(h[:, 0])
     d = dirs / torch.norm(dirs, dim=1, keepdim=True)
-    g = torch.relu(q(rgb_input(d, h)) @ q(P.W3).t())
-    g = torch.relu(q(g) @ q(P.W4).t())
-    rgb = torch.sigmoid((q(g) @ q(P.W5).t())[:, :3])
+    g = torch.relu(rg(q(rgb_input(d, h)) @ q(P.W3).t()))
+    g = torch.relu(rg(q(g) @ q(P.W4).t()))
+    rgb = torch.sigmoid(rg(q(g) @ q(P.W5).t())[:, :3])
     return sig, rgb, h
 
 

@@ -3,7 +3,8 @@ the product path.
 
 * `mark_invisible_cells`: reference models/ngp_mt.py:274-337 (pinhole-K branch), numpy f32.
 * `grid_refresh`: reference models/ngp_mt.py:340-368 (update_density_grid) with the cell sampling
-  of ngp_mt.py:245-262 replaced by the documented deviation of csrc/grid.hip:
+  of ngp_mt.py:245-262 replaced by the documented deviation of csrc/grid.hip,
+  or (sampling="reference") the reference's own draws (`reference_cells`):
   every cell is hit independently with the marginal probability of the reference's M uniform +
   M occupied draws with replacement, decided by the same counter-based hash of (seed, cell, stream)
   as the device (`gr_uniform`, grid.hip), and the hit cells' jitter drawn from the same hash.
@@ -108,18 +109,44 @@ def hit_positions(cells, seed, grid_size, s):
     return out
 
 
-def grid_refresh(grid, density_fn, threshold, warmup, seed, grid_size, scale, decay=0.95):
-    """update_density_grid (ngp_mt.py:340-368) with the device's sampling: returns
-    (new grid (C, G^3) f32, threshold used, bitfield).  `density_fn(xyzs (n,3) f32) -> (n,) f32`."""
+def reference_cells(grid_c, thr, seed, grid_size):
+    """sample_uniform_and_occupied_cells (ngp_mt.py:244-270) for one cascade, the reference's own
+    draws: M = G^3 / 4 uniform cells (random integer coordinates, with replacement) and M draws with
+    replacement from the cells above the threshold; numpy's generator seeded by `seed` stands in for
+    torch's device RNG.  Returns (Morton indices, integer coordinates) in the reference's order."""
+    G = grid_size
+    M = G ** 3 // 4
+    rng = np.random.default_rng(int(seed) % 2 ** 63)
+    coords1 = rng.integers(0, G, (M, 3)).astype(np.int32)
+    idx1 = vren_ref.morton3D(coords1).astype(np.int64)
+    occ = np.nonzero(grid_c > np.float32(thr))[0]
+    idx2 = occ[rng.integers(0, len(occ), M)] if len(occ) > 0 else occ
+    coords2 = vren_ref.morton3D_invert(idx2.astype(np.int32)).reshape(-1, 3)
+    return np.concatenate([idx1, idx2]), np.concatenate([coords1, coords2]).astype(np.float32), rng
+
+
+def grid_refresh(grid, density_fn, threshold, warmup, seed, grid_size, scale, decay=0.95, sampling="device"):
+    """update_density_grid (ngp_mt.py:340-368): returns (new grid (C, G^3) f32, threshold used,
+    bitfield).  `density_fn(xyzs (n,3) f32) -> (n,) f32`.  sampling "device": the HIP refresh's
+    (every cell hit independently with the marginal probability of the reference's draws, DESIGN
+    deviation 7); "reference": the reference's M uniform + M occupied draws with replacement
+    (reference_cells), each drawn cell at its own jittered position, a cell drawn twice keeping the
+    last draw's density (the assignment density_grid_tmp[c, indices] = ... of ngp_mt.py:353)."""
     g = np.array(grid, np.float32, copy=True)
     C = g.shape[0]
     for c in range(C):
         s = min(2 ** (c - 1), scale)
         sc = (int(seed) + 0x9E3779B97F4A7C15 * c) % 2 ** 64
-        cells = hit_cells(g[c], threshold, warmup, sc)
-        sig = np.asarray(density_fn(hit_positions(cells, sc, grid_size, s)), np.float32)
         tmp = np.zeros(g.shape[1], np.float32)
-        tmp[cells] = sig
+        if sampling == "reference" and not warmup:
+            cells, coords, rng = reference_cells(g[c], threshold, sc, grid_size)
+            hg = np.float32(s / grid_size)
+            xyzs = (coords / np.float32(grid_size - 1) * np.float32(2) - np.float32(1)) * np.float32(s - s / grid_size)
+            xyzs = (xyzs + (rng.random(xyzs.shape, dtype=np.float32) * np.float32(2) - np.float32(1)) * hg)
+            tmp[cells] = np.asarray(density_fn(xyzs.astype(np.float32)), np.float32)  # (last write wins)
+        else:
+            cells = hit_cells(g[c], threshold, warmup, sc)
+            tmp[cells] = np.asarray(density_fn(hit_positions(cells, sc, grid_size, s)), np.float32)
         v = g[c]
         # torch.maximum semantics (NaN propagates) as grid.hip's torch_max
         g[c] = np.where(v < 0, v, np.maximum(v * np.float32(decay), tmp)).astype(np.float32)

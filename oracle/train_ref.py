@@ -56,12 +56,19 @@ class CPUTrainer:
     """Hypersim config: scale 0.5, G 128, max_samples 1024, near 0.01, loss weights as the trainer."""
 
     def __init__(self, bitfield, seed=0, lr=1e-2, w_cluster=2e-3, opacity_w=1e-3, num_epochs=None, epoch_steps=1000,
-                 encode_impl="torch", emulate=None):
+                 encode_impl="torch", emulate=None, emulate_bwd=False):
         """encode_impl: "torch" (field_ref.hash_encode, the pure-PyTorch path of config #1) or "c"
         (its C restatement, oracle/hashgrid_ref.c: the same algorithm ~10x faster, for the PSNR
-        seed ensembles)."""
+        seed ensembles).
+        emulate_bwd (with emulate): the field backward's gradients rounded as the HIP kernel's
+        loss-scaled fp16 chain rounds them (field_ref.field_forward_autograd bwd_scale = 128 x S),
+        with the GradScaler that S comes from (torch.cuda.amp.GradScaler defaults, as the HIP
+        optimizer's: init 2^16, a non-finite gradient skips the step and halves S, 2000 finite steps
+        in a row double it)."""
         self.encode_impl = encode_impl
         self.emulate = emulate  # "fp16": the MLP operands rounded as tcnn's / the HIP kernel's (field_ref)
+        self.emulate_bwd = bool(emulate_bwd) and emulate is not None
+        self.amp_S, self.amp_tracker, self.amp_skips = 65536.0, 0, 0
         P, self.levels = field_ref.init_params(seed=seed)
         self.params = [t.requires_grad_(True) for t in P.tensors()]
         self.P = field_ref.FieldParams(*self.params)
@@ -94,8 +101,10 @@ class CPUTrainer:
         rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, self.bitfield, 1, 0.5, 0.0,
                                                                              noise, 128, 1024)
         self.opt.zero_grad()
+        K = 128.0 * self.amp_S if self.emulate_bwd else None
         sig, rgb, _ = field_ref.field_forward_autograd(torch.from_numpy(xyzs), torch.from_numpy(dirs), self.P,
-                                                       self.levels, impl=self.encode_impl, emulate=self.emulate)
+                                                       self.levels, impl=self.encode_impl, emulate=self.emulate,
+                                                       bwd_scale=K)
         _, opacity, depth, rend, _ = _Composite.apply(sig, rgb, torch.from_numpy(deltas), torch.from_numpy(ts),
                                                       torch.from_numpy(rays_a), 1e-4)
         out_rgb = rend + 1.0 * (1 - opacity)[:, None]
@@ -114,6 +123,17 @@ class CPUTrainer:
             w = losses_ref.w_sched(self.w_cluster, global_step)
             loss = loss + w * (losses_ref.validity(ort) + losses_ref.validity(cdot) + losses_ref.validity(cl1))
         loss.backward()
+        if self.emulate_bwd:  # GradScaler.step / update (torch defaults)
+            if not all(bool(torch.isfinite(p.grad).all()) for p in self.params):
+                self.opt.zero_grad()
+                self.amp_S *= 0.5
+                self.amp_tracker = 0
+                self.amp_skips += 1
+                return float(loss.detach()), int(counter[0])
+            self.amp_tracker += 1
+            if self.amp_tracker >= 2000:
+                self.amp_S *= 2.0
+                self.amp_tracker = 0
         torch.nn.utils.clip_grad_norm_(self.params, 0.05)
         self.opt.step()
         return float(loss.detach()), int(counter[0])

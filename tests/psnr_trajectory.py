@@ -83,7 +83,7 @@ PRESET_CLUSTER_W = {"hypersim": 2e-3, "scannet_manhattan": 1e-2}
 
 
 def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, impl="torch", emulate=None,
-            preset="hypersim"):
+            preset="hypersim", emulate_bwd=False, sampling="device"):
     from oracle import field_ref, grid_ref
     from oracle.train_ref import CPUTrainer, render_train_ref
     from ncnerf_amd import synthetic
@@ -91,7 +91,7 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
     torch.set_num_threads(threads)
     scene = SyntheticScene()
     cpu = CPUTrainer(scene.bitfield, seed=init_seed(member), num_epochs=30, epoch_steps=1000, encode_impl=impl,
-                     emulate=emulate, w_cluster=PRESET_CLUSTER_W[preset])
+                     emulate=emulate, w_cluster=PRESET_CLUSTER_W[preset], emulate_bwd=emulate_bwd)
     grid, _ = grid_ref.mark_invisible_cells(camera_K(), scene.poses, (synthetic.IMG_W, synthetic.IMG_H), 0.01, 128,
                                             0.5)
     ev = [scene.batch(N_RAYS, seed=s, gt=GT) for s in EVAL_SEEDS]
@@ -100,7 +100,8 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
         if k % 16 == 0:
             dens = lambda x: field_ref.density(torch.from_numpy(x), cpu.P, cpu.levels, impl=impl,  # noqa: E731
                                                emulate=emulate).numpy()
-            grid, thr, bf = grid_ref.grid_refresh(grid, dens, THRESHOLD, k < 256, grid_seed(k, member), 128, 0.5)
+            grid, thr, bf = grid_ref.grid_refresh(grid, dens, THRESHOLD, k < 256, grid_seed(k, member), 128, 0.5,
+                                                  sampling=sampling)
             cpu.bitfield = np.ascontiguousarray(bf, np.uint8)
         b = scene.batch(n_rays, seed=batch_seed(k, member), gt=GT)
         loss, S = cpu.step(b, global_step=k, noise=noise_of(k, n_rays, member).numpy())
@@ -117,7 +118,8 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
             log(json.dumps(curve[-1]))
             res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": n_rays, "gt": GT,
                    "member": member, "init_seed": init_seed(member), "encode_impl": impl, "emulate": emulate,
-                   "preset": preset, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
+                   "emulate_bwd": emulate_bwd, "grid_sampling": sampling, "amp_scale": cpu.amp_S,
+                   "amp_skips": cpu.amp_skips, "preset": preset, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
                    "curve": curve}
             if out:  # the trajectory so far (a partial run is usable up to its last checkpoint)
                 with open(out, "w") as f:
@@ -210,13 +212,18 @@ def main():
     ap.add_argument("--impl", default="torch", choices=("torch", "c"), help="(ref) the oracle's hash-grid statement")
     ap.add_argument("--emulate", default=None, choices=("fp16", "bf16"),
                     help="(ref) round the MLP operands as tcnn's fp16 FullyFusedMLP / the HIP kernel do")
+    ap.add_argument("--emulate-bwd", action="store_true",
+                    help="(ref, with --emulate) also round the field backward's gradients as the kernel's loss-scaled "
+                         "fp16 chain (with the GradScaler)")
+    ap.add_argument("--sampling", default="device", choices=("device", "reference"),
+                    help="(ref) the grid refresh's cell sampling: the device's (deviation 7) or the reference's draws")
     ap.add_argument("--cross-check", action="store_true",
                     help="(hip) also render the HIP parameters with the train-path renderer and the oracle's")
     a = ap.parse_args()
     log = lambda s: print(s, flush=True)  # noqa: E731
     if a.side == "ref":
         res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl,
-                      emulate=a.emulate, preset=a.preset)
+                      emulate=a.emulate, preset=a.preset, emulate_bwd=a.emulate_bwd, sampling=a.sampling)
     else:
         ref = json.load(open(a.ref)) if a.ref else None
         steps = ref["steps"] if ref else a.steps
