@@ -268,7 +268,7 @@ def distill_opaque(model, trainer, scene, dev, steps=300, n_points=1 << 16, sigm
         loss.backward()
         trainer.opt.step()
     torch.cuda.synchronize()
-    return round(float(loss), 4)
+    return round(float(loss.detach()), 4)
 
 
 def cpu_baseline(n_rays=2048, steps=20, warmup=3):
@@ -415,6 +415,7 @@ def main():
         # (ncn_count_samples: no per-step copies in the timed region)
         count_acc = torch.zeros(2, dtype=torch.float64, device=dev)
         trainer.render_kwargs["count_acc"] = count_acc
+        distill = None
         if state == "refreshed":
             fx = (synthetic.IMG_W / 2) / math.tan(synthetic.HFOV / 2)
             K = torch.tensor([[fx, 0, synthetic.IMG_W / 2], [0, fx, synthetic.IMG_H / 2], [0, 0, 1]])
@@ -424,6 +425,8 @@ def main():
             with torch.no_grad():
                 model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
                 model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
+            if state == "opaque":  # converged opaque surfaces (distill_opaque), then the same timed steps
+                distill = distill_opaque(model, trainer, scene, dev)
         if pretrain > 0:  # a pool of 64 batches
             pool = [scene.torch_batch(args.rays, seed=rank * 10007 + 1000 + i, device=dev, gt=GT) for i in range(64)]
             trainer.update_grid = state == "refreshed"
@@ -477,7 +480,8 @@ def main():
             rank_ms = [round(1e3 * float(g.item()) / steps, 3) for g in gathered]
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        return dict(el=float(elapsed.item()), tot=tot, rank_ms=rank_ms, timing=timing, model=model, batches=batches)
+        return dict(el=float(elapsed.item()), tot=tot, rank_ms=rank_ms, timing=timing, model=model, batches=batches,
+                    distill=distill)
 
     main_run = measure(args.precision, args.steps, True, args.pretrain)
     el, tot, rank_ms, timing = main_run["el"], main_run["tot"], main_run["rank_ms"], main_run["timing"]
@@ -508,8 +512,15 @@ def main():
                                                 "terminate early"),
                 ("pretrained_state", 500, "procedural",
                  "NGPMT trained 500 untimed steps on the procedural occupancy grid (not refreshed meanwhile), then "
-                 "the same timed steps: rays terminate early; the refreshes in the timed steps re-grow the grid "
-                 "from the trained model's densities"),
+                 "the same timed steps; the refreshes in the timed steps re-grow the grid from the trained model's "
+                 "densities.  No ray terminates early in this state (vr_samples_per_ray == rm_samples_per_ray: the "
+                 "photometric + opacity losses keep T well above 1e-4 on this room for thousands of steps, "
+                 "tools/trained_state_probe.py)"),
+                ("opaque_state", 0, "opaque",
+                 "converged opaque surfaces: the field's density fitted to the procedural room's occupancy "
+                 "(bench.distill_opaque: 300 untimed Adam steps on log sigma, sigma 3000 inside occupied voxels), then "
+                 "the same timed training steps: rays terminate at the first surface (vr_samples_per_ray << "
+                 "rm_samples_per_ray), the compositors' early-stop paths on every ray"),
                 ("refreshed_state", 500, "refreshed",
                  "the occupancy grid train_nerf.py maintains itself: mark_invisible_cells, then refreshed from the "
                  "model every 16 steps from step 0 (all cells for 256 steps) over 500 training steps; this "
@@ -517,16 +528,19 @@ def main():
             if pre == args.pretrain and st == "procedural":
                 continue  # (the headline measurement)
             r3 = measure(args.precision, args.steps, False, pre, st)
-            if key == "pretrained_state" and world == 1 and not args.no_eval_render:
+            if key == "opaque_state" and world == 1 and not args.no_eval_render:
                 extra["eval_render"] = dict(eval_render(r3["model"], SyntheticScene(), dev),
-                                            model="the pretrained_state model")
+                                            model="the opaque_state model (converged opaque surfaces)")
             n_r = args.rays * world * args.steps
             extra[key] = {"value": round(n_r / r3["el"], 1), "unit": "rays/s",
                           "ms_per_step": round(1e3 * r3["el"] / args.steps, 3),
                           "samples_per_s": round(float(r3["tot"][0].item()) / r3["el"], 1),
                           "vr_samples_per_s": round(float(r3["tot"][1].item()) / r3["el"], 1),
                           "rm_samples_per_ray": round(float(r3["tot"][0].item()) / n_r, 2),
+                          "vr_samples_per_ray": round(float(r3["tot"][1].item()) / n_r, 2),
                           "pretrain_steps": pre, "state": what}
+            if r3.get("distill") is not None:
+                extra[key]["distill_loss"] = r3["distill"]
             del r3
         # config #5's preset (ScanNet-Manhattan hyper-parameters: cluster weights 1e-2) on the same inputs
         r5 = measure(args.precision, args.steps, False, args.pretrain, "procedural", "scannet_manhattan")
@@ -574,6 +588,7 @@ def main():
         "samples_per_s": round(float(tot[0].item()) / el, 1),
         "vr_samples_per_s": round(float(tot[1].item()) / el, 1),
         "rm_samples_per_ray": round(float(tot[0].item()) / rays_total, 2),
+        "vr_samples_per_ray": round(float(tot[1].item()) / rays_total, 2),
         "roofline": {"kernel": "composite_train_fw (ncn_composite_train_fw_bg, the step's compositor)",
                      "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -1661,6 +1661,46 @@ __device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C
     }
 }
 
+// SC_CELL_CARRY: a lane's samples of a cell unit are ONE contiguous span over the unit's rounds
+// (round r takes the lane's next C), and the run in progress carries from round to round, so a run
+// record ends only where the cell changes (or at the span's end) instead of at every C-sample
+// chunk: on the coarsest levels (a ray stays ~30-40 samples in one level-0 cell) that is ~rounds x
+// fewer records, i.e. fewer same-slot 64-bit LDS adds (the coarse units' bound).
+#ifndef SC_CELL_CARRY
+#define SC_CELL_CARRY 0
+#endif
+struct ScRun {
+    uint32_t px, py, pz;
+    bool any, init;
+    float v[16];
+};
+template <int C>
+__device__ __forceinline__ void sc_cells_run(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
+                                             float* __restrict__ grad, ScRun& st, bool last) {
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        const LevelPos q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
+        const bool change = st.init && (q.px != st.px || q.py != st.py || q.pz != st.pz);
+        if (__ballot(change && st.any)) {  // uniform
+            bool act = change && st.any;
+            sc_add_cell(sh, lane, act, st.px, st.py, st.pz, st.v, L, grad);
+        }
+        if (change || !st.init) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) st.v[j] = 0.f;
+            st.any = false;
+            st.px = q.px; st.py = q.py; st.pz = q.pz;
+            st.init = true;
+        }
+        st.any = st.any || ch.g[i].x != 0.f || ch.g[i].y != 0.f;
+        sc_corner_sums(q, ch.g[i], st.v);
+    }
+    if (last && __ballot(st.any)) {  // uniform: the span's last run
+        bool act = st.any;
+        sc_add_cell(sh, lane, act, st.px, st.py, st.pz, st.v, L, grad);
+    }
+}
+
 // Flush of a cell unit: SC_CELL_VALS lanes per claimed cell (packed: one corner each, decode both
 // sums; 64-bit: one corner component each), form the corner's entry, f32 global adds; lane 0 of
 // the cell resets the key, each lane its value.
@@ -1856,14 +1896,23 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     // lane t of wave w takes chunk t * SC_WAVES + w (neighbouring chunks in different waves); (off)
     // SC_CELL_CONTIG: wave w covers the contiguous chunks 64w .. 64w+63 — measured: levels 6-9 alone
     // 37 -> 31 us, all levels 191 -> 193 us (no gain inside the full launch)
-    const int64_t lane_off = (SC_CELL_CONTIG ? (int64_t)wid * 64 + lane : (int64_t)lane * SC_WAVES + wid) * C;
+    const int64_t lane_id = SC_CELL_CONTIG ? (int64_t)wid * 64 + lane : (int64_t)lane * SC_WAVES + wid;
+    // round r's chunk of the lane: SC_CELL_CARRY — the lane's span is contiguous over the rounds;
+    // otherwise round r covers the unit's r-th slice of SC_THREADS * C samples
+    const int64_t lane_off = SC_CELL_CARRY ? lane_id * rounds * C : lane_id * C;
+    const int64_t r_step = SC_CELL_CARRY ? C : (int64_t)SC_THREADS * C;
     sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, nrm, order);
+    ScRun st;
+    st.init = st.any = false;
+    st.px = st.py = st.pz = 0;
     for (int r = 0; r < rounds; r++) {
         ScChunk<C> nx;
         const bool more = r + 1 < rounds;
-        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * SC_THREADS * C + lane_off, s1, xyzs, dEl, nrm, order);
+        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * r_step + lane_off, s1, xyzs, dEl, nrm, order);
         if (L.direct)
             sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
+        else if (SC_CELL_CARRY)
+            sc_cells_run<C>(sh, lane, ch, L, grad, st, !more);
         else
             sc_cells<C>(sh, lane, ch, L, grad);
         if (more) ch = nx;
