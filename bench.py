@@ -230,21 +230,27 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
                         "big_bytes": float(np.mean(big_bytes))}
 
 
-def _cpu_leg(threads, n_rays, steps, warmup):
+def _cpu_leg(threads, n_rays, steps, warmup, budget_s=30.0):
     from oracle.train_ref import CPUTrainer
     from ncnerf_amd.synthetic import SyntheticScene
     torch.set_num_threads(threads)
     scene = SyntheticScene()
     tr = CPUTrainer(scene.bitfield)
     for k in range(warmup):
+        t0 = time.perf_counter()
         tr.step(scene.batch(n_rays, seed=999 + k))
+        log(f"cpu leg ({threads} threads) warm-up step {k}: {1e3 * (time.perf_counter() - t0):.0f} ms")
     times = []
     for k in range(steps):
         b = scene.batch(n_rays, seed=k)
         t0 = time.perf_counter()
         tr.step(b)
         times.append(time.perf_counter() - t0)
-    return float(np.median(times)), float(sum(times))
+        if k % 5 == 4:
+            log(f"cpu leg ({threads} threads) step {k}: median {1e3 * float(np.median(times)):.0f} ms")
+        if sum(times) > budget_s and len(times) >= 3:
+            break  # bounded sample (an oversubscribed affinity mask can be far slower than the CPU share)
+    return float(np.median(times)), float(sum(times)), len(times)
 
 
 def distill_opaque(model, trainer, scene, dev, steps=300, n_points=1 << 16, sigma_in=3000.0, sigma_out=1e-2):
@@ -273,27 +279,30 @@ def distill_opaque(model, trainer, scene, dev, steps=300, n_points=1 << 16, sigm
 
 def cpu_baseline(n_rays=2048, steps=20, warmup=3):
     """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on the host cores),
-    timed as BASELINE.md §2 asks: median wall time of 20 steps after 3 warm-up steps, twice: on every
+    timed as BASELINE.md §2 asks: median wall time of 20 steps (fewer if a leg's timed steps pass
+    30 s) after 3 warm-up steps, twice: on every
     CPU of this process's affinity mask, and capped by OMP_NUM_THREADS when the box sets it (the GPU
     box's CPU share).  `value` is the faster of the two (the stronger baseline); both are reported."""
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count() or 1
-    legs = {"affinity": affinity}
+    legs = {}
     omp = os.environ.get("OMP_NUM_THREADS", "")
     if omp.isdigit() and int(omp) < affinity:
         legs["omp_num_threads"] = int(omp)
+    legs["affinity"] = affinity
     runs = {}
     for name, threads in legs.items():
-        med, tot = _cpu_leg(threads, n_rays, steps, warmup)
+        med, tot, n = _cpu_leg(threads, n_rays, steps, warmup)
+        log(f"cpu leg {name} ({threads} threads): {med * 1e3:.0f} ms/step")
         runs[name] = {"threads": threads, "rays_per_s": round(n_rays / med, 1), "ms_per_step": round(med * 1e3, 1),
-                      "timed_s": round(tot, 1)}
+                      "timed_steps": n, "timed_s": round(tot, 1)}
     best = max(runs, key=lambda k: runs[k]["rays_per_s"])
     torch.set_num_threads(legs.get("omp_num_threads", affinity))
     return {"value": runs[best]["rays_per_s"], "unit": "rays/s", "cores": runs[best]["threads"], "kind": "port",
             "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "legs": runs,
-            "sample": f"median of {steps} full training steps of {n_rays} rays (config #1) after {warmup} warm-up "
+            "sample": f"median of up to {steps} full training steps (at most ~30 s per leg) of {n_rays} rays (config #1) after {warmup} warm-up "
                       f"steps on the oracle CPU path (oracle/train_ref.py: C marcher/compositor + torch fp32 "
                       f"field/losses), once on all {affinity} CPUs of the affinity mask"
                       + (f" and once on OMP_NUM_THREADS={legs['omp_num_threads']}" if "omp_num_threads" in legs else "")
@@ -321,6 +330,7 @@ def eval_render(model, scene, dev, n_images=3):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             res.append((t1 - t0, st, float(out["opacity"].mean())))
+            log(f"eval_render image {cam}: {1e3 * (t1 - t0):.1f} ms, {st.get('iterations')} iterations")
     wall = float(np.median([r[0] for r in res]))
     its = [r[1].get("iterations", 0) for r in res]
     blocked = [r[1].get("blocked_s", 0.0) / r[0] for r in res]
@@ -332,6 +342,14 @@ def eval_render(model, scene, dev, n_images=3):
                       "loop on ncn_march_test / the field / ncn_composite_test_fw; median wall time of "
                       f"{n_images} images after one warm-up image; host_blocked_share = host time inside the "
                       "loop's syncing statements / wall time"}
+
+
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    print(f"[bench {time.time() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -407,6 +425,7 @@ def main():
         state "procedural": the procedural occupancy grid (BASELINE.md §2), fixed while pretraining;
         "refreshed": mark_invisible_cells, then the grid refreshed from the model every 16 steps from
         step 0 (all cells for the first 256), as train_nerf.py does."""
+        log(f"measure: {precision} {state} pretrain={pretrain} preset={preset}")
         scene = SyntheticScene()
         model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
         trainer = Trainer(model, update_grid=not args.no_grid_update, use_graph=not args.no_graph,
@@ -491,6 +510,7 @@ def main():
         if evs:
             ms = [a.elapsed_time(b) for a, b in evs]
             kern[name] = {"avg_us": round(1e3 * float(np.mean(ms)), 2), "launches": len(ms)}
+    log(f"main run: {args.rays * world * args.steps / el:.1f} rays/s; roofline launches")
     cf_bytes_per_launch, cf_t = composite_fw_roofline(model, batches, dev, SyntheticScene())
     cf_us = cf_t["hbm"]
     traffic, traffic_src = pmc_traffic()
@@ -529,6 +549,7 @@ def main():
                 continue  # (the headline measurement)
             r3 = measure(args.precision, args.steps, False, pre, st)
             if key == "opaque_state" and world == 1 and not args.no_eval_render:
+                log("eval_render")
                 extra["eval_render"] = dict(eval_render(r3["model"], SyntheticScene(), dev),
                                             model="the opaque_state model (converged opaque surfaces)")
             n_r = args.rays * world * args.steps
@@ -621,6 +642,7 @@ def main():
         out["other_precision"] = second
     out.update(extra)
     if world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline")
         out["cpu_baseline"] = cpu_baseline()
     print(json.dumps(out))
     if world > 1:
