@@ -239,7 +239,10 @@ def _cpu_leg(threads, n_rays, steps, warmup, budget_s=30.0):
     for k in range(warmup):
         t0 = time.perf_counter()
         tr.step(scene.batch(n_rays, seed=999 + k))
-        log(f"cpu leg ({threads} threads) warm-up step {k}: {1e3 * (time.perf_counter() - t0):.0f} ms")
+        dt = time.perf_counter() - t0
+        log(f"cpu leg ({threads} threads) warm-up step {k}: {1e3 * dt:.0f} ms")
+        if dt > 15.0:
+            return None, dt, 0  # oversubscribed (threads beyond the CPUs the process really gets)
     times = []
     for k in range(steps):
         b = scene.batch(n_rays, seed=k)
@@ -277,35 +280,65 @@ def distill_opaque(model, trainer, scene, dev, steps=300, n_points=1 << 16, sigm
     return round(float(loss.detach()), 4)
 
 
+def cpu_quota():
+    """CPUs of this process's cgroup CPU quota (cgroup v2 cpu.max, v1 cfs_quota_us), or None."""
+    for path, split in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            text = open(path).read().strip()
+            if split:
+                q, p = split(text)
+            else:
+                q, p = text, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()
+            if q in ("max", "-1"):
+                return None
+            return max(1, math.ceil(int(q) / int(p)))
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def cpu_baseline(n_rays=2048, steps=20, warmup=3):
     """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on the host cores),
     timed as BASELINE.md §2 asks: median wall time of 20 steps (fewer if a leg's timed steps pass
-    30 s) after 3 warm-up steps, twice: on every
-    CPU of this process's affinity mask, and capped by OMP_NUM_THREADS when the box sets it (the GPU
-    box's CPU share).  `value` is the faster of the two (the stronger baseline); both are reported."""
+    30 s) after 3 warm-up steps, on every CPU this process may use: one leg per distinct thread
+    count among OMP_NUM_THREADS (the GPU box's CPU share), the cgroup CPU quota and the affinity
+    mask.  A thread count above the cgroup quota is skipped and reported (on the GPU box the mask
+    holds 256 CPUs under a 16-CPU quota: 256 threads took 80 s per step, round 4).  `value` is the
+    fastest leg (the stronger baseline); every leg is reported."""
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count() or 1
+    quota = cpu_quota()
+    usable = min(affinity, quota) if quota else affinity
     legs = {}
     omp = os.environ.get("OMP_NUM_THREADS", "")
-    if omp.isdigit() and int(omp) < affinity:
+    if omp.isdigit() and 0 < int(omp) < usable:
         legs["omp_num_threads"] = int(omp)
-    legs["affinity"] = affinity
-    runs = {}
+    legs["all_usable_cpus"] = usable
+    runs, skipped = {}, {}
+    if affinity > usable:
+        skipped["affinity"] = f"{affinity} CPUs in the affinity mask > cgroup CPU quota {quota}: oversubscribed"
     for name, threads in legs.items():
         med, tot, n = _cpu_leg(threads, n_rays, steps, warmup)
+        if med is None:
+            skipped[name] = f"{threads} threads: a warm-up step took {tot:.0f} s (oversubscribed); leg abandoned"
+            log(f"cpu leg {name}: {skipped[name]}")
+            continue
         log(f"cpu leg {name} ({threads} threads): {med * 1e3:.0f} ms/step")
         runs[name] = {"threads": threads, "rays_per_s": round(n_rays / med, 1), "ms_per_step": round(med * 1e3, 1),
                       "timed_steps": n, "timed_s": round(tot, 1)}
     best = max(runs, key=lambda k: runs[k]["rays_per_s"])
-    torch.set_num_threads(legs.get("omp_num_threads", affinity))
+    torch.set_num_threads(legs.get("omp_num_threads", usable))
     return {"value": runs[best]["rays_per_s"], "unit": "rays/s", "cores": runs[best]["threads"], "kind": "port",
-            "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "legs": runs,
-            "sample": f"median of up to {steps} full training steps (at most ~30 s per leg) of {n_rays} rays (config #1) after {warmup} warm-up "
-                      f"steps on the oracle CPU path (oracle/train_ref.py: C marcher/compositor + torch fp32 "
-                      f"field/losses), once on all {affinity} CPUs of the affinity mask"
-                      + (f" and once on OMP_NUM_THREADS={legs['omp_num_threads']}" if "omp_num_threads" in legs else "")
+            "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cpu_quota": quota, "legs": runs,
+            "skipped_legs": skipped,
+            "sample": f"median of up to {steps} full training steps (at most ~30 s per leg) of {n_rays} rays "
+                      f"(config #1) after {warmup} warm-up steps on the oracle CPU path (oracle/train_ref.py: C "
+                      f"marcher/compositor + torch fp32 field/losses), on all {usable} usable CPUs "
+                      f"(min of affinity mask {affinity} and cgroup quota {quota})"
+                      + (f" and on OMP_NUM_THREADS={legs['omp_num_threads']}" if "omp_num_threads" in legs else "")
                       + f"; value = the faster ({best})"}
 
 
