@@ -1020,17 +1020,26 @@ constexpr int SC_REC = 64;                 // staged run records per wave (80 B 
 #endif
 constexpr bool SC_PACK = NCN_SC_PACK != 0;
 constexpr int SC_SLOT_BYTES = SC_PACK ? 4 + 8 + 2 : 4 + 8 + 8 + 2;
+// Direct-layout (fine) levels: NCN_SC_F32_DIR = 1 sums an entry's (x, y) in a unit with two f32 LDS
+// atomics into one 8-B slot value (float x, float y) instead of two 64-bit fixed-point sums: half
+// the LDS bytes per corner and 14-B slots (more sets in the same LDS), at the price of a unit sum
+// that depends on the order of its adds (f32 rounding; tcnn sums in fp16 atomics).
+#ifndef NCN_SC_F32_DIR
+#define NCN_SC_F32_DIR 0
+#endif
+constexpr bool SC_F32_DIR = NCN_SC_F32_DIR != 0 && !SC_PACK;
+constexpr int SC_DIR_SLOT_BYTES = SC_F32_DIR ? 4 + 8 + 2 : SC_SLOT_BYTES;
 // Two LDS layouts over one arena: run levels (sets + the record staging, 80 KB at 1024 threads);
 // direct levels (sets only).  Unpacked: 768 / 1536 sets (66 / 132 KB); packed: 1152 / 2560.
 #ifndef NCN_SC_SETS_RUN
 #define NCN_SC_SETS_RUN (SC_PACK ? 1152 : 768)
 #endif
 #ifndef NCN_SC_SETS_DIR
-#define NCN_SC_SETS_DIR (SC_PACK ? 2560 : 1536)
+#define NCN_SC_SETS_DIR (SC_PACK ? 2560 : SC_F32_DIR ? 2432 : 1536)
 #endif
 constexpr int SC_SETS_RUN = NCN_SC_SETS_RUN * SC_THREADS / 1024, SC_SETS_DIR = NCN_SC_SETS_DIR * SC_THREADS / 1024;
 constexpr int sc_layout_bytes(int sets, bool staging) {
-    return sets * SC_WAYS * SC_SLOT_BYTES + (staging ? SC_WAVES * SC_REC * 80 : 0);
+    return sets * SC_WAYS * (staging ? SC_SLOT_BYTES : SC_DIR_SLOT_BYTES) + (staging ? SC_WAVES * SC_REC * 80 : 0);
 }
 // Cell-keyed layout (the coarse levels [0, SC_CELL_HI)): a slot is one grid CELL of the level and
 // holds the packed sums of its 8 corners (corner-major: vals[c * slots + slot]); 70 B per slot.
@@ -1039,11 +1048,18 @@ constexpr int sc_layout_bytes(int sets, bool staging) {
 #endif
 // Values per cell slot: 8 packed words (SC_PACK) or 16 64-bit sums (x and y of the 8 corners).
 constexpr int SC_CELL_VALS = SC_PACK ? 8 : 16;
+// NCN_SC_F32_CELL = 1: the 16 sums of a cell slot as f32 LDS atomics (4 B each: 70-B slots, 480
+// sets in the same LDS) instead of 64-bit fixed point (see NCN_SC_F32_DIR).
+#ifndef NCN_SC_F32_CELL
+#define NCN_SC_F32_CELL 0
+#endif
+constexpr bool SC_F32_CELL = NCN_SC_F32_CELL != 0 && !SC_PACK;
+constexpr int SC_CELL_WORDS = SC_F32_CELL ? 8 : SC_CELL_VALS;  // 8-B words of values per slot
 #ifndef NCN_SC_SETS_CELL
-#define NCN_SC_SETS_CELL (SC_PACK ? 512 : 256)
+#define NCN_SC_SETS_CELL (SC_PACK ? 512 : SC_F32_CELL ? 480 : 256)
 #endif
 constexpr int SC_SETS_CELL = NCN_SC_SETS_CELL * SC_THREADS / 1024;
-constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2); }
+constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + SC_CELL_WORDS * 8 + 2); }
 constexpr int sc_max(int a, int b) { return a > b ? a : b; }
 constexpr int SC_ARENA = sc_max(sc_cell_bytes(SC_SETS_CELL),
                                 sc_max(sc_layout_bytes(SC_SETS_RUN, true), sc_layout_bytes(SC_SETS_DIR, false)));
@@ -1123,7 +1139,8 @@ __device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fil
     sh.slots = (int)sh.sets * SC_WAYS;
     sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used, records (16-B aligned)
     // (packed: one value array; cell mode: 8 corner arrays)
-    sh.valy = mode == SC_MODE_CELL ? sh.valx + (SC_CELL_VALS - 1) * sh.slots : SC_PACK ? sh.valx : sh.valx + sh.slots;
+    sh.valy = mode == SC_MODE_CELL ? sh.valx + (SC_CELL_WORDS - 1) * sh.slots
+            : SC_PACK || (SC_F32_DIR && mode == SC_MODE_DIR) ? sh.valx : sh.valx + sh.slots;
     sh.keys = (uint32_t*)(sh.valy + sh.slots);
     sh.used = (uint16_t*)(sh.keys + sh.slots);
     sh.rec = (ScRec*)(sh.used + sh.slots);
@@ -1137,6 +1154,7 @@ struct ScLevel {
     float scale;
     uint32_t res, params, off;
     bool dense, direct;
+    bool f32;  // (SC_F32_DIR) f32 slot sums
     int k;
 };
 
@@ -1242,6 +1260,10 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
 #ifndef NCN_DIAG_SC_NO_LDSADD
                 if constexpr (SC_PACK) {
                     atomicAdd((unsigned long long*)&sh.valx[sl[b]], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
+                } else if (SC_F32_DIR && L.f32) {
+                    float* pf = (float*)&sh.valx[sl[b]];
+                    atomicAdd(pf, v[2 * c]);
+                    atomicAdd(pf + 1, v[2 * c + 1]);
                 } else {
                     atomicAdd((unsigned long long*)&sh.valx[sl[b]], (unsigned long long)sc_fix(v[2 * c], L.k));
                     atomicAdd((unsigned long long*)&sh.valy[sl[b]], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
@@ -1559,6 +1581,9 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
             if ((v[2 * c] == 0.f && v[2 * c + 1] == 0.f) || ((exm >> c) & 1)) continue;
             if constexpr (SC_PACK) {
                 atomicAdd((unsigned long long*)&sh.valx[c * sh.slots + sl], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
+            } else if constexpr (SC_F32_CELL) {  // f32 arrays 2c, 2c + 1
+                atomicAdd((float*)sh.valx + (2 * c) * sh.slots + sl, v[2 * c]);
+                atomicAdd((float*)sh.valx + (2 * c + 1) * sh.slots + sl, v[2 * c + 1]);
             } else {  // x and y of corner c: arrays 2c, 2c + 1
                 atomicAdd((unsigned long long*)&sh.valx[(2 * c) * sh.slots + sl], (unsigned long long)sc_fix(v[2 * c], L.k));
                 atomicAdd((unsigned long long*)&sh.valx[(2 * c + 1) * sh.slots + sl],
@@ -1710,9 +1735,18 @@ __device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, f
     for (int i = threadIdx.x; i < V * nf; i += SC_THREADS) {
         const int slot = sh.used[i / V], j = i % V;
         const uint32_t key = sh.keys[slot];
-        long long* pv = &sh.valx[j * sh.slots + slot];
-        const long long q = *pv;
-        *pv = 0;
+        long long q;
+        float qf = 0.f;
+        if constexpr (SC_F32_CELL) {
+            float* pf = (float*)sh.valx + j * sh.slots + slot;
+            qf = *pf;
+            *pf = 0.f;
+            q = qf != 0.f;
+        } else {
+            long long* pv = &sh.valx[j * sh.slots + slot];
+            q = *pv;
+            *pv = 0;
+        }
 #ifndef NCN_DIAG_SC_NO_FLUSH
         if (q != 0) {
             const int c = SC_PACK ? j : j >> 1;
@@ -1722,6 +1756,8 @@ __device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, f
                 sc_unpack(q, xs, ys);
                 if (xs) atomicAdd(grad + 2 * (size_t)e, ldexpf((float)xs, -L.k));
                 if (ys) atomicAdd(grad + 2 * (size_t)e + 1, ldexpf((float)ys, -L.k));
+            } else if constexpr (SC_F32_CELL) {
+                atomicAdd(grad + 2 * (size_t)e + (j & 1), qf);
             } else {
                 atomicAdd(grad + 2 * (size_t)e + (j & 1), (float)ldexp((double)q, -L.k));
             }
@@ -1769,6 +1805,7 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     L.dense = (uint64_t)L.res * L.res * L.res <= L.params;  // tcnn: stride stays <= params
     // levels >= SC_DIRECT_FROM: every run's corners straight to global f32 atomics (no LDS table)
     L.direct = !isfinite(m) || l >= SC_DIRECT_FROM;
+    L.f32 = SC_F32_DIR && !RUNS;
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
     // An entry's sum over the unit is at most (unit samples) * m (a sample's 8 corner weights sum
@@ -1832,7 +1869,10 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
         long long* pv = (i & 1) ? &sh.valy[slot] : &sh.valx[slot];
         const long long q = *pv;
         float gv;
-        if constexpr (SC_PACK) {  // both lanes of the pair read the word; the odd one resets it
+        if (SC_F32_DIR && L.f32) {  // (float x, float y) in one word: the odd lane resets it
+            gv = ((const float*)pv)[i & 1];
+            if (i & 1) *pv = 0;
+        } else if constexpr (SC_PACK) {  // both lanes of the pair read the word; the odd one resets it
             int xs, ys;
             sc_unpack(q, xs, ys);
             gv = ldexpf((float)((i & 1) ? ys : xs), -L.k);
@@ -1943,7 +1983,8 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
     if (mode != layout) {  // (re)initialise the table of the new layout
         lds_barrier();
         sh = sc_layout(arena, wmax, fill, mode);
-        const int nv = mode == SC_MODE_CELL ? SC_CELL_VALS * sh.slots : SC_PACK ? sh.slots : 2 * sh.slots;
+        const int nv = mode == SC_MODE_CELL ? SC_CELL_WORDS * sh.slots
+                     : SC_PACK || (SC_F32_DIR && mode == SC_MODE_DIR) ? sh.slots : 2 * sh.slots;
         for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
         for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
         if (threadIdx.x == 0) fill[0] = fill[1] = fill[2] = fill[3] = 0;

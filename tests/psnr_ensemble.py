@@ -7,6 +7,8 @@ measured over seed ensembles on both sides:
       python tests/psnr_trajectory.py ref --member m --rays 2048 --steps 1000 --every 125 --impl c
     for members m = 0..M-1, then  python tests/psnr_ensemble.py merge <files...>;
   * HIP side (GPU):  python tests/psnr_ensemble.py hip --repeats R --out profiles/<round>/psnr_ensemble.json
+  * offline:  python tests/psnr_ensemble.py compare A.json B.json [--out C.json] — A (a HIP output or
+    another oracle ensemble) against the oracle ensemble B, paired by member
     member m with the same initial parameters, batches, marcher noise and refresh seeds, R runs
     each (they differ only by the float-atomic order of the table-gradient flush).
 Statistics per checkpoint: the mean PSNR and its standard error on each side (HIP: the mean of a
@@ -102,7 +104,7 @@ def run_hip_ensemble(members, repeats, steps, every, n_rays, log, preset="hypers
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=("merge", "hip"))
+    ap.add_argument("mode", choices=("merge", "hip", "compare"))
     ap.add_argument("files", nargs="*")
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--members", type=int, default=None, help="(hip) first M members of the fixture")
@@ -112,6 +114,21 @@ def main():
     a = ap.parse_args()
     if a.mode == "merge":
         merge(a.files, a.out or a.fixture)
+        return
+    if a.mode == "compare":
+        # compare A B: paired statistics of A (a hip ensemble output, or an oracle ensemble fixture
+        # taken as one run per member) against the oracle ensemble B, offline
+        ra, ob = json.load(open(a.files[0])), json.load(open(a.files[1]))
+        if "hip_runs" in ra:
+            runs = {int(k): v for k, v in ra["hip_runs"].items()}
+        else:
+            runs = {m["member"]: [m["curve"]] for m in ra["members"]}
+        st = stats(ob, runs)
+        for s in st:
+            print(json.dumps(s))
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump({"a": a.files[0], "b": a.files[1], "stats": st}, f, indent=1)
         return
     log = lambda s: print(s, flush=True)  # noqa: E731
     oracle = json.load(open(a.fixture))
