@@ -50,11 +50,21 @@ def merge(files, out=FIXTURE):
                         "steps": r["steps"], "curve": [{"step": c["step"], "psnr": round(c["psnr"], 5),
                                                         "loss": round(c["loss"], 7)} for c in r["curve"]]})
     members.sort(key=lambda m: m["member"])
-    preset = json.load(open(files[0])).get("preset", "hypersim")
-    res = {"side": "oracle CPU (fp32), oracle/train_ref.py with the C hash-grid statement", "gt": "surface_bright",
-           "eval_rays": 16384, "members": members, "preset": preset,
+    first = json.load(open(files[0]))
+    preset = first.get("preset", "hypersim")
+    emulate, emulate_bwd = first.get("emulate"), bool(first.get("emulate_bwd"))
+    sampling = first.get("grid_sampling", "device")
+    flags = ((f" --emulate {emulate}" if emulate else "") + (" --emulate-bwd" if emulate_bwd else "")
+             + ("" if sampling == "device" else f" --sampling {sampling}")
+             + ("" if preset == "hypersim" else f" --preset {preset}"))
+    side = ("oracle CPU (fp32), oracle/train_ref.py with the C hash-grid statement" if not emulate else
+            f"oracle CPU, oracle/train_ref.py with the C hash-grid statement, MLP operands rounded to {emulate}"
+            + (" and the field backward's loss-scaled fp16 gradient chain emulated (GradScaler)" if emulate_bwd else "")
+            + f"; grid refresh sampling: {sampling}")
+    res = {"side": side, "gt": "surface_bright", "eval_rays": 16384, "members": members, "preset": preset,
+           "emulate": emulate, "emulate_bwd": emulate_bwd, "grid_sampling": sampling,
            "generator": "python tests/psnr_trajectory.py ref --member m --rays 2048 --steps 1000 --every 125 --impl c"
-                        + ("" if preset == "hypersim" else f" --preset {preset}")}
+                        + flags}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(f"{out}: {len(members)} members")
