@@ -191,6 +191,10 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
 #define NCN_PREC_F16 0
 #define NCN_PREC_BF16 1
 int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int precision, void* stream);
+/* The packing's map: src_index[q] (NCN_FIELD_PACKED_HALVES int32) = the master weight index (into the
+ * NCN_FIELD_NW floats) that packed element q holds; every master weight appears at most twice (its
+ * forward and its transposed backward fragment).  Used to build ncn_adam_step_packed's pack_inv. */
+int ncn_field_pack_map(int32_t* src_index, void* stream);
 /* Processing order of a training batch (no reference counterpart: tcnn evaluates in input order):
  * every window of 4096 consecutive samples sorted by the 30-bit Morton code of its normalised
  * positions; order[p] = the sample evaluated at position p (n int32, a permutation of each window).
@@ -401,6 +405,17 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 #define NCN_TCNN_LOSS_SCALE 128.0f /* tcnn fp16 module loss scale (ncn_field_bwd) */
 #define NCN_AMP_GROWTH_INTERVAL 2000
 int64_t ncn_adam_step_work_floats(void);
+/* ncn_adam_step that also refreshes the field's packed MLP fragments (the ncn_field_pack_weights
+ * launch between the optimizer and the next forward, folded into the Adam pass): the parameters
+ * [pack_off, n) are the NCN_FIELD_NW master weights; pack_inv (NCN_FIELD_NW x 2 int32, -1 = none,
+ * built from ncn_field_pack_map) lists the packed elements of each; `packed` receives the updated
+ * (or, on a skipped step, the unchanged) weights rounded to pack_prec (NCN_PREC_F16 / _BF16) — the
+ * same values ncn_field_pack_weights writes. */
+int ncn_adam_step_packed(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+                         float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0,
+                         float wd1, const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state,
+                         const int* gate, const int32_t* pack_inv, int64_t pack_off, uint16_t* packed, int pack_prec,
+                         void* stream);
 /* Data-parallel gradient wire format (replaces DDP's fp16 gradient buckets, train_nerf.py:944-952:
  * the reference's tcnn parameters and gradients are fp16 at the GradScaler's scale, and torch DDP's
  * default hook divides each bucket by the world size before the all-reduce SUM,

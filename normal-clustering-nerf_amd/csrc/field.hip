@@ -116,22 +116,34 @@ __host__ __device__ constexpr int psi(int g, int j) {
     return j < 4 ? 3 + 4 * g + j : ((4 * g + j - 4) < 3 ? (4 * g + j - 4) : 16 + (4 * g + j - 4));
 }
 
-__device__ float frag32_value(const float* __restrict__ W, int f, int lane, int j) {
+// index into the concatenated master weights of packed element (f, lane, j)
+__host__ __device__ constexpr int frag32_index(int f, int lane, int j) {
     const int g = lane >> 4, r = lane & 15, k = phi(g, j);
-    if (f < F_L2) return W[W1_OFF + (16 * (f - F_L1) + r) * 32 + k];
-    if (f < F_L3) return W[W2_OFF + r * 64 + 32 * (f - F_L2) + k];
-    if (f < F_L4) return W[W3_OFF + (16 * (f - F_L3) + r) * 32 + psi(g, j)];
-    if (f < F_L5) { const int t = (f - F_L4) >> 1, s = (f - F_L4) & 1; return W[W4_OFF + (16 * t + r) * 64 + 32 * s + k]; }
-    if (f < B_L4) return W[W5_OFF + r * 64 + 32 * (f - F_L5) + k];
-    if (f < B_L3) { const int t = (f - B_L4) >> 1, s = (f - B_L4) & 1; return W[W4_OFF + (32 * s + k) * 64 + 16 * t + r]; }
-    if (f < B_L1) return W[W3_OFF + (32 * (f - B_L3) + k) * 32 + 3 + r];
-    const int t = (f - B_L1) >> 1, s = (f - B_L1) & 1;
-    return W[W1_OFF + (32 * s + k) * 32 + 16 * t + r];
+    if (f < F_L2) return W1_OFF + (16 * (f - F_L1) + r) * 32 + k;
+    if (f < F_L3) return W2_OFF + r * 64 + 32 * (f - F_L2) + k;
+    if (f < F_L4) return W3_OFF + (16 * (f - F_L3) + r) * 32 + psi(g, j);
+    if (f < F_L5) return W4_OFF + (16 * ((f - F_L4) >> 1) + r) * 64 + 32 * ((f - F_L4) & 1) + k;
+    if (f < B_L4) return W5_OFF + r * 64 + 32 * (f - F_L5) + k;
+    if (f < B_L3) return W4_OFF + (32 * ((f - B_L4) & 1) + k) * 64 + 16 * ((f - B_L4) >> 1) + r;
+    if (f < B_L1) return W3_OFF + (32 * (f - B_L3) + k) * 32 + 3 + r;
+    return W1_OFF + (32 * ((f - B_L1) & 1) + k) * 32 + 16 * ((f - B_L1) >> 1) + r;
 }
-__device__ float frag16_value(const float* __restrict__ W, int f, int lane, int j) {
+__host__ __device__ constexpr int frag16_index(int f, int lane, int j) {
     const int g = lane >> 4, r = lane & 15, k = 4 * g + j;
-    if (f < B_L2) return W[W5_OFF + k * 64 + 16 * (f - B_L5) + r];
-    return W[W2_OFF + k * 64 + 16 * (f - B_L2) + r];
+    return f < B_L2 ? W5_OFF + k * 64 + 16 * (f - B_L5) + r : W2_OFF + k * 64 + 16 * (f - B_L2) + r;
+}
+__device__ float frag32_value(const float* __restrict__ W, int f, int lane, int j) { return W[frag32_index(f, lane, j)]; }
+__device__ float frag16_value(const float* __restrict__ W, int f, int lane, int j) { return W[frag16_index(f, lane, j)]; }
+
+// packed position -> master weight index (ncn_field_pack_map)
+__global__ void pack_map_kernel(int32_t* __restrict__ src) {
+    const int f = blockIdx.x, lane = threadIdx.x;
+    if (f < N_FRAG32) {
+        for (int j = 0; j < 8; j++) src[(f * 64 + lane) * 8 + j] = frag32_index(f, lane, j);
+    } else {
+        const int f16 = f - N_FRAG32;
+        for (int j = 0; j < 4; j++) src[N_FRAG32 * 512 + (f16 * 64 + lane) * 4 + j] = frag16_index(f16, lane, j);
+    }
 }
 
 template <typename T>
@@ -2195,6 +2207,12 @@ static void launch_bwd_part(int precision, int nb, hipStream_t st, const float* 
 }
 
 extern "C" {
+
+int ncn_field_pack_map(int32_t* src_index, void* stream) {
+    hipLaunchKernelGGL(pack_map_kernel, dim3(N_FRAG32 + N_FRAG16), dim3(64), 0, (hipStream_t)stream, src_index);
+    NCN_LAUNCH_CHECK("ncn_field_pack_map");
+    return 0;
+}
 
 int ncn_field_pack_weights(const float* w_master, uint16_t* weights_packed, int precision, void* stream) {
     NCN_REQUIRE(precision == NCN_PREC_F16 || precision == NCN_PREC_BF16, hipErrorInvalidValue,

@@ -201,13 +201,38 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
 #else
 #define NCN_ADAM_ATTR
 #endif
-template <bool ZERO>
+// Packed-fragment refresh folded into the Adam pass (PK: 0 none, 1 fp16, 2 bf16): parameter e in
+// [poff, n) is master weight e - poff, written rounded to the operand type at its (up to two)
+// packed positions pinv[2 (e - poff) + {0, 1}].
+template <int PK>
+__device__ __forceinline__ void adam_pack1(int64_t e, float x, const int32_t* __restrict__ pinv, int64_t poff,
+                                           int64_t n, void* __restrict__ packed) {
+    if (PK == 0 || e < poff || e >= n) return;
+    const int64_t w = e - poff;
+    const int2 q = ((const int2*)pinv)[w];
+    if (PK == 1) {
+        const _Float16 h = (_Float16)x;
+        if (q.x >= 0) ((_Float16*)packed)[q.x] = h;
+        if (q.y >= 0) ((_Float16*)packed)[q.y] = h;
+    } else {
+        const __bf16 h = (__bf16)x;
+        if (q.x >= 0) ((__bf16*)packed)[q.x] = h;
+        if (q.y >= 0) ((__bf16*)packed)[q.y] = h;
+    }
+}
+template <bool ZERO, int PK>
 __global__ __launch_bounds__(256) NCN_ADAM_ATTR void adam_apply_kernel(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                          int64_t n0, float b1, float b2, float eps, float wd0,
-                                                         float wd1, const float* __restrict__ sc) {
+                                                         float wd1, const float* __restrict__ sc,
+                                                         const int32_t* __restrict__ pinv, int64_t poff,
+                                                         void* __restrict__ packed) {
     const float cf = sc[0], bc1 = sc[1], bc2 = sc[2], lr = sc[3];
     if (sc[4] != 0.f) {  // (uniform) skipped AMP step: only the gradient is consumed
+        if (PK) {  // (the packed fragments re-written from the unchanged weights: always consistent)
+            const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
+            for (int64_t e = poff + tid; e < n; e += nth) adam_pack1<PK>(e, p[e], pinv, poff, n, packed);
+        }
         if (ZERO) {
             const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nth = (int64_t)gridDim.x * 256;
             for (int64_t i = tid; i < n / 4; i += nth) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -235,6 +260,12 @@ __global__ __launch_bounds__(256) NCN_ADAM_ATTR void adam_apply_kernel(float* __
         ((float4*)p)[i] = P;
         ((float4*)m)[i] = M;
         ((float4*)v)[i] = V;
+        if (PK && e + 3 >= poff) {
+            adam_pack1<PK>(e, P.x, pinv, poff, n, packed);
+            adam_pack1<PK>(e + 1, P.y, pinv, poff, n, packed);
+            adam_pack1<PK>(e + 2, P.z, pinv, poff, n, packed);
+            adam_pack1<PK>(e + 3, P.w, pinv, poff, n, packed);
+        }
         // (the table gradient is sparse — most hash entries get no contribution in a step — so only
         // the non-zero float4s are written back as zeros: less HBM write traffic, same contents)
         if (ZERO && (G.x != 0.f || G.y != 0.f || G.z != 0.f || G.w != 0.f))
@@ -242,6 +273,7 @@ __global__ __launch_bounds__(256) NCN_ADAM_ATTR void adam_apply_kernel(float* __
     }
     for (int64_t i = 4 * n4 + tid; i < n; i += nth) {
         upd(p[i], g[i], m[i], v[i], i < n0 ? wd0 : wd1);
+        adam_pack1<PK>(i, p[i], pinv, poff, n, packed);
         if (ZERO) g[i] = 0.f;
     }
 }
@@ -378,10 +410,25 @@ int ncn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_s
     return 0;
 }
 
-int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
-                  float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
-                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, const int* gate,
-                  void* stream) {
+}  // extern "C"
+
+template <int PK>
+static void launch_apply(int zero, int blocks, hipStream_t st, float* params, float* grads, float* exp_avg,
+                         float* exp_avg_sq, int64_t n, int64_t n_group0, double beta1, double beta2, float eps,
+                         float wd0, float wd1, const float* sc, const int32_t* pinv, int64_t poff, void* packed) {
+    if (zero)
+        hipLaunchKernelGGL((adam_apply_kernel<true, PK>), dim3(blocks), dim3(256), 0, st, params, grads, exp_avg,
+                           exp_avg_sq, n, n_group0, (float)beta1, (float)beta2, eps, wd0, wd1, sc, pinv, poff, packed);
+    else
+        hipLaunchKernelGGL((adam_apply_kernel<false, PK>), dim3(blocks), dim3(256), 0, st, params, grads, exp_avg,
+                           exp_avg_sq, n, n_group0, (float)beta1, (float)beta2, eps, wd0, wd1, sc, pinv, poff, packed);
+}
+
+static int adam_step_impl(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+                          float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0,
+                          float wd1, const float* lr_dev, int* step_dev, float* work, int zero_grads,
+                          float* amp_state, const int* gate, const int32_t* pinv, int64_t poff, void* packed, int pk,
+                          void* stream) {
     if (n <= 0) return 0;
     NCN_REQUIRE(((((uintptr_t)params) | ((uintptr_t)grads) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) == 0,
                 hipErrorInvalidValue, "ncn_adam_step: buffers must be 16-byte aligned");
@@ -393,16 +440,42 @@ int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     NCN_LAUNCH_CHECK("ncn_adam_step (prep)");
     // two float4 per thread (8 loads of p/g/m/v in flight): ~n/2048 workgroups
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, cdiv(n, 2048)), 16384);
-    if (zero_grads)
-        hipLaunchKernelGGL(adam_apply_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
-                           exp_avg, exp_avg_sq, n, n_group0, (float)beta1, (float)beta2, eps, wd0, wd1,
-                           work + ADAM_BLOCKS + 4);
+    const float* sc = work + ADAM_BLOCKS + 4;
+    const hipStream_t st = (hipStream_t)stream;
+    if (pk == 0)
+        launch_apply<0>(zero_grads, blocks, st, params, grads, exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0,
+                        wd1, sc, nullptr, 0, nullptr);
+    else if (pk == 1)
+        launch_apply<1>(zero_grads, blocks, st, params, grads, exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0,
+                        wd1, sc, pinv, poff, packed);
     else
-        hipLaunchKernelGGL(adam_apply_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
-                           exp_avg, exp_avg_sq, n, n_group0, (float)beta1, (float)beta2, eps, wd0, wd1,
-                           work + ADAM_BLOCKS + 4);
+        launch_apply<2>(zero_grads, blocks, st, params, grads, exp_avg, exp_avg_sq, n, n_group0, beta1, beta2, eps, wd0,
+                        wd1, sc, pinv, poff, packed);
     NCN_LAUNCH_CHECK("ncn_adam_step");
     return 0;
+}
+
+extern "C" {
+
+int ncn_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+                  float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0, float wd1,
+                  const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state, const int* gate,
+                  void* stream) {
+    return adam_step_impl(params, grads, exp_avg, exp_avg_sq, n, n_group0, grad_scale, max_norm, lr, beta1, beta2, eps,
+                          wd0, wd1, lr_dev, step_dev, work, zero_grads, amp_state, gate, nullptr, 0, nullptr, 0, stream);
+}
+
+int ncn_adam_step_packed(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, int64_t n_group0,
+                         float grad_scale, float max_norm, float lr, double beta1, double beta2, float eps, float wd0,
+                         float wd1, const float* lr_dev, int* step_dev, float* work, int zero_grads, float* amp_state,
+                         const int* gate, const int32_t* pack_inv, int64_t pack_off, uint16_t* packed, int pack_prec,
+                         void* stream) {
+    NCN_REQUIRE(pack_inv && packed && (pack_prec == NCN_PREC_F16 || pack_prec == NCN_PREC_BF16) && pack_off >= 0 &&
+                    n - pack_off == NCN_FIELD_NW && (((uintptr_t)pack_inv) & 7) == 0,
+                hipErrorInvalidValue, "ncn_adam_step_packed: pack_inv/packed/pack_prec/pack_off invalid");
+    return adam_step_impl(params, grads, exp_avg, exp_avg_sq, n, n_group0, grad_scale, max_norm, lr, beta1, beta2, eps,
+                          wd0, wd1, lr_dev, step_dev, work, zero_grads, amp_state, gate, pack_inv, pack_off, packed,
+                          pack_prec == NCN_PREC_F16 ? 1 : 2, stream);
 }
 
 int64_t ncn_adam_step_work_floats(void) { return ADAM_BLOCKS + 12; }

@@ -46,6 +46,7 @@ SIGNATURES = {
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, I32, P],
+    "ncn_field_pack_map": [P, P],
     "ncn_field_sort_windows": [P, I64, P, F32, F32, P, P],
     "ncn_field_fwd": [P, P, I64, P, P, P, P, F32, F32, P, I32, I32, P, P, P, P],
     "ncn_field_bwd_blocks": [I64],
@@ -74,6 +75,8 @@ SIGNATURES = {
     "ncn_sumsq": [P, I64, P, P, P],
     "ncn_adam": [P, P, P, P, I64, P, F32, F32, F32, F32, F32, F32, I32, P, P, P],
     "ncn_adam_step": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P, P, P],
+    "ncn_adam_step_packed": [P, P, P, P, I64, I64, F32, F32, F32, F64, F64, F32, F32, F32, P, P, P, I32, P, P,
+                             P, I64, P, I32, P],
     "ncn_adam_step_work_floats": [],
     "ncn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "ncn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],

@@ -280,6 +280,27 @@ class NGPMT(nn.Module):
             return self._packed
         return self._pack_weights()
 
+    def pack_target(self):
+        """(pack_inv, pack_off, packed, precision) for ncn_adam_step_packed: the optimizer refreshes
+        the packed MLP fragments itself (no pack launch between it and the next forward).  pack_inv
+        (NCN_FIELD_NW x 2 int32, -1 = none) lists each master weight's packed elements, from
+        ncn_field_pack_map; built once.  The packed buffer is allocated (and packed) if needed."""
+        if self._packed is None or self._packed.device != self._flat.device:
+            self._pack_weights()
+        inv = getattr(self, "_pack_inv", None)
+        if inv is None or inv.device != self._flat.device:
+            src = torch.empty(N_PACKED_HALVES, dtype=torch.int32, device=self._flat.device)
+            call("ncn_field_pack_map", ptr(src), stream())
+            s = src.cpu().numpy()
+            table = np.full((N_W, 2), -1, np.int32)
+            fill = np.zeros(N_W, np.int64)
+            for q, w in enumerate(s):
+                assert 0 <= w < N_W and fill[w] < 2, (q, w)
+                table[w, fill[w]] = q
+                fill[w] += 1
+            inv = self._pack_inv = torch.from_numpy(table).to(self._flat.device)
+        return inv, self._n_table, self._packed, self._prec
+
     def _pack_weights(self):
         if self._packed is None or self._packed.device != self._flat.device:
             self._packed = torch.empty(N_PACKED_HALVES, dtype=torch.float16, device=self._flat.device)

@@ -39,6 +39,10 @@ class FlatAdam:
         # gate of a deferred step inside a captured graph (Trainer(defer_optimizer=True)): 0 = no
         # gradient pending, the step is skipped
         self.gate = torch.ones((), dtype=torch.int32, device=flat.device)
+        # refresh the model's packed MLP fragments inside the Adam pass (models with pack_target)
+        self.pack_fused = hasattr(model, "pack_target")
+        if self.pack_fused:
+            model.pack_target()  # (the map is built here, eagerly: a later first call may be inside a capture)
 
     def zero_grad(self):
         self.model.flat_grad().zero_()
@@ -59,10 +63,19 @@ class FlatAdam:
         p = self.model.flat_params()
         g = self.model.flat_grad()
         b1, b2 = self.betas
-        call("ncn_adam_step", ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table),
-             F32(grad_scale), F32(self.max_norm), F32(self.lr), _lib.F64(b1), _lib.F64(b2), F32(self.eps), F32(self.wd[0]), F32(self.wd[1]),
-             ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work), I32(1 if self.zero_grad_on_step else 0),
-             ptr(getattr(self.model, "amp_state", None)), ptr(self.gate if gated else None), stream())
+        args = [ptr(p), ptr(g), ptr(self.m), ptr(self.v), I64(p.numel()), I64(self.n_table), F32(grad_scale),
+                F32(self.max_norm), F32(self.lr), _lib.F64(b1), _lib.F64(b2), F32(self.eps), F32(self.wd[0]),
+                F32(self.wd[1]), ptr(self.lr_dev), ptr(self.step_dev), ptr(self.work),
+                I32(1 if self.zero_grad_on_step else 0), ptr(getattr(self.model, "amp_state", None)),
+                ptr(self.gate if gated else None)]
+        if self.pack_fused:
+            # the field's packed MLP fragments refreshed by the Adam pass itself (ncn_adam_step_packed):
+            # afterwards they match the parameters whether the step applied or was skipped
+            inv, off, packed, prec = self.model.pack_target()
+            call("ncn_adam_step_packed", *args, ptr(inv), I64(off), ptr(packed), I32(prec), stream())
+            self.model._packed_fresh = True
+        else:
+            call("ncn_adam_step", *args, stream())
 
     def state_tensors(self):
         """Every tensor the step mutates (parameters, moments, device counters)."""

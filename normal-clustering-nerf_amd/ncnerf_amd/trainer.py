@@ -125,8 +125,9 @@ class Trainer:
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 self.opt.step(gated=True, grad_scale=self._grad_scale)
-                m._pack_weights()  # the MLP's fp16 fragments of the updated weights, also beside the marcher
-                m._packed_fresh = True
+                if not self.opt.pack_fused:
+                    m._pack_weights()  # the MLP's fp16 fragments of the updated weights, also beside the marcher
+                m._packed_fresh = True  # (pack_fused: the Adam pass has written them)
             kw["premarched"] = march_train_fused(m, batch["rays_o"], batch["rays_d"], kw["near_distance"],
                                                  kw["max_samples"], kw.get("march_noise"), kw.get("march_rng"))
             cur.wait_stream(side)

@@ -135,3 +135,50 @@ def test_amp_grad_scaler_semantics(dev):
     torch.cuda.synchronize()
     assert f.amp_state.tolist() == [65536.0, 0.0] and int(opt.step_dev) == 2
     assert not torch.equal(p, p1)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_adam_step_packed_matches_pack_weights(dev, precision):
+    """ncn_adam_step_packed (FlatAdam on an NGPMT): the packed MLP fragments the Adam pass writes are
+    bit-identical to ncn_field_pack_weights of the updated parameters — after a normal step, a
+    clipped step, an AMP-skipped step (non-finite gradient: weights unchanged, fragments rewritten
+    from them even if the buffer was stale) and a gated-off deferred step; and the parameters equal
+    those of ncn_adam_step without the fold."""
+    from ncnerf_amd import _lib
+    from ncnerf_amd._lib import I32, ptr, stream
+    from ncnerf_amd.ngp_mt import NGPMT, N_PACKED_HALVES
+    torch.manual_seed(0)
+    m = NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev)
+    flat = m.flat_params()
+    with torch.no_grad():
+        flat.copy_(torch.randn_like(flat) * 0.05)
+    ref = _Flat(flat.clone(), m._n_table)
+    if m.amp_state is None:  # (bf16: a GradScaler state all the same, for the skipped step)
+        m.amp_state = torch.tensor([65536.0, 0.0], device=dev)
+    ref.amp_state = m.amp_state.clone()
+    opt = FlatAdam(m, lr=1e-2, max_norm=0.05, zero_grad_on_step=True)
+    opt_ref = FlatAdam(ref, lr=1e-2, max_norm=0.05, zero_grad_on_step=True)
+    assert opt.pack_fused and not opt_ref.pack_fused
+
+    def expected():
+        out = torch.empty(N_PACKED_HALVES, dtype=torch.float16, device=dev)
+        assert _lib.lib().ncn_field_pack_weights(ptr(flat[m._n_table:]), ptr(out), I32(m._prec), stream()) == 0
+        return out
+
+    g = torch.Generator(device=dev).manual_seed(3)
+    for k, mag in enumerate((1e-4, 10.0, "inf", "gate", 1e-3)):
+        gr = torch.randn(flat.numel(), device=dev, generator=g) * (1e-3 if isinstance(mag, str) else mag)
+        if mag == "inf":
+            gr[flat.numel() - 5] = float("inf")
+        m.flat_grad().copy_(gr)
+        ref.flat_grad().copy_(gr)
+        m._packed.fill_(0)  # stale: the pass must rewrite every fragment
+        gated = mag == "gate"
+        opt.gate.fill_(0 if gated else 1)
+        opt_ref.gate.fill_(0 if gated else 1)
+        opt.step(gated=gated)
+        opt_ref.step(gated=gated)
+        torch.cuda.synchronize()
+        assert torch.equal(flat, ref.flat_params()), k
+        assert torch.equal(m._packed, expected()), k
+    assert torch.equal(m.amp_state, ref.amp_state) and float(m.amp_state[0]) == 32768.0
