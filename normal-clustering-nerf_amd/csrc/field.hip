@@ -1168,6 +1168,8 @@ struct ScLevel {
     bool dense, direct;
     bool f32;  // (SC_F32_DIR) f32 slot sums
     int k;
+    uint32_t rep_sets;  // (cell levels) sets per replica of the cell table
+    int rep_mask;       // replicas - 1
 };
 
 __device__ __forceinline__ void sc_corner_entries(const ScLevel& L, uint32_t px, uint32_t py, uint32_t pz,
@@ -1547,12 +1549,26 @@ __device__ __forceinline__ uint32_t sc_corner_entry(const ScLevel& L, uint32_t p
     return (x ^ (y * 2654435761u) ^ (z * 805459861u)) & (L.params - 1);
 }
 
+// Replicas of the cell table (coarse levels: a unit of 8-16 K samples touches only ~20-180 cells,
+// so hundreds of records land on each cell and their 16 ds_add_u64 serialise on the same slots).
+#ifndef SC_CELL_REP_A
+#define SC_CELL_REP_A 1  // levels 0-5
+#endif
+#ifndef SC_CELL_REP_B
+#define SC_CELL_REP_B 1  // levels 6-9
+#endif
+#ifndef SC_CELL_REP_BY_WAVE
+#define SC_CELL_REP_BY_WAVE 0  // replica = wave index (else lane index), modulo the replica count
+#endif
 __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, uint32_t px, uint32_t py, uint32_t pz,
                                             const float (&v)[16], const ScLevel& L, float* __restrict__ grad) {
     const bool inkey = px < 2048u && py < 2048u && pz < 1024u;
     const uint32_t key = px | (py << 11) | (pz << 22);
     const bool go = act && inkey;
-    const int p0 = SC_WAYS * (int)sc_set(key, sh.sets);
+    // replica of the cell table this lane adds into (lanes, or waves, of one cell spread over
+    // L.rep_mask + 1 copies: fewer same-slot LDS atomics; each copy's slots are flushed on their own)
+    const int rp = (SC_CELL_REP_BY_WAVE ? (int)(threadIdx.x >> 6) : lane) & L.rep_mask;
+    const int p0 = SC_WAYS * (rp * (int)L.rep_sets + (int)sc_set(key, L.rep_sets));
     int sl = -1;
     bool isnew = false;
     uint4 kk = make_uint4(0u, 0u, 0u, 0u);
@@ -1818,6 +1834,8 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     // levels >= SC_DIRECT_FROM: every run's corners straight to global f32 atomics (no LDS table)
     L.direct = !isfinite(m) || l >= SC_DIRECT_FROM;
     L.f32 = SC_F32_DIR && !RUNS;
+    L.rep_mask = 0;
+    L.rep_sets = sh.sets;
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
     // An entry's sum over the unit is at most (unit samples) * m (a sample's 8 corner weights sum
@@ -1944,6 +1962,11 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     // |sum| <= (unit samples) * m * 2^k + rounding: below 2^31 (packed 32-bit halves) / 2^62 (64-bit)
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
     L.k = (SC_PACK ? 30 : 61) - lg_unit - e2;
+    {
+        const int R = l < 6 ? SC_CELL_REP_A : SC_CELL_REP_B;  // (powers of two)
+        L.rep_mask = R - 1;
+        L.rep_sets = sh.sets / R;
+    }
     ScChunk<C> ch;
     // lane t of wave w takes chunk t * SC_WAVES + w (neighbouring chunks in different waves); (off)
     // SC_CELL_CONTIG: wave w covers the contiguous chunks 64w .. 64w+63 — measured: levels 6-9 alone
