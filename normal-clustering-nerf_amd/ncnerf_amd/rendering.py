@@ -65,6 +65,18 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
     min_samples = 1 if exp_step_factor == 0 else 4
     hits_t0 = hits_t[:, 0].contiguous()
     stats = kwargs.get("loop_stats")  # (extension) iteration count and host time blocked at the syncs
+    # Fused iteration (default; kwargs test_fused=False keeps the reference's structure): the field
+    # runs over the whole (alive x N_samples) march output, invalid slots included (the marcher
+    # zero-fills them, and the compositor reads only each ray's first N_eff samples, which are its
+    # valid ones), so the valid mask, its host-synced count, the masked gathers and the scatter back
+    # into zero-filled sigmas / rgbs are gone; outputs are bit-identical (the field's arithmetic is
+    # per sample).  An all-invalid round composites nothing and retires every ray instead of breaking
+    # out of the loop, which ends the loop one round later with the same outputs.
+    fused = (kwargs.get("test_fused", True) and not model.pred_norm and not model.pred_sem
+             and hasattr(model, "_field_fwd"))
+    fwd_kwargs = {k: v for k, v in kwargs.items() if k not in ("loop_stats", "test_fused")}
+    if fused and hasattr(model, "prepare_weights"):
+        model.prepare_weights()
     while samples < max_samples:
         N_alive = len(alive_indices)
         if N_alive == 0:
@@ -77,6 +89,22 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
         total_samples += N_eff_samples.sum()
         xyzs = rearrange(xyzs, "n1 n2 c -> (n1 n2) c")
         dirs = rearrange(dirs, "n1 n2 c -> (n1 n2) c")
+        if fused:
+            if stats is not None:
+                stats["iterations"] = stats.get("iterations", 0) + 1
+                stats["samples_marched"] = stats.get("samples_marched", 0) + N_alive * N_samples
+            if hasattr(model, "prepare_weights"):
+                model._packed_fresh = True  # (packed once before the loop: the weights do not change in it)
+            sig, rgb = model._field_fwd(xyzs, dirs, None, 0, False)[:2]
+            vren.composite_test_multi_fw(sig.view(N_alive, N_samples), rgb.view(N_alive, N_samples, 3), deltas, ts,
+                                         hits_t0, alive_indices, kwargs.get("T_threshold", 1e-4), N_eff_samples,
+                                         opacity, depth, rend)
+            if stats is not None:
+                t0 = time.perf_counter()
+            alive_indices = alive_indices[alive_indices >= 0]  # (host sync: the compaction's size)
+            if stats is not None:
+                stats["blocked_s"] = stats.get("blocked_s", 0.0) + time.perf_counter() - t0
+            continue
         valid_mask = ~torch.all(dirs == 0, dim=1)
         if stats is not None:
             t0 = time.perf_counter()
@@ -86,7 +114,7 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
             stats["blocked_s"] = stats.get("blocked_s", 0.0) + time.perf_counter() - t0
             stats["iterations"] = stats.get("iterations", 0) + 1
             stats["samples_marched"] = stats.get("samples_marched", 0) + N_alive * N_samples
-        output = model(xyzs[valid_mask], dirs[valid_mask], **{k: v for k, v in kwargs.items() if k != "loop_stats"})
+        output = model(xyzs[valid_mask], dirs[valid_mask], **fwd_kwargs)
         sigmas = torch.zeros(len(xyzs), device=device)
         sigmas[valid_mask] = output["sigmas"].float()
         sigmas = rearrange(sigmas, "(n1 n2) -> n1 n2", n2=N_samples)

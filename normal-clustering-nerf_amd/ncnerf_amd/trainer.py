@@ -174,6 +174,9 @@ class Trainer:
                 self._body(self._static, self._step_dev, self._with_opt)
         torch.cuda.current_stream(dev).wait_stream(side)
         self.model._deferred = []  # (the warm-ups' deferred scatters are dropped with their gradients)
+        # the warm-ups' optimizer steps also refreshed the packed MLP fragments (FlatAdam.pack_fused):
+        # the captured forward packs for itself unless the deferred optimizer in the body does it
+        self.model._packed_fresh = False
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._out = self._body(self._static, self._step_dev, self._with_opt)
@@ -183,6 +186,8 @@ class Trainer:
         self.model._deferred = []
         for t, v in zip(state, saved):
             t.copy_(v)
+        if hasattr(self.model, "prepare_weights"):
+            self.model.prepare_weights()  # (the fragments of the restored parameters)
         self.opt.step_count = saved_count
         self.model.flat_grad().zero_()  # (the warm-ups without the optimizer left gradients behind)
 
