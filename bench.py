@@ -364,6 +364,17 @@ def eval_render(model, scene, dev, n_images=3):
             t1 = time.perf_counter()
             res.append((t1 - t0, st, float(out["opacity"].mean())))
             log(f"eval_render image {cam}: {1e3 * (t1 - t0):.1f} ms, {st.get('iterations')} iterations")
+    # the same images through the loop in the reference's structure (test_fused=False), for comparison
+    ref_wall = []
+    with torch.no_grad():
+        for cam in range(1, n_images + 1):
+            o, d = scene.image_rays(cam, dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            render(model, o, d, test_fused=False, **kw)
+            torch.cuda.synchronize()
+            ref_wall.append(time.perf_counter() - t0)
+            log(f"eval_render (reference loop) image {cam}: {1e3 * ref_wall[-1]:.1f} ms")
     wall = float(np.median([r[0] for r in res]))
     its = [r[1].get("iterations", 0) for r in res]
     blocked = [r[1].get("blocked_s", 0.0) / r[0] for r in res]
@@ -371,8 +382,11 @@ def eval_render(model, scene, dev, n_images=3):
             "rays_per_s": round(o.shape[0] / wall, 1), "images": n_images,
             "loop_iterations": its, "samples_marched_per_image": [int(r[1].get("samples_marched", 0)) for r in res],
             "host_blocked_share": round(float(np.median(blocked)), 3), "mean_opacity": [round(r[2], 3) for r in res],
+            "reference_loop_ms_per_image": round(float(np.median(ref_wall)) * 1e3, 2),
             "method": "render(model, rays of one synthetic camera's full image, test_time=True): rendering.py:45-149's "
-                      "loop on ncn_march_test / the field / ncn_composite_test_fw; median wall time of "
+                      "loop on ncn_march_test / the field / ncn_composite_test_fw, fused iteration (the field over "
+                      "the whole march output; reference_loop_ms_per_image: the loop in the reference's structure, "
+                      "test_fused=False, bit-identical outputs); median wall time of "
                       f"{n_images} images after one warm-up image; host_blocked_share = host time inside the "
                       "loop's syncing statements / wall time"}
 
