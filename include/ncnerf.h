@@ -163,6 +163,20 @@ int ncn_composite_train_bw_bg(const float* dL_dopacity, const float* dL_ddepth, 
 int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* deltas, const float* ts,
                           int64_t* alive, int64_t n_alive, int n_samples, int n_rend, float T_threshold,
                           const int32_t* n_eff, float* opacity, float* depth, float* rend, void* stream);
+/* Fused test-render iteration (no reference counterpart; rendering.py:80-101's valid mask + masked
+ * field evaluation + scatter back, restructured): ncn_test_compact copies the valid samples of the
+ * ncn_march_test output (ray n's first n_eff[n] of n_samples slots) to consecutive rows of xyz_c /
+ * dir_c (n_alive * n_samples x 3 capacity), ray n's rows from offsets[n] (n_alive int32), and writes
+ * the total to count[0] (device int32, set by the call) — the field then runs on *count rows
+ * (n_dev); ncn_composite_test_fw_compact is ncn_composite_test_fw reading sigmas / raws through
+ * offsets (deltas / ts stay in the (n_alive, n_samples) layout).  Outputs equal the reference
+ * structure's bit for bit (the field's arithmetic is per sample). */
+int ncn_test_compact(const float* xyzs, const float* dirs, const int32_t* n_eff, int64_t n_alive, int n_samples,
+                     int32_t* offsets, float* xyz_c, float* dir_c, int32_t* count, void* stream);
+int ncn_composite_test_fw_compact(const float* sigmas_c, const float* raws_c, const int32_t* offsets,
+                                  const float* deltas, const float* ts, int64_t* alive, int64_t n_alive,
+                                  int n_samples, int n_rend, float T_threshold, const int32_t* n_eff, float* opacity,
+                                  float* depth, float* rend, void* stream);
 
 /* ---- NGPMT field: replaces tcnn Encoding(Grid/Hash) + sigma_net + rgb_net + TruncExp
  *      (ngp_mt.py:70-113, 157-229; custom_functions.py:162-173).

@@ -1859,6 +1859,8 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_dws(
 }
 
 // composite_test_multi_fw (volumerendering.cu:504-550): lane per alive ray, serial (test path).
+// offsets (ncn_composite_test_fw_compact): NULL, or the start of ray n's samples in compacted
+// sigmas / raws (ncn_test_compact); deltas / ts stay in the marcher's (alive, NS) layout.
 __global__ __launch_bounds__(256) void composite_test_kernel(const float* __restrict__ sigmas,
                                                              const float* __restrict__ raws,
                                                              const float* __restrict__ deltas,
@@ -1866,7 +1868,8 @@ __global__ __launch_bounds__(256) void composite_test_kernel(const float* __rest
                                                              int64_t A, int NS, int C, float T_thr,
                                                              const int32_t* __restrict__ n_eff,
                                                              float* __restrict__ opacity, float* __restrict__ depth,
-                                                             float* __restrict__ rend) {
+                                                             float* __restrict__ rend,
+                                                             const int32_t* __restrict__ offsets) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= A) return;
     if (n_eff[n] == 0) {
@@ -1874,12 +1877,13 @@ __global__ __launch_bounds__(256) void composite_test_kernel(const float* __rest
         return;
     }
     const int64_t r = alive[n];
+    const int64_t base = offsets ? (int64_t)offsets[n] : n * (int64_t)NS;
     float T = 1.0f - opacity[r];
     for (int s = 0; s < n_eff[n]; s++) {
-        const int64_t k = n * (int64_t)NS + s;
-        const float a = 1.0f - __expf(-sigmas[k] * deltas[k]);
+        const int64_t k = n * (int64_t)NS + s, kc = base + s;
+        const float a = 1.0f - __expf(-sigmas[kc] * deltas[k]);
         const float w = a * T;
-        for (int i = 0; i < C; i++) rend[r * C + i] = fmaf(w, raws[k * C + i], rend[r * C + i]);
+        for (int i = 0; i < C; i++) rend[r * C + i] = fmaf(w, raws[kc * C + i], rend[r * C + i]);
         depth[r] = fmaf(w, ts[k], depth[r]);
         opacity[r] += w;
         T *= 1.0f - a;
@@ -1887,6 +1891,48 @@ __global__ __launch_bounds__(256) void composite_test_kernel(const float* __rest
             alive[n] = -1;
             break;
         }
+    }
+}
+
+// Compaction of the test marcher's output (the fused test-render iteration): the valid samples of
+// every alive ray (its first n_eff of NS slots) copied to consecutive rows of xyz_c / dir_c, ray n's
+// rows starting at offsets[n]; count[0] = the total.  A workgroup scans its 256 rays' n_eff and
+// reserves its rows with one atomic on count, so the workgroups' order in the output is arbitrary
+// (the compositor reads through offsets; the field's arithmetic is per sample).  count must be 0.
+__global__ __launch_bounds__(256) void test_compact_kernel(const float* __restrict__ xyzs,
+                                                           const float* __restrict__ dirs,
+                                                           const int32_t* __restrict__ n_eff, int64_t A, int NS,
+                                                           int32_t* __restrict__ offsets, float* __restrict__ xyz_c,
+                                                           float* __restrict__ dir_c, int32_t* __restrict__ count) {
+    __shared__ int wsum[4];
+    __shared__ int base;
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int c = n < A ? n_eff[n] : 0;
+    int incl = c;  // wave inclusive scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    int pre = base;
+    for (int w = 0; w < wid; w++) pre += wsum[w];
+    const int off = pre + incl - c;
+    if (n >= A) return;
+    offsets[n] = off;
+    const float* X = xyzs + n * (int64_t)NS * 3;
+    const float* D = dirs + n * (int64_t)NS * 3;
+    for (int s = 0; s < c; s++) {
+        const int64_t o = (int64_t)(off + s) * 3;
+        xyz_c[o] = X[3 * s]; xyz_c[o + 1] = X[3 * s + 1]; xyz_c[o + 2] = X[3 * s + 2];
+        dir_c[o] = D[3 * s]; dir_c[o + 1] = D[3 * s + 1]; dir_c[o + 2] = D[3 * s + 2];
     }
 }
 
@@ -2196,8 +2242,38 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
                           const int32_t* n_eff, float* opacity, float* depth, float* rend, void* stream) {
     if (n_alive <= 0) return 0;
     hipLaunchKernelGGL(composite_test_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, sigmas,
-                       raws, deltas, ts, alive, n_alive, n_samples, n_rend, T_threshold, n_eff, opacity, depth, rend);
+                       raws, deltas, ts, alive, n_alive, n_samples, n_rend, T_threshold, n_eff, opacity, depth, rend,
+                       (const int32_t*)nullptr);
     NCN_LAUNCH_CHECK("ncn_composite_test_fw");
+    return 0;
+}
+
+int ncn_test_compact(const float* xyzs, const float* dirs, const int32_t* n_eff, int64_t n_alive, int n_samples,
+                     int32_t* offsets, float* xyz_c, float* dir_c, int32_t* count, void* stream) {
+    NCN_REQUIRE(n_alive >= 0 && n_samples >= 1 && n_alive * (int64_t)n_samples < (int64_t)INT32_MAX,
+                hipErrorInvalidValue, "ncn_test_compact: n_alive * n_samples must fit int32");
+    const hipError_t e = hipMemsetAsync(count, 0, sizeof(int32_t), (hipStream_t)stream);
+    if (e != hipSuccess) {
+        ncn::set_error("ncn_test_compact: memset failed: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    if (n_alive == 0) return 0;
+    hipLaunchKernelGGL(test_compact_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
+                       n_eff, n_alive, n_samples, offsets, xyz_c, dir_c, count);
+    NCN_LAUNCH_CHECK("ncn_test_compact");
+    return 0;
+}
+
+int ncn_composite_test_fw_compact(const float* sigmas_c, const float* raws_c, const int32_t* offsets,
+                                  const float* deltas, const float* ts, int64_t* alive, int64_t n_alive,
+                                  int n_samples, int n_rend, float T_threshold, const int32_t* n_eff, float* opacity,
+                                  float* depth, float* rend, void* stream) {
+    if (n_alive <= 0) return 0;
+    NCN_REQUIRE(offsets != nullptr, hipErrorInvalidValue, "ncn_composite_test_fw_compact: offsets required");
+    hipLaunchKernelGGL(composite_test_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, sigmas_c,
+                       raws_c, deltas, ts, alive, n_alive, n_samples, n_rend, T_threshold, n_eff, opacity, depth, rend,
+                       offsets);
+    NCN_LAUNCH_CHECK("ncn_composite_test_fw_compact");
     return 0;
 }
 

@@ -19,7 +19,7 @@ import torch
 from einops import rearrange
 
 from .custom_functions import CountJob, RayAABBIntersector, RayMarcher, VolumeRenderer, VolumeRendererBg
-from . import vren
+from . import _lib, vren
 
 
 @torch.autocast("cuda")
@@ -65,13 +65,14 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
     min_samples = 1 if exp_step_factor == 0 else 4
     hits_t0 = hits_t[:, 0].contiguous()
     stats = kwargs.get("loop_stats")  # (extension) iteration count and host time blocked at the syncs
-    # Fused iteration (default; kwargs test_fused=False keeps the reference's structure): the field
-    # runs over the whole (alive x N_samples) march output, invalid slots included (the marcher
-    # zero-fills them, and the compositor reads only each ray's first N_eff samples, which are its
-    # valid ones), so the valid mask, its host-synced count, the masked gathers and the scatter back
-    # into zero-filled sigmas / rgbs are gone; outputs are bit-identical (the field's arithmetic is
-    # per sample).  An all-invalid round composites nothing and retires every ray instead of breaking
-    # out of the loop, which ends the loop one round later with the same outputs.
+    # Fused iteration (default; kwargs test_fused=False keeps the reference's structure): a ray's
+    # valid samples are its first N_eff of the marcher's N_samples slots, so one kernel compacts
+    # them (ncn_test_compact: per-ray offsets + a device count), the field runs on that device count
+    # and the compositor reads through the offsets — the valid mask, its host-synced count, the
+    # masked gathers and the scatter back into zero-filled sigmas / rgbs are gone; outputs are
+    # bit-identical (the field's arithmetic is per sample).  An all-invalid round composites nothing
+    # and retires every ray instead of breaking out of the loop: the loop ends one round later with
+    # the same outputs.
     fused = (kwargs.get("test_fused", True) and not model.pred_norm and not model.pred_sem
              and hasattr(model, "_field_fwd"))
     fwd_kwargs = {k: v for k, v in kwargs.items() if k not in ("loop_stats", "test_fused")}
@@ -95,10 +96,21 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
                 stats["samples_marched"] = stats.get("samples_marched", 0) + N_alive * N_samples
             if hasattr(model, "prepare_weights"):
                 model._packed_fresh = True  # (packed once before the loop: the weights do not change in it)
-            sig, rgb = model._field_fwd(xyzs, dirs, None, 0, False)[:2]
-            vren.composite_test_multi_fw(sig.view(N_alive, N_samples), rgb.view(N_alive, N_samples, 3), deltas, ts,
-                                         hits_t0, alive_indices, kwargs.get("T_threshold", 1e-4), N_eff_samples,
-                                         opacity, depth, rend)
+            # the valid samples compacted on the device (ncn_test_compact), the field on their device
+            # count, the compositor through the per-ray offsets
+            cap = N_alive * N_samples
+            xyz_c = torch.empty(cap, 3, dtype=torch.float32, device=device)
+            dir_c = torch.empty(cap, 3, dtype=torch.float32, device=device)
+            offs = torch.empty(N_alive, dtype=torch.int32, device=device)
+            cnt = torch.empty(1, dtype=torch.int32, device=device)
+            _lib.call("ncn_test_compact", _lib.ptr(xyzs), _lib.ptr(dirs), _lib.ptr(N_eff_samples), _lib.I64(N_alive),
+                      _lib.I32(N_samples), _lib.ptr(offs), _lib.ptr(xyz_c), _lib.ptr(dir_c), _lib.ptr(cnt),
+                      _lib.stream())
+            sig, rgb = model._field_fwd(xyz_c, dir_c, cnt, 0, False)[:2]
+            _lib.call("ncn_composite_test_fw_compact", _lib.ptr(sig), _lib.ptr(rgb), _lib.ptr(offs), _lib.ptr(deltas),
+                      _lib.ptr(ts), _lib.ptr(alive_indices), _lib.I64(N_alive), _lib.I32(N_samples), _lib.I32(3),
+                      _lib.F32(float(kwargs.get("T_threshold", 1e-4))), _lib.ptr(N_eff_samples), _lib.ptr(opacity),
+                      _lib.ptr(depth), _lib.ptr(rend), _lib.stream())
             if stats is not None:
                 t0 = time.perf_counter()
             alive_indices = alive_indices[alive_indices >= 0]  # (host sync: the compaction's size)
