@@ -177,6 +177,29 @@ int ncn_composite_test_fw_compact(const float* sigmas_c, const float* raws_c, co
                                   const float* deltas, const float* ts, int64_t* alive, int64_t n_alive,
                                   int n_samples, int n_rend, float T_threshold, const int32_t* n_eff, float* opacity,
                                   float* depth, float* rend, void* stream);
+/* Device-driven test loop (the fused iteration without a host read per iteration): ctrl is a
+ * device int32[8] = {0 alive rays A, 1 samples per ray NS, 2 samples so far, 3 done, 4 valid samples
+ * of the iteration, 5 next alive count, 6 iterations run, 7 sum of A x NS}; the caller initialises it
+ * for the first iteration ({n_rays, NS0, NS0, 0, 0, 0, 0, 0}, NS0 = max(1, min_samples)) and sizes
+ * every per-sample buffer for n_rays x min_samples samples (A x NS never exceeds it) and every
+ * per-ray buffer for max_alive = n_rays.  One iteration: ncn_test_loop_march (ncn_march_test with
+ * A / NS from ctrl), ncn_test_loop_compact (count into ctrl[4], which must be 0), the field on that
+ * count, ncn_test_loop_composite, then ncn_test_loop_next (the kept rays of `alive` compacted into
+ * alive_next, total_samples += ctrl[4], and the next A / NS formed as rendering.py:68-73 does:
+ * done when no ray is alive or samples >= max_samples).  A done loop keeps A = 0: further iterations
+ * launch empty, so the caller reads ctrl[3] only every few iterations. */
+int ncn_test_loop_march(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive,
+                        int64_t max_alive, const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
+                        int grid_size, int max_samples, const int32_t* ctrl, float* xyzs, float* dirs, float* deltas,
+                        float* ts, int32_t* n_eff, void* stream);
+int ncn_test_loop_compact(const float* xyzs, const float* dirs, const int32_t* n_eff, int64_t max_alive,
+                          int32_t* ctrl, int32_t* offsets, float* xyz_c, float* dir_c, void* stream);
+int ncn_test_loop_composite(const float* sigmas_c, const float* raws_c, const int32_t* offsets, const float* deltas,
+                            const float* ts, int64_t* alive, int64_t max_alive, const int32_t* ctrl, int n_rend,
+                            float T_threshold, const int32_t* n_eff, float* opacity, float* depth, float* rend,
+                            void* stream);
+int ncn_test_loop_next(const int64_t* alive, int64_t* alive_next, int64_t max_alive, int32_t* ctrl,
+                       int64_t* total_samples, int n_rays, int max_samples, int min_samples, void* stream);
 
 /* ---- NGPMT field: replaces tcnn Encoding(Grid/Hash) + sigma_net + rgb_net + TruncExp
  *      (ngp_mt.py:70-113, 157-229; custom_functions.py:162-173).

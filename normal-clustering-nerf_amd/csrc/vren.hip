@@ -683,7 +683,11 @@ __global__ __launch_bounds__(64) void march_test_kernel(const float* __restrict_
                                                         float scale, float esf, int G, int max_samples, int NS,
                                                         float* __restrict__ xyzs, float* __restrict__ dirs,
                                                         float* __restrict__ deltas, float* __restrict__ ts,
-                                                        int32_t* __restrict__ n_eff) {
+                                                        int32_t* __restrict__ n_eff, const int32_t* __restrict__ ctrl) {
+    if (ctrl) {  // (device-driven test loop) alive count and samples per ray of this iteration
+        A = ctrl[0];
+        NS = ctrl[1];
+    }
     const int64_t n = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (n >= A) return;
     const MarchConst m = make_march_const(cascades, scale, esf, G, max_samples, (float)cascades);
@@ -1869,7 +1873,12 @@ __global__ __launch_bounds__(256) void composite_test_kernel(const float* __rest
                                                              const int32_t* __restrict__ n_eff,
                                                              float* __restrict__ opacity, float* __restrict__ depth,
                                                              float* __restrict__ rend,
-                                                             const int32_t* __restrict__ offsets) {
+                                                             const int32_t* __restrict__ offsets,
+                                                             const int32_t* __restrict__ ctrl) {
+    if (ctrl) {
+        A = ctrl[0];
+        NS = ctrl[1];
+    }
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= A) return;
     if (n_eff[n] == 0) {
@@ -1903,7 +1912,13 @@ __global__ __launch_bounds__(256) void test_compact_kernel(const float* __restri
                                                            const float* __restrict__ dirs,
                                                            const int32_t* __restrict__ n_eff, int64_t A, int NS,
                                                            int32_t* __restrict__ offsets, float* __restrict__ xyz_c,
-                                                           float* __restrict__ dir_c, int32_t* __restrict__ count) {
+                                                           float* __restrict__ dir_c, int32_t* __restrict__ count,
+                                                           const int32_t* __restrict__ ctrl) {
+    if (ctrl) {
+        A = ctrl[0];
+        NS = ctrl[1];
+        if ((int64_t)blockIdx.x * 256 >= A) return;  // (uniform)
+    }
     __shared__ int wsum[4];
     __shared__ int base;
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1934,6 +1949,57 @@ __global__ __launch_bounds__(256) void test_compact_kernel(const float* __restri
         xyz_c[o] = X[3 * s]; xyz_c[o + 1] = X[3 * s + 1]; xyz_c[o + 2] = X[3 * s + 2];
         dir_c[o] = D[3 * s]; dir_c[o + 1] = D[3 * s + 1]; dir_c[o + 2] = D[3 * s + 2];
     }
+}
+
+// Device-driven test loop (rendering.py:68-105 without a host read per iteration): ctrl (int32) =
+// {0 alive rays A, 1 samples per ray NS, 2 samples so far, 3 done, 4 valid samples of the iteration,
+//  5 next alive count, 6 iterations run, 7 alive x NS summed}.  After the compositor: the rays it
+// kept (alive >= 0) are compacted into alive_next (order irrelevant: every ray is independent) and
+// one thread forms the next iteration exactly as the reference's loop head does — stop when no ray
+// is alive or samples >= max_samples, else NS = max(min(n_rays / A, 64), min_samples).  A done loop
+// has A = 0, so further iterations launch empty.
+__global__ __launch_bounds__(256) void test_alive_compact_kernel(const int64_t* __restrict__ alive,
+                                                                 int64_t* __restrict__ alive_next,
+                                                                 int32_t* __restrict__ ctrl) {
+    const int64_t A = ctrl[0];
+    if ((int64_t)blockIdx.x * 256 >= A) return;  // (uniform)
+    __shared__ int wsum[4];
+    __shared__ int base;
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t r = n < A ? alive[n] : -1;
+    const int keep = r >= 0;
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) wsum[wid] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        base = tot ? atomicAdd(ctrl + 5, tot) : 0;
+    }
+    __syncthreads();
+    int pre = base;
+    for (int w = 0; w < wid; w++) pre += wsum[w];
+    if (keep) alive_next[pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = r;
+}
+__global__ void test_loop_next_kernel(int32_t* __restrict__ ctrl, int64_t* __restrict__ total, int n_rays,
+                                      int max_samples, int min_samples) {
+    if (threadIdx.x != 0 || ctrl[3]) return;
+    total[0] += ctrl[4];
+    ctrl[6] += 1;
+    ctrl[7] += ctrl[0] * ctrl[1];
+    const int na = ctrl[5];
+    ctrl[4] = 0;
+    ctrl[5] = 0;
+    const int samples = ctrl[2];
+    if (na == 0 || samples >= max_samples) {
+        ctrl[3] = 1;
+        ctrl[0] = 0;
+        return;
+    }
+    const int ns = max(min(n_rays / na, 64), min_samples);
+    ctrl[0] = na;
+    ctrl[1] = ns;
+    ctrl[2] = samples + ns;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2138,11 +2204,11 @@ int ncn_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
     if (cascades == 1)
         hipLaunchKernelGGL(march_test_kernel<true>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, alive,
                            n_alive, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, n_samples,
-                           xyzs, dirs, deltas, ts, n_eff);
+                           xyzs, dirs, deltas, ts, n_eff, (const int32_t*)nullptr);
     else
         hipLaunchKernelGGL(march_test_kernel<false>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, alive,
                            n_alive, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, n_samples,
-                           xyzs, dirs, deltas, ts, n_eff);
+                           xyzs, dirs, deltas, ts, n_eff, (const int32_t*)nullptr);
     NCN_LAUNCH_CHECK("ncn_march_test");
     return 0;
 }
@@ -2243,7 +2309,7 @@ int ncn_composite_test_fw(const float* sigmas, const float* raws, const float* d
     if (n_alive <= 0) return 0;
     hipLaunchKernelGGL(composite_test_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, sigmas,
                        raws, deltas, ts, alive, n_alive, n_samples, n_rend, T_threshold, n_eff, opacity, depth, rend,
-                       (const int32_t*)nullptr);
+                       (const int32_t*)nullptr, (const int32_t*)nullptr);
     NCN_LAUNCH_CHECK("ncn_composite_test_fw");
     return 0;
 }
@@ -2259,7 +2325,7 @@ int ncn_test_compact(const float* xyzs, const float* dirs, const int32_t* n_eff,
     }
     if (n_alive == 0) return 0;
     hipLaunchKernelGGL(test_compact_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
-                       n_eff, n_alive, n_samples, offsets, xyz_c, dir_c, count);
+                       n_eff, n_alive, n_samples, offsets, xyz_c, dir_c, count, (const int32_t*)nullptr);
     NCN_LAUNCH_CHECK("ncn_test_compact");
     return 0;
 }
@@ -2272,8 +2338,59 @@ int ncn_composite_test_fw_compact(const float* sigmas_c, const float* raws_c, co
     NCN_REQUIRE(offsets != nullptr, hipErrorInvalidValue, "ncn_composite_test_fw_compact: offsets required");
     hipLaunchKernelGGL(composite_test_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, sigmas_c,
                        raws_c, deltas, ts, alive, n_alive, n_samples, n_rend, T_threshold, n_eff, opacity, depth, rend,
-                       offsets);
+                       offsets, (const int32_t*)nullptr);
     NCN_LAUNCH_CHECK("ncn_composite_test_fw_compact");
+    return 0;
+}
+
+int ncn_test_loop_march(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive,
+                        int64_t max_alive, const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
+                        int grid_size, int max_samples, const int32_t* ctrl, float* xyzs, float* dirs, float* deltas,
+                        float* ts, int32_t* n_eff, void* stream) {
+    if (max_alive <= 0) return 0;
+    NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && ctrl, hipErrorInvalidValue, "ncn_test_loop_march: bad args");
+    dim3 g(cdiv(max_alive, 64)), b(64);
+    if (cascades == 1)
+        hipLaunchKernelGGL(march_test_kernel<true>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, alive,
+                           max_alive, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, 1, xyzs,
+                           dirs, deltas, ts, n_eff, ctrl);
+    else
+        hipLaunchKernelGGL(march_test_kernel<false>, g, b, 0, (hipStream_t)stream, rays_o, rays_d, hits_t, alive,
+                           max_alive, bitfield, cascades, scale, exp_step_factor, grid_size, max_samples, 1, xyzs,
+                           dirs, deltas, ts, n_eff, ctrl);
+    NCN_LAUNCH_CHECK("ncn_test_loop_march");
+    return 0;
+}
+
+int ncn_test_loop_compact(const float* xyzs, const float* dirs, const int32_t* n_eff, int64_t max_alive,
+                          int32_t* ctrl, int32_t* offsets, float* xyz_c, float* dir_c, void* stream) {
+    if (max_alive <= 0) return 0;
+    hipLaunchKernelGGL(test_compact_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
+                       n_eff, max_alive, 1, offsets, xyz_c, dir_c, ctrl + 4, (const int32_t*)ctrl);
+    NCN_LAUNCH_CHECK("ncn_test_loop_compact");
+    return 0;
+}
+
+int ncn_test_loop_composite(const float* sigmas_c, const float* raws_c, const int32_t* offsets, const float* deltas,
+                            const float* ts, int64_t* alive, int64_t max_alive, const int32_t* ctrl, int n_rend,
+                            float T_threshold, const int32_t* n_eff, float* opacity, float* depth, float* rend,
+                            void* stream) {
+    if (max_alive <= 0) return 0;
+    hipLaunchKernelGGL(composite_test_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, sigmas_c,
+                       raws_c, deltas, ts, alive, max_alive, 1, n_rend, T_threshold, n_eff, opacity, depth, rend,
+                       offsets, ctrl);
+    NCN_LAUNCH_CHECK("ncn_test_loop_composite");
+    return 0;
+}
+
+int ncn_test_loop_next(const int64_t* alive, int64_t* alive_next, int64_t max_alive, int32_t* ctrl,
+                       int64_t* total_samples, int n_rays, int max_samples, int min_samples, void* stream) {
+    if (max_alive <= 0) return 0;
+    hipLaunchKernelGGL(test_alive_compact_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, alive,
+                       alive_next, ctrl);
+    hipLaunchKernelGGL(test_loop_next_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctrl, total_samples, n_rays,
+                       max_samples, min_samples);
+    NCN_LAUNCH_CHECK("ncn_test_loop_next");
     return 0;
 }
 

@@ -46,6 +46,10 @@ SIGNATURES = {
     "ncn_composite_train_bw_bg": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, F32, P, P, P],
     "ncn_test_compact": [P, P, P, I64, I32, P, P, P, P, P],
     "ncn_composite_test_fw_compact": [P, P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
+    "ncn_test_loop_march": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, P, P, P, P, P, P, P],
+    "ncn_test_loop_compact": [P, P, P, I64, P, P, P, P, P],
+    "ncn_test_loop_composite": [P, P, P, P, P, P, I64, P, I32, F32, P, P, P, P, P],
+    "ncn_test_loop_next": [P, P, I64, P, P, I32, I32, I32, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_field_pack_weights": [P, P, I32, P],
     "ncn_field_pack_map": [P, P],

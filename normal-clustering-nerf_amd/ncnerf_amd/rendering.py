@@ -73,11 +73,17 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
     # bit-identical (the field's arithmetic is per sample).  An all-invalid round composites nothing
     # and retires every ray instead of breaking out of the loop: the loop ends one round later with
     # the same outputs.
-    fused = (kwargs.get("test_fused", True) and not model.pred_norm and not model.pred_sem
-             and hasattr(model, "_field_fwd"))
+    mode = kwargs.get("test_fused", True)
+    fused = bool(mode) and not model.pred_norm and not model.pred_sem and hasattr(model, "_field_fwd")
     fwd_kwargs = {k: v for k, v in kwargs.items() if k not in ("loop_stats", "test_fused")}
     if fused and hasattr(model, "prepare_weights"):
         model.prepare_weights()
+    if fused and mode is True and N_rays > 0:
+        # the same fused iterations driven from the device (no host read per iteration)
+        total_samples = _test_loop_device(model, rays_o, rays_d, hits_t0, alive_indices, exp_step_factor, max_samples,
+                                          min_samples, float(kwargs.get("T_threshold", 1e-4)), opacity, depth, rend,
+                                          stats)
+        samples = max_samples  # (loop done)
     while samples < max_samples:
         N_alive = len(alive_indices)
         if N_alive == 0:
@@ -160,6 +166,61 @@ def render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
     rgb_bg = torch.ones(3, device=device) if exp_step_factor == 0 else torch.zeros(3, device=device)
     results["rgb"] += rgb_bg * rearrange(1 - opacity, "n -> n 1")
     return results
+
+
+TEST_LOOP_CHECK = 4  # iterations launched between two reads of the device loop's done flag
+
+
+def _test_loop_device(model, rays_o, rays_d, hits_t0, alive, exp_step_factor, max_samples, min_samples, T_threshold,
+                      opacity, depth, rend, stats):
+    """render_rays_test's loop (rendering.py:68-105) with the fused iteration, its control on the
+    device (ncn_test_loop_*: the alive count, N_samples and the stop test of the loop head formed by
+    a kernel after each iteration); the host launches TEST_LOOP_CHECK iterations between reads of the
+    done flag (iterations past the end launch empty).  Same outputs as the host-driven loop bit for
+    bit: every ray's march and composite are independent of its position in the alive list.  Returns
+    total_samples (device int64)."""
+    from ._lib import F32, I32, I64, call, ptr, stream
+    R, dev = rays_o.shape[0], rays_o.device
+    cap = R * min_samples
+    f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)  # noqa: E731
+    xyzs, dirs, deltas, ts = f(cap, 3), f(cap, 3), f(cap), f(cap)
+    xyz_c, dir_c = f(cap, 3), f(cap, 3)
+    n_eff = torch.empty(R, dtype=torch.int32, device=dev)
+    offs = torch.empty(R, dtype=torch.int32, device=dev)
+    bufs = [alive, torch.empty(R, dtype=torch.int64, device=dev)]
+    ns0 = max(min(R // R, 64), min_samples)
+    ctrl = torch.tensor([R, ns0, ns0, 0, 0, 0, 0, 0], dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    count = ctrl[4:5]
+    it = 0
+    blocked = 0.0
+    while it <= max_samples:  # (every iteration adds >= 1 to samples: at most max_samples run)
+        for _ in range(TEST_LOOP_CHECK):
+            a, b = bufs[it % 2], bufs[(it + 1) % 2]
+            call("ncn_test_loop_march", ptr(rays_o), ptr(rays_d), ptr(hits_t0), ptr(a), I64(R), ptr(model.density_bitfield),
+                 I32(int(model.cascades)), F32(float(model.scale)), F32(float(exp_step_factor)), I32(int(model.grid_size)),
+                 I32(int(max_samples)), ptr(ctrl), ptr(xyzs), ptr(dirs), ptr(deltas), ptr(ts), ptr(n_eff), stream())
+            call("ncn_test_loop_compact", ptr(xyzs), ptr(dirs), ptr(n_eff), I64(R), ptr(ctrl), ptr(offs), ptr(xyz_c),
+                 ptr(dir_c), stream())
+            model._packed_fresh = True  # (packed before the loop: the weights do not change in it)
+            sig, rgb = model._field_fwd(xyz_c, dir_c, count, 0, False)[:2]
+            call("ncn_test_loop_composite", ptr(sig), ptr(rgb), ptr(offs), ptr(deltas), ptr(ts), ptr(a), I64(R),
+                 ptr(ctrl), I32(3), F32(T_threshold), ptr(n_eff), ptr(opacity), ptr(depth), ptr(rend), stream())
+            call("ncn_test_loop_next", ptr(a), ptr(b), I64(R), ptr(ctrl), ptr(total), I32(R), I32(int(max_samples)),
+                 I32(int(min_samples)), stream())
+            it += 1
+        t0 = time.perf_counter()
+        done = bool(ctrl[3].item())  # (host sync)
+        blocked += time.perf_counter() - t0
+        if done:
+            break
+    if stats is not None:
+        c = ctrl.tolist()
+        stats["iterations"] = stats.get("iterations", 0) + c[6]
+        stats["samples_marched"] = stats.get("samples_marched", 0) + c[7]
+        stats["blocked_s"] = stats.get("blocked_s", 0.0) + blocked
+        stats["launched_iterations"] = stats.get("launched_iterations", 0) + it
+    return total[0]
 
 
 def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):

@@ -1,5 +1,6 @@
-"""The fused test-time render iteration (rendering.render_rays_test, default) against the loop in the
-reference's structure (test_fused=False: valid mask, host-synced count, masked field evaluation,
+"""The fused test-time render iteration (rendering.render_rays_test; default: driven from the device,
+ncn_test_loop_*; test_fused="host": one host read of the alive count per iteration) against the loop
+in the reference's structure (test_fused=False: valid mask, host-synced count, masked field evaluation,
 scatter back into zero-filled sigmas / rgbs; rendering.py:45-149): opacity, depth, rgb and
 total_samples bit-identical, on a random-init model (no ray terminates: the loop runs to the
 sample budget) and on a model whose densities were fitted to the room's occupancy (rays stop at the
@@ -40,17 +41,18 @@ def test_fused_test_render_bit_identical(dev, opaque):
     n = ro.shape[0] // (4 if not opaque else 1)  # (the random model marches the whole budget)
     o, d = ro[:n].contiguous(), rd[:n].contiguous()
     outs = []
-    for fused in (False, True):
+    for fused in (False, "host", True):
         st = {}
         with torch.no_grad():
             r = render(m, o, d, near_distance=0.01, max_samples=1024, test_time=True, test_fused=fused,
                        loop_stats=st)
         torch.cuda.synchronize()
         outs.append((r, st))
-    (a, sa), (b, sb) = outs
-    for k in ("opacity", "depth", "rgb"):
-        assert torch.equal(a[k], b[k]), k
-    assert int(a["total_samples"]) == int(b["total_samples"])
-    assert sa["iterations"] <= sb["iterations"] <= sa["iterations"] + 1
+    (a, sa) = outs[0]
+    for b, sb in outs[1:]:
+        for k in ("opacity", "depth", "rgb"):
+            assert torch.equal(a[k], b[k]), k
+        assert int(a["total_samples"]) == int(b["total_samples"])
+        assert sa["iterations"] <= sb["iterations"] <= sa["iterations"] + 1, (sa, sb)
     if opaque:
         assert float(a["opacity"].mean()) > 0.9  # the fitted model's rays do stop
