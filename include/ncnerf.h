@@ -183,8 +183,10 @@ int ncn_composite_test_fw_compact(const float* sigmas_c, const float* raws_c, co
  * for the first iteration ({n_rays, NS0, NS0, 0, 0, 0, 0, 0}, NS0 = max(1, min_samples)) and sizes
  * every per-sample buffer for n_rays x min_samples samples (A x NS never exceeds it) and every
  * per-ray buffer for max_alive = n_rays.  One iteration: ncn_test_loop_march (ncn_march_test with
- * A / NS from ctrl), ncn_test_loop_compact (count into ctrl[4], which must be 0), the field on that
- * count, ncn_test_loop_composite, then ncn_test_loop_next (the kept rays of `alive` compacted into
+ * A / NS from ctrl), ncn_test_loop_index (the valid slots' indices into idx, their count into
+ * ctrl[4], which must be 0), ncn_field_fwd on the march output with n_dev = ctrl + 4 and
+ * order = idx (it evaluates and writes back exactly those slots), ncn_test_loop_composite (offsets
+ * NULL: the (A, NS) layout), then ncn_test_loop_next (the kept rays of `alive` compacted into
  * alive_next, total_samples += ctrl[4], and the next A / NS formed as rendering.py:68-73 does:
  * done when no ray is alive or samples >= max_samples).  A done loop keeps A = 0: further iterations
  * launch empty, so the caller reads ctrl[3] only every few iterations. */
@@ -192,8 +194,7 @@ int ncn_test_loop_march(const float* rays_o, const float* rays_d, float* hits_t,
                         int64_t max_alive, const uint8_t* bitfield, int cascades, float scale, float exp_step_factor,
                         int grid_size, int max_samples, const int32_t* ctrl, float* xyzs, float* dirs, float* deltas,
                         float* ts, int32_t* n_eff, void* stream);
-int ncn_test_loop_compact(const float* xyzs, const float* dirs, const int32_t* n_eff, int64_t max_alive,
-                          int32_t* ctrl, int32_t* offsets, float* xyz_c, float* dir_c, void* stream);
+int ncn_test_loop_index(const int32_t* n_eff, int64_t max_alive, int32_t* ctrl, int32_t* idx, void* stream);
 int ncn_test_loop_composite(const float* sigmas_c, const float* raws_c, const int32_t* offsets, const float* deltas,
                             const float* ts, int64_t* alive, int64_t max_alive, const int32_t* ctrl, int n_rend,
                             float T_threshold, const int32_t* n_eff, float* opacity, float* depth, float* rend,

@@ -1912,13 +1912,7 @@ __global__ __launch_bounds__(256) void test_compact_kernel(const float* __restri
                                                            const float* __restrict__ dirs,
                                                            const int32_t* __restrict__ n_eff, int64_t A, int NS,
                                                            int32_t* __restrict__ offsets, float* __restrict__ xyz_c,
-                                                           float* __restrict__ dir_c, int32_t* __restrict__ count,
-                                                           const int32_t* __restrict__ ctrl) {
-    if (ctrl) {
-        A = ctrl[0];
-        NS = ctrl[1];
-        if ((int64_t)blockIdx.x * 256 >= A) return;  // (uniform)
-    }
+                                                           float* __restrict__ dir_c, int32_t* __restrict__ count) {
     __shared__ int wsum[4];
     __shared__ int base;
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1958,6 +1952,38 @@ __global__ __launch_bounds__(256) void test_compact_kernel(const float* __restri
 // one thread forms the next iteration exactly as the reference's loop head does — stop when no ray
 // is alive or samples >= max_samples, else NS = max(min(n_rays / A, 64), min_samples).  A done loop
 // has A = 0, so further iterations launch empty.
+// The valid slots of the iteration as a list of (alive, NS)-layout indices (ray n's first n_eff[n]
+// slots), in workgroup-arbitrary order; count into ctrl[4].  The field evaluates x[idx[p]] for
+// p < count and writes its outputs at idx[p] (its `order` operand), so nothing is copied.
+__global__ __launch_bounds__(256) void test_index_kernel(const int32_t* __restrict__ n_eff, int32_t* __restrict__ ctrl,
+                                                         int32_t* __restrict__ idx) {
+    const int64_t A = ctrl[0];
+    const int NS = ctrl[1];
+    if ((int64_t)blockIdx.x * 256 >= A) return;  // (uniform)
+    __shared__ int wsum[4];
+    __shared__ int base;
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int c = n < A ? n_eff[n] : 0;
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        base = tot ? atomicAdd(ctrl + 4, tot) : 0;
+    }
+    __syncthreads();
+    int pre = base;
+    for (int w = 0; w < wid; w++) pre += wsum[w];
+    const int off = pre + incl - c;
+    const int first = (int)(n * NS);
+    for (int s = 0; s < c; s++) idx[off + s] = first + s;
+}
 __global__ __launch_bounds__(256) void test_alive_compact_kernel(const int64_t* __restrict__ alive,
                                                                  int64_t* __restrict__ alive_next,
                                                                  int32_t* __restrict__ ctrl) {
@@ -2325,7 +2351,7 @@ int ncn_test_compact(const float* xyzs, const float* dirs, const int32_t* n_eff,
     }
     if (n_alive == 0) return 0;
     hipLaunchKernelGGL(test_compact_kernel, dim3(cdiv(n_alive, 256)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
-                       n_eff, n_alive, n_samples, offsets, xyz_c, dir_c, count, (const int32_t*)nullptr);
+                       n_eff, n_alive, n_samples, offsets, xyz_c, dir_c, count);
     NCN_LAUNCH_CHECK("ncn_test_compact");
     return 0;
 }
@@ -2362,12 +2388,11 @@ int ncn_test_loop_march(const float* rays_o, const float* rays_d, float* hits_t,
     return 0;
 }
 
-int ncn_test_loop_compact(const float* xyzs, const float* dirs, const int32_t* n_eff, int64_t max_alive,
-                          int32_t* ctrl, int32_t* offsets, float* xyz_c, float* dir_c, void* stream) {
+int ncn_test_loop_index(const int32_t* n_eff, int64_t max_alive, int32_t* ctrl, int32_t* idx, void* stream) {
     if (max_alive <= 0) return 0;
-    hipLaunchKernelGGL(test_compact_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, xyzs, dirs,
-                       n_eff, max_alive, 1, offsets, xyz_c, dir_c, ctrl + 4, (const int32_t*)ctrl);
-    NCN_LAUNCH_CHECK("ncn_test_loop_compact");
+    hipLaunchKernelGGL(test_index_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, n_eff, ctrl,
+                       idx);
+    NCN_LAUNCH_CHECK("ncn_test_loop_index");
     return 0;
 }
 

@@ -47,7 +47,7 @@ SIGNATURES = {
     "ncn_test_compact": [P, P, P, I64, I32, P, P, P, P, P],
     "ncn_composite_test_fw_compact": [P, P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],
     "ncn_test_loop_march": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, P, P, P, P, P, P, P],
-    "ncn_test_loop_compact": [P, P, P, I64, P, P, P, P, P],
+    "ncn_test_loop_index": [P, I64, P, P, P],
     "ncn_test_loop_composite": [P, P, P, P, P, P, I64, P, I32, F32, P, P, P, P, P],
     "ncn_test_loop_next": [P, P, I64, P, P, I32, I32, I32, P],
     "ncn_composite_test_fw": [P, P, P, P, P, I64, I32, I32, F32, P, P, P, P, P],

@@ -184,9 +184,11 @@ def _test_loop_device(model, rays_o, rays_d, hits_t0, alive, exp_step_factor, ma
     cap = R * min_samples
     f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)  # noqa: E731
     xyzs, dirs, deltas, ts = f(cap, 3), f(cap, 3), f(cap), f(cap)
-    xyz_c, dir_c = f(cap, 3), f(cap, 3)
+    sig, rgb = f(cap), f(cap, 3)
     n_eff = torch.empty(R, dtype=torch.int32, device=dev)
-    offs = torch.empty(R, dtype=torch.int32, device=dev)
+    idx = torch.empty(cap, dtype=torch.int32, device=dev)
+    model._packed_fresh = True
+    packed = model._take_packed()  # (packed before the loop: the weights do not change in it)
     bufs = [alive, torch.empty(R, dtype=torch.int64, device=dev)]
     ns0 = max(min(R // R, 64), min_samples)
     ctrl = torch.tensor([R, ns0, ns0, 0, 0, 0, 0, 0], dtype=torch.int32, device=dev)
@@ -200,11 +202,12 @@ def _test_loop_device(model, rays_o, rays_d, hits_t0, alive, exp_step_factor, ma
             call("ncn_test_loop_march", ptr(rays_o), ptr(rays_d), ptr(hits_t0), ptr(a), I64(R), ptr(model.density_bitfield),
                  I32(int(model.cascades)), F32(float(model.scale)), F32(float(exp_step_factor)), I32(int(model.grid_size)),
                  I32(int(max_samples)), ptr(ctrl), ptr(xyzs), ptr(dirs), ptr(deltas), ptr(ts), ptr(n_eff), stream())
-            call("ncn_test_loop_compact", ptr(xyzs), ptr(dirs), ptr(n_eff), I64(R), ptr(ctrl), ptr(offs), ptr(xyz_c),
-                 ptr(dir_c), stream())
-            model._packed_fresh = True  # (packed before the loop: the weights do not change in it)
-            sig, rgb = model._field_fwd(xyz_c, dir_c, count, 0, False)[:2]
-            call("ncn_test_loop_composite", ptr(sig), ptr(rgb), ptr(offs), ptr(deltas), ptr(ts), ptr(a), I64(R),
+            call("ncn_test_loop_index", ptr(n_eff), I64(R), ptr(ctrl), ptr(idx), stream())
+            # the field on exactly the valid slots (order = their indices, count on the device)
+            call("ncn_field_fwd", ptr(xyzs), ptr(dirs), I64(cap), ptr(count), ptr(idx), ptr(model.xyz_encoder.params),
+                 model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(model._prec), I32(0),
+                 ptr(sig), ptr(rgb), ptr(None), stream())
+            call("ncn_test_loop_composite", ptr(sig), ptr(rgb), ptr(None), ptr(deltas), ptr(ts), ptr(a), I64(R),
                  ptr(ctrl), I32(3), F32(T_threshold), ptr(n_eff), ptr(opacity), ptr(depth), ptr(rend), stream())
             call("ncn_test_loop_next", ptr(a), ptr(b), I64(R), ptr(ctrl), ptr(total), I32(R), I32(int(max_samples)),
                  I32(int(min_samples)), stream())
