@@ -1952,60 +1952,82 @@ __global__ __launch_bounds__(256) void test_compact_kernel(const float* __restri
 // one thread forms the next iteration exactly as the reference's loop head does — stop when no ray
 // is alive or samples >= max_samples, else NS = max(min(n_rays / A, 64), min_samples).  A done loop
 // has A = 0, so further iterations launch empty.
-// The valid slots of the iteration as a list of (alive, NS)-layout indices (ray n's first n_eff[n]
-// slots), in workgroup-arbitrary order; count into ctrl[4].  The field evaluates x[idx[p]] for
-// p < count and writes its outputs at idx[p] (its `order` operand), so nothing is copied.
-__global__ __launch_bounds__(256) void test_index_kernel(const int32_t* __restrict__ n_eff, int32_t* __restrict__ ctrl,
-                                                         int32_t* __restrict__ idx) {
-    const int64_t A = ctrl[0];
-    const int NS = ctrl[1];
-    if ((int64_t)blockIdx.x * 256 >= A) return;  // (uniform)
-    __shared__ int wsum[4];
-    __shared__ int base;
-    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// Block-range compaction for the device test loop: workgroup b owns a contiguous range of the
+// A items (a multiple of 256 long), counts its output, reserves it with ONE atomic on the counter
+// (a few hundred arrivals instead of one per 256 items: same-address atomics serialise at the
+// memory side), then writes its items in order with a running offset.
+constexpr int TL_BLOCKS = 256;
+__device__ __forceinline__ int tl_block_excl(int v, int& total, int* wsum) {  // 256-thread exclusive scan
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int c = n < A ? n_eff[n] : 0;
-    int incl = c;
+    int incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const int o = __shfl_up(incl, d, 64);
         if (lane >= d) incl += o;
     }
+    __syncthreads();  // (wsum reuse)
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        base = tot ? atomicAdd(ctrl + 4, tot) : 0;
-    }
-    __syncthreads();
-    int pre = base;
+    int pre = 0;
     for (int w = 0; w < wid; w++) pre += wsum[w];
-    const int off = pre + incl - c;
-    const int first = (int)(n * NS);
-    for (int s = 0; s < c; s++) idx[off + s] = first + s;
+    total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    return pre + incl - v;
 }
+// The valid slots of the iteration as a list of (alive, NS)-layout indices (ray n's first n_eff[n]
+// slots), count into ctrl[4].  The field evaluates x[idx[p]] for p < count and writes its outputs at
+// idx[p] (its `order` operand), so nothing is copied.
+__global__ __launch_bounds__(256) void test_index_kernel(const int32_t* __restrict__ n_eff, int32_t* __restrict__ ctrl,
+                                                         int32_t* __restrict__ idx) {
+    const int64_t A = ctrl[0];
+    const int NS = ctrl[1];
+    const int64_t per = ((A + TL_BLOCKS - 1) / TL_BLOCKS + 255) & ~(int64_t)255;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = min(A, lo + per);
+    if (lo >= hi) return;  // (uniform)
+    __shared__ int wsum[4];
+    __shared__ int base;
+    int cnt = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) cnt += n_eff[i];
+    int total;
+    (void)tl_block_excl(cnt, total, wsum);
+    if (threadIdx.x == 0) base = total ? atomicAdd(ctrl + 4, total) : 0;
+    __syncthreads();
+    int run = base;
+    for (int64_t c0 = lo; c0 < hi; c0 += 256) {
+        const int64_t n = c0 + threadIdx.x;
+        const int c = n < hi ? n_eff[n] : 0;
+        int tot;
+        const int off = run + tl_block_excl(c, tot, wsum);
+        const int first = (int)(n * NS);
+        for (int s = 0; s < c; s++) idx[off + s] = first + s;
+        run += tot;
+    }
+}
+// After the compositor: the rays it kept (alive >= 0) compacted into alive_next (order irrelevant:
+// every ray is independent), their count into ctrl[5].
 __global__ __launch_bounds__(256) void test_alive_compact_kernel(const int64_t* __restrict__ alive,
                                                                  int64_t* __restrict__ alive_next,
                                                                  int32_t* __restrict__ ctrl) {
     const int64_t A = ctrl[0];
-    if ((int64_t)blockIdx.x * 256 >= A) return;  // (uniform)
+    const int64_t per = ((A + TL_BLOCKS - 1) / TL_BLOCKS + 255) & ~(int64_t)255;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = min(A, lo + per);
+    if (lo >= hi) return;  // (uniform)
     __shared__ int wsum[4];
     __shared__ int base;
-    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t r = n < A ? alive[n] : -1;
-    const int keep = r >= 0;
-    const uint64_t m = __ballot(keep);
-    if (lane == 0) wsum[wid] = __popcll(m);
+    int cnt = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) cnt += alive[i] >= 0;
+    int total;
+    (void)tl_block_excl(cnt, total, wsum);
+    if (threadIdx.x == 0) base = total ? atomicAdd(ctrl + 5, total) : 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        base = tot ? atomicAdd(ctrl + 5, tot) : 0;
+    int run = base;
+    for (int64_t c0 = lo; c0 < hi; c0 += 256) {
+        const int64_t n = c0 + threadIdx.x;
+        const int64_t r = n < hi ? alive[n] : -1;
+        int tot;
+        const int off = run + tl_block_excl(r >= 0, tot, wsum);
+        if (r >= 0) alive_next[off] = r;
+        run += tot;
     }
-    __syncthreads();
-    int pre = base;
-    for (int w = 0; w < wid; w++) pre += wsum[w];
-    if (keep) alive_next[pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = r;
 }
 __global__ void test_loop_next_kernel(int32_t* __restrict__ ctrl, int64_t* __restrict__ total, int n_rays,
                                       int max_samples, int min_samples) {
@@ -2390,8 +2412,7 @@ int ncn_test_loop_march(const float* rays_o, const float* rays_d, float* hits_t,
 
 int ncn_test_loop_index(const int32_t* n_eff, int64_t max_alive, int32_t* ctrl, int32_t* idx, void* stream) {
     if (max_alive <= 0) return 0;
-    hipLaunchKernelGGL(test_index_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, n_eff, ctrl,
-                       idx);
+    hipLaunchKernelGGL(test_index_kernel, dim3(TL_BLOCKS), dim3(256), 0, (hipStream_t)stream, n_eff, ctrl, idx);
     NCN_LAUNCH_CHECK("ncn_test_loop_index");
     return 0;
 }
@@ -2411,7 +2432,7 @@ int ncn_test_loop_composite(const float* sigmas_c, const float* raws_c, const in
 int ncn_test_loop_next(const int64_t* alive, int64_t* alive_next, int64_t max_alive, int32_t* ctrl,
                        int64_t* total_samples, int n_rays, int max_samples, int min_samples, void* stream) {
     if (max_alive <= 0) return 0;
-    hipLaunchKernelGGL(test_alive_compact_kernel, dim3(cdiv(max_alive, 256)), dim3(256), 0, (hipStream_t)stream, alive,
+    hipLaunchKernelGGL(test_alive_compact_kernel, dim3(TL_BLOCKS), dim3(256), 0, (hipStream_t)stream, alive,
                        alive_next, ctrl);
     hipLaunchKernelGGL(test_loop_next_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctrl, total_samples, n_rays,
                        max_samples, min_samples);
