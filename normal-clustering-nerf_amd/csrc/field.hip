@@ -1073,8 +1073,13 @@ constexpr int SC_CELL_WORDS = SC_F32_CELL ? 8 : SC_CELL_VALS;  // 8-B words of v
 constexpr int SC_SETS_CELL = NCN_SC_SETS_CELL * SC_THREADS / 1024;
 constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + SC_CELL_WORDS * 8 + 2); }
 constexpr int sc_max(int a, int b) { return a > b ? a : b; }
+#ifndef SC_RUN_LEVELS
+#define SC_RUN_LEVELS 10
+#endif
+// (the run layout — record staging — only when some level uses it: SC_RUN_LEVELS > SC_CELL_HI)
 constexpr int SC_ARENA = sc_max(sc_cell_bytes(SC_SETS_CELL),
-                                sc_max(sc_layout_bytes(SC_SETS_RUN, true), sc_layout_bytes(SC_SETS_DIR, false)));
+                                sc_max(SC_RUN_LEVELS > SC_CELL_HI ? sc_layout_bytes(SC_SETS_RUN, true) : 0,
+                                       sc_layout_bytes(SC_SETS_DIR, false)));
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
@@ -1107,9 +1112,6 @@ __device__ __forceinline__ void sc_unpack(long long q, int& xs, int& ys) {
 // levels 0-9: 8 samples per lane with run records (unit = 8192 samples); levels 10-15 (cells
 // shorter than ~2 steps, runs rarely longer than one sample): 2 samples per lane, each added
 // directly (unit = 2048 samples)
-#ifndef SC_RUN_LEVELS
-#define SC_RUN_LEVELS 10
-#endif
 #ifndef SC_C_RUN
 #define SC_C_RUN 4  // samples per lane on the run levels (unit = 1024 * SC_C_RUN samples)
 #endif
@@ -2087,7 +2089,17 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
         sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
 }
 
-__global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
+// (experiment) waves per SIMD the scatter is compiled for: 0 = the compiler's choice (128 VGPRs, one
+// 1024-thread workgroup per CU); with the LDS tables halved two workgroups fit a CU's LDS
+#ifndef NCN_SC_WPE
+#define NCN_SC_WPE 0
+#endif
+#if NCN_SC_WPE > 0
+#define NCN_SC_ATTR __attribute__((amdgpu_waves_per_eu(NCN_SC_WPE)))
+#else
+#define NCN_SC_ATTR
+#endif
+__global__ __launch_bounds__(SC_THREADS) NCN_SC_ATTR void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
                                                                    const float2* __restrict__ dE,
