@@ -2198,182 +2198,6 @@ __global__ __launch_bounds__(SC_THREADS) NCN_SC_ATTR void field_scatter_kernel(c
     }
 }
 
-// ---- lean fine-level scatter (experiment, NCN_SCF) ----
-// The hashed levels [SC_CELL_HI, 16) in a kernel of their own, written for 8 waves per SIMD (two
-// 1024-thread workgroups per CU: <= 64 VGPRs, <= 80 KB of LDS each) instead of the shared kernel's
-// 4: one sample and one corner at a time per lane (no corner batches, no run sums: at these levels
-// a cell rarely holds two consecutive samples), the same 4-way LDS sets of exact 64-bit fixed-point
-// sums, claim list and f32 flush per unit.  Units: 4096 samples (2048 from SC_DIR_HALF), taken in
-// grabs of 64 lanes x 2 samples from an LDS counter.
-#ifndef NCN_SCF
-#define NCN_SCF 0
-#endif
-#ifndef NCN_SCF_SETS
-#define NCN_SCF_SETS 880  // 880 x 4 ways x 22 B = 77 440 B
-#endif
-constexpr int SCF_THREADS = 1024, SCF_WAVES = SCF_THREADS / 64;
-constexpr int SCF_SETS = NCN_SCF_SETS, SCF_SLOTS = SCF_SETS * SC_WAYS;
-__device__ __forceinline__ void scf_add(uint32_t* keys, long long* vx_, long long* vy_, uint16_t* used, int* fill,
-                                        int lane, bool act, uint32_t e, float vx, float vy, int k, uint32_t off,
-                                        float* __restrict__ grad) {
-    int sl = -1;
-    bool isnew = false;
-    if (act) {
-        const int p0 = SC_WAYS * (int)sc_set(e, SCF_SETS);
-        uint4 kk = *(const uint4*)&keys[p0];
-        sl = kk.x == e ? p0 : kk.y == e ? p0 + 1 : kk.z == e ? p0 + 2 : kk.w == e ? p0 + 3 : -1;
-        for (int attempt = 0; attempt < 2 && sl < 0; attempt++) {
-            if (attempt) {
-                asm volatile("" ::: "memory");
-                kk = *(const uint4*)&keys[p0];
-                sl = kk.x == e ? p0 : kk.y == e ? p0 + 1 : kk.z == e ? p0 + 2 : kk.w == e ? p0 + 3 : -1;
-                if (sl >= 0) break;
-            }
-            const int cl = kk.x == SC_EMPTY ? p0 : kk.y == SC_EMPTY ? p0 + 1 : kk.z == SC_EMPTY ? p0 + 2
-                         : kk.w == SC_EMPTY ? p0 + 3 : -1;
-            if (cl < 0) break;  // set full
-            const uint32_t got = atomicCAS(&keys[cl], SC_EMPTY, e);
-            if (got == SC_EMPTY) { sl = cl; isnew = true; }
-            else if (got == e) sl = cl;
-        }
-        if (sl >= 0) {
-            atomicAdd((unsigned long long*)&vx_[sl], (unsigned long long)sc_fix(vx, k));
-            atomicAdd((unsigned long long*)&vy_[sl], (unsigned long long)sc_fix(vy, k));
-        } else {  // set full: straight to the table gradient
-            if (vx != 0.f) atomicAdd(grad + 2 * (size_t)(off + e), vx);
-            if (vy != 0.f) atomicAdd(grad + 2 * (size_t)(off + e) + 1, vy);
-        }
-    }
-    const uint64_t nm = __ballot(isnew);
-    if (nm) {  // (uniform) append the claimed slots: one LDS atomic per wave
-        int base = 0;
-        if (lane == 0) base = atomicAdd(fill, (int)__popcll(nm));
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (isnew)
-            used[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0))] =
-                (uint16_t)sl;
-    }
-}
-
-__global__ __launch_bounds__(SCF_THREADS) __attribute__((amdgpu_waves_per_eu(8)))
-void field_scatter_fine_kernel(const float* __restrict__ xyzs, int64_t n_stride, const int32_t* __restrict__ n_dev,
-                               LevelTable Lt, float xyz_min, float xyz_extent, const float2* __restrict__ dE,
-                               float* __restrict__ grad, const float* __restrict__ level_max, int lm_rows,
-                               int level_lo, int level_hi, const int32_t* __restrict__ order) {
-    __shared__ __attribute__((aligned(16))) long long vals[2 * SCF_SLOTS];
-    __shared__ __attribute__((aligned(16))) uint32_t keys[SCF_SLOTS];
-    __shared__ uint16_t used[SCF_SLOTS];
-    __shared__ int fill[4];
-    __shared__ float lmax_s[16];
-    long long* const vx_ = vals;
-    long long* const vy_ = vals + SCF_SLOTS;
-    if (threadIdx.x < 16) lmax_s[threadIdx.x] = 0.f;
-    if (threadIdx.x < 4) fill[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < SCF_SLOTS; i += SCF_THREADS) {
-        keys[i] = SC_EMPTY;
-        vx_[i] = 0;
-        vy_[i] = 0;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < lm_rows * 16; i += SCF_THREADS)
-        atomicMax((unsigned*)&lmax_s[i & 15], __float_as_uint(level_max[i]));
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
-    const int64_t e_stride = (n_stride + 3) & ~(int64_t)3;
-    ScNorm nrm;
-    nrm.mn = xyz_min;
-    nrm.ext = xyz_extent;
-    nrm.inv = 1.0f / xyz_extent;
-    nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
-    const int lo = max(level_lo, SC_CELL_HI), mid = max(lo, min(level_hi, SC_DIR_HALF));
-    const int64_t u4 = (n + 4095) / 4096, u2 = (n + 2047) / 2048;
-    const int64_t n_units = (int64_t)(mid - lo) * u4 + (int64_t)max(0, level_hi - mid) * u2;
-    int par = 0;
-    for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-        int l;
-        int64_t s0, span;
-        if (u < (int64_t)(mid - lo) * u4) {
-            l = lo + (int)(u / u4);
-            span = 4096;
-            s0 = (u % u4) * span;
-        } else {
-            const int64_t v = u - (int64_t)(mid - lo) * u4;
-            l = mid + (int)(v / u2);
-            span = 2048;
-            s0 = (v % u2) * span;
-        }
-        const int64_t s1 = min(n, s0 + span);
-        const float m = lmax_s[l];
-        if (m == 0.f) continue;  // (uniform)
-        const bool direct = !isfinite(m);
-        int e2 = 0;
-        (void)frexpf(direct ? 1.f : m, &e2);
-        const int k = 46 - e2;
-        const float scale = Lt.scale[l];
-        const uint32_t off = Lt.offset[l], params = Lt.params[l], mask = params - 1, res = Lt.res[l];
-        const bool dense = (uint64_t)res * res * res <= params;  // (a fine level of a small scene)
-        const float2* dEl = dE + (int64_t)l * e_stride;
-        int* const fl = fill + par;
-        int* const grab = fill + 2 + par;
-        if (threadIdx.x == 0) { fill[par ^ 1] = 0; fill[2 + (par ^ 1)] = 0; }
-        par ^= 1;
-        const int NG = (int)(span / 128);  // grabs of 64 lanes x 2 samples
-        for (int g = wid; g < NG;) {  // (wave-uniform)
-            const int64_t sb = s0 + ((int64_t)lane * NG + g) * 2;
-#pragma unroll 1
-            for (int j = 0; j < 2; j++) {
-                const int64_t p = sb + j;
-                const bool in = p < s1;
-                const int64_t src = in ? (order ? (int64_t)order[p] : p) : 0;
-                const float2 gv = in ? dEl[p] : make_float2(0.f, 0.f);
-                const LevelPos q = level_pos(scale, nrm(xyzs[3 * src]), nrm(xyzs[3 * src + 1]), nrm(xyzs[3 * src + 2]));
-                const bool act = gv.x != 0.f || gv.y != 0.f;
-                const uint32_t hy0 = q.py * 2654435761u, hy1 = (q.py + 1) * 2654435761u;
-                const uint32_t hz0 = q.pz * 805459861u, hz1 = (q.pz + 1) * 805459861u;
-#pragma unroll 1
-                for (int c = 0; c < 8; c++) {
-                    const float w = ((c & 1 ? q.fx : 1.0f - q.fx) * ((c >> 1) & 1 ? q.fy : 1.0f - q.fy)) *
-                                    ((c >> 2) & 1 ? q.fz : 1.0f - q.fz);
-                    const float vx = w * gv.x, vy = w * gv.y;
-                    uint32_t e = ((q.px + (c & 1)) ^ ((c & 2) ? hy1 : hy0) ^ ((c & 4) ? hz1 : hz0)) & mask;
-                    if (dense) {  // (uniform) as sc_corner_entries
-                        e = (q.px + (c & 1)) + res * (q.py + ((c >> 1) & 1)) + res * res * (q.pz + ((c >> 2) & 1));
-                        e = e < params ? e : e % params;
-                    }
-                    if (direct) {
-                        if (act) {
-                            atomicAdd(grad + 2 * (size_t)(off + e), vx);
-                            atomicAdd(grad + 2 * (size_t)(off + e) + 1, vy);
-                        }
-                    } else {
-                        scf_add(keys, vx_, vy_, used, fl, lane, act && (vx != 0.f || vy != 0.f), e, vx, vy, k, off,
-                                grad);
-                    }
-                }
-            }
-            int kn = 0;
-            if (lane == 0) kn = atomicAdd(grab, 1);
-            g = __builtin_amdgcn_readfirstlane(kn) + SCF_WAVES;
-        }
-        lds_barrier();
-        const int nf = *fl;
-        for (int i = threadIdx.x; i < 2 * nf; i += SCF_THREADS) {
-            const int slot = used[i >> 1];
-            const uint32_t key = keys[slot];
-            long long* pv = (i & 1) ? &vy_[slot] : &vx_[slot];
-            const float gvv = (float)ldexp((double)*pv, -k);
-            *pv = 0;
-            if (gvv != 0.f) atomicAdd(grad + 2 * (size_t)(off + key) + (i & 1), gvv);
-            if (!(i & 1)) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                keys[slot] = SC_EMPTY;
-            }
-        }
-        lds_barrier();
-    }
-}
-
 static int scatter_grid(int64_t n_cap) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(256 * 1024 / SC_THREADS, (n_cap + 255) / 256));  // 1024 threads per CU
 }
@@ -2569,20 +2393,9 @@ int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, 
     const LevelTable Lt = make_table(levels);
     int grid = scatter_grid(n);
     if (max_blocks > 0) grid = std::min(grid, max_blocks);
-    // (NCN_SCF) the hashed levels by the lean fine-level kernel, after the shared one
-    const int hi_main = NCN_SCF ? std::min(level_hi, std::max(level_lo, SC_CELL_HI)) : level_hi;
-    if (hi_main > level_lo || slab)
-        hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev,
-                           Lt, xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max,
-                           ncn_field_bwd_blocks(n), level_lo, hi_main, order, slab, n_blocks_sigma, n_blocks_rgb,
-                           grad_w);
-    if (NCN_SCF && level_hi > hi_main) {
-        int gf = (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 255) / 256));
-        if (max_blocks > 0) gf = std::min(gf, 2 * max_blocks);
-        hipLaunchKernelGGL(field_scatter_fine_kernel, dim3(gf), dim3(SCF_THREADS), 0, (hipStream_t)stream, xyzs, n,
-                           n_dev, Lt, xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max,
-                           ncn_field_bwd_blocks(n), std::max(level_lo, hi_main), level_hi, order);
-    }
+    hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
+                       xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
+                       level_lo, level_hi, order, slab, n_blocks_sigma, n_blocks_rgb, grad_w);
     NCN_LAUNCH_CHECK("ncn_field_scatter");
     return 0;
 }
