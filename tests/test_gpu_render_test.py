@@ -33,8 +33,9 @@ def _model(dev, scene, opaque):
     return m
 
 
-@pytest.mark.parametrize("opaque", [False, True])
-def test_fused_test_render_bit_identical(dev, opaque):
+@pytest.mark.parametrize("opaque,esf", [(False, 0.0), (True, 0.0), (False, 1.0 / 256)])
+def test_fused_test_render_bit_identical(dev, opaque, esf):
+    """esf > 0: exponential stepping, where the loop's minimum samples per ray is 4 (rendering.py:65)."""
     scene = SyntheticScene()
     m = _model(dev, scene, opaque)
     ro, rd = scene.image_rays(1, device=dev)
@@ -45,7 +46,7 @@ def test_fused_test_render_bit_identical(dev, opaque):
         st = {}
         with torch.no_grad():
             r = render(m, o, d, near_distance=0.01, max_samples=1024, test_time=True, test_fused=fused,
-                       loop_stats=st)
+                       exp_step_factor=esf, loop_stats=st)
         torch.cuda.synchronize()
         outs.append((r, st))
     (a, sa) = outs[0]
