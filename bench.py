@@ -298,48 +298,53 @@ def cpu_quota():
     return None
 
 
-def cpu_baseline(n_rays=2048, steps=20, warmup=3):
-    """Oracle CPU port of the same step (config #1: 2048 rays, pure PyTorch + C on the host cores),
-    timed as BASELINE.md §2 asks: median wall time of 20 steps (fewer if a leg's timed steps pass
-    30 s) after 3 warm-up steps, on every CPU this process may use: one leg per distinct thread
-    count among OMP_NUM_THREADS (the GPU box's CPU share), the cgroup CPU quota and the affinity
-    mask.  A thread count above the cgroup quota is skipped and reported (on the GPU box the mask
-    holds 256 CPUs under a 16-CPU quota: 256 threads took 80 s per step, round 4).  `value` is the
-    fastest leg (the stronger baseline); every leg is reported."""
+def cpu_baseline(ray_counts=(2048, 8192), steps=20, warmup=3):
+    """Oracle CPU port of the same step (pure PyTorch + C on the host cores) at config #1's 2048 rays
+    and config #2's 8192 rays, timed as BASELINE.md §2 asks: median wall time of 20
+    steps (fewer if a leg's timed steps pass 30 s) after 3 warm-up steps, on every CPU this process
+    may use: one leg per distinct thread count among OMP_NUM_THREADS (the GPU box's CPU share) and
+    the usable CPUs (the affinity mask capped by the cgroup CPU quota).  A thread count above the
+    quota is skipped and reported (on the GPU box the mask holds 256 CPUs under a 16-CPU quota: 256
+    threads took 80 s per step, round 4).  `value` is the fastest leg (the stronger baseline); every
+    leg is reported."""
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count() or 1
     quota = cpu_quota()
     usable = min(affinity, quota) if quota else affinity
-    legs = {}
+    threads_legs = {}
     omp = os.environ.get("OMP_NUM_THREADS", "")
     if omp.isdigit() and 0 < int(omp) < usable:
-        legs["omp_num_threads"] = int(omp)
-    legs["all_usable_cpus"] = usable
+        threads_legs["omp_num_threads"] = int(omp)
+    threads_legs["all_usable_cpus"] = usable
     runs, skipped = {}, {}
     if affinity > usable:
         skipped["affinity"] = f"{affinity} CPUs in the affinity mask > cgroup CPU quota {quota}: oversubscribed"
-    for name, threads in legs.items():
-        med, tot, n = _cpu_leg(threads, n_rays, steps, warmup)
-        if med is None:
-            skipped[name] = f"{threads} threads: a warm-up step took {tot:.0f} s (oversubscribed); leg abandoned"
-            log(f"cpu leg {name}: {skipped[name]}")
-            continue
-        log(f"cpu leg {name} ({threads} threads): {med * 1e3:.0f} ms/step")
-        runs[name] = {"threads": threads, "rays_per_s": round(n_rays / med, 1), "ms_per_step": round(med * 1e3, 1),
-                      "timed_steps": n, "timed_s": round(tot, 1)}
+    for n_rays in ray_counts:
+        for tname, threads in threads_legs.items():
+            name = f"{tname}_{n_rays}_rays"
+            med, tot, n = _cpu_leg(threads, n_rays, steps, warmup)
+            if med is None:
+                skipped[name] = f"{threads} threads: a warm-up step took {tot:.0f} s (oversubscribed); leg abandoned"
+                log(f"cpu leg {name}: {skipped[name]}")
+                continue
+            log(f"cpu leg {name} ({threads} threads): {med * 1e3:.0f} ms/step")
+            runs[name] = {"threads": threads, "rays_per_step": n_rays, "rays_per_s": round(n_rays / med, 1),
+                          "ms_per_step": round(med * 1e3, 1), "timed_steps": n, "timed_s": round(tot, 1)}
     best = max(runs, key=lambda k: runs[k]["rays_per_s"])
-    torch.set_num_threads(legs.get("omp_num_threads", usable))
+    torch.set_num_threads(threads_legs.get("omp_num_threads", usable))
     return {"value": runs[best]["rays_per_s"], "unit": "rays/s", "cores": runs[best]["threads"], "kind": "port",
             "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cpu_quota": quota, "legs": runs,
             "skipped_legs": skipped,
-            "sample": f"median of up to {steps} full training steps (at most ~30 s per leg) of {n_rays} rays "
-                      f"(config #1) after {warmup} warm-up steps on the oracle CPU path (oracle/train_ref.py: C "
-                      f"marcher/compositor + torch fp32 field/losses), on all {usable} usable CPUs "
-                      f"(min of affinity mask {affinity} and cgroup quota {quota})"
-                      + (f" and on OMP_NUM_THREADS={legs['omp_num_threads']}" if "omp_num_threads" in legs else "")
-                      + f"; value = the faster ({best})"}
+            "sample": f"median of up to {steps} full training steps (at most ~30 s per leg) of "
+                      + " and ".join(str(r) for r in ray_counts)
+                      + f" rays (configs #1 / #2) after {warmup} warm-up steps on the oracle CPU path "
+                      f"(oracle/train_ref.py: C marcher/compositor + torch fp32 field/losses), on all {usable} usable "
+                      f"CPUs (min of affinity mask {affinity} and cgroup quota {quota})"
+                      + (f" and on OMP_NUM_THREADS={threads_legs['omp_num_threads']}" if "omp_num_threads" in threads_legs
+                         else "")
+                      + f"; value = the fastest leg ({best})"}
 
 
 def eval_render(model, scene, dev, n_images=3):
