@@ -649,9 +649,9 @@ def main():
         "data": "synthetic Hypersim-shaped batches (ai_001_001 box, 8x8 patches, procedural room, "
                 "surface_bright target colours); " + (
                     f"NGPMT pretrained {args.pretrain} untimed steps from random init on the procedural occupancy "
-                    f"grid (rays terminate early)" if args.pretrain > 0 else
-                    "random-init NGPMT on the procedural occupancy grid (trained states: pretrained_state, "
-                    "refreshed_state)"),
+                    f"grid" if args.pretrain > 0 else
+                    "random-init NGPMT on the procedural occupancy grid (other states: pretrained_state, "
+                    "opaque_state, refreshed_state)"),
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
