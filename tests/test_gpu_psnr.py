@@ -18,8 +18,9 @@ the standard error of the paired difference (tests/psnr_ensemble.py):
   0.1 dB (2x the north_star tolerance: the full ensemble's mean at step 125 is -0.026 +- 0.014 dB,
   so a 3-SE bound of 0.042 dB would sit ~1 SE from it).  Bounds: +-0.10 dB at 125, +-0.22 at 250
   (round 3: +-0.22 / +-0.41 over 4 members against the fp32 oracle);
-  [scannet_manhattan]: config #5's 8-member fp32 oracle ensemble (cluster weights 1e-2),
-  tests/golden/psnr_hip_ensemble_scannet.json (round-4 HIP runs) for the spread;
+  [scannet_manhattan]: config #5's 8-member fp16-fw+bw oracle ensemble (cluster weights 1e-2,
+  which ramp in from step 500), re-trained to step 750 and checked at every 125 steps, the spread
+  from tests/golden/psnr_hip_ensemble_scannet_f16bw.json (bounds +-0.10 .. +-1.50 dB);
 * test_psnr_parity_short: one pair (same init, batches, noise; 1024-ray batches, 40 steps) within
   0.1 dB, and the HIP test renderer vs the oracle renderer on the SAME parameters within 0.05 dB
   (the renderers themselves agree to ~1e-3 dB)."""
@@ -46,19 +47,21 @@ def test_psnr_parity_short():
 
 @pytest.mark.parametrize("preset", ["hypersim", "scannet_manhattan"])
 def test_psnr_ensemble_vs_oracle(preset):
-    """preset scannet_manhattan: config #5's cluster weights (1e-2) against its own oracle ensemble
-    (tests/golden/psnr_oracle_ensemble_scannet.json, 8 members; HIP statistics from
-    profiles/round4/psnr_hip_ensemble_scannet.json)."""
+    """preset scannet_manhattan: config #5's cluster weights (1e-2) against its own fp16-fw+bw oracle
+    ensemble (tests/golden/psnr_oracle_ensemble_scannet_f16bw.json, 8 members; HIP statistics from
+    profiles/round4/psnr_hip_ensemble_scannet.json), to step 750: the cluster terms ramp in from step
+    500 (losses.py:217), so before that the preset trains exactly as config #1."""
     import psnr_ensemble as pe
-    name, stats_name = (("psnr_oracle_ensemble_f16bw.json", "psnr_hip_ensemble_f16bw.json") if preset == "hypersim"
-                        else ("psnr_oracle_ensemble_scannet.json", "psnr_hip_ensemble_scannet.json"))
+    name, stats_name, steps = (("psnr_oracle_ensemble_f16bw.json", "psnr_hip_ensemble_f16bw.json", 250)
+                               if preset == "hypersim" else
+                               ("psnr_oracle_ensemble_scannet_f16bw.json", "psnr_hip_ensemble_scannet_f16bw.json", 750))
     oracle = json.load(open(os.path.join(G, name)))
     assert oracle.get("preset", "hypersim") == preset
     ref_stats = {s["step"]: s for s in json.load(open(os.path.join(G, stats_name)))["stats"]}
     members = [m["member"] for m in oracle["members"]]
-    runs = pe.run_hip_ensemble(members, 1, 250, 125, oracle["members"][0]["rays_per_step"], print, preset)
+    runs = pe.run_hip_ensemble(members, 1, steps, 125, oracle["members"][0]["rays_per_step"], print, preset)
     st = pe.stats(oracle, runs)
-    assert [s["step"] for s in st] == [125, 250]
+    assert [s["step"] for s in st] == list(range(125, steps + 1, 125))
     for s in st:
         sd = ref_stats[s["step"]]["paired_delta_sd"]  # paired-difference spread of the full ensemble
         bound = max(3.0 * sd / math.sqrt(s["members"]), 0.1)
