@@ -19,8 +19,9 @@ the standard error of the paired difference (tests/psnr_ensemble.py):
   so a 3-SE bound of 0.042 dB would sit ~1 SE from it).  Bounds: +-0.10 dB at 125, +-0.22 at 250
   (round 3: +-0.22 / +-0.41 over 4 members against the fp32 oracle);
   [scannet_manhattan]: config #5's 8-member fp16-fw+bw oracle ensemble (cluster weights 1e-2,
-  which ramp in from step 500), re-trained to step 750 and checked at every 125 steps, the spread
-  from tests/golden/psnr_hip_ensemble_scannet_f16bw.json (bounds +-0.10 .. +-1.50 dB);
+  which ramp in from step 500), re-trained to step 750 and checked at steps 500, 625 and 750 (before
+  500 both sides train exactly as config #1), the spread from
+  tests/golden/psnr_hip_ensemble_scannet_f16bw.json (bounds +-0.79 / +-1.24 / +-1.50 dB);
 * test_psnr_parity_short: one pair (same init, batches, noise; 1024-ray batches, 40 steps) within
   0.1 dB, and the HIP test renderer vs the oracle renderer on the SAME parameters within 0.05 dB
   (the renderers themselves agree to ~1e-3 dB)."""
@@ -62,6 +63,8 @@ def test_psnr_ensemble_vs_oracle(preset):
     runs = pe.run_hip_ensemble(members, 1, steps, 125, oracle["members"][0]["rays_per_step"], print, preset)
     st = pe.stats(oracle, runs)
     assert [s["step"] for s in st] == list(range(125, steps + 1, 125))
+    if preset != "hypersim":  # (before step 500 the preset's trajectories are config #1's, checked there)
+        st = [s for s in st if s["step"] >= 500]
     for s in st:
         sd = ref_stats[s["step"]]["paired_delta_sd"]  # paired-difference spread of the full ensemble
         bound = max(3.0 * sd / math.sqrt(s["members"]), 0.1)
