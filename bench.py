@@ -89,7 +89,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
-TIMED = ("ncn_composite_train_fw_sm", "ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
+HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured (79 % of the spec)
+TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
          "ncn_field_bwd", "ncn_field_bwd_mlp_part", "ncn_field_scatter", "ncn_cluster_loss")
 
 
@@ -106,10 +107,9 @@ def pmc_traffic():
 
 def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
     """Live HIP-event measurement of the roofline kernel, the training step's compositor
-    (ncn_composite_train_fw_bg over the fused marcher's rays_a, long rays first; the sample-major
-    ncn_composite_train_fw_sm timed beside it on the same sets).  `n_sets` input sets (the bench
-    batches marched with different jitter and run through the field as in the step, ~16.5 MB each:
-    n_sets x that > the 256 MiB Infinity Cache) are prepared; then
+    (ncn_composite_train_fw_bg over the fused marcher's rays_a, long rays first).  `n_sets` input
+    sets (the bench batches marched with different jitter and run through the field as in the step,
+    ~16.5 MB each: 24 sets ~ 400 MB, ~1.5x the 256 MiB Infinity Cache) are prepared; then
       hbm:     `reps` back-to-back launches cycling through the sets behind a GPU spin: every launch
                reads inputs the launches between evicted from the caches (HBM-bound), the average
                launch duration -> `achieved` / `frac`;
@@ -122,13 +122,7 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
     from ncnerf_amd import vren
     from ncnerf_amd.rendering import march_buffers, march_train_fused
     fn = _lib.lib().ncn_composite_train_fw_bg  # the step's compositor (ray-major)
-    fn_sm = _lib.lib().ncn_composite_train_fw_sm  # the sample-major alternative, timed beside it
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-
-    def sm_args(k, R, S, n_dev=None, grid=None):
-        return [ptr(k["sig"]), ptr(k["rgb"]), ptr(k["dl"]), ptr(k["ts"]), ptr(k["codes"]), ptr(k["ra"]), I64(R),
-                I64(S), ptr(n_dev), I64(grid or S), I32(3), F32(1e-4)] + [ptr(t) for t in k["res"][:5]] + [
-                    F32(1.0), ptr(k["res"][5]), stream()]
 
     def rm_args(k, R, S):
         return [ptr(k["sig"]), ptr(k["rgb"]), ptr(k["dl"]), ptr(k["ts"]), ptr(k["ra"]), I64(R), I64(S), I32(3),
@@ -141,7 +135,7 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
             o, d = batch["rays_o"].contiguous(), batch["rays_d"].contiguous()
             R = o.shape[0]
             mk = march_train_fused(model, o, d, 0.01, 1024, noise=torch.rand(R, device=dev),
-                                   out=march_buffers(R, 1024, dev, codes=True))
+                                   out=march_buffers(R, 1024, dev))
             S = int(mk["counter"][0].item())
             out = model(mk["xyzs"], mk["dirs"], n_samples_dev=mk["counter"])
             res = [torch.empty(R, dtype=torch.int64, device=dev), torch.empty(R, device=dev), torch.empty(R, device=dev),
@@ -149,7 +143,7 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
             if j < len(batches):  # in-step: right behind the field forward that produced the inputs, as
                 # the step launches it (capacity-sized arrays)
                 full = {"sig": out["sigmas"], "rgb": out["rgbs"], "dl": mk["deltas"], "ts": mk["ts"],
-                        "codes": mk["sample_ray"], "ra": mk["rays_a"],
+                        "ra": mk["rays_a"],
                         "res": res[:4] + [torch.empty(mk["ts"].shape[0], device=dev), res[5]]}
                 args = rm_args(full, R, mk["ts"].shape[0])
                 for rep in range(2):  # (rep 0 warms up)
@@ -164,14 +158,11 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
                 del full
             # compact copies (S rows) so the sets are disjoint, cache-sized data
             keep = {"sig": out["sigmas"][:S].clone(), "rgb": out["rgbs"][:S].clone(), "dl": mk["deltas"][:S].clone(),
-                    "ts": mk["ts"][:S].clone(), "ra": mk["rays_a"].clone(), "codes": mk["sample_ray"][:S].clone(),
-                    "res": res}
+                    "ts": mk["ts"][:S].clone(), "ra": mk["rays_a"].clone(), "res": res}
             keep["args"] = rm_args(keep, R, S)
-            keep["args_sm"] = sm_args(keep, R, S)
             sets.append(keep)
             del out, mk
         for k in sets:  # (first-call costs, and the algorithmic bytes of each set)
-            assert fn_sm(*k["args_sm"]) == 0
             assert fn(*k["args"]) == 0
         torch.cuda.synchronize()
         nbytes = [24.0 * float(k["res"][0].sum().item()) + 4.0 * k["sig"].shape[0] + 52.0 * k["ra"].shape[0]
@@ -190,8 +181,6 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
 
         t_hbm = b2b(fn, [k["args"] for k in sets])
         t_warm = b2b(fn, [sets[0]["args"]])
-        t_hbm_sm = b2b(fn_sm, [k["args_sm"] for k in sets])
-        t_warm_sm = b2b(fn_sm, [sets[0]["args_sm"]])
         # the same kernel on config #4's global batch (65536 rays, one launch): 3 sets of ~140 MB
         # cycled (> the Infinity Cache), so each launch reads from HBM
         big = []
@@ -225,8 +214,8 @@ def composite_fw_roofline(model, batches, dev, scene_big, reps=48, n_sets=24):
         t_big = b2b(fn, [k["args"] for k in big], n=12)
         del big
     mean_bytes = float(np.mean([nbytes[i % len(sets)] for i in range(reps)]))
-    return mean_bytes, {"hbm": t_hbm, "warm": t_warm, "in_step": float(np.mean(t_in)), "hbm_sm": t_hbm_sm,
-                        "warm_sm": t_warm_sm, "warm_bytes": nbytes[0], "big_us": t_big,
+    return mean_bytes, {"hbm": t_hbm, "warm": t_warm, "in_step": float(np.mean(t_in)), "warm_bytes": nbytes[0],
+                        "big_us": t_big,
                         "big_bytes": float(np.mean(big_bytes))}
 
 
@@ -655,8 +644,10 @@ def main():
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
-                   "grad_wire": ("fp16 (S*g, the reference's DDP wire)" if args.precision == "fp16" and
-                                 distributed.DP_WIRE != "fp32" else "fp32") if world > 1 else None,
+                   "grad_wire": ("fp16(fp16(S*g)/world): the reference's DDP wire, divided by the world before "
+                                 "the SUM as DDP's default hook; optimizer grad_scale 1" if args.precision == "fp16" and
+                                 distributed.DP_WIRE != "fp32" else "fp32 (SUM, 1/world in the optimizer)")
+                   if world > 1 else None,
                    "step": "eager" if args.no_graph else "hip_graph" + (
                        "" if args.no_defer else " (optimizer of step k beside the marcher of step k+1)") + (
                        "" if args.no_split else " (photometric backward beside the normal clustering)")},
@@ -667,26 +658,28 @@ def main():
         "roofline": {"kernel": "composite_train_fw (ncn_composite_train_fw_bg, the step's compositor)",
                      "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
+                     "measured_copy_gbs": HBM_COPY_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": round(cf_bytes_per_launch),
                      "avg_launch_us": round(cf_us, 2),
                      "warm_us": round(cf_t["warm"], 2),
                      "frac_warm": round(cf_t["warm_bytes"] / (cf_t["warm"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                      "in_step_us": round(cf_t["in_step"], 2),
-                     "sample_major": {"kernel": "ncn_composite_train_fw_sm (per-sample ray codes, no rays_a "
-                                                "dependency; opt-in: NCN_COMPOSITE=sm)",
-                                      "avg_launch_us": round(cf_t["hbm_sm"], 2),
-                                      "frac": round(cf_bytes_per_launch / (cf_t["hbm_sm"] * 1e-6) / 1e9 /
-                                                    HBM_PEAK_GBS, 4),
-                                      "warm_us": round(cf_t["warm_sm"], 2)},
                      "batch65536": {"avg_launch_us": round(cf_t["big_us"], 2),
                                     "algorithmic_bytes_per_launch": round(cf_t["big_bytes"]),
                                     "frac": round(cf_t["big_bytes"] / (cf_t["big_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                                     "method": "one launch over config #4's global batch (65536 rays), 12 launches "
                                               "cycling through 3 sets of ~140 MB (HBM-cold), HIP events around all"},
+                     "single_launch_floor": {"us": 5.1, "frac": 0.41,
+                                             "note": "a load-only kernel of the same grid over the same ~19 MB "
+                                                     "(round 4, DESIGN section 7): the launch ramp plus one round "
+                                                     "of loads at ~6.3 TB/s bound one 8192-ray launch at ~0.41 of "
+                                                     "the 8 TB/s spec before any arithmetic"},
                      "method": "avg_launch_us (-> achieved, frac): 48 back-to-back launches cycling through 24 "
-                               "input sets (~16.5 MB each, 24x > the 256 MiB Infinity Cache: every launch reads "
-                               "from HBM), HIP events on the launch stream around all of them behind a GPU spin; "
+                               "input sets (~16.5 MB each, ~400 MB in all, ~1.5x the 256 MiB Infinity Cache, so "
+                               "each set is evicted before it is read again), HIP events on the launch stream "
+                               "around all of them behind a GPU spin; "
                                "warm_us: the same on one set (cache-resident); in_step_us: one launch right behind "
                                "the field forward that produced its inputs, its own event pair (launch ramp and "
                                "event overhead included). Algorithmic bytes 24*S_vr + 4*S + 52*R (SURVEY 8d)"},

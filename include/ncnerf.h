@@ -95,16 +95,14 @@ int ncn_march_train_pack(const float* rays_d, const int64_t* rays_a, int64_t n_r
  * valid) and counter = {S, R}.  Sample segments are in ray order; rays_a ROWS put the rays with
  * more than 256 samples first (each class in ray order), so the compositors start them first (the
  * reference's rows are in atomicAdd order: any row order is within its contract).  Slabs as ncn_march_train_walk; work =
- * ncn_march_train_fused_work_bytes(R) bytes of scratch.  R <= 16384.
- * sample_ray: NULL, or (capacity) int32 per-sample ray codes for ncn_composite_train_fw_sm:
- * ray + 1 for rays of at most 256 samples, -(ray + 1) for longer ones (max_samples <= 1024). */
+ * ncn_march_train_fused_work_bytes(R) bytes of scratch.  R <= 16384. */
 int64_t ncn_march_train_fused_work_bytes(int64_t n_rays);
 int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_rays, float cx, float cy, float cz,
                           float hx, float hy, float hz, float near_distance, const float* noise, uint64_t seed,
                           const int64_t* rng_counter, const uint8_t* bitfield, int cascades, float scale,
                           int grid_size, int max_samples, float* slab_xyz, float* slab_t, float* slab_dt, void* work,
                           int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
-                          int32_t* sample_ray, void* stream);
+                          void* stream);
 
 /* ---- test-time marcher: replaces vren.raymarching_test (raymarching.cu:407-454).
  * Outputs (A,N_samples[,3]) are fully written (zeros past n_eff).  Mutates hits_t[r][0]. ---- */
@@ -125,20 +123,6 @@ int ncn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, con
                            const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
                            int64_t n_samples, int n_rend, const float* opacity, const float* depth,
                            const float* rend, float T_threshold, float* dL_dsigmas, float* dL_draws, void* stream);
-
-/* The training step's compositor (same outputs as ncn_composite_train_fw_bg), sample-major: waves
- * own fixed ranges of 256 consecutive samples and find the segments from the per-sample ray codes
- * of ncn_march_train_fused (sample_ray), so no sample load waits for rays_a; rays of more than 256
- * samples are taken from rays_a's first rows (long rays first, as the fused marcher orders them),
- * rays without samples from a pass over rays_a.  Samples [0, count) with count = *n_samples_dev
- * (device) or n_samples (host, when n_samples_dev is NULL); with n_samples_dev, n_samples is the
- * arrays' capacity and the grid covers grid_samples samples in one pass (the waves loop over any
- * beyond).  ws is written for samples [0, count). */
-int ncn_composite_train_fw_sm(const float* sigmas, const float* raws, const float* deltas, const float* ts,
-                              const int32_t* sample_ray, const int64_t* rays_a, int64_t n_rays, int64_t n_samples,
-                              const int32_t* n_samples_dev, int64_t grid_samples, int n_rend, float T_threshold,
-                              int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws, float bg,
-                              float* rgb_bg, void* stream);
 
 /* VolumeRenderer.forward's total_samples.sum() (custom_functions.py:139-146) -> *sum_out (int64),
  * one workgroup; with acc != NULL also acc[0] += counter[0] (the marcher's sample count; counter may
@@ -386,6 +370,12 @@ int64_t ncn_cluster_workspace_words(int K);
  * the photometric part only — so no gradient of a timed-out clustering is ever applied.  The
  * caller reads the word outside the hot loop (the training step: every few steps) and fails. */
 int64_t ncn_cluster_status_offset(int K);
+/* Co-residency guarantee of ncn_cluster_loss's grid barriers: its workgroups (16 x 512 threads) must
+ * all be resident at once.  *capacity = (the device's CUs - busy_cus) x the kernel's workgroups per
+ * CU; returns 0 when that holds the 16, else hipErrorCooperativeLaunchTooLarge (a caller that runs
+ * work beside the clustering — the split step's rgb pass, one workgroup per CU — checks it before
+ * capturing the step; ncn_cluster_loss itself refuses when the idle device cannot hold them). */
+int ncn_cluster_coresidency(int K, int busy_cus, int* capacity);
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, const uint32_t* kmeans_plan,
                      float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,

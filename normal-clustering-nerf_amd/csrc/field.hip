@@ -160,9 +160,6 @@ __global__ void pack_weights_kernel(const float* __restrict__ W, T* __restrict__
 }
 
 // ---- hash grid ----
-#ifndef NCN_ENC_LEVEL_MAJOR
-#define NCN_ENC_LEVEL_MAJOR 1  // density pass scratch level-major (encode_xcd_kernel / field_fwd mode 2)
-#endif
 struct LevelTable {
     float scale[16];
     uint32_t res[16], params[16], offset[16];
@@ -387,23 +384,13 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_windows_kernel(const float*
 
 // ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
-// Waves per SIMD the field forward is compiled for (0: the compiler's choice — the training
-// instantiation takes 120 VGPRs + 8 AGPRs, 4 waves/SIMD).  Measured on a build whose training loop
-// still carried the density read (128 + 8, 3 waves/SIMD; tools/scatter_probe.py, same box): 4 waves
-// 101.1 us, default 101.5, 5 (17 VGPRs spilled) 124.6, 6 (34 spilled) 147.7 — not occupancy-bound.
-#ifndef NCN_FWD_WPE
-#define NCN_FWD_WPE 0
-#endif
-#if NCN_FWD_WPE > 0
-#define NCN_FWD_ATTR __attribute__((amdgpu_waves_per_eu(NCN_FWD_WPE)))
-#else
-#define NCN_FWD_ATTR
-#endif
+// (Measured: the field forward at 4 waves/SIMD (amdgpu_waves_per_eu) 101.1 us vs the compiler's
+// choice 101.5, 5 and 6 waves/SIMD spill (124.6 / 147.7 us) — it is not occupancy-bound.)
 // DENSITY: the grid refresh's mode 2 (encodings from encode_xcd_kernel's scratch, sigma only) as its
 // own instantiation — the training forward's loop then carries no trace of it (with the scratch read
 // inside the shared loop the training kernel took 136 registers, 3 waves/SIMD, and ran ~10 % slower).
 template <typename T, bool DENSITY>
-__global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
+__global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                         int64_t n, const int32_t* __restrict__ n_dev,
                                                         const float2* __restrict__ table, LevelTable Lt,
                                                         float xyz_min, float xyz_extent,
@@ -434,15 +421,11 @@ __global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float
         const int64_t s = valid && order ? (int64_t)order[pos] : pos;
         v8 e;
         if constexpr (DENSITY) {  // the encodings of encode_xcd_kernel (mode 2: density only)
-#if NCN_ENC_LEVEL_MAJOR
             typedef T t2 __attribute__((ext_vector_type(2)));
             const t2* el = (const t2*)enc_cache + pos;  // levels 2g, 2g+1 | 8+2g, 9+2g of sample pos
             const t2 a0 = el[(2 * g) * n16], a1 = el[(2 * g + 1) * n16];
             const t2 b0 = el[(8 + 2 * g) * n16], b1 = el[(9 + 2 * g) * n16];
             e = v8{a0[0], a0[1], a1[0], a1[1], b0[0], b0[1], b1[0], b1[1]};
-#else
-            e = enc_cache[grp * 64 + lane];
-#endif
         } else {
             float x = 0.f, y = 0.f, z = 0.f;
             if (valid) {
@@ -482,8 +465,7 @@ __global__ __launch_bounds__(256) NCN_FWD_ATTR void field_fwd_kernel(const float
 // 4 MB L2 holds at most two levels' tables instead of serving all 16 (45.8 MB) from the Infinity
 // Cache (the sample-major forward on Morton-ordered grid points: 436 us; with every hashed level
 // reading one table: 206 us — tools/field_probe.py).  Output: a level-major scratch [16][n16] of T
-// pairs (NCN_ENC_LEVEL_MAJOR; 172 vs 179 us for the pass with the forward's fragment-order layout,
-// tools/density_probe.py), each level's pairs written by its own block; field_fwd_kernel mode 2
+// pairs (172 vs 179 us for the pass with the forward's fragment-order layout, tools/density_probe.py), each level's pairs written by its own block; field_fwd_kernel mode 2
 // gathers lane (g, r)'s levels {2g, 2g+1 | 8+2g, 9+2g} from it and runs sigma_net.  Same
 // encode_level and operand rounding as the sample-major forward: bit-identical sigmas.
 template <typename T>
@@ -506,16 +488,10 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
     const float z = (xyzs[3 * s + 2] - xyz_min) / xyz_extent;
     const float2 a = encode_level(table, L, l, x, y, z);
     typedef T t2 __attribute__((ext_vector_type(2)));
-#if NCN_ENC_LEVEL_MAJOR
     // level-major scratch [16][n16] of T pairs: a workgroup's 256 points of one level are one
-    // contiguous 1 KB store (the fragment-order layout below scattered 4-byte pieces of 64-byte
-    // records over 16 workgroups on 8 XCDs)
+    // contiguous 1 KB store (a fragment-order layout scattered 4-byte pieces of 64-byte records over
+    // 16 workgroups on 8 XCDs: 179 vs 172 us for the pass)
     ((t2*)enc)[(int64_t)l * n16 + s] = t2{(T)a.x, (T)a.y};
-#else
-    const int g = (l & 7) >> 1, half = l >> 3, sub = l & 1;
-    const int lane = g * 16 + (int)(s & 15);
-    *(t2*)(enc + ((s >> 4) * 64 + lane) * 8 + half * 4 + sub * 2) = t2{(T)a.x, (T)a.y};
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1000,87 +976,39 @@ __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb_sigma
 // coarse level for tens of steps, and the rays of a patch re-touch the same entries (per
 // 2-8K-sample span the contributions per distinct entry are ~460 at level 0 and still ~6 at
 // level 15).  So the work is organised around runs and a per-workgroup LDS table:
-//  * a unit of work is (span of consecutive samples, level); the span is 8192 samples on levels
-//    0-9, 4096 on 10-11, 2048 on 12-15 (1024 lanes x 8/4/2 samples), so that a unit's distinct
-//    entries fit the table;
-//  * phase A, lane-sequential: every lane walks its 8/4/2 consecutive samples and sums the eight
-//    corner contributions of consecutive samples in the same cell in registers (a run); a cell
-//    change (or the lane's last sample) emits a run record (cell, 16 sums) into the wave's LDS
-//    staging area (ballot + mbcnt compaction, 64 records);
-//  * phase B, when the staging area is full: one record per lane, its 8 corners looked up in a
-//    4-way set-associative LDS table (one ds_read_b128 per set, ds_cmpst to claim a way) and
-//    added with ds_add_u64 as 64-bit FIXED-POINT sums (exact integer arithmetic: order-independent
-//    and reproducible; an LDS f32 atomic costs ~3 cycles per active lane on gfx950, a u64 add
-//    ~13 per wave-instruction).  Per unit the scale is 2^k with k = 46 - e, max|dE| < 2^e: a
-//    record sums at most 8 samples and an entry gets at most 8192 contributions, so the sums
-//    stay below 2^62.  A corner whose set is full goes straight to a global f32 atomic;
+//  * a unit of work is (span of consecutive samples, level): 1024 lanes x C samples x rounds;
+//  * a lane sums the eight corner contributions of its consecutive samples in the same cell in
+//    registers (a run) and hands a finished run to the table;
+//  * coarse levels [0, SC_CELL_HI) are CELL-keyed (sc_add_cell): a run is one lookup of its cell in
+//    a 4-way set-associative LDS table and 16 ds_add_u64 into the cell's corner-major sums; fine
+//    levels are ENTRY-keyed (sc_add): each of the 8 corners looked up in its own 4-way set (one
+//    ds_read_b128 per set, ds_cmpst to claim a way) and its (x, y) added with two ds_add_u64;
+//  * sums are 64-bit FIXED-POINT (exact integer arithmetic: order-independent and reproducible; an
+//    LDS f32 atomic costs ~3 cycles per active lane on gfx950 against ~13 per wave-instruction for a
+//    u64 add, and f32 slot sums measured 2-3x slower under the same-slot conflicts).  The
+//    scale of a level is 2^k, k = 61 - log2(unit samples) - e, max|dE| < 2^e (the MLP pass records
+//    max|dE| per level), so an entry's unit sum stays below 2^62.  A corner whose set is full goes
+//    straight to a global f32 atomic;
 //  * at the end of the unit the claimed slots (the `used` list) are flushed with one f32 global
-//    atomic per non-zero sum and reset.  A unit whose gradient is not finite adds every record
-//    straight to global memory (NaN/Inf propagate as in the f32 path).
-#ifndef NCN_SC_THREADS
-#define NCN_SC_THREADS 1024
-#endif
-constexpr int SC_THREADS = NCN_SC_THREADS;  // workgroups per CU: 1024 / SC_THREADS (tables scale with it)
+//    atomic per non-zero sum and reset.  A unit whose gradient is not finite adds every run straight
+//    to global memory (NaN/Inf propagate as in the f32 path).
+constexpr int SC_THREADS = 1024;  // one workgroup per CU (the LDS table takes the CU's LDS)
 constexpr int SC_WAVES = SC_THREADS / 64;
-constexpr int SC_WAYS = 4;                 // 4-way set associative: one ds_read_b128 per lookup
-constexpr int SC_REC = 64;                 // staged run records per wave (80 B each: 80 KB)
-// Slot value: NCN_SC_PACK = 1 keeps the (x, y) sums of an entry as two 32-bit fixed-point halves of
-// ONE 64-bit word (y * 2^32 + x: one ds_add_u64 per corner, 14 B per slot); 0 keeps two 64-bit sums
-// (22 B per slot).
-#ifndef NCN_SC_PACK
-#define NCN_SC_PACK 0
-#endif
-constexpr bool SC_PACK = NCN_SC_PACK != 0;
-constexpr int SC_SLOT_BYTES = SC_PACK ? 4 + 8 + 2 : 4 + 8 + 8 + 2;
-// Direct-layout (fine) levels: NCN_SC_F32_DIR = 1 sums an entry's (x, y) in a unit with two f32 LDS
-// atomics into one 8-B slot value (float x, float y) instead of two 64-bit fixed-point sums: half
-// the LDS bytes per corner and 14-B slots (more sets in the same LDS), at the price of a unit sum
-// that depends on the order of its adds (f32 rounding; tcnn sums in fp16 atomics).
-#ifndef NCN_SC_F32_DIR
-#define NCN_SC_F32_DIR 0
-#endif
-constexpr bool SC_F32_DIR = NCN_SC_F32_DIR != 0 && !SC_PACK;
-constexpr int SC_DIR_SLOT_BYTES = SC_F32_DIR ? 4 + 8 + 2 : SC_SLOT_BYTES;
-// Two LDS layouts over one arena: run levels (sets + the record staging, 80 KB at 1024 threads);
-// direct levels (sets only).  Unpacked: 768 / 1536 sets (66 / 132 KB); packed: 1152 / 2560.
-#ifndef NCN_SC_SETS_RUN
-#define NCN_SC_SETS_RUN (SC_PACK ? 1152 : 768)
-#endif
-#ifndef NCN_SC_SETS_DIR
-#define NCN_SC_SETS_DIR (SC_PACK ? 2560 : SC_F32_DIR ? 2432 : 1536)
-#endif
-constexpr int SC_SETS_RUN = NCN_SC_SETS_RUN * SC_THREADS / 1024, SC_SETS_DIR = NCN_SC_SETS_DIR * SC_THREADS / 1024;
-constexpr int sc_layout_bytes(int sets, bool staging) {
-    return sets * SC_WAYS * (staging ? SC_SLOT_BYTES : SC_DIR_SLOT_BYTES) + (staging ? SC_WAVES * SC_REC * 80 : 0);
-}
+constexpr int SC_WAYS = 4;        // 4-way set associative: one ds_read_b128 per lookup
+constexpr int SC_SLOT_BYTES = 4 + 8 + 8 + 2;  // key, x and y sums, `used` entry
+constexpr int SC_SETS_DIR = 1536;  // entry-keyed layout: 6 144 slots (132 KB)
 // Cell-keyed layout (the coarse levels [0, SC_CELL_HI)): a slot is one grid CELL of the level and
-// holds the packed sums of its 8 corners (corner-major: vals[c * slots + slot]); 70 B per slot.
-#ifndef SC_CELL_HI
-#define SC_CELL_HI 10
-#endif
-// Values per cell slot: 8 packed words (SC_PACK) or 16 64-bit sums (x and y of the 8 corners).
-constexpr int SC_CELL_VALS = SC_PACK ? 8 : 16;
-// NCN_SC_F32_CELL = 1: the 16 sums of a cell slot as f32 LDS atomics (4 B each: 70-B slots, 480
-// sets in the same LDS) instead of 64-bit fixed point (see NCN_SC_F32_DIR).
-#ifndef NCN_SC_F32_CELL
-#define NCN_SC_F32_CELL 0
-#endif
-constexpr bool SC_F32_CELL = NCN_SC_F32_CELL != 0 && !SC_PACK;
-constexpr int SC_CELL_WORDS = SC_F32_CELL ? 8 : SC_CELL_VALS;  // 8-B words of values per slot
-#ifndef NCN_SC_SETS_CELL
-#define NCN_SC_SETS_CELL (SC_PACK ? 512 : SC_F32_CELL ? 480 : 256)
-#endif
-constexpr int SC_SETS_CELL = NCN_SC_SETS_CELL * SC_THREADS / 1024;
-constexpr int sc_cell_bytes(int sets) { return sets * SC_WAYS * (4 + SC_CELL_WORDS * 8 + 2); }
+// holds the 64-bit sums of its 8 corners' x and y (corner-major: vals[(2c + xy) * slots + slot]).
+constexpr int SC_CELL_HI = 10;
+constexpr int SC_CELL_VALS = 16;
+constexpr int SC_SETS_CELL = 256;  // 1 024 cell slots (137 KB)
 constexpr int sc_max(int a, int b) { return a > b ? a : b; }
-#ifndef SC_RUN_LEVELS
-#define SC_RUN_LEVELS 10
-#endif
-// (the run layout — record staging — only when some level uses it: SC_RUN_LEVELS > SC_CELL_HI)
-constexpr int SC_ARENA = sc_max(sc_cell_bytes(SC_SETS_CELL),
-                                sc_max(SC_RUN_LEVELS > SC_CELL_HI ? sc_layout_bytes(SC_SETS_RUN, true) : 0,
-                                       sc_layout_bytes(SC_SETS_DIR, false)));
+constexpr int SC_ARENA = sc_max(SC_SETS_CELL * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2), SC_SETS_DIR * SC_WAYS * SC_SLOT_BYTES);
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
+constexpr int SC_BATCH = 2;  // corners per batch of set reads in sc_add (2: 232 us, 4: 238 us (spills), 8: 298 us)
+constexpr int SC_C_DIR = 4;  // samples per lane on the fine levels (unit = 4096 samples, in grabs of 64 x 2)
+constexpr int SC_DIR_HALF = 15;  // fine levels from here on: 2 samples per lane (units of 2048; 13: 198, 14: 202, 15: 190, none: 202 us)
+constexpr int SC_C_CELL = 4;     // samples per lane per round on the cell levels
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
 
@@ -1093,72 +1021,25 @@ __device__ __forceinline__ long long sc_fix(float v, int k) {
     return __double_as_longlong(y) - __double_as_longlong(magic);
 }
 
-// (packed slots) round(x * 2^k) + round(y * 2^k) * 2^32 as one 64-bit addend: with x_i < 0 the high
-// half borrows one, so sums of addends are sum(y_i) * 2^32 + sum(x_i) exactly while |sum| < 2^31
-// (the scale k guarantees it); sc_unpack recovers both sums.
-__device__ __forceinline__ unsigned long long sc_fix2(float x, float y, int k) {
-    const int xi = __float2int_rn(ldexpf(x, k)), yi = __float2int_rn(ldexpf(y, k));
-    return ((unsigned long long)(uint32_t)(yi + (xi >> 31)) << 32) | (uint32_t)xi;
-}
-__device__ __forceinline__ float sc_q(float v, int k) { return ldexpf(rintf(ldexpf(v, k)), -k); }
-// a non-zero v that rounds to 0 on the grid 2^-k
-__device__ __forceinline__ bool sc_sub_quantum(float v, int k) { return v != 0.f && fabsf(ldexpf(v, k)) < 0.5f; }
-__device__ __forceinline__ void sc_unpack(long long q, int& xs, int& ys) {
-    xs = (int)(uint32_t)q;
-    ys = (int)((q - (long long)xs) >> 32);
-}
-
-// samples per lane (log2) and span of a unit on level l
-// levels 0-9: 8 samples per lane with run records (unit = 8192 samples); levels 10-15 (cells
-// shorter than ~2 steps, runs rarely longer than one sample): 2 samples per lane, each added
-// directly (unit = 2048 samples)
-#ifndef SC_C_RUN
-#define SC_C_RUN 4  // samples per lane on the run levels (unit = 1024 * SC_C_RUN samples)
-#endif
-#ifndef SC_BATCH
-#define SC_BATCH 2  // corners per batch of set reads in sc_add (2: 232 us, 4: 238 us (spills), 8: 298 us)
-#endif
-#ifndef SC_C_DIR
-#define SC_C_DIR 4  // samples per lane on the direct levels (unit = one sort window)
-#endif
-#ifndef SC_DIR_DYN
-#define SC_DIR_DYN 2  // direct units of C = 4 in dynamic grabs of 64 x 2 (sc_unit): 2 = grab after the adds (191 us all levels vs 195 static); 1 = grab one ahead (194: 9 VGPRs spilled); 0 = static
-#endif
-#ifndef SC_DIR_HALF
-#define SC_DIR_HALF 15  // direct levels from here on: 2 samples per lane (units of 2048; 13: 198, 14: 202, 15: 190, none: 202 us)
-#endif
-
-struct ScRec {
-    uint32_t k0, k1, pad0, pad1;  // cell: k0 = px | py << 16, k1 = pz
-    float v[16];                  // corner c: (x, y) sums at 2c, 2c+1
-};
-
-// The current layout's arrays inside the arena (uniform pointers) and the per-workgroup scalars.
+// The current layout's arrays inside the arena (uniform pointers) and the per-workgroup counters.
 struct ScShared {
     uint32_t* keys;
-    long long *valx, *valy;
-    uint16_t* used;  // slots claimed since the last flush, in claim order
-    ScRec* rec;      // [SC_WAVES][SC_REC] (run layout only)
+    long long *valx, *valy;  // (cell layout: valx = the 16 corner-major arrays)
+    uint16_t* used;          // slots claimed since the last flush, in claim order
     uint32_t sets;
     int slots;
-    float* wmax;
     int* fill;
-    int* grab;  // (SC_DIR_DYN) the unit's grab counter
+    int* grab;  // the unit's grab counter (fine levels)
 };
-enum { SC_MODE_DIR = 0, SC_MODE_RUN = 1, SC_MODE_CELL = 2 };
-__device__ __forceinline__ ScShared sc_layout(char* arena, float* wmax, int* fill, int mode) {
+enum { SC_MODE_DIR = 0, SC_MODE_CELL = 1 };
+__device__ __forceinline__ ScShared sc_layout(char* arena, int* fill, int mode) {
     ScShared sh;
-    const bool run = mode == SC_MODE_RUN;
-    sh.sets = mode == SC_MODE_CELL ? SC_SETS_CELL : run ? SC_SETS_RUN : SC_SETS_DIR;
+    sh.sets = mode == SC_MODE_CELL ? SC_SETS_CELL : SC_SETS_DIR;
     sh.slots = (int)sh.sets * SC_WAYS;
-    sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used, records (16-B aligned)
-    // (packed: one value array; cell mode: 8 corner arrays)
-    sh.valy = mode == SC_MODE_CELL ? sh.valx + (SC_CELL_WORDS - 1) * sh.slots
-            : SC_PACK || (SC_F32_DIR && mode == SC_MODE_DIR) ? sh.valx : sh.valx + sh.slots;
+    sh.valx = (long long*)arena;  // 8-B arrays first, then keys, used
+    sh.valy = mode == SC_MODE_CELL ? sh.valx + (SC_CELL_VALS - 1) * sh.slots : sh.valx + sh.slots;
     sh.keys = (uint32_t*)(sh.valy + sh.slots);
     sh.used = (uint16_t*)(sh.keys + sh.slots);
-    sh.rec = (ScRec*)(sh.used + sh.slots);
-    sh.wmax = wmax;
     sh.fill = fill;
     return sh;
 }
@@ -1168,10 +1049,7 @@ struct ScLevel {
     float scale;
     uint32_t res, params, off;
     bool dense, direct;
-    bool f32;  // (SC_F32_DIR) f32 slot sums
     int k;
-    uint32_t rep_sets;  // (cell levels) sets per replica of the cell table
-    int rep_mask;       // replicas - 1
 };
 
 __device__ __forceinline__ void sc_corner_entries(const ScLevel& L, uint32_t px, uint32_t py, uint32_t pz,
@@ -1192,7 +1070,7 @@ __device__ __forceinline__ void sc_corner_entries(const ScLevel& L, uint32_t px,
     }
 }
 
-// Phase B core: one contribution set per lane (cell px,py,pz; v = the 8 corners' (x, y) sums).
+// Entry-keyed table: one contribution set per lane (cell px,py,pz; v = the 8 corners' (x, y) sums).
 // Called by the whole wave; lanes with all-zero v add nothing.
 __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint32_t py, uint32_t pz,
                                        const float (&v)[16], const ScLevel& L, float* __restrict__ grad) {
@@ -1227,23 +1105,15 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
             kk[b] = *(const uint4*)&sh.keys[p0[b]];
         }
         int sl[SC_BATCH];
-        bool vc[SC_BATCH], ex[SC_BATCH], miss = false;
+        bool vc[SC_BATCH], miss = false;
 #pragma unroll
         for (int b = 0; b < SC_BATCH; b++) {
             const uint32_t k = e[c0 + b];
-            const float vx = v[2 * (c0 + b)], vy = v[2 * (c0 + b) + 1];
-            // (packed) a non-zero component below half the fixed-point quantum would round to 0: the
-            // corner goes to global memory exactly, so every entry the oracle's f32 sums give a
-            // gradient gets one (Adam with eps 1e-15 steps a tiny gradient by a full lr)
-            ex[b] = SC_PACK && (sc_sub_quantum(vx, L.k) || sc_sub_quantum(vy, L.k));
-            vc[b] = ((vx != 0.f) | (vy != 0.f)) && !ex[b];
+            vc[b] = (v[2 * (c0 + b)] != 0.f) | (v[2 * (c0 + b) + 1] != 0.f);
             sl[b] = kk[b].x == k ? p0[b] : kk[b].y == k ? p0[b] + 1 : kk[b].z == k ? p0[b] + 2
                   : kk[b].w == k ? p0[b] + 3 : -1;
             miss |= vc[b] && sl[b] < 0;
         }
-#ifdef NCN_DIAG_SC_NO_CLAIM
-        miss = false;  // diagnostic: misses are neither claimed nor added
-#endif
         if (__ballot(miss)) {  // uniform
 #pragma unroll
             for (int b = 0; b < SC_BATCH; b++) {
@@ -1273,37 +1143,20 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
             const int c = c0 + b;
             slot[c] = sl[b];
             if (vc[b] && sl[b] >= 0) {
-#ifndef NCN_DIAG_SC_NO_LDSADD
-                if constexpr (SC_PACK) {
-                    atomicAdd((unsigned long long*)&sh.valx[sl[b]], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
-                } else if (SC_F32_DIR && L.f32) {
-                    float* pf = (float*)&sh.valx[sl[b]];
-                    atomicAdd(pf, v[2 * c]);
-                    atomicAdd(pf + 1, v[2 * c + 1]);
-                } else {
-                    atomicAdd((unsigned long long*)&sh.valx[sl[b]], (unsigned long long)sc_fix(v[2 * c], L.k));
-                    atomicAdd((unsigned long long*)&sh.valy[sl[b]], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
-                }
-#endif
+                atomicAdd((unsigned long long*)&sh.valx[sl[b]], (unsigned long long)sc_fix(v[2 * c], L.k));
+                atomicAdd((unsigned long long*)&sh.valy[sl[b]], (unsigned long long)sc_fix(v[2 * c + 1], L.k));
             }
         }
         bool full = false;
 #pragma unroll
-        for (int b = 0; b < SC_BATCH; b++) full |= (vc[b] && sl[b] < 0) || ex[b];
-        if (__ballot(full)) {  // uniform: some lane's set is full of other entries, or an exact corner
+        for (int b = 0; b < SC_BATCH; b++) full |= vc[b] && sl[b] < 0;
+        if (__ballot(full)) {  // uniform: some lane's set is full of other entries
 #pragma unroll
             for (int b = 0; b < SC_BATCH; b++) {
                 const int c = c0 + b;
-                if ((vc[b] && sl[b] < 0) || ex[b]) {
-#ifndef NCN_DIAG_SC_NO_FALLBACK
-                    // (packed: a set-full corner is rounded to the table's fixed-point grid like every
-                    // LDS addend, so which corners fall back — claim order — moves the result by
-                    // float-add order only; a sub-quantum one is added exactly)
-                    const float gx = SC_PACK && !ex[b] ? sc_q(v[2 * c], L.k) : v[2 * c];
-                    const float gy = SC_PACK && !ex[b] ? sc_q(v[2 * c + 1], L.k) : v[2 * c + 1];
-                    if (gx != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + e[c]), gx);
-                    if (gy != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, gy);
-#endif
+                if (vc[b] && sl[b] < 0) {
+                    if (v[2 * c] != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + e[c]), v[2 * c]);
+                    if (v[2 * c + 1] != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + e[c]) + 1, v[2 * c + 1]);
                 }
             }
         }
@@ -1321,42 +1174,6 @@ __device__ __forceinline__ void sc_add(ScShared& sh, int lane, uint32_t px, uint
         for (int c = 0; c < 8; c++)
             if (newmask & (1u << c)) sh.used[pos++] = (uint16_t)slot[c];
     }
-}
-
-// Phase B of the staged records 0..cnt-1 of this wave (one per lane).
-__device__ __forceinline__ void sc_phase_b(ScShared& sh, int wid, int lane, int cnt, const ScLevel& L,
-                                           float* __restrict__ grad) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's record writes are visible
-    const bool act = lane < cnt;
-    const ScRec& R = sh.rec[wid * SC_REC + (act ? lane : 0)];
-    const uint32_t k0 = R.k0, k1 = R.k1;
-    float v[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = act ? R.v[i] : 0.f;
-    sc_add(sh, lane, k0 & 0xFFFFu, k0 >> 16, k1, v, L, grad);
-}
-
-// Stage the records of the lanes with `em` (cell px,py,pz and the 16 sums); a full staging area
-// is processed first.  Called by the whole wave.
-__device__ __forceinline__ void sc_emit(ScShared& sh, int wid, int lane, int& staged, bool em, uint32_t px,
-                                        uint32_t py, uint32_t pz, const float (&acc)[16], const ScLevel& L,
-                                        float* __restrict__ grad) {
-    const uint64_t m = __ballot(em);
-    const int cnt = __popcll(m);
-    if (cnt == 0) return;
-    if (staged + cnt > SC_REC) {
-        sc_phase_b(sh, wid, lane, staged, L, grad);
-        staged = 0;
-    }
-    if (em) {
-        const int pos = staged + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-        ScRec& R = sh.rec[wid * SC_REC + pos];
-        *(uint4*)&R.k0 = make_uint4(px | (py << 16), pz, 0u, 0u);
-#pragma unroll
-        for (int i = 0; i < 16; i += 4) *(float4*)&R.v[i] = make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
-    }
-    staged += cnt;
 }
 
 // Sample position in [0,1]^3 as the forward computes it ((x - min) / extent; a power-of-two
@@ -1469,42 +1286,9 @@ __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_
     }
 }
 
-// Phase A over the lane's chunk; step C emits the last run.  The loop is not unrolled (one emit
-// site: phase B is inlined once); the chunk is walked as a shift register instead of indexed.
-template <int C>
-__device__ __forceinline__ void sc_phase_a(ScShared& sh, int wid, int lane, ScChunk<C>& ch, const ScLevel& L,
-                                           float* __restrict__ grad, int& staged) {
-    bool have = false;
-    uint32_t cx = 0, cy = 0, cz = 0;
-    float acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) acc[i] = 0.f;
-#pragma unroll 1
-    for (int i = 0; i <= C; i++) {
-        const float2 g = ch.g[0];
-        const bool valid = g.x != 0.f || g.y != 0.f;
-        const LevelPos p = level_pos(L.scale, ch.x[0], ch.y[0], ch.z[0]);
-#pragma unroll
-        for (int j = 0; j + 1 < C; j++) {
-            ch.g[j] = ch.g[j + 1]; ch.x[j] = ch.x[j + 1]; ch.y[j] = ch.y[j + 1]; ch.z[j] = ch.z[j + 1];
-        }
-        ch.g[C - 1] = make_float2(0.f, 0.f);
-        const bool change = have && (i == C || (valid && (p.px != cx || p.py != cy || p.pz != cz)));
-        sc_emit(sh, wid, lane, staged, change, cx, cy, cz, acc, L, grad);
-        const bool start = valid && (change || !have);
-        cx = start ? p.px : cx;
-        cy = start ? p.py : cy;
-        cz = start ? p.pz : cz;
-        have = have || valid;
-#pragma unroll
-        for (int j = 0; j < 16; j++) acc[j] = start ? 0.f : acc[j];
-        sc_corner_sums(p, g, acc);  // g == 0 on an invalid step: adds nothing
-    }
-}
-
-// Direct form (fine levels, no record staging): the lane's consecutive samples in the same cell are
-// summed in registers (a run), and a run's 8 corners go to the table when the cell changes (sc_add
-// is called by the whole wave; lanes without a finished run take part with zeros).
+// Fine levels: the lane's consecutive samples in the same cell are summed in registers (a run), and
+// a run's 8 corners go to the table when the cell changes (sc_add is called by the whole wave;
+// lanes without a finished run take part with zeros).
 template <int C>
 __device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
                                           float* __restrict__ grad) {
@@ -1537,9 +1321,9 @@ __device__ __forceinline__ void sc_direct(ScShared& sh, int lane, const ScChunk<
 }
 
 // ---- cell-keyed form (coarse levels) ----
-// One LDS lookup per run record instead of one per corner: the record's cell (px, py, pz) is the
-// key (px | py << 11 | pz << 22; cells outside that range go straight to global memory) and its 8
-// corner sums are 8 packed ds_add_u64 into the slot's corner arrays.  The flush forms each claimed
+// One LDS lookup per run instead of one per corner: the run's cell (px, py, pz) is the key
+// (px | py << 11 | pz << 22; cells outside that range go straight to global memory) and its 8
+// corners' sums are 16 ds_add_u64 into the slot's corner arrays.  The flush forms each claimed
 // cell's corner entries and adds them to the table gradient (a corner shared by several cells of
 // the unit gets one global add per cell: coarse levels have few cells per unit).
 __device__ __forceinline__ uint32_t sc_corner_entry(const ScLevel& L, uint32_t px, uint32_t py, uint32_t pz, int c) {
@@ -1551,26 +1335,12 @@ __device__ __forceinline__ uint32_t sc_corner_entry(const ScLevel& L, uint32_t p
     return (x ^ (y * 2654435761u) ^ (z * 805459861u)) & (L.params - 1);
 }
 
-// Replicas of the cell table (coarse levels: a unit of 8-16 K samples touches only ~20-180 cells,
-// so hundreds of records land on each cell and their 16 ds_add_u64 serialise on the same slots).
-#ifndef SC_CELL_REP_A
-#define SC_CELL_REP_A 1  // levels 0-5
-#endif
-#ifndef SC_CELL_REP_B
-#define SC_CELL_REP_B 1  // levels 6-9
-#endif
-#ifndef SC_CELL_REP_BY_WAVE
-#define SC_CELL_REP_BY_WAVE 0  // replica = wave index (else lane index), modulo the replica count
-#endif
 __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, uint32_t px, uint32_t py, uint32_t pz,
                                             const float (&v)[16], const ScLevel& L, float* __restrict__ grad) {
     const bool inkey = px < 2048u && py < 2048u && pz < 1024u;
     const uint32_t key = px | (py << 11) | (pz << 22);
     const bool go = act && inkey;
-    // replica of the cell table this lane adds into (lanes, or waves, of one cell spread over
-    // L.rep_mask + 1 copies: fewer same-slot LDS atomics; each copy's slots are flushed on their own)
-    const int rp = (SC_CELL_REP_BY_WAVE ? (int)(threadIdx.x >> 6) : lane) & L.rep_mask;
-    const int p0 = SC_WAYS * (rp * (int)L.rep_sets + (int)sc_set(key, L.rep_sets));
+    const int p0 = SC_WAYS * (int)sc_set(key, sh.sets);
     int sl = -1;
     bool isnew = false;
     uint4 kk = make_uint4(0u, 0u, 0u, 0u);
@@ -1597,42 +1367,24 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
             }
         }
     }
-    // (packed) sub-quantum corners (a non-zero component that would round to 0) go to global
-    // memory exactly
-    uint32_t exm = 0;
-    if constexpr (SC_PACK) {
-#pragma unroll
-        for (int c = 0; c < 8; c++)
-            exm |= (sc_sub_quantum(v[2 * c], L.k) || sc_sub_quantum(v[2 * c + 1], L.k)) ? 1u << c : 0u;
-    }
     if (go && sl >= 0) {
 #pragma unroll
         for (int c = 0; c < 8; c++) {
-            if ((v[2 * c] == 0.f && v[2 * c + 1] == 0.f) || ((exm >> c) & 1)) continue;
-            if constexpr (SC_PACK) {
-                atomicAdd((unsigned long long*)&sh.valx[c * sh.slots + sl], sc_fix2(v[2 * c], v[2 * c + 1], L.k));
-            } else if constexpr (SC_F32_CELL) {  // f32 arrays 2c, 2c + 1
-                atomicAdd((float*)sh.valx + (2 * c) * sh.slots + sl, v[2 * c]);
-                atomicAdd((float*)sh.valx + (2 * c + 1) * sh.slots + sl, v[2 * c + 1]);
-            } else {  // x and y of corner c: arrays 2c, 2c + 1
-                atomicAdd((unsigned long long*)&sh.valx[(2 * c) * sh.slots + sl], (unsigned long long)sc_fix(v[2 * c], L.k));
-                atomicAdd((unsigned long long*)&sh.valx[(2 * c + 1) * sh.slots + sl],
-                          (unsigned long long)sc_fix(v[2 * c + 1], L.k));
-            }
+            if (v[2 * c] == 0.f && v[2 * c + 1] == 0.f) continue;
+            // x and y of corner c: arrays 2c, 2c + 1
+            atomicAdd((unsigned long long*)&sh.valx[(2 * c) * sh.slots + sl], (unsigned long long)sc_fix(v[2 * c], L.k));
+            atomicAdd((unsigned long long*)&sh.valx[(2 * c + 1) * sh.slots + sl],
+                      (unsigned long long)sc_fix(v[2 * c + 1], L.k));
         }
     }
     const bool fb = act && sl < 0;
-    if (__ballot(fb || (act && exm))) {  // uniform: set full / cell outside the key range / exact corners
-        if (fb || (act && exm)) {
+    if (__ballot(fb)) {  // uniform: set full / cell outside the key range
+        if (fb) {
 #pragma unroll
             for (int c = 0; c < 8; c++) {
-                const bool exact = (exm >> c) & 1;
-                if (!fb && !exact) continue;
                 const uint32_t e = L.off + sc_corner_entry(L, px, py, pz, c);
-                const float gx = exact || !SC_PACK ? v[2 * c] : sc_q(v[2 * c], L.k);
-                const float gy = exact || !SC_PACK ? v[2 * c + 1] : sc_q(v[2 * c + 1], L.k);
-                if (gx != 0.f) atomicAdd(grad + 2 * (size_t)e, gx);
-                if (gy != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, gy);
+                if (v[2 * c] != 0.f) atomicAdd(grad + 2 * (size_t)e, v[2 * c]);
+                if (v[2 * c + 1] != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, v[2 * c + 1]);
             }
         }
     }
@@ -1645,40 +1397,6 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
         if (isnew)
             sh.used[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0))] =
                 (uint16_t)sl;
-    }
-}
-
-// (Experiment, off) Wave-level merge of the finished runs that share a cell: up to SC_CELL_MERGE
-// groups of lanes with equal keys summed by one wave reduction each (wave_sum_multi) into the
-// group's first lane before the LDS adds.  Measured (tools/scatter_probe.py, bench batch, levels
-// alone / all): 3 groups 63 -> 69 us on level 0, 191 -> 227 us all levels; 8 groups worse still —
-// the reductions (and the spills they cause at 128 VGPRs) cost more than the same-slot LDS atomics
-// they remove.
-#ifndef SC_CELL_MERGE
-#define SC_CELL_MERGE 0
-#endif
-__device__ __forceinline__ void sc_merge_cells(int lane, bool& act, uint32_t px, uint32_t py, uint32_t pz,
-                                               float (&v)[16]) {
-    uint64_t rem = __ballot(act);
-#pragma unroll 1
-    for (int it = 0; it < SC_CELL_MERGE && rem; it++) {
-        const int leader = (int)__builtin_ctzll(rem);
-        const uint32_t kx = __builtin_amdgcn_readlane(px, leader), ky = __builtin_amdgcn_readlane(py, leader),
-                       kz = __builtin_amdgcn_readlane(pz, leader);
-        const bool mine = act && px == kx && py == ky && pz == kz;
-        const uint64_t grp = __ballot(mine);
-        if (__popcll(grp) < 2) break;  // (uniform) a lone record: leave it and the rest to the per-lane adds
-        float s[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) s[j] = mine ? v[j] : 0.f;
-        wave_sum_multi<16>(s);
-        if (lane == leader) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = s[j];
-        } else if (mine) {
-            act = false;
-        }
-        rem &= ~grp;
     }
 }
 
@@ -1701,11 +1419,8 @@ __device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C
             q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
             emit = q.px != p.px || q.py != p.py || q.pz != p.pz;
         }
-        if (__ballot(emit && any)) {  // uniform
-            bool act = emit && any;
-            if (SC_CELL_MERGE > 0 && !L.direct) sc_merge_cells(lane, act, p.px, p.py, p.pz, v);
-            sc_add_cell(sh, lane, act, p.px, p.py, p.pz, v, L, grad);
-        }
+        if (__ballot(emit && any))  // uniform
+            sc_add_cell(sh, lane, emit && any, p.px, p.py, p.pz, v, L, grad);
         if (i < C) {
 #pragma unroll
             for (int j = 0; j < 16; j++) v[j] = emit ? 0.f : v[j];
@@ -1716,83 +1431,21 @@ __device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C
     }
 }
 
-// SC_CELL_CARRY: a lane's samples of a cell unit are ONE contiguous span over the unit's rounds
-// (round r takes the lane's next C), and the run in progress carries from round to round, so a run
-// record ends only where the cell changes (or at the span's end) instead of at every C-sample
-// chunk: on the coarsest levels (a ray stays ~30-40 samples in one level-0 cell) that is ~rounds x
-// fewer records, i.e. fewer same-slot 64-bit LDS adds (the coarse units' bound).
-#ifndef SC_CELL_CARRY
-#define SC_CELL_CARRY 0
-#endif
-struct ScRun {
-    uint32_t px, py, pz;
-    bool any, init;
-    float v[16];
-};
-template <int C>
-__device__ __forceinline__ void sc_cells_run(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
-                                             float* __restrict__ grad, ScRun& st, bool last) {
-#pragma unroll
-    for (int i = 0; i < C; i++) {
-        const LevelPos q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
-        const bool change = st.init && (q.px != st.px || q.py != st.py || q.pz != st.pz);
-        if (__ballot(change && st.any)) {  // uniform
-            bool act = change && st.any;
-            sc_add_cell(sh, lane, act, st.px, st.py, st.pz, st.v, L, grad);
-        }
-        if (change || !st.init) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) st.v[j] = 0.f;
-            st.any = false;
-            st.px = q.px; st.py = q.py; st.pz = q.pz;
-            st.init = true;
-        }
-        st.any = st.any || ch.g[i].x != 0.f || ch.g[i].y != 0.f;
-        sc_corner_sums(q, ch.g[i], st.v);
-    }
-    if (last && __ballot(st.any)) {  // uniform: the span's last run
-        bool act = st.any;
-        sc_add_cell(sh, lane, act, st.px, st.py, st.pz, st.v, L, grad);
-    }
-}
-
-// Flush of a cell unit: SC_CELL_VALS lanes per claimed cell (packed: one corner each, decode both
-// sums; 64-bit: one corner component each), form the corner's entry, f32 global adds; lane 0 of
-// the cell resets the key, each lane its value.
+// Flush of a cell unit: 16 lanes per claimed cell (one corner component each), form the corner's
+// entry, f32 global adds; lane 0 of the cell resets the key, each lane its value.
 __device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, float* __restrict__ grad) {
     const int nf = *sh.fill;
     constexpr int V = SC_CELL_VALS;
     for (int i = threadIdx.x; i < V * nf; i += SC_THREADS) {
         const int slot = sh.used[i / V], j = i % V;
         const uint32_t key = sh.keys[slot];
-        long long q;
-        float qf = 0.f;
-        if constexpr (SC_F32_CELL) {
-            float* pf = (float*)sh.valx + j * sh.slots + slot;
-            qf = *pf;
-            *pf = 0.f;
-            q = qf != 0.f;
-        } else {
-            long long* pv = &sh.valx[j * sh.slots + slot];
-            q = *pv;
-            *pv = 0;
-        }
-#ifndef NCN_DIAG_SC_NO_FLUSH
+        long long* pv = &sh.valx[j * sh.slots + slot];
+        const long long q = *pv;
+        *pv = 0;
         if (q != 0) {
-            const int c = SC_PACK ? j : j >> 1;
-            const uint32_t e = L.off + sc_corner_entry(L, key & 2047u, (key >> 11) & 2047u, key >> 22, c);
-            if constexpr (SC_PACK) {
-                int xs, ys;
-                sc_unpack(q, xs, ys);
-                if (xs) atomicAdd(grad + 2 * (size_t)e, ldexpf((float)xs, -L.k));
-                if (ys) atomicAdd(grad + 2 * (size_t)e + 1, ldexpf((float)ys, -L.k));
-            } else if constexpr (SC_F32_CELL) {
-                atomicAdd(grad + 2 * (size_t)e + (j & 1), qf);
-            } else {
-                atomicAdd(grad + 2 * (size_t)e + (j & 1), (float)ldexp((double)q, -L.k));
-            }
+            const uint32_t e = L.off + sc_corner_entry(L, key & 2047u, (key >> 11) & 2047u, key >> 22, j >> 1);
+            atomicAdd(grad + 2 * (size_t)e + (j & 1), (float)ldexp((double)q, -L.k));
         }
-#endif
         if (j == 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the cell's other lanes have read the key: same wave)
             sh.keys[slot] = SC_EMPTY;
@@ -1800,89 +1453,67 @@ __device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, f
     }
 }
 
-// One unit: load the chunk, phase A/B or direct, flush.  The fixed-point scale is per level, from
-// the max |dE| the MLP pass recorded (level_max): no per-unit reduction or barrier.
+// Diagnostic builds (tools/scatter_probe.py): NCN_DIAG_SC_TIMES records wave 0's cycles per phase of
+// the fine-level units; NCN_DIAG_SC_LEVELS_MASK skips the levels whose bit is clear.
 #ifdef NCN_DIAG_SC_TIMES
-__device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: cycles per phase x {run, dir}
+__device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: cycles per phase
 #define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
-#define SC_TADD(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2 + (RUNS ? 0 : 1)] += (b) - (a)
+#define SC_TADD(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2 + 1] += (b) - (a)
 #else
 #define SC_TNOW(v)
 #define SC_TADD(i, a, b)
 #endif
-// (Experiment, off) levels >= SC_DIRECT_FROM without the LDS table, every run's corners added with
-// global f32 atomics: measured (tools/scatter_probe.py) 190 -> 627 us from level 15, 1079 us from 14.
-#ifndef SC_DIRECT_FROM
-#define SC_DIRECT_FROM 16
-#endif
-template <int C, bool RUNS>
-__device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
-                                        const float* __restrict__ xyzs, const float2* __restrict__ dEl,
-                                        const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
-                                        const int32_t* __restrict__ order) {
-    SC_TNOW(t0);
-    ScChunk<C> ch;
-    // chunk of lane t of wave w: t * SC_WAVES + w — the 64 lanes of one wave-instruction hold chunks
-    // SC_WAVES * C positions apart, so in the Morton processing order (where neighbouring positions
-    // share cells) they rarely address the same LDS slot at once (same-address LDS atomics serialise)
-    constexpr bool DYN = SC_DIR_DYN && !RUNS && C == 4;
-    if (!DYN) sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, nrm, order);
+
+__device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m, int kbase) {
     ScLevel L;
     L.scale = Lt.scale[l];
     L.res = Lt.res[l];
     L.params = Lt.params[l];
     L.off = Lt.offset[l];
     L.dense = (uint64_t)L.res * L.res * L.res <= L.params;  // tcnn: stride stays <= params
-    // levels >= SC_DIRECT_FROM: every run's corners straight to global f32 atomics (no LDS table)
-    L.direct = !isfinite(m) || l >= SC_DIRECT_FROM;
-    L.f32 = SC_F32_DIR && !RUNS;
-    L.rep_mask = 0;
-    L.rep_sets = sh.sets;
+    L.direct = !isfinite(m);  // (uniform) non-finite gradient: every corner straight to global memory
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
-    // An entry's sum over the unit is at most (unit samples) * m (a sample's 8 corner weights sum
-    // to 1), plus half a unit of rounding per addend: 64-bit sums take k = 46 - e2 (a record sums
-    // at most 8 samples, an entry at most 8192); packed 32-bit halves k = 30 - log2(samples) - e2.
-    constexpr int lg_unit = 31 - __builtin_clz(SC_THREADS * C);
-    L.k = SC_PACK ? 30 - lg_unit - e2 : 46 - e2;
+    // |sum| <= (unit samples) * m * 2^k + rounding (a sample's 8 corner weights sum to 1): < 2^62
+    L.k = kbase - e2;
+    return L;
+}
+
+// One fine-level unit: the samples in grabs, then the flush of the claimed slots.
+template <int C>
+__device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
+                                        const float* __restrict__ xyzs, const float2* __restrict__ dEl,
+                                        const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
+                                        const int32_t* __restrict__ order) {
+    SC_TNOW(t0);
+    // (a fine unit holds at most 4096 samples: 2^46 leaves the sums four bits of headroom below 2^62)
+    const ScLevel L = sc_level(Lt, l, m, 46);
     SC_TNOW(t1);
-    if (RUNS) {
-        int staged = 0;
-        sc_phase_a<C>(sh, wid, lane, ch, L, grad, staged);
-        if (staged) sc_phase_b(sh, wid, lane, staged, L, grad);
-    } else {
-        if constexpr (DYN) {
-            // The unit's samples in grabs of 64 lanes x 2: grab k gives lane t the samples
-            // s0 + (t * NG + k) * 2 (lanes NG * 2 = 64 positions apart, as the static mapping).
-            // Wave w takes grab w, then draws grabs from the unit's LDS counter one grab ahead
-            // (its chunk loads overlap the current grab), so a wave slowed by claims / set-full
-            // fallbacks takes fewer grabs and the waves reach the unit's barrier together.
-            constexpr int NG = SC_THREADS * C / 128;
-            int k = wid;
-            ScChunk<2> cg;
-            sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, nrm, order);
-            while (k < NG) {  // (wave-uniform)
-                if constexpr (SC_DIR_DYN == 2) {  // (variant) no prefetch: grab after the grab's adds
-                    sc_direct<2>(sh, lane, cg, L, grad);
-                    int kn = 0;
-                    if (lane == 0) kn = atomicAdd(sh.grab, 1);
-                    kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
-                    if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, nrm, order);
-                    k = kn;
-                } else {
-                    int kn = 0;
-                    if (lane == 0) kn = atomicAdd(sh.grab, 1);
-                    kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
-                    ScChunk<2> nx;
-                    if (kn < NG) sc_load_chunk<2>(nx, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, nrm, order);
-                    sc_direct<2>(sh, lane, cg, L, grad);
-                    if (kn < NG) cg = nx;
-                    k = kn;
-                }
-            }
-        } else {
-            sc_direct<C>(sh, lane, ch, L, grad);
+    if constexpr (C == 4) {
+        // The unit's 4096 samples in grabs of 64 lanes x 2: grab k gives lane t the samples
+        // s0 + (t * NG + k) * 2 — the 64 lanes of one wave-instruction hold samples 2 * NG = 64
+        // positions apart, so they rarely address the same LDS slot at once (same-address LDS atomics
+        // serialise).  Wave w takes grab w first, then draws grabs from the unit's LDS counter after
+        // each grab's adds, so a wave slowed by claims / set-full fallbacks takes fewer grabs and the
+        // waves reach the unit's barrier together (191 vs 195 us static; drawing one grab ahead so
+        // that its loads overlap spills 9 VGPRs: 194).
+        constexpr int NG = SC_THREADS * C / 128;
+        int k = wid;
+        ScChunk<2> cg;
+        sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, nrm, order);
+        while (k < NG) {  // (wave-uniform)
+            sc_direct<2>(sh, lane, cg, L, grad);
+            int kn = 0;
+            if (lane == 0) kn = atomicAdd(sh.grab, 1);
+            kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
+            if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, nrm, order);
+            k = kn;
         }
+    } else {
+        // chunk of lane t of wave w: t * SC_WAVES + w (lanes SC_WAVES * C positions apart)
+        ScChunk<C> ch;
+        sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, nrm, order);
+        sc_direct<C>(sh, lane, ch, L, grad);
     }
     SC_TNOW(t2);
 #ifdef NCN_DIAG_SC_TIMES
@@ -1899,23 +1530,9 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
         const int slot = sh.used[i >> 1];
         const uint32_t key = sh.keys[slot];
         long long* pv = (i & 1) ? &sh.valy[slot] : &sh.valx[slot];
-        const long long q = *pv;
-        float gv;
-        if (SC_F32_DIR && L.f32) {  // (float x, float y) in one word: the odd lane resets it
-            gv = ((const float*)pv)[i & 1];
-            if (i & 1) *pv = 0;
-        } else if constexpr (SC_PACK) {  // both lanes of the pair read the word; the odd one resets it
-            int xs, ys;
-            sc_unpack(q, xs, ys);
-            gv = ldexpf((float)((i & 1) ? ys : xs), -L.k);
-            if (i & 1) *pv = 0;
-        } else {
-            gv = (float)ldexp((double)q, -L.k);
-            *pv = 0;
-        }
-#ifndef NCN_DIAG_SC_NO_FLUSH
+        const float gv = (float)ldexp((double)*pv, -L.k);
+        *pv = 0;
         if (gv != 0.f) atomicAdd(grad + 2 * (size_t)(L.off + key) + (i & 1), gv);
-#endif
         if (!(i & 1)) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the odd lane has read the key: same wave)
             sh.keys[slot] = SC_EMPTY;
@@ -1933,63 +1550,26 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
 // Cell units: `rounds` consecutive chunks of 1024 x C samples per unit (no barrier between them),
 // then one flush.  Rounds per level: coarse levels have few cells, so longer units mean fewer
 // flushes and barriers.
-#ifndef SC_C_CELL
-#define SC_C_CELL 4
-#endif
-#ifndef SC_CELL_ROUNDS_A
-#define SC_CELL_ROUNDS_A 4  // levels 0-5
-#endif
-#ifndef SC_CELL_ROUNDS_B
-#define SC_CELL_ROUNDS_B 2  // levels 6-9
-#endif
-__device__ __forceinline__ int sc_cell_rounds(int l) { return l < 6 ? SC_CELL_ROUNDS_A : l < 10 ? SC_CELL_ROUNDS_B : 1; }
+__device__ __forceinline__ int sc_cell_rounds(int l) { return l < 6 ? 4 : l < 10 ? 2 : 1; }
 
-#ifndef SC_CELL_CONTIG
-#define SC_CELL_CONTIG 0
-#endif
 template <int C>
 __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1, int rounds,
                                              const float* __restrict__ xyzs, const float2* __restrict__ dEl,
                                              const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
                                              const int32_t* __restrict__ order) {
-    ScLevel L;
-    L.scale = Lt.scale[l];
-    L.res = Lt.res[l];
-    L.params = Lt.params[l];
-    L.off = Lt.offset[l];
-    L.dense = (uint64_t)L.res * L.res * L.res <= L.params;
-    L.direct = !isfinite(m);  // (uniform) non-finite gradient: every corner straight to global memory
-    int e2 = 0;
-    (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
-    // |sum| <= (unit samples) * m * 2^k + rounding: below 2^31 (packed 32-bit halves) / 2^62 (64-bit)
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
-    L.k = (SC_PACK ? 30 : 61) - lg_unit - e2;
-    {
-        const int R = l < 6 ? SC_CELL_REP_A : SC_CELL_REP_B;  // (powers of two)
-        L.rep_mask = R - 1;
-        L.rep_sets = sh.sets / R;
-    }
+    const ScLevel L = sc_level(Lt, l, m, 61 - lg_unit);
+    // lane t of wave w takes chunk t * SC_WAVES + w of each round (neighbouring chunks in different
+    // waves); round r covers the unit's r-th slice of SC_THREADS * C samples
+    const int64_t lane_off = ((int64_t)lane * SC_WAVES + wid) * C;
     ScChunk<C> ch;
-    // lane t of wave w takes chunk t * SC_WAVES + w (neighbouring chunks in different waves); (off)
-    // SC_CELL_CONTIG: wave w covers the contiguous chunks 64w .. 64w+63 — measured: levels 6-9 alone
-    // 37 -> 31 us, all levels 191 -> 193 us (no gain inside the full launch)
-    const int64_t lane_id = SC_CELL_CONTIG ? (int64_t)wid * 64 + lane : (int64_t)lane * SC_WAVES + wid;
-    // round r's chunk of the lane: SC_CELL_CARRY — the lane's span is contiguous over the rounds;
-    // otherwise round r covers the unit's r-th slice of SC_THREADS * C samples
-    const int64_t lane_off = SC_CELL_CARRY ? lane_id * rounds * C : lane_id * C;
-    const int64_t r_step = SC_CELL_CARRY ? C : (int64_t)SC_THREADS * C;
     sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, nrm, order);
-    ScRun st;
-    st.init = st.any = false;
-    st.px = st.py = st.pz = 0;
     for (int r = 0; r < rounds; r++) {
         ScChunk<C> nx;
         const bool more = r + 1 < rounds;
-        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * r_step + lane_off, s1, xyzs, dEl, nrm, order);
+        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * SC_THREADS * C + lane_off, s1, xyzs, dEl, nrm, order);
         if (L.direct)
             sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
-        else if (SC_CELL_CARRY)
-            sc_cells_run<C>(sh, lane, ch, L, grad, st, !more);
         else
             sc_cells<C>(sh, lane, ch, L, grad);
         if (more) ch = nx;
@@ -1999,29 +1579,18 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     lds_barrier();
 }
 
-// Unit queues of field_scatter_kernel (SC_DYN), one per first level of a launch (a launch over
-// [level_lo, level_hi) uses queue level_lo; launches with the same level_lo are stream-ordered).
-// Zero between launches: each launch's last ticket resets its queue.
-#ifndef SC_DYN
-#define SC_DYN 0  // measured: 191 vs 196 us, then 194 vs 190 (static): no gain beyond noise
-#endif
-__device__ unsigned sc_queue[16];
-
 // One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
-__device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n_run, int64_t n_dir4, int64_t ud,
-                                            int64_t ud2, int64_t ur, int64_t n, int cell_lo, int run_lo, int dir_lo,
-                                            int dir_mid, int& layout, int& par, ScShared& sh, char* arena,
-                                            float* wmax, int* fill, const float* lmax_s, int wid, int lane,
+__device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n_dir4, int64_t ud, int64_t ud2, int64_t n,
+                                            int cell_lo, int dir_lo, int dir_mid, int& layout, int& par, ScShared& sh,
+                                            char* arena, int* fill, const float* lmax_s, int wid, int lane,
                                             const float* __restrict__ xyzs, const float2* __restrict__ dE,
                                             int64_t e_stride, const ScNorm& nrm, const LevelTable& Lt,
                                             float* __restrict__ grad, const int32_t* __restrict__ order) {
-    constexpr int C_RUN = SC_C_RUN, C_DIR = SC_C_DIR, C_CELL = SC_C_CELL;
-    const int mode = u < n_cell ? SC_MODE_CELL : u < n_cell + n_run ? SC_MODE_RUN : SC_MODE_DIR;
+    const int mode = u < n_cell ? SC_MODE_CELL : SC_MODE_DIR;
     if (mode != layout) {  // (re)initialise the table of the new layout
         lds_barrier();
-        sh = sc_layout(arena, wmax, fill, mode);
-        const int nv = mode == SC_MODE_CELL ? SC_CELL_WORDS * sh.slots
-                     : SC_PACK || (SC_F32_DIR && mode == SC_MODE_DIR) ? sh.slots : 2 * sh.slots;
+        sh = sc_layout(arena, fill, mode);
+        const int nv = mode == SC_MODE_CELL ? SC_CELL_VALS * sh.slots : 2 * sh.slots;
         for (int i = threadIdx.x; i < sh.slots; i += SC_THREADS) sh.keys[i] = SC_EMPTY;
         for (int i = threadIdx.x; i < nv; i += SC_THREADS) sh.valx[i] = 0;
         if (threadIdx.x == 0) fill[0] = fill[1] = fill[2] = fill[3] = 0;
@@ -2036,7 +1605,7 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
         l = cell_lo;
         for (;; l++) {  // (uniform, at most SC_CELL_HI steps)
             rounds = sc_cell_rounds(l);
-            const int64_t span = (int64_t)SC_THREADS * C_CELL * rounds;
+            const int64_t span = (int64_t)SC_THREADS * SC_C_CELL * rounds;
             const int64_t nu = (n + span - 1) / span;
             if (v < nu) {
                 s0 = v * span;
@@ -2045,19 +1614,13 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
             }
             v -= nu;
         }
-    } else if (mode == SC_MODE_RUN) {
-        const int64_t v = u - n_cell;
-        const int li = (int)(v / ur);
-        l = run_lo + li;
-        s0 = (v - li * ur) * (SC_THREADS * C_RUN);
-        s1 = min(n, s0 + SC_THREADS * C_RUN);
     } else {
-        int64_t v = u - n_cell - n_run;
+        int64_t v = u - n_cell;
         if (v < n_dir4) {
             const int li = (int)(v / ud);
             l = dir_lo + li;
-            s0 = (v - li * ud) * (SC_THREADS * C_DIR);
-            s1 = min(n, s0 + SC_THREADS * C_DIR);
+            s0 = (v - li * ud) * (SC_THREADS * SC_C_DIR);
+            s1 = min(n, s0 + SC_THREADS * SC_C_DIR);
         } else {
             v -= n_dir4;
             const int li = (int)(v / ud2);
@@ -2080,26 +1643,14 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
     par ^= 1;
     const float2* dEl = dE + (int64_t)l * e_stride;
     if (mode == SC_MODE_CELL)
-        sc_cell_unit<C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
-    else if (mode == SC_MODE_RUN)
-        sc_unit<C_RUN, true>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
     else if (rounds == 2)
-        sc_unit<2, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+        sc_unit<2>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
     else
-        sc_unit<C_DIR, false>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+        sc_unit<SC_C_DIR>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
 }
 
-// (experiment) waves per SIMD the scatter is compiled for: 0 = the compiler's choice (128 VGPRs, one
-// 1024-thread workgroup per CU); with the LDS tables halved two workgroups fit a CU's LDS
-#ifndef NCN_SC_WPE
-#define NCN_SC_WPE 0
-#endif
-#if NCN_SC_WPE > 0
-#define NCN_SC_ATTR __attribute__((amdgpu_waves_per_eu(NCN_SC_WPE)))
-#else
-#define NCN_SC_ATTR
-#endif
-__global__ __launch_bounds__(SC_THREADS) NCN_SC_ATTR void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
+__global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
                                                                    const float2* __restrict__ dE,
@@ -2111,7 +1662,6 @@ __global__ __launch_bounds__(SC_THREADS) NCN_SC_ATTR void field_scatter_kernel(c
                                                                    int nb_sigma = 0, int nb_rgb = 0,
                                                                    float* __restrict__ gw = nullptr) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
-    __shared__ float wmax[SC_WAVES];
     __shared__ int fill[4];  // claimed-slot counts [0, 2) and grab counters [2, 4), alternating per unit (reset one unit ahead)
     // per-level max |dE| over the MLP pass's workgroup rows (the fixed-point scale of each level);
     // visible to every thread at the first layout barrier
@@ -2145,57 +1695,31 @@ __global__ __launch_bounds__(SC_THREADS) NCN_SC_ATTR void field_scatter_kernel(c
     nrm.inv = 1.0f / xyz_extent;
     nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
     // units, level-major over the levels [level_lo, level_hi): cell levels [0, SC_CELL_HI) in spans
-    // of 1024 * C_CELL * rounds(l) samples, run levels [SC_CELL_HI, SC_RUN_LEVELS) in spans of
-    // 1024 * SC_C_RUN, direct levels in spans of 1024 * SC_C_DIR
-    constexpr int C_RUN = SC_C_RUN, C_DIR = SC_C_DIR, C_CELL = SC_C_CELL;
-    const int64_t ur = (n + SC_THREADS * C_RUN - 1) / (SC_THREADS * C_RUN);
-    const int64_t ud = (n + SC_THREADS * C_DIR - 1) / (SC_THREADS * C_DIR);
+    // of 1024 * C_CELL * rounds(l) samples, fine levels in spans of 1024 * SC_C_DIR, those from
+    // SC_DIR_HALF on in spans of 1024 * 2 (their ~1 distinct entry per sample would overfill the
+    // 4-way sets of a 4096-sample unit)
+    const int64_t ud = (n + SC_THREADS * SC_C_DIR - 1) / (SC_THREADS * SC_C_DIR);
+    const int64_t ud2 = (n + SC_THREADS * 2 - 1) / (SC_THREADS * 2);
     const int cell_lo = level_lo, cell_hi = min(level_hi, SC_CELL_HI);
-    const int run_lo = max(level_lo, SC_CELL_HI), run_hi = min(level_hi, SC_RUN_LEVELS);
-    const int dir_lo = max(level_lo, max(SC_CELL_HI, SC_RUN_LEVELS)), dir_hi = level_hi;
+    const int dir_lo = max(level_lo, SC_CELL_HI), dir_hi = level_hi;
     int64_t n_cell = 0;
     for (int l = cell_lo; l < cell_hi; l++) {
-        const int64_t span = (int64_t)SC_THREADS * C_CELL * sc_cell_rounds(l);
+        const int64_t span = (int64_t)SC_THREADS * SC_C_CELL * sc_cell_rounds(l);
         n_cell += (n + span - 1) / span;
     }
-    const int64_t n_run = run_hi > run_lo ? (int64_t)(run_hi - run_lo) * ur : 0;
-    // direct levels >= SC_DIR_HALF take half-size units (C = 2: their ~1 distinct entry per sample
-    // would overfill the 4-way sets of a 4096-sample unit)
-    const int64_t ud2 = (n + SC_THREADS * 2 - 1) / (SC_THREADS * 2);
     const int dir_mid = max(dir_lo, min(dir_hi, SC_DIR_HALF));
     const int64_t n_dir4 = dir_mid > dir_lo ? (int64_t)(dir_mid - dir_lo) * ud : 0;
     const int64_t n_dir2 = dir_hi > dir_mid ? (int64_t)(dir_hi - dir_mid) * ud2 : 0;
-    const int64_t n_units = n_cell + n_run + n_dir4 + n_dir2;
-    // Units are ordered heaviest first (the coarse cell levels' long units, then the finer levels).
-    // Workgroup b takes unit b; with SC_DYN every later unit is drawn from a device queue (ticket
-    // t -> unit gridDim.x + t), so a workgroup that finishes early takes the next unit instead of a
-    // fixed stride (the units' costs differ ~10x across levels).  The ticket for the next unit is
-    // drawn at the start of the current one (its latency hides behind the unit) and handed to the
-    // workgroup through LDS at the unit's end.  Tickets are monotone, so a workgroup's units still
-    // go cell -> run -> direct (at most two layout switches).  The holder of the launch's last ticket
-    // (every workgroup's last draw fails, so it is the last access to the counter) resets it.
-    int layout = -1, par = 0, qb = 0;
+    const int64_t n_units = n_cell + n_dir4 + n_dir2;
+    // Units are ordered heaviest first (the coarse cell levels' long units, then the finer levels);
+    // workgroup b takes units b, b + gridDim.x, ...  (a dynamic unit queue measured no better: 191 vs
+    // 196 us, then 194 vs 190 — the static stride is not load-imbalanced).  A workgroup's units go
+    // cell -> fine: at most one layout switch.
+    int layout = -1, par = 0;
     ScShared sh;
-    __shared__ unsigned qnext[2];
-    unsigned* const queue = sc_queue + level_lo;
-    const int64_t n_tickets = max<int64_t>(0, n_units - gridDim.x) + min<int64_t>(gridDim.x, n_units);
-    for (int64_t u = blockIdx.x; u < n_units;) {
-        unsigned tk = 0;
-        if (SC_DYN && threadIdx.x == 0) tk = atomicAdd(queue, 1u);
-        sc_one_unit(u, n_cell, n_run, n_dir4, ud, ud2, ur, n, cell_lo, run_lo, dir_lo, dir_mid, layout, par, sh,
-                    arena, wmax, fill, lmax_s, wid, lane, xyzs, dE, e_stride, nrm, Lt, grad, order);
-        if (SC_DYN) {
-            if (threadIdx.x == 0) {
-                qnext[qb] = tk;
-                if ((int64_t)tk == n_tickets - 1) atomicExch(queue, 0u);  // (the launch's last draw)
-            }
-            __syncthreads();
-            u = (int64_t)gridDim.x + qnext[qb];
-            qb ^= 1;
-        } else {
-            u += gridDim.x;
-        }
-    }
+    for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x)
+        sc_one_unit(u, n_cell, n_dir4, ud, ud2, n, cell_lo, dir_lo, dir_mid, layout, par, sh, arena, fill, lmax_s, wid,
+                    lane, xyzs, dE, e_stride, nrm, Lt, grad, order);
 }
 
 static int scatter_grid(int64_t n_cap) {
@@ -2213,9 +1737,8 @@ static LevelTable make_table(const uint32_t* levels) {
     return t;
 }
 
-#ifndef NCN_FWD_MAX_BLOCKS
-#define NCN_FWD_MAX_BLOCKS 4096
-#endif
+
+constexpr int64_t NCN_FWD_MAX_BLOCKS = 4096;
 static int fwd_grid(int64_t n) {
     const int64_t groups = (n + 15) / 16;
     const int64_t g = std::min<int64_t>(std::max<int64_t>((groups + 3) / 4, 1), NCN_FWD_MAX_BLOCKS);

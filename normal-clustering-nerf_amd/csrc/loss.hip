@@ -275,34 +275,17 @@ __device__ __forceinline__ bool valid_normal(float a, float b, float c) {
 }
 
 // argmax_k <x, C_k> with ((x0 c0 + x1 c1) + x2 c2) in f32, no FMA (contract(off) above); ties ->
-// lowest k.  Two clusters per packed-f32 instruction (v_pk_mul_f32 / v_pk_add_f32: the same IEEE
-// products and sums per half), then the compares in k order.
-#ifndef KM_PACKED_DOT
-#define KM_PACKED_DOT 0  // packed: 87 vs 82 us for the whole kernel (the pair building costs more than it saves)
-#endif
+// lowest k.  (Tried: two clusters per packed-f32 instruction, v_pk_mul_f32 / v_pk_add_f32 with the
+// same IEEE products and sums per half — 87 vs 82 us for the whole kernel: building the register
+// pairs from the LDS centroids costs more than the halved multiplies save.)
 template <int K>
 __device__ __forceinline__ int nearest(const float (*C)[3], float x, float y, float z) {
-    if constexpr (!KM_PACKED_DOT) {  // (A/B switch) one cluster at a time
-        int best = 0;
-        float bv = x * C[0][0] + y * C[0][1] + z * C[0][2];
-#pragma unroll
-        for (int k = 1; k < K; k++) {
-            const float v = x * C[k][0] + y * C[k][1] + z * C[k][2];
-            if (v > bv) { bv = v; best = k; }
-        }
-        return best;
-    }
-    static_assert(K % 2 == 0, "clusters in pairs");
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    const f2 X = {x, x}, Y = {y, y}, Z = {z, z};
     int best = 0;
-    float bv = -INFINITY;
+    float bv = x * C[0][0] + y * C[0][1] + z * C[0][2];
 #pragma unroll
-    for (int k = 0; k < K; k += 2) {
-        const f2 c0 = {C[k][0], C[k + 1][0]}, c1 = {C[k][1], C[k + 1][1]}, c2 = {C[k][2], C[k + 1][2]};
-        const f2 v = (X * c0 + Y * c1) + Z * c2;
-        if (k == 0 || v.x > bv) { bv = v.x; best = k; }
-        if (v.y > bv) { bv = v.y; best = k + 1; }
+    for (int k = 1; k < K; k++) {
+        const float v = x * C[k][0] + y * C[k][1] + z * C[k][2];
+        if (v > bv) { bv = v; best = k; }
     }
     return best;
 }
@@ -379,17 +362,27 @@ __device__ __forceinline__ void km_grid_sync(unsigned* sync, unsigned phase) {
 }
 // Every workgroup calls this once, last: the final departure resets the barrier words and advances
 // the launch sequence of the Lloyd tags (every launch, so a launch that did not cluster never
-// leaves the next one with the tags of an older launch's partials).
-__device__ __forceinline__ void km_grid_exit(unsigned* sync) {
+// leaves the next one with the tags of an older launch's partials).  Returns (to every thread of
+// the LAST departing workgroup only) whether the error word is set: every workgroup's output
+// stores are drained (vmcnt(0)) before its departure, so that workgroup can still overwrite the
+// whole launch's outputs — the drop decision is then uniform even when a workgroup timed out after
+// another one had read the word.
+__device__ __forceinline__ bool km_grid_exit(unsigned* sync) {
+    __shared__ int late_drop;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned d = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        late_drop = 0;
+        const unsigned d = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (d == KM_BLOCKS - 1) {  // everyone has passed every barrier: nobody polls any more
+            late_drop = __hip_atomic_load(&sync[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
             __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(&sync[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // launch sequence (tags)
         }
     }
+    __syncthreads();
+    return late_drop != 0;
 }
 
 // This workgroup's contiguous chunk of the compacted points.
@@ -1061,7 +1054,17 @@ __global__ __launch_bounds__(KM_THREADS) void cluster_kernel(
         }
     }
     CL_STAMP(60);
-    km_grid_exit(ws.sync);  // every launch (clustered or not) advances the tag sequence
+    // every launch (clustered or not) advances the tag sequence; the last workgroup out re-reads the
+    // error word and, when it is set, drops the cluster terms of the WHOLE launch (a workgroup that
+    // read the word before a late timeout set it has applied its gradient rows: they are zeroed here)
+    if (km_grid_exit(ws.sync)) {
+        for (int64_t i = tid; i < 3 * T3; i += KM_THREADS) dn[i] = 0.f;
+        if (tid == 0) {
+            out_losses[0] = out_losses[1] = out_losses[2] = 0.f;
+            out_losses[4] = out_losses[5] = out_losses[6] = 0.f;
+            if (photo) out_losses[10] = photo[0] + photo[1];
+        }
+    }
 }
 
 template <int K>
@@ -1225,6 +1228,28 @@ int ncn_diag_cl_times(unsigned long long* host) {
 }
 #endif
 
+// Co-residency of the clustering kernel's KM_BLOCKS workgroups (they meet at grid barriers and
+// poll each other's partials, so all of them must be resident at once): per-CU occupancy of the
+// kernel (registers, LDS, waves) x the CUs left free by `busy_cus` CUs that concurrent work can
+// hold entirely (the split step's rgb pass: one workgroup per CU, its LDS takes the CU).
+int ncn_cluster_coresidency(int K, int busy_cus, int* capacity) {
+    NCN_REQUIRE(K == 10 || K == 20, hipErrorInvalidValue, "ncn_cluster_coresidency: K must be 10 or 20 (got %d)", K);
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = K == 20 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cluster_kernel<20>, KM_THREADS, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cluster_kernel<10>, KM_THREADS, 0);
+    NCN_REQUIRE(e == hipSuccess, e, "ncn_cluster_coresidency: device query failed (%s)", hipGetErrorString(e));
+    const int cap = std::max(0, cus - std::max(0, busy_cus)) * per_cu;
+    if (capacity) *capacity = cap;
+    NCN_REQUIRE(cap >= KM_BLOCKS, hipErrorCooperativeLaunchTooLarge,
+                "ncn_cluster_coresidency: the clustering's %d workgroups cannot all be resident: %d CUs - %d busy "
+                "= %d free x %d workgroups per CU = %d", KM_BLOCKS, cus, busy_cus, std::max(0, cus - busy_cus), per_cu,
+                cap);
+    return 0;
+}
+
 int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, const uint32_t* kmeans_plan, float t_similar,
                      float w_ort, float w_dot, float w_l1, const float* w_dev, const int64_t* step_dev,
                      float sched_start, float sched_grow, const float* photo_loss, float* out_losses,
@@ -1232,6 +1257,12 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, cons
                      void* stream) {
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
                 "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
+    // refuse (rather than spin into the barrier timeout) on a device that cannot hold the workgroups
+    // at all; checked once per process (the answer depends only on the device and the kernel)
+    static int coresident = -1;
+    if (coresident < 0 && (K == 10 || K == 20)) coresident = ncn_cluster_coresidency(K, 0, nullptr) == 0 ? 1 : 0;
+    NCN_REQUIRE(coresident != 0, hipErrorCooperativeLaunchTooLarge,
+                "ncn_cluster_loss: the device cannot hold the clustering's %d co-resident workgroups", KM_BLOCKS);
     NCN_REQUIRE(niter >= 0 && niter <= 30, hipErrorInvalidValue, "ncn_cluster_loss: niter must be in [0, 30]");
     NCN_REQUIRE(kmeans_plan != nullptr, hipErrorInvalidValue, "ncn_cluster_loss: kmeans_plan required (ncn_kmeans_plan_fill)");
     hipStream_t s = (hipStream_t)stream;

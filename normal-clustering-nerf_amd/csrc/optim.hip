@@ -190,17 +190,9 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_prep_kernel(const float* __
         }
     }
 }
-// Waves per SIMD adam_apply is compiled for (0: the compiler's choice, 83 VGPRs = 5 waves/SIMD).
-// Measured (tools/adam_probe.py, prep + apply over 11.45 M parameters): default 74.2 / 72.9 us,
-// 6 waves 72.7 / 73.1, 8 waves 75.0 / 75.7 — HBM-bound, so the default stays.
-#ifndef NCN_ADAM_WPE
-#define NCN_ADAM_WPE 0
-#endif
-#if NCN_ADAM_WPE > 0
-#define NCN_ADAM_ATTR __attribute__((amdgpu_waves_per_eu(NCN_ADAM_WPE)))
-#else
-#define NCN_ADAM_ATTR
-#endif
+// (adam_apply takes 83 VGPRs: 5 waves/SIMD.  Measured with forced 6 / 8 waves per SIMD
+// (tools/adam_probe.py, prep + apply over 11.45 M parameters): 72.7-73.1 / 75.0-75.7 us against
+// 72.9-74.2 — HBM-bound.)
 // Packed-fragment refresh folded into the Adam pass (PK: 0 none, 1 fp16, 2 bf16): parameter e in
 // [poff, n) is master weight e - poff, written rounded to the operand type at its (up to two)
 // packed positions pinv[2 (e - poff) + {0, 1}].
@@ -221,7 +213,7 @@ __device__ __forceinline__ void adam_pack1(int64_t e, float x, const int32_t* __
     }
 }
 template <bool ZERO, int PK>
-__global__ __launch_bounds__(256) NCN_ADAM_ATTR void adam_apply_kernel(float* __restrict__ p, float* __restrict__ g,
+__global__ __launch_bounds__(256) void adam_apply_kernel(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                          int64_t n0, float b1, float b2, float eps, float wd0,
                                                          float wd1, const float* __restrict__ sc,

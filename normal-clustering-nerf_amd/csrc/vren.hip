@@ -567,8 +567,7 @@ __global__ __launch_bounds__(256) void march_train_place_kernel(
     const float* __restrict__ rays_d, int64_t R, int max_samples, const int32_t* __restrict__ counts,
     const int32_t* __restrict__ wg_sum, const float* __restrict__ slab_xyz, const float* __restrict__ slab_t,
     const float* __restrict__ slab_dt, int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
-    float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts, int32_t* __restrict__ counter,
-    int32_t* __restrict__ sample_ray) {
+    float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts, int32_t* __restrict__ counter) {
     __shared__ int red[4], redl[4], redt[4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.x;
@@ -665,10 +664,6 @@ __global__ __launch_bounds__(256) void march_train_place_kernel(
     for (int k = PF * 64 + lane; k < n; k += 64) {
         ts[start + k] = st[k];
         deltas[start + k] = sd[k];
-    }
-    if (sample_ray) {  // per-sample ray codes of the sample-major compositor (composite_fw_sm_kernel)
-        const int code = n > PLACE_LONG ? -(int)(r + 1) : (int)(r + 1);
-        for (int k = lane; k < n; k += 64) sample_ray[start + k] = code;
     }
 }
 
@@ -1128,387 +1123,6 @@ __global__ __launch_bounds__(64 * CF_WPB) void composite_fw_kernel(
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Sample-major forward compositor (the training step's; volumerendering.cu:97-137 per ray).
-// The ray-major kernel above cannot issue a sample load before its wave has read the ray's rays_a
-// row: two dependent memory rounds per launch, the second behind a latency-bound scalar load.  Here
-// a wave owns a fixed range of 256 consecutive samples, 4 consecutive ones per lane (16-B loads),
-// and learns the segmentation from the per-sample ray codes the training marcher writes beside the
-// samples (march_train_place: sample_ray[k] = ray + 1, or -(ray + 1) for rays of more than CF_LONG
-// samples; 0 past the count), so every load of the range issues in the first round, addressed from
-// the block index alone.
-//   * a wave composites the segments whose FIRST sample lies in its range; the segment running in
-//     from the previous range is the previous wave's, which follows its own last segment into the
-//     next rows (SM_LA rows of 64 loaded with the range, more one row at a time: a short ray has at
-//     most CF_LONG samples);
-//   * per lane, serially over its 4 samples: heads (code differs from the previous sample's), the
-//     lane-local transmittance chain restarted at each head, stops, w = a T and the local sums of
-//     (w, w t, w raw, counted); across lanes ONE segmented product scan of the lanes' chain products
-//     gives the transmittance entering each lane, one ballot the stops of the preceding lanes of the
-//     segment, and unsegmented prefix sums of the lanes' last-part sums (differences at the
-//     segment's last lane) the segment totals;
-//   * rays of more than CF_LONG samples are the composite_fw_coop workgroups' (rays_a rows, long rays
-//     first), rays without samples get their outputs from a pass over rays_a.
-// Float order: T = (transmittance entering the lane) x (the lane's local chain); segment sums are
-// differences of wave prefix sums (absolute error ~ulp of the wave's total) — within the
-// compositor's tolerance.  VALU work per sample is a few ops: the cross-lane scans run once per 4.
-#ifndef SM_LA
-#define SM_LA 1
-#endif
-static_assert(SM_LA >= 1, "the look-ahead row's first code ends or continues the range's last segment");
-constexpr int SM_WPB = 4;     // waves per workgroup
-constexpr int SM_SPW = 256;   // samples a wave owns: 4 per lane
-
-// Segmented inclusive product scan over the 64 lanes: lanes with f set start a new segment.
-__device__ __forceinline__ float seg_incl_prod(float v, int f) {
-#define NCN_SEG_STEP(CTRL, RM)                                                                   \
-    {                                                                                            \
-        const float vs = __int_as_float(                                                         \
-            __builtin_amdgcn_update_dpp(__float_as_int(1.0f), __float_as_int(v), CTRL, RM, 0xF, false)); \
-        const int fs = __builtin_amdgcn_update_dpp(0, f, CTRL, RM, 0xF, false);                 \
-        v = f ? v : vs * v;                                                                      \
-        f |= fs;                                                                                 \
-    }
-    NCN_SEG_STEP(0x111, 0xF)
-    NCN_SEG_STEP(0x112, 0xF)
-    NCN_SEG_STEP(0x114, 0xF)
-    NCN_SEG_STEP(0x118, 0xF)
-    NCN_SEG_STEP(0x142, 0xA)
-    NCN_SEG_STEP(0x143, 0xC)
-#undef NCN_SEG_STEP
-    return v;
-}
-__device__ __forceinline__ int wave_shr1_i(int v, int first) {
-    return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int wave_shl1_i(int v, int last) {  // value of lane l + 1 (`last` for lane 63)
-    return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int wave_incl_sum_i_dpp(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
-    return v;
-}
-__device__ __forceinline__ float bperm_f(int src_lane, float v) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
-}
-
-template <int C>
-struct SmCarry {  // the owned segment running past the range (wave-uniform)
-    bool valid;
-    bool stopped;
-    int code, cnt;
-    float T;
-    float acc[2 + C];
-};
-template <int C>
-struct SmOut {
-    int64_t* total_samples;
-    float *opacity, *depth, *rend, *rgb_bg;
-    float bg;
-    __device__ __forceinline__ void put(int ray, const float (&acc)[2 + C], int cnt) const {
-#ifdef SM_DIAG_NOSTORE
-        if (bg != -12345.f) return;
-#endif
-        opacity[ray] = acc[0];
-        depth[ray] = acc[1];
-#pragma unroll
-        for (int i = 0; i < C; i++) rend[(int64_t)ray * C + i] = acc[2 + i];
-        if (rgb_bg) {  // render()'s background, rendering.py:232-240
-#pragma unroll
-            for (int i = 0; i < C; i++) rgb_bg[(int64_t)ray * C + i] = acc[2 + i] + bg * (1 - acc[0]);
-        }
-        total_samples[ray] = cnt;
-    }
-};
-
-// One continuation row (lane l: sample k0 + l) of the carried segment: it covers the lanes before
-// the first other code.  Plain product scan from the carried T, one ballot for the stop.
-template <int C>
-__device__ __forceinline__ void sm_tail_row(float sg, float dl, float tt, const float (&rr)[C], int code, int64_t k0,
-                                            float T_thr, int lane, SmCarry<C>& cr, float* __restrict__ ws,
-                                            const SmOut<C>& out) {
-    const uint64_t other = __ballot(code != cr.code);
-    const int fh = other ? __builtin_ctzll(other) : 64;
-    const bool act = lane < fh;
-    const float a = act ? 1.0f - __expf(-sg * dl) : 0.f;
-    const float P = wave_incl_prod_dpp_fused(1.0f - a);
-    const float Ta = cr.T * P;
-    const float Tb = cr.T * wave_shr1_dpp(P, 1.0f);
-    const uint64_t sm = __ballot(act && Ta <= T_thr);
-    const int fs = sm ? __builtin_ctzll(sm) : 64;  // the stopping sample (composited, not counted: q6)
-    const bool comp = act && !cr.stopped && lane <= fs;
-    const float w = comp ? a * Tb : 0.f;
-    if (act) ws[k0 + lane] = w;
-    float v[2 + C];
-    v[0] = w;
-    v[1] = comp ? w * tt : 0.f;
-#pragma unroll
-    for (int i = 0; i < C; i++) v[2 + i] = comp ? w * rr[i] : 0.f;
-    wave_sum_multi<2 + C>(v);
-#pragma unroll
-    for (int c = 0; c < 2 + C; c++) cr.acc[c] += v[c];
-    if (!cr.stopped) cr.cnt += min(fs, fh);
-    cr.stopped = cr.stopped || sm != 0;
-    if (fh < 64) {
-        if (lane == 0) out.put(cr.code - 1, cr.acc, cr.cnt);
-        cr.valid = false;
-    } else {
-        cr.T = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta), 63));
-    }
-}
-
-template <int C>
-__global__ __launch_bounds__(64 * SM_WPB) void composite_fw_sm_kernel(
-    const float* __restrict__ sigmas, const float* __restrict__ raws, const float* __restrict__ deltas,
-    const float* __restrict__ ts, const int32_t* __restrict__ sample_ray, const int64_t* __restrict__ rays_a,
-    int64_t R, int64_t S_host, const int32_t* __restrict__ S_dev, float T_thr, int64_t* __restrict__ total_samples,
-    float* __restrict__ opacity, float* __restrict__ depth, float* __restrict__ rend, float* __restrict__ ws, float bg,
-    float* __restrict__ rgb_bg, int n_coop, int n_zero) {
-    int blk = (int)blockIdx.x;
-#ifdef SM_DIAG_NOCOOP
-    if (blk < n_coop) return;
-#endif
-    if (blk < n_coop) {  // rays longer than CF_LONG: whole workgroups (rows long-first)
-        for (int64_t row = blk; row < R; row += n_coop) {
-            const int N = (int)rays_a[3 * row + 2];
-            if (N <= CF_LONG) break;
-            composite_fw_coop<C>(sigmas, raws, deltas, ts, rays_a, row, T_thr, total_samples, opacity, depth, rend, ws,
-                                 bg, rgb_bg);
-        }
-        return;
-    }
-    blk -= n_coop;
-    const SmOut<C> out{total_samples, opacity, depth, rend, rgb_bg, bg};
-    constexpr int NC = 2 + C;  // float channels: w, w t, w raw
-    if (blk < n_zero) {  // rays without samples (no code marks them)
-        const int64_t row = (int64_t)blk * (64 * SM_WPB) + threadIdx.x;
-        if (row < R && rays_a[3 * row + 2] == 0) {
-            float z[NC];
-#pragma unroll
-            for (int c = 0; c < NC; c++) z[c] = 0.f;
-            out.put((int)rays_a[3 * row], z, 0);
-        }
-        return;
-    }
-    blk -= n_zero;
-    const int lane = threadIdx.x & 63;
-    const int64_t S = S_dev ? (int64_t)*S_dev : S_host;
-    const int64_t nw = (int64_t)(gridDim.x - n_coop - n_zero) * SM_WPB;
-    for (int64_t wv = (int64_t)blk * SM_WPB + (threadIdx.x >> 6); wv * SM_SPW < S; wv += nw) {
-        const int64_t base = __builtin_amdgcn_readfirstlane((int)(wv * SM_SPW));
-        const uint32_t rem = (uint32_t)(S - base);  // samples [base, S) behind the descriptors
-        const auto r_s = buf_rsrc(sigmas + base, rem * 4u), r_d = buf_rsrc(deltas + base, rem * 4u);
-        const auto r_t = buf_rsrc(ts + base, rem * 4u), r_r = buf_rsrc(raws + base * C, rem * 4u * C);
-        const auto r_c = buf_rsrc(sample_ray + base, rem * 4u);
-        // ---- round 1: the lane's 4 samples (16-B loads) and the look-ahead rows (row layout) ----
-        const uint32_t q = (uint32_t)lane * 16u;
-        const auto cq = __builtin_amdgcn_raw_buffer_load_b128(r_c, q, 0, 0);
-        const auto sq = __builtin_amdgcn_raw_buffer_load_b128(r_s, q, 0, 0);
-        const auto dq = __builtin_amdgcn_raw_buffer_load_b128(r_d, q, 0, 0);
-        const auto tq = __builtin_amdgcn_raw_buffer_load_b128(r_t, q, 0, 0);
-        std::remove_const_t<decltype(cq)> rq[C];
-#pragma unroll
-        for (int i = 0; i < C; i++) rq[i] = __builtin_amdgcn_raw_buffer_load_b128(r_r, q * C + 16u * i, 0, 0);
-        int lc[SM_LA];
-        float ls[SM_LA], ld[SM_LA], lt[SM_LA], lr[SM_LA][C];
-#pragma unroll
-        for (int r = 0; r < SM_LA; r++) {
-            const uint32_t k = (uint32_t)(SM_SPW + r * 64 + lane);
-            lc[r] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_c, k * 4u, 0, 0);
-            ls[r] = buf_load(r_s, k * 4u);
-            ld[r] = buf_load(r_d, k * 4u);
-            lt[r] = buf_load(r_t, k * 4u);
-#pragma unroll
-            for (int i = 0; i < C; i++) lr[r][i] = buf_load(r_r, k * (4u * C) + 4u * i);
-        }
-        const int prev = base > 0 ? sample_ray[base - 1] : 0;
-#ifdef SM_DIAG_LOADONLY
-        {
-            float z = __uint_as_float(sq[0] + dq[1] + tq[2] + (uint32_t)cq[3]) + ls[0] + ld[0] + lt[0] + lr[0][0] + (float)lc[0] + (float)prev;
-#pragma unroll
-            for (int i = 0; i < C; i++) z += __uint_as_float(rq[i][0] ^ rq[i][3]);
-            z = wave_sum_dpp(z);
-            if (lane == 0 && z == 1.2345f) ws[base] = z;
-            continue;
-        }
-#endif
-        // ---- the lane's samples ----
-        int c[4];
-        float a[4], tt[4], rr[4][C];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            c[j] = (uint32_t)(4 * lane + j) < rem ? (int)cq[j] : 0;  // (0 past the count)
-            tt[j] = __uint_as_float(tq[j]);
-#pragma unroll
-            for (int i = 0; i < C; i++) rr[j][i] = __uint_as_float(rq[(j * C + i) >> 2][(j * C + i) & 3]);
-        }
-        const int pc = wave_shr1_i(c[3], prev);  // the code of the sample in front of the lane
-        bool h[4];
-        h[0] = c[0] != pc;
-#pragma unroll
-        for (int j = 1; j < 4; j++) h[j] = c[j] != c[j - 1];
-        const bool hasH = h[0] || h[1] || h[2] || h[3];
-        const uint64_t hm = __ballot(hasH);
-        const uint64_t hbelow = hm & ((1ull << lane) - 1ull);
-        const int hstar = hbelow ? 63 - __builtin_clzll(hbelow) : -1;  // last earlier lane with a head
-        // owned: a head at or before the sample inside the range; active: owned, short ray, < S
-        bool act[4], pre[4];
-        {
-            bool seen = hstar >= 0, p = true;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                seen = seen || h[j];
-                p = p && !h[j];
-                pre[j] = p;  // before the lane's first head: the segment entering the lane
-                act[j] = seen && c[j] > 0;
-            }
-        }
-        // lane-local transmittance chains (restarted at heads)
-        float TbL[4], TaL[4], T = 1.0f;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            a[j] = act[j] ? 1.0f - __expf(-__uint_as_float(sq[j]) * __uint_as_float(dq[j])) : 0.f;
-            if (h[j]) T = 1.0f;
-            TbL[j] = T;
-            T *= 1.0f - a[j];  // T *= 1 - a (volumerendering.cu:132)
-            TaL[j] = T;
-        }
-        // transmittance entering the lane: product of the preceding lanes' chains back to the head
-        const float E = wave_shr1_dpp(seg_incl_prod(T, hasH ? 1 : 0), 1.0f);
-        // stops: per sample, and whether the segment entering the lane stopped in an earlier lane
-        bool stop[4];
-        bool ls_any = false;  // a stop in the lane's last part (from its last head)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            stop[j] = act[j] && (pre[j] ? E * TaL[j] : TaL[j]) <= T_thr;
-            if (h[j]) ls_any = false;
-            ls_any = ls_any || stop[j];
-        }
-        const uint64_t lsm = __ballot(ls_any);
-        const bool stopped_in = hstar >= 0 && ((lsm & ((1ull << lane) - 1ull)) >> hstar) != 0ull;
-        // weights, ws, and the lane's sums: `first` = the entering segment's part, `cur` = the
-        // segment opened by the latest head (inner segments are written as they close)
-        const int nxt_h = wave_shl1_i(h[0] ? 1 : 0, 1);  // the next lane's first sample is a head
-        const int la0 = __builtin_amdgcn_readfirstlane(lc[0]);
-        const bool end3 = lane == 63 ? la0 != c[3] : nxt_h != 0;  // the lane's last sample ends a segment
-        float first[NC], cur[NC];
-        int first_n = 0, cur_n = 0;
-#pragma unroll
-        for (int i = 0; i < NC; i++) first[i] = cur[i] = 0.f;
-        bool sb = stopped_in;  // the current segment has stopped before this sample
-        bool opened = false;   // a head seen in this lane
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (h[j]) {
-                // an inner segment (head and end in this lane) ends at j - 1
-                if (j > 0 && opened && act[j > 0 ? j - 1 : 0]) out.put(c[j > 0 ? j - 1 : 0] - 1, cur, cur_n);
-                opened = true;
-                sb = false;
-#pragma unroll
-                for (int i = 0; i < NC; i++) cur[i] = 0.f;
-                cur_n = 0;
-            }
-            const float Tb = pre[j] ? E * TbL[j] : TbL[j];
-            const bool comp = act[j] && !sb;
-            const float w = comp ? a[j] * Tb : 0.f;
-#ifdef SM_DIAG_NOSTORE
-            if (act[j] && T_thr < 0.f) ws[base + 4 * lane + j] = w;
-#else
-            if (act[j]) ws[base + 4 * lane + j] = w;
-#endif
-            float v[NC];
-            v[0] = w;
-            v[1] = comp ? w * tt[j] : 0.f;
-#pragma unroll
-            for (int i = 0; i < C; i++) v[2 + i] = comp ? w * rr[j][i] : 0.f;
-            const int n1 = (comp && !stop[j]) ? 1 : 0;
-            if (pre[j]) {
-#pragma unroll
-                for (int i = 0; i < NC; i++) first[i] += v[i];
-                first_n += n1;
-            } else {
-#pragma unroll
-                for (int i = 0; i < NC; i++) cur[i] += v[i];
-                cur_n += n1;
-            }
-            sb = sb || stop[j];
-        }
-        // the lane's last part (from its last head, or the whole lane): summed across lanes
-        float lp[NC];
-#pragma unroll
-        for (int i = 0; i < NC; i++) lp[i] = hasH ? cur[i] : first[i];
-        const int lp_n = hasH ? cur_n : first_n;
-        float Q[NC];
-#pragma unroll
-        for (int i = 0; i < NC; i++) Q[i] = wave_incl_sum_dpp(lp[i]);
-        const int Qn = wave_incl_sum_i_dpp(lp_n);
-        // the entering segment's sums over the lanes [hstar, lane): exclusive prefix differences
-        const int src = hstar < 0 ? 0 : hstar;
-        float in[NC];
-#pragma unroll
-        for (int i = 0; i < NC; i++) {
-            const float qx = wave_shr1_dpp(Q[i], 0.f);
-            in[i] = hstar < 0 ? 0.f : qx - bperm_f(src, qx) + first[i];
-        }
-        const int qnx = wave_shr1_i(Qn, 0);
-        const int in_n = hstar < 0 ? 0 : qnx - __builtin_amdgcn_ds_bpermute(src << 2, qnx) + first_n;
-        // the entering segment ends in this lane: at the sample before the first head, or at the
-        // lane's last sample
-        if (act[0] && pre[0]) {
-            if (hasH) {
-                if (!h[0]) out.put(c[0] - 1, in, in_n);
-            } else if (end3) {
-                out.put(c[0] - 1, in, in_n);
-            }
-        }
-        // the lane's last opened segment ends at its last sample
-        if (hasH && end3 && act[3]) out.put(c[3] - 1, cur, cur_n);
-        // ---- the owned segment running past the range: continuation rows ----
-        SmCarry<C> cr;
-        {
-            float open[NC];
-#pragma unroll
-            for (int i = 0; i < NC; i++) open[i] = hasH ? cur[i] : in[i];
-            const int open_n = hasH ? cur_n : in_n;
-            const bool open_stopped = hasH ? ls_any : (stopped_in || ls_any);
-            const float Ta3 = pre[3] ? E * TaL[3] : TaL[3];
-            cr.valid = __builtin_amdgcn_readlane((int)(act[3] && !end3), 63) != 0;
-            cr.code = __builtin_amdgcn_readlane(c[3], 63);
-            cr.T = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Ta3), 63));
-            cr.stopped = __builtin_amdgcn_readlane((int)open_stopped, 63) != 0;
-            cr.cnt = __builtin_amdgcn_readlane(open_n, 63);
-#pragma unroll
-            for (int i = 0; i < NC; i++) cr.acc[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(open[i]), 63));
-        }
-#ifdef SM_DIAG_NOCONT
-        cr.valid = false;
-#endif
-        int r = 0;
-#pragma unroll
-        for (; r < SM_LA; r++) {
-            if (!cr.valid) break;
-            if (base + SM_SPW + r * 64 >= S) break;
-            sm_tail_row<C>(ls[r], ld[r], lt[r], lr[r], lc[r], base + SM_SPW + r * 64, T_thr, lane, cr, ws, out);
-        }
-        // (rare: a ray of up to CF_LONG samples starting near the end of the range) one row at a time
-        for (; cr.valid && base + SM_SPW + r * 64 < S; r++) {
-            const uint32_t k = (uint32_t)(SM_SPW + r * 64 + lane);
-            const int c1 = (int)__builtin_amdgcn_raw_buffer_load_b32(r_c, k * 4u, 0, 0);
-            float r1[C];
-#pragma unroll
-            for (int i = 0; i < C; i++) r1[i] = buf_load(r_r, k * (4u * C) + 4u * i);
-            sm_tail_row<C>(buf_load(r_s, k * 4u), buf_load(r_d, k * 4u), buf_load(r_t, k * 4u), r1, c1,
-                           base + SM_SPW + r * 64, T_thr, lane, cr, ws, out);
-        }
-        if (cr.valid && lane == 0) out.put(cr.code - 1, cr.acc, cr.cnt);  // (the segment ends at S)
-    }
-}
-
 // Backward, one block of a ray's rows (volumerendering.cu:297-364).  T is the post-update
 // transmittance (quirk q10); d/r are inclusive prefix sums of w*t and w*raw; (sum - pre[s]) is the
 // suffix of dL_dws*ws over the WHOLE marched segment (:331-335).  Evaluation order of dL_dsigmas
@@ -1806,19 +1420,11 @@ __device__ __forceinline__ void composite_bw_coop(
     }
 }
 
-// Waves per SIMD composite_bw_kernel_nodws is compiled for (0: the compiler's choice, 80 VGPRs at
-// C = 3 = 6 waves/SIMD).  Measured (tools/composite_bw_probe.py, 8192 marched rays): default 9.6 us,
-// 7 waves (2 VGPRs spilled) 9.9-10.0, 8 waves (6 spilled) 10.3-10.5 — the default stays.
-#ifndef NCN_CBW_WPE
-#define NCN_CBW_WPE 0
-#endif
-#if NCN_CBW_WPE > 0
-#define NCN_CBW_ATTR __attribute__((amdgpu_waves_per_eu(NCN_CBW_WPE)))
-#else
-#define NCN_CBW_ATTR
-#endif
+// (composite_bw_kernel_nodws takes 80 VGPRs at C = 3: 6 waves/SIMD.  Measured with forced 7 / 8
+// waves per SIMD (tools/composite_bw_probe.py, 8192 marched rays): 9.9-10.0 / 10.3-10.5 us against
+// 9.6 — spills.)
 template <int C>
-__global__ __launch_bounds__(64 * CF_WPB) NCN_CBW_ATTR void composite_bw_kernel_nodws(
+__global__ __launch_bounds__(64 * CF_WPB) void composite_bw_kernel_nodws(
     const float* __restrict__ dL_dopacity, const float* __restrict__ dL_ddepth, const float* __restrict__ dL_drend,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ raws,
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
@@ -2195,13 +1801,10 @@ int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_ra
                           const int64_t* rng_counter, const uint8_t* bitfield, int cascades, float scale,
                           int grid_size, int max_samples, float* slab_xyz, float* slab_t, float* slab_dt, void* work,
                           int64_t* rays_a, float* xyzs, float* dirs, float* deltas, float* ts, int32_t* counter,
-                          int32_t* sample_ray, void* stream) {
+                          void* stream) {
     if (n_rays <= 0) return 0;
     NCN_REQUIRE(cascades >= 1 && grid_size >= 1 && grid_size <= 1024 && max_samples >= 1 && work != nullptr,
                 hipErrorInvalidValue, "ncn_march_train_fused: bad cascades/grid_size/max_samples/work");
-    NCN_REQUIRE(sample_ray == nullptr || max_samples <= CF_COOP_MAX, hipErrorInvalidValue,
-                "ncn_march_train_fused: sample codes need max_samples <= %d (the compositor's longest ray)",
-                CF_COOP_MAX);
     const int64_t nwg = cdiv(n_rays, 4);
     NCN_REQUIRE(nwg <= PLACE_MAX_WG && n_rays * (int64_t)max_samples < (1ll << 31) && max_samples < (1 << 24),
                 hipErrorInvalidValue,
@@ -2220,7 +1823,7 @@ int ncn_march_train_fused(const float* rays_o, const float* rays_d, int64_t n_ra
 #undef NCN_WALK2_ARGS
     NCN_LAUNCH_CHECK("ncn_march_train_fused(walk)");
     hipLaunchKernelGGL(march_train_place_kernel, g, b, 0, s, rays_d, n_rays, max_samples, counts, wg_sum, slab_xyz,
-                       slab_t, slab_dt, rays_a, xyzs, dirs, deltas, ts, counter, sample_ray);
+                       slab_t, slab_dt, rays_a, xyzs, dirs, deltas, ts, counter);
     NCN_LAUNCH_CHECK("ncn_march_train_fused(place)");
     return 0;
 }
@@ -2286,27 +1889,6 @@ int ncn_composite_train_fw_bg(const float* sigmas, const float* raws, const floa
                    (hipStream_t)stream, sigmas, raws, deltas, ts, rays_a, n_rays, T_threshold, total_samples, opacity,
                    depth, rend, ws, bg, rgb_bg, n_coop);
     NCN_LAUNCH_CHECK("ncn_composite_train_fw");
-    return 0;
-}
-
-int ncn_composite_train_fw_sm(const float* sigmas, const float* raws, const float* deltas, const float* ts,
-                              const int32_t* sample_ray, const int64_t* rays_a, int64_t n_rays, int64_t n_samples,
-                              const int32_t* n_samples_dev, int64_t grid_samples, int n_rend, float T_threshold,
-                              int64_t* total_samples, float* opacity, float* depth, float* rend, float* ws, float bg,
-                              float* rgb_bg, void* stream) {
-    if (n_rays <= 0) return 0;
-    NCN_REQUIRE((sample_ray != nullptr || (n_samples == 0 && !n_samples_dev)) && n_samples >= 0 &&
-                    n_samples * 4 * std::max(n_rend, 1) < (1ll << 32),
-                hipErrorInvalidValue, "ncn_composite_train_fw_sm: needs sample_ray and n_samples * 4 * n_rend < 2^32");
-    const int n_coop = cf_coop_blocks(n_rays);
-    const int n_zero = (int)cdiv(n_rays, 64 * SM_WPB);
-    const int64_t cover = n_samples_dev ? std::min(std::max<int64_t>(grid_samples, 1), std::max<int64_t>(n_samples, 1))
-                                        : std::max<int64_t>(n_samples, 1);
-    const int n_sm = (int)cdiv(cover, (int64_t)SM_SPW * SM_WPB);
-    NCN_DISPATCH_C(n_rend, composite_fw_sm_kernel, dim3(n_coop + n_zero + n_sm), dim3(64 * SM_WPB), 0,
-                   (hipStream_t)stream, sigmas, raws, deltas, ts, sample_ray, rays_a, n_rays, n_samples, n_samples_dev,
-                   T_threshold, total_samples, opacity, depth, rend, ws, bg, rgb_bg, n_coop, n_zero);
-    NCN_LAUNCH_CHECK("ncn_composite_train_fw_sm");
     return 0;
 }
 

@@ -34,11 +34,10 @@ SIGNATURES = {
     "ncn_march_train_scan": [P, I64, P, P, P],
     "ncn_march_train_fused_work_bytes": [I64],
     "ncn_march_train_fused": [P, P, I64, F32, F32, F32, F32, F32, F32, F32, P, U64, P, P, I32, F32, I32, I32, P, P, P,
-                              P, P, P, P, P, P, P, P, P],
+                              P, P, P, P, P, P, P, P],
     "ncn_march_train_pack": [P, P, I64, I32, P, P, P, P, P, P, P, P],
     "ncn_march_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
     "ncn_composite_train_fw": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, P],
-    "ncn_composite_train_fw_sm": [P, P, P, P, P, P, I64, I64, P, I64, I32, F32, P, P, P, P, P, F32, P, P],
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],
     "ncn_composite_train_fw_bg": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, F32, P, P],
     "ncn_count_samples": [P, I64, P, P, P, P],
@@ -74,6 +73,7 @@ SIGNATURES = {
     "ncn_photo_loss_bwd": [P, P, P, I64, F32, P, P, P, P, P],
     "ncn_cluster_workspace_words": [I32],
     "ncn_cluster_status_offset": [I32],
+    "ncn_cluster_coresidency": [I32, I32, P],
     "ncn_kmeans_plan_words": [I32, I32],
     "ncn_kmeans_plan_fill": [I32, I32, U32, P],
     "ncn_cluster_loss": [P, I64, I32, I32, P, F32, F32, F32, F32, P, P, F32, F32, P, P, P, P, P, P, P],

@@ -112,13 +112,10 @@ class VolumeRendererBg(torch.autograd.Function):
 
     @staticmethod
     @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg, count=None, sm=None):
-        """sm: None, or (per-sample ray codes, device sample counter, grid samples) of the fused
-        training marcher: the sample-major compositor (ncn_composite_train_fw_sm)."""
+    def forward(ctx, sigmas, raws, deltas, ts, rays_a, T_threshold, bg, count=None):
         sigmas = sigmas.contiguous(); raws = raws.contiguous()
-        kw = {} if sm is None else dict(sample_ray=sm[0], n_samples_dev=sm[1], grid_samples=sm[2])
         total_samples, opacity, depth, rend, ws, rgb = vren.composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a,
-                                                                                       T_threshold, bg=bg, **kw)
+                                                                                       T_threshold, bg=bg)
         ctx.save_for_backward(sigmas, raws, deltas, ts, rays_a, opacity, depth, rend, ws)
         ctx.T_threshold, ctx.bg = T_threshold, bg
         ctx.set_materialize_grads(False)

@@ -270,9 +270,17 @@ class NGPMT(nn.Module):
             self._deferred = []
 
     def prepare_weights(self):
-        """Pack the MLP weights now (after the optimizer step) so the next forward reuses them."""
+        """Pack the MLP weights now (after the optimizer step) so the next forward reuses them.
+        The packed fragments are reused by the next forward while `_packed_fresh` is set (FlatAdam's
+        packed step sets it: its Adam pass writes the fragments of the weights it updates).  A caller
+        that changes the parameters any other way (an in-place edit, a copy from another model, a
+        broadcast) must call prepare_weights() afterwards; load_state_dict clears the flag itself."""
         self._pack_weights()
         self._packed_fresh = True
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self._packed_fresh = False  # (the loaded weights: the next forward packs them)
 
     def _take_packed(self):
         if getattr(self, "_packed_fresh", False) and self._packed is not None:

@@ -12,7 +12,6 @@ read of the counter), which is what lets Trainer capture the whole step in one H
 kwargs['premarched'] (a march_train_static() result) skips intersect + march: the pipelined step
 marches the next batch while the current one is rendered.
 """
-import os
 import time
 
 import torch
@@ -190,7 +189,9 @@ def _test_loop_device(model, rays_o, rays_d, hits_t0, alive, exp_step_factor, ma
     model._packed_fresh = True
     packed = model._take_packed()  # (packed before the loop: the weights do not change in it)
     bufs = [alive, torch.empty(R, dtype=torch.int64, device=dev)]
-    ns0 = max(min(R // R, 64), min_samples)
+    # the loop head's N_samples = max(min(N_rays // N_alive, 64), min_samples) (rendering.py:69-70); on
+    # the first iteration N_alive == N_rays, so it is max(1, min_samples); test_loop_next forms the rest
+    ns0 = max(1, min_samples)
     ctrl = torch.tensor([R, ns0, ns0, 0, 0, 0, 0, 0], dtype=torch.int32, device=dev)
     total = torch.zeros(1, dtype=torch.int64, device=dev)
     count = ctrl[4:5]
@@ -276,9 +277,6 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
     fuse_bg = exp_step_factor == 0 and raws.shape[1] == 3  # white background, rgb only
     renderer = VolumeRendererBg if fuse_bg else VolumeRenderer
     extra = (1.0,) if fuse_bg else ()
-    sm = None  # the fused marcher's per-sample ray codes: the sample-major compositor
-    if fuse_bg and pm is not None and pm.get("sample_ray") is not None:
-        sm = (pm["sample_ray"], pm["counter"], rays_a.shape[0] * SM_GRID_SAMPLES_PER_RAY)
     job = CountJob() if fuse_bg and kwargs.get("count_in_loss") else None
     if fuse_bg and (kwargs.get("count_acc") is not None or job is not None):
         # (extension) device-side throughput counters; count_in_loss: the sample count is taken by
@@ -287,8 +285,6 @@ def render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
         rm = rm if isinstance(rm, torch.Tensor) and rm.dtype == torch.int32 and rm.is_cuda else None
         acc = kwargs.get("count_acc")
         extra = (1.0, (rm if acc is not None else None, acc, job))
-    if sm is not None:
-        extra = (extra + (None,))[:2] + (sm,)
     (results["vr_samples"], results["opacity"], results["depth"], rend, results["ws"]) = renderer.apply(
         sigmas, raws.contiguous(), results["deltas"], results["ts"], rays_a, kwargs.get("T_threshold", 1e-4), *extra)
     if job is not None and job.out is not None:
@@ -340,18 +336,6 @@ def _fused_march_ok(model, kw, n_rays):
                         if k not in ("march_noise", "march_rng", "count_acc")))
 
 
-SM_MAX_SAMPLES = 1024  # the sample-major compositor's longest ray (its long-ray workgroups)
-# The training step's compositor: "ray" (ray-major ncn_composite_train_fw_bg, the default) or "sm"
-# (sample-major ncn_composite_train_fw_sm over the fused marcher's per-sample ray codes).  Measured
-# (DESIGN section 5): the sample-major form removes the rays_a -> sample load dependency but its
-# cross-lane segment work and the continuation of range-crossing rays cost more than that saves
-# (9.7 vs 6.6 us HBM-cold, 7.3 vs 4.4 warm on the bench's 8192-ray sets), so it is opt-in.
-SM_COMPOSITE = os.environ.get("NCN_COMPOSITE", "ray") == "sm"
-# samples per ray the sample-major compositor's grid covers in one pass when the count is on the
-# device (graph-captured step; its waves loop over any beyond)
-SM_GRID_SAMPLES_PER_RAY = int(os.environ.get("NCN_SM_SPR", "96"))
-
-
 @torch.no_grad()
 def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=None, rng=None, out=None):
     """ncn_march_train_fused: RayAABBIntersector + near clamp (rendering.py:24-28) + RayMarcher
@@ -385,15 +369,13 @@ def march_train_fused(model, rays_o, rays_d, near_distance, max_samples, noise=N
          F32(h[1]), F32(h[2]), F32(near_distance), ptr(noise), U64(int(seed) % 2 ** 64), ptr(ctr),
          ptr(model.density_bitfield), I32(int(model.cascades)), F32(float(model.scale)), I32(int(model.grid_size)),
          I32(ms), ptr(slab_xyz), ptr(slab_t), ptr(slab_dt), ptr(ws), ptr(out["rays_a"]), ptr(out["xyzs"]),
-         ptr(out["dirs"]), ptr(out["deltas"]), ptr(out["ts"]), ptr(out["counter"]), ptr(out.get("sample_ray")),
-         stream())
+         ptr(out["dirs"]), ptr(out["deltas"]), ptr(out["ts"]), ptr(out["counter"]), stream())
     return out
 
 
-def march_buffers(R, max_samples, device, share_scratch=None, codes=None):
+def march_buffers(R, max_samples, device, share_scratch=None):
     """Output + scratch buffers of march_train_fused for R rays (capacity R*max_samples samples);
-    share_scratch: another march_buffers() whose scratch (slabs, work) is reused (never concurrently);
-    codes: also the per-sample ray codes of the sample-major compositor (default: SM_COMPOSITE)."""
+    share_scratch: another march_buffers() whose scratch (slabs, work) is reused (never concurrently)."""
     from ._lib import I64, lib
     cap = R * int(max_samples)
     f = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=device)
@@ -406,9 +388,6 @@ def march_buffers(R, max_samples, device, share_scratch=None, codes=None):
     out = {"rays_a": torch.empty(R, 3, dtype=torch.int64, device=device), "xyzs": f(cap, 3), "dirs": f(cap, 3),
            "deltas": f(cap), "ts": f(cap), "counter": torch.empty(2, dtype=torch.int32, device=device),
            "_slab": scratch}
-    if (SM_COMPOSITE if codes is None else codes) and int(max_samples) <= SM_MAX_SAMPLES:
-        # per-sample ray codes: the sample-major compositor's input
-        out["sample_ray"] = torch.empty(cap, dtype=torch.int32, device=device)
     return out
 
 

@@ -28,13 +28,15 @@ pass uses at most SPLIT_BLOCKS workgroups so the clustering's 16 co-resident wor
 of their own (an rgb-pass workgroup takes a whole CU's LDS); the sigma pass keeps only the
 sigma_net's fragments and exchange tiles in LDS and runs two workgroups per CU.  Only the fused-loss configuration takes this path (split_eligible); any other
 falls back to the autograd step."""
+import ctypes
+
 import torch
 
 from . import _lib, vren
 from ._lib import F32, I32, I64, call, ptr, stream
 from .losses import N_OUT, _cluster_workspace, _standard_patch_offsets, kmeans_plan
 from .ngp_mt import N_W
-from .rendering import SM_GRID_SAMPLES_PER_RAY, march_train_fused
+from .rendering import march_train_fused
 
 SPLIT_BLOCKS = 240  # MLP-backward workgroups of each split pass: 256 CUs - the clustering's 16
 K_CLUSTERS, K_ITERS = 20, 20  # NeRFMTLoss._fused (losses.py:86-89: faiss.Kmeans(3, 20, niter=20))
@@ -62,9 +64,20 @@ class SplitStep:
     """One training step (forward + split backward) of `trainer`'s model; run() is graph-capturable
     (no host reads).  Buffers that depend only on the batch size are allocated once."""
 
-    def __init__(self, trainer):
+    def __init__(self, trainer, rgb_blocks=SPLIT_BLOCKS):
+        """rgb_blocks: the rgb pass's workgroups (one per CU), which run beside the clustering.  The
+        clustering's workgroups meet at grid barriers, so they must all stay resident on the CUs the
+        rgb pass leaves: checked here (ncn_cluster_coresidency), before the step is captured — a
+        device where they cannot is refused instead of spinning into the barrier timeout.  (At N > 1
+        nothing else shares the step: the all-reduce of step k is stream-ordered before graph k+1,
+        and RCCL's channels run beside the deferred coarse-level scatter, which leaves them 32 CUs,
+        distributed.DP_SCATTER_BLOCKS.)"""
         self.tr = trainer
         self._tri = None
+        self.rgb_blocks = int(rgb_blocks)
+        cap = ctypes.c_int(0)
+        call("ncn_cluster_coresidency", I32(K_CLUSTERS), I32(self.rgb_blocks), ctypes.byref(cap))
+        self.cluster_capacity = cap.value
 
     def _triangles(self, R, dev):
         # the 8x8 patch triangles of losses.py:307-313 (x1/x2/x3 = the standard patch offsets)
@@ -92,10 +105,8 @@ class SplitStep:
         n_dev = pm["counter"][0]
         n = xyzs.shape[0]
         sigmas, rgbs, enc, packed, order = m._field_fwd(xyzs, dirs, n_dev, 0, True)
-        sm = {} if pm.get("sample_ray") is None else dict(
-            sample_ray=pm["sample_ray"], n_samples_dev=pm["counter"], grid_samples=R * SM_GRID_SAMPLES_PER_RAY)
         total_s, opacity, depth, rend, ws, rgb = vren.composite_train_multi_fw(sigmas, rgbs, deltas, ts, rays_a,
-                                                                              T_thr, bg=1.0, **sm)
+                                                                              T_thr, bg=1.0)
         # ---- NeRFMTLoss forward (_NeRFLossFused.forward) ----
         x1, x2, x3 = self._triangles(R, dev)
         T = x1.shape[0]
@@ -117,7 +128,7 @@ class SplitStep:
         w = (L.norm_D_C_ort_dot_w, L.norm_D_C_centr_dot_w, L.norm_D_C_centr_L1_w)
         one = tr._unit(dev)
         lib = _lib.lib()
-        nb = (min(SPLIT_BLOCKS, int(lib.ncn_field_bwd_part_blocks(I64(n), I32(1)))),
+        nb = (min(self.rgb_blocks, int(lib.ncn_field_bwd_part_blocks(I64(n), I32(1)))),
               int(lib.ncn_field_bwd_part_blocks(I64(n), I32(2))))  # (the sigma pass: two workgroups per CU)
         drgb, dop, ddepth = torch.empty_like(rgb), torch.empty_like(opacity), torch.empty_like(depth)
         slab = torch.empty(max(nb) * N_W, dtype=torch.float32, device=dev)

@@ -142,13 +142,9 @@ def count_samples(total_samples, counter=None, acc=None):
     return out
 
 
-def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold, bg=None, sample_ray=None,
-                             n_samples_dev=None, grid_samples=None):
+def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold, bg=None):
     """volumerendering.cu:140-176 -> [total_samples i64 (R), opacity (R), depth (R), rend (R,C), ws (S)]
-    Extension: bg (float) also returns rgb_bg = rend + bg * (1 - opacity) as a sixth output.
-    Extension: sample_ray (the fused training marcher's per-sample ray codes) selects the
-    sample-major compositor (ncn_composite_train_fw_sm); n_samples_dev (int32 device tensor whose
-    first element is the sample count of capacity-sized arrays) and grid_samples go with it."""
+    Extension: bg (float) also returns rgb_bg = rend + bg * (1 - opacity) as a sixth output."""
     for t, n in ((sigmas, "sigmas"), (raws, "raws"), (deltas, "deltas"), (ts, "ts"), (rays_a, "rays_a")):
         check_input(t, n)
     R, S, C = rays_a.shape[0], sigmas.shape[0], raws.shape[1]
@@ -158,17 +154,6 @@ def composite_train_multi_fw(sigmas, raws, deltas, ts, rays_a, T_threshold, bg=N
     depth = torch.empty(R, dtype=torch.float32, device=dev)
     rend = torch.empty(R, C, dtype=torch.float32, device=dev)
     ws = torch.empty(S, dtype=torch.float32, device=dev)
-    if sample_ray is not None:
-        check_input(sample_ray, "sample_ray")
-        if sample_ray.dtype != torch.int32 or sample_ray.shape[0] < S:
-            raise RuntimeError("sample_ray must be an int32 tensor of at least n_samples elements")
-        rgb_bg = torch.empty(R, C, dtype=torch.float32, device=dev) if bg is not None else None
-        if n_samples_dev is not None:
-            check_input(n_samples_dev, "n_samples_dev")
-        call("ncn_composite_train_fw_sm", ptr(sigmas), ptr(raws), ptr(deltas), ptr(ts), ptr(sample_ray), ptr(rays_a),
-             I64(R), I64(S), ptr(n_samples_dev), I64(int(grid_samples or S)), I32(C), F32(float(T_threshold)),
-             ptr(total), ptr(opacity), ptr(depth), ptr(rend), ptr(ws), F32(float(bg or 0.0)), ptr(rgb_bg), stream())
-        return [total, opacity, depth, rend, ws] + ([rgb_bg] if bg is not None else [])
     if bg is None:
         call("ncn_composite_train_fw", ptr(sigmas), ptr(raws), ptr(deltas), ptr(ts), ptr(rays_a), I64(R), I64(S),
              I32(C), F32(float(T_threshold)), ptr(total), ptr(opacity), ptr(depth), ptr(rend), ptr(ws), stream())

@@ -88,8 +88,33 @@ class CPUTrainer:
         for g in self.opt.param_groups:
             g["lr"] = lr
 
-    def step(self, batch, global_step=3000, noise=None):
-        """One training step; `noise` (R,) injects the marcher's perturbation (default torch.rand)."""
+    def load_state(self, flat_params, exp_avg, exp_avg_sq, adam_step, amp_scale=None, amp_tracker=0, bitfield=None):
+        """Continue from another trainer's state (a HIP training snapshot): the flat fp32 parameter
+        buffer [table | W1 | W2 | W3 | W4 | W5] (ncnerf_amd NGPMT.flat_params order), Adam's flat first
+        and second moments and its step count (AdamW's per-parameter `step`, identical for every
+        parameter), the GradScaler's scale / growth tracker, the occupancy bitfield."""
+        flat = [torch.as_tensor(np.asarray(a, np.float32)).reshape(-1) for a in (flat_params, exp_avg, exp_avg_sq)]
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                n = p.numel()
+                p.copy_(flat[0][off:off + n].view_as(p))
+                self.opt.state[p] = {"step": torch.tensor(float(adam_step)),
+                                     "exp_avg": flat[1][off:off + n].view_as(p).clone(),
+                                     "exp_avg_sq": flat[2][off:off + n].view_as(p).clone()}
+                off += n
+        assert off == flat[0].numel(), (off, flat[0].numel())
+        if amp_scale is not None:
+            self.amp_S, self.amp_tracker = float(amp_scale), int(amp_tracker)
+        if bitfield is not None:
+            self.bitfield = np.ascontiguousarray(bitfield, np.uint8)
+
+    def step(self, batch, global_step=3000, noise=None, record=None):
+        """One training step; `noise` (R,) injects the marcher's perturbation (default torch.rand).
+        record (a dict, optional) receives the step's intermediate values: the loss terms (as
+        NeRFMTLoss names them, weighted), the unweighted cluster terms, the valid-normal mask and the
+        cluster labels of the valid normals, the gradient of every parameter before the clip (the
+        unscaled gradient the optimizer receives) and whether the GradScaler skipped the step."""
         o, d = batch["rays_o"], batch["rays_d"]
         R = o.shape[0]
         _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
@@ -101,39 +126,54 @@ class CPUTrainer:
         rays_a, xyzs, dirs, deltas, ts, counter = vren_ref.raymarching_train(o, d, ht, self.bitfield, 1, 0.5, 0.0,
                                                                              noise, 128, 1024)
         self.opt.zero_grad()
-        K = 128.0 * self.amp_S if self.emulate_bwd else None
+        # the kernel's backward chain scale: fp16 at tcnn's 128 x the GradScaler's S; bf16 unscaled (no
+        # GradScaler: PL's bf16 mode, tcnn's non-fp16 modules)
+        K = (128.0 * self.amp_S if self.emulate == "fp16" else 1.0) if self.emulate_bwd else None
         sig, rgb, _ = field_ref.field_forward_autograd(torch.from_numpy(xyzs), torch.from_numpy(dirs), self.P,
                                                        self.levels, impl=self.encode_impl, emulate=self.emulate,
                                                        bwd_scale=K)
         _, opacity, depth, rend, _ = _Composite.apply(sig, rgb, torch.from_numpy(deltas), torch.from_numpy(ts),
                                                       torch.from_numpy(rays_a), 1e-4)
         out_rgb = rend + 1.0 * (1 - opacity)[:, None]
-        loss = ((out_rgb - torch.from_numpy(batch["rgb"])) ** 2).mean()
+        l_rgb = ((out_rgb - torch.from_numpy(batch["rgb"])) ** 2).mean()
         oo = opacity + 1e-10
-        loss = loss + self.opacity_w * (-oo * torch.log(oo)).mean()
+        l_op = self.opacity_w * (-oo * torch.log(oo)).mean()
+        loss = l_rgb + l_op
+        rec = {} if record is None else record
+        rec.update(rgb=float(l_rgb.detach()), opacity=float(l_op.detach()), samples=int(counter[0]))
         x1, x2, x3 = losses_ref.patch_triangle_index(R)
         dt = torch.from_numpy(d)
         n = losses_ref.normals_from_depth(dt, dt, depth, x1, x2, x3)  # rays_o := rays_d (quirk q1)
         valid = losses_ref.valid_normals_mask(n.detach())
         nv = n[valid]
+        rec["valid"] = valid.numpy().copy()
         if nv.shape[0] >= 20:
             C, a = losses_ref.spherical_kmeans(nv.detach().numpy(), K=20, niter=20, seed=1234)
             lab, _ = losses_ref.cluster_select(C, a, 0.99)
             ort, cdot, cl1 = losses_ref.cluster_losses(nv, torch.from_numpy(lab))
             w = losses_ref.w_sched(self.w_cluster, global_step)
-            loss = loss + w * (losses_ref.validity(ort) + losses_ref.validity(cdot) + losses_ref.validity(cl1))
+            terms = [losses_ref.validity(t) for t in (ort, cdot, cl1)]
+            rec.update(labels=np.asarray(lab).copy(), w_cluster=float(w),
+                       norm_D_C_ort_dot=float(w * terms[0].detach()), norm_D_C_centr_dot=float(w * terms[1].detach()),
+                       norm_D_C_centr_L1=float(w * terms[2].detach()), raw_cluster=[float(t.detach()) for t in terms])
+            loss = loss + w * (terms[0] + terms[1] + terms[2])
+        rec["total"] = float(loss.detach())
         loss.backward()
-        if self.emulate_bwd:  # GradScaler.step / update (torch defaults)
+        if record is not None:
+            rec["grads"] = [p.grad.detach().clone() for p in self.params]
+        if self.emulate_bwd and self.emulate == "fp16":  # GradScaler.step / update (torch defaults)
             if not all(bool(torch.isfinite(p.grad).all()) for p in self.params):
                 self.opt.zero_grad()
                 self.amp_S *= 0.5
                 self.amp_tracker = 0
                 self.amp_skips += 1
+                rec["skipped"] = True
                 return float(loss.detach()), int(counter[0])
             self.amp_tracker += 1
             if self.amp_tracker >= 2000:
                 self.amp_S *= 2.0
                 self.amp_tracker = 0
+        rec["skipped"] = False
         torch.nn.utils.clip_grad_norm_(self.params, 0.05)
         self.opt.step()
         return float(loss.detach()), int(counter[0])

@@ -44,7 +44,10 @@ def _load_params(model, tensors):
 
 
 def run(steps=60, n_rays=1024, eval_batches=4, eval_rays=8192, oracle_eval_rays=1024, seed=4, step0=3000,
-        threads=None, use_graph=True, log=None):
+        threads=None, use_graph=True, log=None, precision="fp16", emulate=None):
+    """precision: the HIP field's MLP operand type (config #3: "bf16"); emulate: the oracle's operand
+    and backward-chain rounding (None: plain fp32; "fp16"/"bf16": as the kernel rounds, with the
+    fp16 GradScaler) — returns the PSNRs and the per-step losses of both sides."""
     from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
     from ncnerf_amd.rendering import render
     from ncnerf_amd.synthetic import SyntheticScene
@@ -54,12 +57,12 @@ def run(steps=60, n_rays=1024, eval_batches=4, eval_rays=8192, oracle_eval_rays=
         torch.set_num_threads(threads)
     dev = torch.device("cuda:0")
     scene = SyntheticScene()
-    cpu = CPUTrainer(scene.bitfield, seed=seed)
+    cpu = CPUTrainer(scene.bitfield, seed=seed, emulate=emulate, emulate_bwd=emulate is not None)
     init = [t.detach().clone() for t in cpu.params]
     bf = torch.from_numpy(scene.bitfield).to(dev)
 
     def gpu_model(tensors):
-        m = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+        m = register_grid_buffers(NGPMT(scale=0.5, grid_size=128, precision=precision).to(dev))
         _load_params(m, tensors)
         m.density_bitfield.copy_(bf)
         return m
@@ -67,6 +70,7 @@ def run(steps=60, n_rays=1024, eval_batches=4, eval_rays=8192, oracle_eval_rays=
     m = gpu_model(init)
     tr = Trainer(m, update_grid=False, use_graph=use_graph)
     t_cpu = t_gpu = 0.0
+    losses = []
     for k in range(steps):
         b = scene.batch(n_rays, seed=10_000 + k)
         noise = torch.rand(n_rays, generator=torch.Generator().manual_seed(20_000 + k))
@@ -79,6 +83,7 @@ def run(steps=60, n_rays=1024, eval_batches=4, eval_rays=8192, oracle_eval_rays=
         _, ld = tr.step(bt, global_step=step0 + k)
         l_gpu = float(ld["total"])
         t_gpu += time.perf_counter() - t
+        losses.append((l_cpu, l_gpu))
         if log and (k % 20 == 0 or k == steps - 1):
             log(f"step {k}: loss ref {l_cpu:.5f} hip {l_gpu:.5f}")
 
@@ -93,6 +98,7 @@ def run(steps=60, n_rays=1024, eval_batches=4, eval_rays=8192, oracle_eval_rays=
             se[key] += float(((res["rgb"].clamp(0, 1) - b["rgb"]) ** 2).sum())
         n_px += eval_rays * 3
     out = {"steps": steps, "rays_per_step": n_rays, "step0": step0, "eval_rays": eval_batches * eval_rays,
+           "precision": precision, "oracle_emulate": emulate, "losses_ref_hip": losses,
            "psnr_hip": _psnr(se["hip"] / n_px), "psnr_ref": _psnr(se["ref"] / n_px)}
     out["delta_db"] = out["psnr_hip"] - out["psnr_ref"]
     # renderer pin: the oracle's own (train-path, zero-noise) render of the oracle-trained

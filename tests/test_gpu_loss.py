@@ -325,3 +325,32 @@ def test_cluster_timeout_drops_cluster_terms(dev, tmp_path):
           f"full step vs photometric-only: {rel(full, photo):.2e}")
     assert rel(dropped, photo) < 1e-5
     assert rel(full, photo) > 1e-3
+
+
+def test_cluster_coresidency_refuses(dev):
+    """The clustering kernel's 16 workgroups meet at grid barriers, so all of them must be resident
+    at once.  ncn_cluster_coresidency reports how many fit beside `busy` CUs of
+    concurrent work; the split step checks it for its rgb pass (one workgroup per CU) before it is
+    captured, and refuses — raises, launching nothing — when the clustering could not stay resident,
+    instead of spinning into the barrier timeout."""
+    import ctypes
+    from ncnerf_amd import _lib
+    from ncnerf_amd.ngp_mt import NGPMT, register_grid_buffers
+    from ncnerf_amd.split_step import SPLIT_BLOCKS, SplitStep
+    from ncnerf_amd.trainer import Trainer
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    cap = ctypes.c_int(0)
+    assert _lib.lib().ncn_cluster_coresidency(20, 0, ctypes.byref(cap)) == 0
+    per_cu = cap.value // cus
+    assert per_cu >= 1 and cap.value >= 16, (cap.value, cus)
+    assert _lib.lib().ncn_cluster_coresidency(20, SPLIT_BLOCKS, ctypes.byref(cap)) == 0
+    assert cap.value == (cus - SPLIT_BLOCKS) * per_cu >= 16
+    busy = cus - (16 - 1) // per_cu  # leaves fewer free CUs than 16 workgroups need
+    rc = _lib.lib().ncn_cluster_coresidency(20, busy, ctypes.byref(cap))
+    assert rc != 0 and cap.value < 16, (rc, cap.value)
+    assert "cannot all be resident" in _lib.lib().ncn_last_error().decode()
+    m = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
+    tr = Trainer(m, update_grid=False, use_graph=True)
+    assert SplitStep(tr).cluster_capacity >= 16
+    with pytest.raises(_lib.NcnError, match="cannot all be resident"):
+        SplitStep(tr, rgb_blocks=busy)

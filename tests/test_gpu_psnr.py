@@ -46,6 +46,22 @@ def test_psnr_parity_short():
     assert abs(r["psnr_ref_hip_render_same_rays"] - r["psnr_ref_oracle_render"]) <= 0.05, r
 
 
+def test_psnr_parity_short_bf16():
+    """Config #3 end to end: the bf16 HIP step against the oracle that rounds the MLP operands and
+    the (unscaled) backward chain to bf16 as the kernel does — one pair, same init, batches and noise,
+    40 steps of 1024 rays: the first step's losses within 1e-3, every step's within 1 %, PSNR within
+    0.1 dB on the same renderer."""
+    r = run(steps=40, n_rays=1024, eval_batches=2, eval_rays=4096, oracle_eval_rays=512, threads=8,
+            precision="bf16", emulate="bf16")
+    print({k: v for k, v in r.items() if k != "losses_ref_hip"})
+    l0_ref, l0_hip = r["losses_ref_hip"][0]
+    assert abs(l0_hip - l0_ref) <= 1e-3 * abs(l0_ref), r["losses_ref_hip"][:3]
+    for k, (lr_, lh) in enumerate(r["losses_ref_hip"]):
+        assert abs(lh - lr_) <= 1e-2 * abs(lr_), (k, lr_, lh)
+    assert r["psnr_hip"] > 7.0 and r["psnr_ref"] > 7.0, r
+    assert abs(r["delta_db"]) <= 0.1, r
+
+
 @pytest.mark.parametrize("preset", ["hypersim", "scannet_manhattan"])
 def test_psnr_ensemble_vs_oracle(preset):
     """preset scannet_manhattan: config #5's cluster weights (1e-2) against its own fp16-fw+bw oracle
