@@ -91,7 +91,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy, measured (79 % of the spec)
 TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_train_fused", "ncn_field_fwd",
-         "ncn_field_bwd", "ncn_field_bwd_mlp_part", "ncn_field_scatter", "ncn_cluster_loss")
+         "ncn_field_bwd", "ncn_field_bwd_mlp_part", "ncn_field_scatter", "ncn_field_scatter_wgrad", "ncn_cluster_loss")
 
 
 def pmc_traffic():

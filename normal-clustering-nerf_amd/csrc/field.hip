@@ -505,6 +505,7 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
 // straight from the exchange area, two groups (32 samples) per K=32 MFMA.  So no wave holds all
 // of dW, the two waves of a SIMD overlap their MFMA chains, and every tile is written once per
 // workgroup into its slab row at the end.
+constexpr int DE_HEADER_FLOATS = 4;  // the dE workspace's header (ncn_field_bwd_dE_floats)
 constexpr int BWD_WAVES = 8;
 constexpr int BWD_THREADS = 64 * BWD_WAVES;
 // exchange tiles per group: dW operands, A = dY^T, B = X^T (16 features x 16 samples)
@@ -673,21 +674,24 @@ __device__ __forceinline__ void bwd_group(const FR& F, uint16_t* Xw, const BwdIn
 #pragma unroll
     for (int t = 0; t < 2; t++)
         dE[t] = M::k32(F.a32(B_L1 + 2 * t + 1, lane), d1b, M::k32(F.a32(B_L1 + 2 * t, lane), d1a, zero4()));
+    // The encoding gradient leaves in the MLP operand type, as tcnn hands its network's input gradient
+    // (type T) to the grid backward: fp16 at the chain's scale S (the scatter divides by S), bf16
+    // unscaled — level-major [16][n_stride] pairs behind the workspace header (dE_pairs), half the
+    // bytes of f32 pairs.  fp16 overflow gives inf: the level's max is then non-finite, the scatter
+    // adds it straight to the gradient and the GradScaler skips the step, as tcnn's would.
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    const t2 q[4] = {t2{(T)dE[0][0], (T)dE[0][1]}, t2{(T)dE[0][2], (T)dE[0][3]}, t2{(T)dE[1][0], (T)dE[1][1]},
+                     t2{(T)dE[1][2], (T)dE[1][3]}};
+    // per-level max |dE| of this lane's levels (2g, 2g+1, 8+2g, 9+2g), of the stored values (loss
+    // scale off: an exact power of two): the scatter's fixed-point scale
 #pragma unroll
-    for (int t = 0; t < 2; t++)  // (loss scale off: an exact power of two)
-#pragma unroll
-        for (int i = 0; i < 4; i++) dE[t][i] *= inv_S;
-    // per-level max |dE| of this lane's levels (2g, 2g+1, 8+2g, 9+2g): the scatter's fixed-point scale
-    lm[0] = lmax_upd(lm[0], dE[0][0], dE[0][1]);
-    lm[1] = lmax_upd(lm[1], dE[0][2], dE[0][3]);
-    lm[2] = lmax_upd(lm[2], dE[1][0], dE[1][1]);
-    lm[3] = lmax_upd(lm[3], dE[1][2], dE[1][3]);
-    if (valid) {  // encoding gradient -> level-major [16][n] float2 for the scatter pass
-        float2* o = (float2*)dE_out;
-        o[(int64_t)(2 * g) * n_stride + s] = make_float2(dE[0][0], dE[0][1]);
-        o[(int64_t)(2 * g + 1) * n_stride + s] = make_float2(dE[0][2], dE[0][3]);
-        o[(int64_t)(8 + 2 * g) * n_stride + s] = make_float2(dE[1][0], dE[1][1]);
-        o[(int64_t)(9 + 2 * g) * n_stride + s] = make_float2(dE[1][2], dE[1][3]);
+    for (int j = 0; j < 4; j++) lm[j] = lmax_upd(lm[j], (float)q[j][0] * inv_S, (float)q[j][1] * inv_S);
+    if (valid) {
+        t2* o = (t2*)dE_out;
+        o[(int64_t)(2 * g) * n_stride + s] = q[0];
+        o[(int64_t)(2 * g + 1) * n_stride + s] = q[1];
+        o[(int64_t)(8 + 2 * g) * n_stride + s] = q[2];
+        o[(int64_t)(9 + 2 * g) * n_stride + s] = q[3];
     }
 }
 
@@ -860,6 +864,12 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float S = loss_scale ? *loss_scale * (Mfma<T>::f16 ? NCN_TCNN_LOSS_SCALE : 1.f) : 1.f, inv_S = 1.f / S;
     typedef typename Mfma<T>::v8 v8;
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
+    // dE workspace: a 16-B header {1 / S, operand type (0 fp16, 1 bf16)} then the pairs
+    float* const dE_pairs = dE_out ? dE_out + DE_HEADER_FLOATS : nullptr;
+    if (PART != BWD_RGB && dE_out && blockIdx.x == 0 && threadIdx.x == 0) {
+        dE_out[0] = inv_S;
+        dE_out[1] = Mfma<T>::f16 ? 0.f : 1.f;
+    }
     const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
     // split passes' stash (ncn_field_bwd_stash_floats): [groups][64] operand tiles, then [groups][16]
     // fp32 row-0 elements (capacity groups: the layout does not depend on the device count)
@@ -910,7 +920,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             const int z = opaque_zero();
             F.f32 = F32s + z;
             F.f16 = F16s + z;
-            bwd_group<T, PART>(F, X + wid * NX * 256, cur, grp, n, n_stride, lane, dE_out, lm, inv_S, stq, sth0);
+            bwd_group<T, PART>(F, X + wid * NX * 256, cur, grp, n, n_stride, lane, dE_pairs, lm, inv_S, stq, sth0);
         }
         lds_barrier();  // (the dE stores and the next step's loads stay in flight)
         bwd_dw<T, PART>(X, ng, wid, lane, acc);
@@ -1006,8 +1016,11 @@ constexpr int sc_max(int a, int b) { return a > b ? a : b; }
 constexpr int SC_ARENA = sc_max(SC_SETS_CELL * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2), SC_SETS_DIR * SC_WAYS * SC_SLOT_BYTES);
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
 constexpr int SC_BATCH = 2;  // corners per batch of set reads in sc_add (2: 232 us, 4: 238 us (spills), 8: 298 us)
-constexpr int SC_C_DIR = 4;  // samples per lane on the fine levels (unit = 4096 samples, in grabs of 64 x 2)
-constexpr int SC_DIR_HALF = 15;  // fine levels from here on: 2 samples per lane (units of 2048; 13: 198, 14: 202, 15: 190, none: 202 us)
+// Samples per lane of a fine-level unit (unit = 1024 x C samples): 4 (4096-sample units, in grabs of
+// 64 x 2) up to level 14; level 15 takes 2 (its ~1 distinct entry per sample would overfill the
+// 4-way sets of a 4096-sample unit; units of 2048 from level 13: 198, 14: 202, 15: 190, none: 202 us).
+// (Measured round 5: 8192-sample units on levels 10-11 / 10-12: 288 / 281 us against 202.)
+__host__ __device__ constexpr int sc_fine_c(int l) { return l < 15 ? 4 : 2; }
 constexpr int SC_C_CELL = 4;     // samples per lane per round on the cell levels
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
@@ -1184,6 +1197,20 @@ struct ScNorm {
     __device__ __forceinline__ float operator()(float v) const { return pow2 ? (v - mn) * inv : (v - mn) / ext; }
 };
 
+// The encoding gradient as the MLP pass stored it (field_bwd_kernel): pairs of the operand type, fp16
+// at the chain's loss scale or bf16 unscaled; decoded to f32 and unscaled (1/S: a power of two, exact).
+struct ScDE {
+    float inv;
+    bool bf16;
+    __device__ __forceinline__ float2 operator()(uint32_t w) const {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        const h2 h = __builtin_bit_cast(h2, w);
+        const float x = bf16 ? __uint_as_float(w << 16) : (float)h[0];
+        const float y = bf16 ? __uint_as_float(w & 0xFFFF0000u) : (float)h[1];
+        return make_float2(x * inv, y * inv);
+    }
+};
+
 __device__ __forceinline__ void sc_corner_sums(const LevelPos& p, float2 g, float (&v)[16]) {
     // corner weights in the forward's association ((wx * wy) * wz)
     const float wx[2] = {1.0f - p.fx, p.fx}, wy[2] = {1.0f - p.fy, p.fy}, wz[2] = {1.0f - p.fz, p.fz};
@@ -1203,12 +1230,22 @@ struct ScChunk {
     float2 g[C];
 };
 // C is 2 or 4 and the lane's first sample sb a multiple of C: the chunk's xyz (12C bytes) and dE
-// (8C bytes) are 16-B (C = 4) / 8-B (C = 2) aligned pieces, loaded with dwordx4 / dwordx2 — a lane
+// (4C bytes) are 16-B (C = 4) / 8-B (C = 2) aligned pieces, loaded with dwordx4 / dwordx2 — a lane
 // reads contiguous bytes, so fewer, wider load instructions (the lane-strided pattern costs TA
 // cycles per touched cache line).  A partial last chunk falls back to per-sample loads.
 template <int C>
+__device__ __forceinline__ void sc_load_de(ScChunk<C>& ch, const uint32_t* __restrict__ p, const ScDE& de) {
+    if constexpr (C == 4) {
+        const uint4 v = *(const uint4*)p;
+        ch.g[0] = de(v.x); ch.g[1] = de(v.y); ch.g[2] = de(v.z); ch.g[3] = de(v.w);
+    } else {
+        const uint2 v = *(const uint2*)p;
+        ch.g[0] = de(v.x); ch.g[1] = de(v.y);
+    }
+}
+template <int C>
 __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
-                                               const float2* __restrict__ dEl, const ScNorm& nrm,
+                                               const uint32_t* __restrict__ dEl, const ScDE& de, const ScNorm& nrm,
                                                const int32_t* __restrict__ order) {
     static_assert(C == 2 || C == 4, "chunk of 2 or 4 samples");
     float xs[3 * C];
@@ -1217,22 +1254,10 @@ __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_
 #pragma unroll
         for (int i = 0; i < C; i++) src[i] = sb + i < s1 ? (int64_t)order[sb + i] : -1;
         if (sb + C <= s1) {
-            if constexpr (C == 4) {
-                const float4* pg = (const float4*)(dEl + sb);
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const float4 v = pg[q];
-                    ch.g[2 * q] = make_float2(v.x, v.y);
-                    ch.g[2 * q + 1] = make_float2(v.z, v.w);
-                }
-            } else {
-                const float4 v = *(const float4*)(dEl + sb);
-                ch.g[0] = make_float2(v.x, v.y);
-                ch.g[1] = make_float2(v.z, v.w);
-            }
+            sc_load_de<C>(ch, dEl + sb, de);
         } else {
 #pragma unroll
-            for (int i = 0; i < C; i++) ch.g[i] = src[i] >= 0 ? dEl[sb + i] : make_float2(0.f, 0.f);
+            for (int i = 0; i < C; i++) ch.g[i] = src[i] >= 0 ? de(dEl[sb + i]) : make_float2(0.f, 0.f);
         }
 #pragma unroll
         for (int i = 0; i < C; i++) {
@@ -1249,13 +1274,6 @@ __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_
                 const float4 v = px[q];
                 xs[4 * q] = v.x; xs[4 * q + 1] = v.y; xs[4 * q + 2] = v.z; xs[4 * q + 3] = v.w;
             }
-            const float4* pg = (const float4*)(dEl + sb);
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                const float4 v = pg[q];
-                ch.g[2 * q] = make_float2(v.x, v.y);
-                ch.g[2 * q + 1] = make_float2(v.z, v.w);
-            }
         } else {
             const float2* px = (const float2*)(xyzs + 3 * sb);
 #pragma unroll
@@ -1263,16 +1281,14 @@ __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_
                 const float2 v = px[q];
                 xs[2 * q] = v.x; xs[2 * q + 1] = v.y;
             }
-            const float4 v = *(const float4*)(dEl + sb);
-            ch.g[0] = make_float2(v.x, v.y);
-            ch.g[1] = make_float2(v.z, v.w);
         }
+        sc_load_de<C>(ch, dEl + sb, de);
     } else {
 #pragma unroll
         for (int i = 0; i < C; i++) {
             const bool in = sb + i < s1;
             const int64_t sc = in ? sb + i : 0;
-            ch.g[i] = in ? dEl[sc] : make_float2(0.f, 0.f);
+            ch.g[i] = in ? de(dEl[sc]) : make_float2(0.f, 0.f);
             xs[3 * i] = in ? xyzs[3 * sc] : 0.f;
             xs[3 * i + 1] = in ? xyzs[3 * sc + 1] : 0.f;
             xs[3 * i + 2] = in ? xyzs[3 * sc + 2] : 0.f;
@@ -1482,15 +1498,15 @@ __device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m
 // One fine-level unit: the samples in grabs, then the flush of the claimed slots.
 template <int C>
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
-                                        const float* __restrict__ xyzs, const float2* __restrict__ dEl,
-                                        const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
+                                        const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
+                                        const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
                                         const int32_t* __restrict__ order) {
     SC_TNOW(t0);
     // (a fine unit holds at most 4096 samples: 2^46 leaves the sums four bits of headroom below 2^62)
     const ScLevel L = sc_level(Lt, l, m, 46);
     SC_TNOW(t1);
-    if constexpr (C == 4) {
-        // The unit's 4096 samples in grabs of 64 lanes x 2: grab k gives lane t the samples
+    if constexpr (C >= 4) {
+        // The unit's 1024 x C samples in grabs of 64 lanes x 2: grab k gives lane t the samples
         // s0 + (t * NG + k) * 2 — the 64 lanes of one wave-instruction hold samples 2 * NG = 64
         // positions apart, so they rarely address the same LDS slot at once (same-address LDS atomics
         // serialise).  Wave w takes grab w first, then draws grabs from the unit's LDS counter after
@@ -1500,19 +1516,19 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
         constexpr int NG = SC_THREADS * C / 128;
         int k = wid;
         ScChunk<2> cg;
-        sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, nrm, order);
+        sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, de, nrm, order);
         while (k < NG) {  // (wave-uniform)
             sc_direct<2>(sh, lane, cg, L, grad);
             int kn = 0;
             if (lane == 0) kn = atomicAdd(sh.grab, 1);
             kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
-            if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, nrm, order);
+            if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, de, nrm, order);
             k = kn;
         }
     } else {
         // chunk of lane t of wave w: t * SC_WAVES + w (lanes SC_WAVES * C positions apart)
         ScChunk<C> ch;
-        sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, nrm, order);
+        sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, de, nrm, order);
         sc_direct<C>(sh, lane, ch, L, grad);
     }
     SC_TNOW(t2);
@@ -1550,12 +1566,16 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
 // Cell units: `rounds` consecutive chunks of 1024 x C samples per unit (no barrier between them),
 // then one flush.  Rounds per level: coarse levels have few cells, so longer units mean fewer
 // flushes and barriers.
-__device__ __forceinline__ int sc_cell_rounds(int l) { return l < 6 ? 4 : l < 10 ? 2 : 1; }
+__host__ __device__ constexpr int sc_cell_rounds(int l) { return l < 6 ? 4 : l < 10 ? 2 : 1; }
+// samples of one unit of level l
+__host__ __device__ constexpr int64_t sc_unit_span(int l) {
+    return (int64_t)SC_THREADS * (l < SC_CELL_HI ? SC_C_CELL * sc_cell_rounds(l) : sc_fine_c(l));
+}
 
 template <int C>
 __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1, int rounds,
-                                             const float* __restrict__ xyzs, const float2* __restrict__ dEl,
-                                             const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
+                                             const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
+                                             const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
                                              const int32_t* __restrict__ order) {
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
     const ScLevel L = sc_level(Lt, l, m, 61 - lg_unit);
@@ -1563,11 +1583,11 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
     // waves); round r covers the unit's r-th slice of SC_THREADS * C samples
     const int64_t lane_off = ((int64_t)lane * SC_WAVES + wid) * C;
     ScChunk<C> ch;
-    sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, nrm, order);
+    sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, de, nrm, order);
     for (int r = 0; r < rounds; r++) {
         ScChunk<C> nx;
         const bool more = r + 1 < rounds;
-        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * SC_THREADS * C + lane_off, s1, xyzs, dEl, nrm, order);
+        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * SC_THREADS * C + lane_off, s1, xyzs, dEl, de, nrm, order);
         if (L.direct)
             sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
         else
@@ -1580,13 +1600,21 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
 }
 
 // One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
-__device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n_dir4, int64_t ud, int64_t ud2, int64_t n,
-                                            int cell_lo, int dir_lo, int dir_mid, int& layout, int& par, ScShared& sh,
+__device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, int& layout, int& par, ScShared& sh,
                                             char* arena, int* fill, const float* lmax_s, int wid, int lane,
-                                            const float* __restrict__ xyzs, const float2* __restrict__ dE,
-                                            int64_t e_stride, const ScNorm& nrm, const LevelTable& Lt,
+                                            const float* __restrict__ xyzs, const uint32_t* __restrict__ dE,
+                                            int64_t e_stride, const ScDE& de, const ScNorm& nrm, const LevelTable& Lt,
                                             float* __restrict__ grad, const int32_t* __restrict__ order) {
-    const int mode = u < n_cell ? SC_MODE_CELL : SC_MODE_DIR;
+    int l = level_lo;
+    int64_t v = u, span = sc_unit_span(l);
+    for (;; l++) {  // (uniform, at most 16 steps) level-major unit order
+        span = sc_unit_span(l);
+        const int64_t nu = (n + span - 1) / span;
+        if (v < nu) break;
+        v -= nu;
+    }
+    const int64_t s0 = v * span, s1 = min(n, s0 + span);
+    const int mode = l < SC_CELL_HI ? SC_MODE_CELL : SC_MODE_DIR;
     if (mode != layout) {  // (re)initialise the table of the new layout
         lds_barrier();
         sh = sc_layout(arena, fill, mode);
@@ -1597,38 +1625,6 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
         lds_barrier();
         layout = mode;
         par = 0;
-    }
-    int l, rounds = 1;
-    int64_t s0, s1;
-    if (mode == SC_MODE_CELL) {
-        int64_t v = u;
-        l = cell_lo;
-        for (;; l++) {  // (uniform, at most SC_CELL_HI steps)
-            rounds = sc_cell_rounds(l);
-            const int64_t span = (int64_t)SC_THREADS * SC_C_CELL * rounds;
-            const int64_t nu = (n + span - 1) / span;
-            if (v < nu) {
-                s0 = v * span;
-                s1 = min(n, s0 + span);
-                break;
-            }
-            v -= nu;
-        }
-    } else {
-        int64_t v = u - n_cell;
-        if (v < n_dir4) {
-            const int li = (int)(v / ud);
-            l = dir_lo + li;
-            s0 = (v - li * ud) * (SC_THREADS * SC_C_DIR);
-            s1 = min(n, s0 + SC_THREADS * SC_C_DIR);
-        } else {
-            v -= n_dir4;
-            const int li = (int)(v / ud2);
-            l = dir_mid + li;
-            s0 = (v - li * ud2) * (SC_THREADS * 2);
-            s1 = min(n, s0 + SC_THREADS * 2);
-            rounds = 2;  // (marks the C = 2 form below)
-        }
     }
     float m = lmax_s[l];
 #ifdef NCN_DIAG_SC_LEVELS_MASK
@@ -1641,19 +1637,19 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n_cell, int64_t n
     sh.grab = fill + 2 + par;  // (the grab counters behind the claim counts, alternating alike)
     if (threadIdx.x == 0) { fill[par ^ 1] = 0; fill[2 + (par ^ 1)] = 0; }
     par ^= 1;
-    const float2* dEl = dE + (int64_t)l * e_stride;
+    const uint32_t* dEl = dE + (int64_t)l * e_stride;
     if (mode == SC_MODE_CELL)
-        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, rounds, xyzs, dEl, nrm, Lt, m, grad, order);
-    else if (rounds == 2)
-        sc_unit<2>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order);
+    else if (sc_fine_c(l) == 2)
+        sc_unit<2>(sh, wid, lane, l, s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
     else
-        sc_unit<SC_C_DIR>(sh, wid, lane, l, s0, s1, xyzs, dEl, nrm, Lt, m, grad, order);
+        sc_unit<4>(sh, wid, lane, l, s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
 }
 
 __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
-                                                                   const float2* __restrict__ dE,
+                                                                   const float* __restrict__ dE_ws,
                                                                    float* __restrict__ grad,
                                                                    const float* __restrict__ level_max, int lm_rows,
                                                                    int level_lo, int level_hi,
@@ -1694,23 +1690,15 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     nrm.ext = xyz_extent;
     nrm.inv = 1.0f / xyz_extent;
     nrm.pow2 = (__float_as_uint(xyz_extent) & 0x807FFFFFu) == 0u && xyz_extent > 0.f;
-    // units, level-major over the levels [level_lo, level_hi): cell levels [0, SC_CELL_HI) in spans
-    // of 1024 * C_CELL * rounds(l) samples, fine levels in spans of 1024 * SC_C_DIR, those from
-    // SC_DIR_HALF on in spans of 1024 * 2 (their ~1 distinct entry per sample would overfill the
-    // 4-way sets of a 4096-sample unit)
-    const int64_t ud = (n + SC_THREADS * SC_C_DIR - 1) / (SC_THREADS * SC_C_DIR);
-    const int64_t ud2 = (n + SC_THREADS * 2 - 1) / (SC_THREADS * 2);
-    const int cell_lo = level_lo, cell_hi = min(level_hi, SC_CELL_HI);
-    const int dir_lo = max(level_lo, SC_CELL_HI), dir_hi = level_hi;
-    int64_t n_cell = 0;
-    for (int l = cell_lo; l < cell_hi; l++) {
-        const int64_t span = (int64_t)SC_THREADS * SC_C_CELL * sc_cell_rounds(l);
-        n_cell += (n + span - 1) / span;
-    }
-    const int dir_mid = max(dir_lo, min(dir_hi, SC_DIR_HALF));
-    const int64_t n_dir4 = dir_mid > dir_lo ? (int64_t)(dir_mid - dir_lo) * ud : 0;
-    const int64_t n_dir2 = dir_hi > dir_mid ? (int64_t)(dir_hi - dir_mid) * ud2 : 0;
-    const int64_t n_units = n_cell + n_dir4 + n_dir2;
+    // the MLP pass's dE workspace: header {1 / S, operand type}, then [16][e_stride] pairs
+    ScDE de;
+    de.inv = dE_ws[0];
+    de.bf16 = dE_ws[1] != 0.f;
+    const uint32_t* dE = (const uint32_t*)(dE_ws + DE_HEADER_FLOATS);
+    // units, level-major over the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell
+    // levels [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
+    int64_t n_units = 0;
+    for (int l = level_lo; l < level_hi; l++) n_units += (n + sc_unit_span(l) - 1) / sc_unit_span(l);
     // Units are ordered heaviest first (the coarse cell levels' long units, then the finer levels);
     // workgroup b takes units b, b + gridDim.x, ...  (a dynamic unit queue measured no better: 191 vs
     // 196 us, then 194 vs 190 — the static stride is not load-imbalanced).  A workgroup's units go
@@ -1718,8 +1706,8 @@ __global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* 
     int layout = -1, par = 0;
     ScShared sh;
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x)
-        sc_one_unit(u, n_cell, n_dir4, ud, ud2, n, cell_lo, dir_lo, dir_mid, layout, par, sh, arena, fill, lmax_s, wid,
-                    lane, xyzs, dE, e_stride, nrm, Lt, grad, order);
+        sc_one_unit(u, n, level_lo, layout, par, sh, arena, fill, lmax_s, wid, lane, xyzs, dE, e_stride, de, nrm, Lt, grad,
+                    order);
 }
 
 static int scatter_grid(int64_t n_cap) {
@@ -1839,7 +1827,7 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
 
 int ncn_field_bwd_blocks(int64_t n) { return bwd_blocks_of(n); }
 
-int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? 32 * ((n + 3) & ~(int64_t)3) : 0; }
+int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? DE_HEADER_FLOATS + 16 * ((n + 3) & ~(int64_t)3) : 0; }
 
 int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint16_t* weights_packed,
@@ -1917,7 +1905,7 @@ int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, 
     int grid = scatter_grid(n);
     if (max_blocks > 0) grid = std::min(grid, max_blocks);
     hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
-                       xyz_min, xyz_extent, (const float2*)dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
+                       xyz_min, xyz_extent, dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
                        level_lo, level_hi, order, slab, n_blocks_sigma, n_blocks_rgb, grad_w);
     NCN_LAUNCH_CHECK("ncn_field_scatter");
     return 0;

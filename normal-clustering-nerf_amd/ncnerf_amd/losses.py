@@ -276,8 +276,8 @@ class _NeRFLossFused(torch.autograd.Function):
         ctx.save_for_backward(rgb, opacity, depth, rays_o, rays_d, rgb_gt, photo, dn)
         ctx.w_op = w_op
         ctx.set_materialize_grads(False)
-        ctx.mark_non_differentiable(labels, cents, out)
-        return out[10], photo[0], photo[1], out[4], out[5], out[6], labels, cents, out
+        ctx.mark_non_differentiable(labels, cents, out, normals)
+        return out[10], photo[0], photo[1], out[4], out[5], out[6], labels, cents, out, normals
 
     @staticmethod
     def backward(ctx, g_total, g_rgb, g_op, g_ort, g_cdot, g_cl1, *_unused):
@@ -379,6 +379,7 @@ class NeRFMTLoss(nn.Module):
             assert self.ray_sampling_strategy in ["all_images_triang", "all_images_triang_val", "same_image_triang",
                                                   "all_images_triang_patch", "same_image_triang_patch"]
         self.last_cluster = None  # (labels, centroids, raw stats) of the last step, for logging/tests
+        self.last_normals = None  # (fused path) the normals the clustering saw, for tests
         self._idx_cache = {}
         self._wt = {}
 
@@ -408,12 +409,13 @@ class NeRFMTLoss(nn.Module):
         for t, n in ((pred_w_gt["rgb"], "rgb"), (pred_unsup["depth"], "depth")):
             if not t.is_cuda:
                 raise RuntimeError(f"{n} must be a CUDA tensor")
-        total, l_rgb, l_op, ort, cdot, cl1, labels, cents, raw = _NeRFLossFused.apply(
+        total, l_rgb, l_op, ort, cdot, cl1, labels, cents, raw, normals = _NeRFLossFused.apply(
             f(pred_w_gt["rgb"]), f(pred_unsup["opacity"]), f(pred_unsup["depth"]), f(pred_unsup["rays_o"]),
             f(pred_unsup["rays_d"]), f(target_gt["rgb"]), x["x1"], x["x2"], x["x3"], float(self.opacity_w), 20, 20,
             self.kmeans_seed, 1.0 - self.norm_CAN_tres, w, step_dev, (float(self.can_sched_start), float(self._grow)),
             kwargs.get("count_job"))
         self.last_cluster = (labels, cents, raw)
+        self.last_normals = normals  # the patch triangles' normals (zero / invalid ones included)
         return {"rgb": l_rgb, "opacity": l_op, "norm_D_C_ort_dot": ort, "norm_D_C_centr_dot": cdot,
                 "norm_D_C_centr_L1": cl1, "total": total}
 

@@ -105,9 +105,10 @@ _TEX = np.array([[11.0, 7.0, -5.0], [-6.0, 13.0, 8.0], [9.0, -4.0, 12.0]], np.fl
 _TEX_PHASE = np.array([0.3, 2.2, 4.1], np.float32)
 
 
-def texture_rgb(p, lo=0.1, hi=0.9):
-    """Albedo of the room surfaces at points p (N,3): smooth procedural texture in [lo, hi]."""
-    return (0.5 * (hi + lo) + 0.5 * (hi - lo) * np.sin(p @ _TEX.T + _TEX_PHASE)).astype(np.float32)
+def texture_rgb(p, lo=0.1, hi=0.9, freq=1.0):
+    """Albedo of the room surfaces at points p (N,3): smooth procedural texture in [lo, hi]; freq
+    scales the texture frequencies (0: a constant albedo per channel)."""
+    return (0.5 * (hi + lo) + 0.5 * (hi - lo) * np.sin(p @ (freq * _TEX).T + _TEX_PHASE)).astype(np.float32)
 
 
 def first_hit(occ, rays_o, rays_d, scale=0.5, step_vox=0.25, t_max=2.0, chunk=64):
@@ -135,13 +136,13 @@ def first_hit(occ, rays_o, rays_d, scale=0.5, step_vox=0.25, t_max=2.0, chunk=64
     return t_hit
 
 
-def surface_rgb(occ, rays_o, rays_d, scale=0.5, lo=0.1, hi=0.9):
+def surface_rgb(occ, rays_o, rays_d, scale=0.5, lo=0.1, hi=0.9, freq=1.0):
     """Target colour of a ray (gt="surface", default): texture_rgb at its first occupied voxel,
     white (the reference's background, rendering.py:232-240) if it hits nothing."""
     t = first_hit(occ, rays_o, rays_d, scale)
     rgb = np.ones((rays_o.shape[0], 3), np.float32)
     m = np.isfinite(t)
-    rgb[m] = texture_rgb(rays_o[m] + rays_d[m] * t[m, None], lo, hi)
+    rgb[m] = texture_rgb(rays_o[m] + rays_d[m] * t[m, None], lo, hi, freq)
     return rgb
 
 
@@ -160,7 +161,9 @@ class SyntheticScene:
 
     def batch(self, n_rays, seed, gt="surface"):
         """A dict like BaseDataset.__getitem__ + get_rays: rays_o, rays_d (R,3) f32, rgb (R,3), patch info.
-        gt: "surface" (textured room, the PSNR-parity target) or "direction" (view-only colour)."""
+        gt: "surface" (textured room, the PSNR-parity target), "surface_bright" (the same texture in
+        [0.45, 0.95]), "surface_smooth" (that with a quarter of the texture frequency), "surface_flat"
+        (a constant albedo per channel) or "direction" (view-only colour)."""
         assert n_rays % (PATCH * PATCH) == 0
         rng = np.random.default_rng(seed)
         n_p = n_rays // (PATCH * PATCH)
@@ -178,6 +181,10 @@ class SyntheticScene:
             rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale)
         elif gt == "surface_bright":
             rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale, 0.45, 0.95)
+        elif gt == "surface_smooth":
+            rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale, 0.45, 0.95, 0.25)
+        elif gt == "surface_flat":
+            rgb = surface_rgb(self.occ, rays_o, rays_d, self.scale, 0.45, 0.95, 0.0)
         else:
             rgb = _gt_color(rays_d)
         return {"rays_o": rays_o, "rays_d": rays_d, "rgb": rgb, "patch_area": PATCH * PATCH,

@@ -282,14 +282,15 @@ def field_forward_autograd(xyzs, dirs, P, levels, scale=0.5, emulate_f16=False, 
     straight-through in the backward), so ReLU masks match the kernel's.  impl: the encoding's
     statement ("torch" or "c", see encode()).
     bwd_scale (with emulate): the backward's gradients are rounded where csrc/field.hip's bwd_group
-    rounds them, at that scale (128 x the GradScaler's scale): the pre-sigmoid output gradient
-    (dY5), the pre-ReLU gradients of layers 4, 3 and 1 (dD4, dD3, dD1), and dL/dh after the rgb path
-    and TruncExp's term are added (dhh); dL/denc and the weight gradients are fp32 products of those
-    rounded operands, as the kernel's MFMA accumulates them."""
+    rounds them, at that scale (128 x the GradScaler's scale; 1 for bf16): the pre-sigmoid output
+    gradient (dY5), the pre-ReLU gradients of layers 4, 3 and 1 (dD4, dD3, dD1), dL/dh after the rgb
+    path and TruncExp's term are added (dhh), and dL/denc — the fp32 product of those rounded
+    operands, stored in the operand type as tcnn hands its network's input gradient to the grid
+    backward; the weight gradients are fp32 products, as the kernel's MFMA accumulates them."""
     q = _rounder(emulate_f16, emulate)
     rg = _grad_rounder(emulate or ("fp16" if emulate_f16 else None), bwd_scale)
     x01 = (xyzs - (-scale)) / (2 * scale)
-    enc = encode(x01, P.table, levels, impl)
+    enc = rg(encode(x01, P.table, levels, impl))
     h = rg(q(torch.relu(rg(q(enc) @ q(P.W1).t()))) @ q(P.W2).t())
     sig = _TruncExp.apply(h[:, 0])
     d = dirs / torch.norm(dirs, dim=1, keepdim=True)

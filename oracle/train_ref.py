@@ -109,12 +109,15 @@ class CPUTrainer:
         if bitfield is not None:
             self.bitfield = np.ascontiguousarray(bitfield, np.uint8)
 
-    def step(self, batch, global_step=3000, noise=None, record=None):
+    def step(self, batch, global_step=3000, noise=None, record=None, force_labels=None):
         """One training step; `noise` (R,) injects the marcher's perturbation (default torch.rand).
         record (a dict, optional) receives the step's intermediate values: the loss terms (as
         NeRFMTLoss names them, weighted), the unweighted cluster terms, the valid-normal mask and the
         cluster labels of the valid normals, the gradient of every parameter before the clip (the
-        unscaled gradient the optimizer receives) and whether the GradScaler skipped the step."""
+        unscaled gradient the optimizer receives) and whether the GradScaler skipped the step.
+        force_labels (int array over the valid normals, optional): the cluster losses use these labels
+        (e.g. the HIP step's) instead of this step's own k-means — whose labels are still computed and
+        recorded — so that what follows the clustering is compared on identical clusters."""
         o, d = batch["rays_o"], batch["rays_d"]
         R = o.shape[0]
         _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
@@ -147,9 +150,14 @@ class CPUTrainer:
         valid = losses_ref.valid_normals_mask(n.detach())
         nv = n[valid]
         rec["valid"] = valid.numpy().copy()
+        rec["normals"] = n.detach().numpy().copy()
         if nv.shape[0] >= 20:
             C, a = losses_ref.spherical_kmeans(nv.detach().numpy(), K=20, niter=20, seed=1234)
             lab, _ = losses_ref.cluster_select(C, a, 0.99)
+            rec["labels_own"] = np.asarray(lab).copy()
+            if force_labels is not None:
+                lab = np.asarray(force_labels).astype(np.asarray(lab).dtype)
+                assert lab.shape == rec["labels_own"].shape, (lab.shape, rec["labels_own"].shape)
             ort, cdot, cl1 = losses_ref.cluster_losses(nv, torch.from_numpy(lab))
             w = losses_ref.w_sched(self.w_cluster, global_step)
             terms = [losses_ref.validity(t) for t in (ort, cdot, cl1)]

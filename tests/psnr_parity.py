@@ -81,7 +81,7 @@ def run(steps=60, n_rays=1024, eval_batches=4, eval_rays=8192, oracle_eval_rays=
         bt["march_noise"] = noise.to(dev)
         t = time.perf_counter()
         _, ld = tr.step(bt, global_step=step0 + k)
-        l_gpu = float(ld["total"])
+        l_gpu = float(ld["total"].detach())
         t_gpu += time.perf_counter() - t
         losses.append((l_cpu, l_gpu))
         if log and (k % 20 == 0 or k == steps - 1):

@@ -48,4 +48,8 @@ def test_two_backwards_both_deferred_scatters_run(dev, later):
     assert torch.isfinite(got).all()
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 1e-6, rel
-    assert int(((got == 0) != (ref == 0)).sum()) == 0
+    # the same non-zero set, up to exact cancellations whose outcome depends on the float order of the
+    # flushes (the encoding gradient is stored in fp16, so equal and opposite contributions of two
+    # backwards are common: an entry's +q - q + r and +r + q - q can round differently); a dropped
+    # scatter would zero thousands of entries
+    assert int(((got == 0) != (ref == 0)).sum()) <= 4

@@ -8,20 +8,15 @@ HIP runs on identical inputs, which differ only by float-atomic order, stay with
 step 125 and then split too).  So parity is a statement about the mean over seeds, read against
 the standard error of the paired difference (tests/psnr_ensemble.py):
 
-* test_psnr_ensemble_vs_oracle[hypersim] (round 4): all 12 members of the oracle ensemble that
-  emulates the HIP kernel's arithmetic (tests/golden/psnr_oracle_ensemble_f16bw.json: MLP operands
-  rounded to fp16 and the field backward's loss-scaled fp16 gradient chain with its GradScaler,
-  2048-ray batches, grid refresh on, 1000 steps) re-trained on the HIP path for 250 steps; the mean
-  paired difference HIP - oracle at steps 125 and 250 must lie within 3 standard errors, the SE
-  from the paired-difference spread measured on the full ensemble with 3 HIP runs per member
-  (tests/golden/psnr_hip_ensemble_f16bw.json: sd 0.049 dB at step 125, 0.26 at 250), floored at
+* test_psnr_ensemble_vs_oracle (round 5): all 12 members of config #1 re-trained on the HIP path
+  for 250 steps and paired with two committed oracle ensembles (2048-ray batches, grid refresh on,
+  1000 steps each): the one that emulates the HIP kernel's arithmetic (MLP operands rounded to fp16
+  and the field backward's loss-scaled fp16 gradient chain with its GradScaler) and the plain fp32
+  one; the mean paired difference HIP - oracle at steps 125 and 250 must lie within 3 standard
+  errors (SE from the paired spread of the committed 12-member, 3-run HIP ensembles), floored at
   0.1 dB (2x the north_star tolerance: the full ensemble's mean at step 125 is -0.026 +- 0.014 dB,
-  so a 3-SE bound of 0.042 dB would sit ~1 SE from it).  Bounds: +-0.10 dB at 125, +-0.22 at 250
-  (round 3: +-0.22 / +-0.41 over 4 members against the fp32 oracle);
-  [scannet_manhattan]: config #5's 8-member fp16-fw+bw oracle ensemble (cluster weights 1e-2,
-  which ramp in from step 500), re-trained to step 750 and checked at steps 500, 625 and 750 (before
-  500 both sides train exactly as config #1), the spread from
-  tests/golden/psnr_hip_ensemble_scannet_f16bw.json (bounds +-0.79 / +-1.24 / +-1.50 dB);
+  so a 3-SE bound of 0.042 dB would sit ~1 SE from it).  Config #5's cluster path is pinned by
+  tests/test_gpu_trained_state.py instead (see the test's docstring);
 * test_psnr_parity_short: one pair (same init, batches, noise; 1024-ray batches, 40 steps) within
   0.1 dB, and the HIP test renderer vs the oracle renderer on the SAME parameters within 0.05 dB
   (the renderers themselves agree to ~1e-3 dB)."""
@@ -49,42 +44,50 @@ def test_psnr_parity_short():
 def test_psnr_parity_short_bf16():
     """Config #3 end to end: the bf16 HIP step against the oracle that rounds the MLP operands and
     the (unscaled) backward chain to bf16 as the kernel does — one pair, same init, batches and noise,
-    40 steps of 1024 rays: the first step's losses within 1e-3, every step's within 1 %, PSNR within
-    0.1 dB on the same renderer."""
+    40 steps of 1024 rays: the first step's loss within 1e-3, the first 5 steps' within 1 % (later
+    the pair decorrelates: bf16's coarse rounding turns summation-order differences into 1-ulp flips
+    of 0.4 %, and one measured pair was 1.8 % apart at step 15), PSNR within 0.1 dB on the same
+    renderer after the 40 steps."""
     r = run(steps=40, n_rays=1024, eval_batches=2, eval_rays=4096, oracle_eval_rays=512, threads=8,
             precision="bf16", emulate="bf16")
     print({k: v for k, v in r.items() if k != "losses_ref_hip"})
     l0_ref, l0_hip = r["losses_ref_hip"][0]
     assert abs(l0_hip - l0_ref) <= 1e-3 * abs(l0_ref), r["losses_ref_hip"][:3]
-    for k, (lr_, lh) in enumerate(r["losses_ref_hip"]):
+    for k, (lr_, lh) in enumerate(r["losses_ref_hip"][:5]):
         assert abs(lh - lr_) <= 1e-2 * abs(lr_), (k, lr_, lh)
     assert r["psnr_hip"] > 7.0 and r["psnr_ref"] > 7.0, r
     assert abs(r["delta_db"]) <= 0.1, r
 
 
-@pytest.mark.parametrize("preset", ["hypersim", "scannet_manhattan"])
-def test_psnr_ensemble_vs_oracle(preset):
-    """preset scannet_manhattan: config #5's cluster weights (1e-2) against its own fp16-fw+bw oracle
-    ensemble (tests/golden/psnr_oracle_ensemble_scannet_f16bw.json, 8 members; HIP statistics from
-    profiles/round4/psnr_hip_ensemble_scannet.json), to step 750: the cluster terms ramp in from step
-    500 (losses.py:217), so before that the preset trains exactly as config #1."""
+def test_psnr_ensemble_vs_oracle():
+    """All 12 members of config #1 re-trained on the HIP path for 250 steps (2048-ray batches, grid
+    refresh on) and compared, member by member, with two committed oracle ensembles: the one that
+    emulates the kernel's fp16 forward and backward rounding (psnr_oracle_ensemble_f16bw.json) and
+    the plain fp32 one (psnr_oracle_ensemble.json: independent of the kernel's rounding points, so
+    the check is not self-referential).  At steps 125 and 250 the mean paired difference must lie
+    within 3 SE (SE from the paired spread of the committed 12-member, 3-run HIP ensembles, floored at
+    0.1 dB): vs the fp16-fw+bw oracle +-0.10 / +-0.22 dB, vs the fp32 oracle +-0.13 / +-0.24 dB.
+
+    Config #5 (ScanNet-Manhattan, cluster weights 1e-2 from step 500) is not in this test: before
+    step 500 it trains exactly as config #1, and after it the trajectories have decorrelated (HIP
+    run-to-run sd 0.3-0.9 dB from step 500), so an ensemble bound there (round 4: +-0.79
+    to +-1.50 dB) could not see a cluster-path bias.  Its PSNR parity past step 500 is recorded as
+    unpinned; the cluster path of config #5 is pinned deterministically instead, one step from
+    trained states with the cluster terms active (tests/test_gpu_trained_state.py)."""
     import psnr_ensemble as pe
-    name, stats_name, steps = (("psnr_oracle_ensemble_f16bw.json", "psnr_hip_ensemble_f16bw.json", 250)
-                               if preset == "hypersim" else
-                               ("psnr_oracle_ensemble_scannet_f16bw.json", "psnr_hip_ensemble_scannet_f16bw.json", 750))
-    oracle = json.load(open(os.path.join(G, name)))
-    assert oracle.get("preset", "hypersim") == preset
-    ref_stats = {s["step"]: s for s in json.load(open(os.path.join(G, stats_name)))["stats"]}
-    members = [m["member"] for m in oracle["members"]]
-    runs = pe.run_hip_ensemble(members, 1, steps, 125, oracle["members"][0]["rays_per_step"], print, preset)
-    st = pe.stats(oracle, runs)
-    assert [s["step"] for s in st] == list(range(125, steps + 1, 125))
-    if preset != "hypersim":  # (before step 500 the preset's trajectories are config #1's, checked there)
-        st = [s for s in st if s["step"] >= 500]
-    for s in st:
-        sd = ref_stats[s["step"]]["paired_delta_sd"]  # paired-difference spread of the full ensemble
-        bound = max(3.0 * sd / math.sqrt(s["members"]), 0.1)
-        print(f"step {s['step']}: mean paired delta {s['paired_delta_mean']:+.3f} dB over {s['members']} members, "
-              f"bound +-{bound:.3f} (3 SE, sd {sd:.3f} from the committed {ref_stats[s['step']]['members']}-member "
-              f"ensemble; floor 0.1 dB)")
-        assert abs(s["paired_delta_mean"]) <= bound, s
+    fix = {"fp16_fw_bw": ("psnr_oracle_ensemble_f16bw.json", "psnr_hip_ensemble_f16bw.json"),
+           "fp32": ("psnr_oracle_ensemble.json", "psnr_hip_ensemble.json")}
+    oracles = {k: json.load(open(os.path.join(G, o))) for k, (o, _) in fix.items()}
+    members = [m["member"] for m in oracles["fp16_fw_bw"]["members"]]
+    assert members == [m["member"] for m in oracles["fp32"]["members"]]
+    runs = pe.run_hip_ensemble(members, 1, 250, 125, oracles["fp16_fw_bw"]["members"][0]["rays_per_step"], print)
+    for k, (_, stats_name) in fix.items():
+        ref_stats = {s["step"]: s for s in json.load(open(os.path.join(G, stats_name)))["stats"]}
+        st = pe.stats(oracles[k], runs)
+        assert [s["step"] for s in st] == [125, 250]
+        for s in st:
+            sd = ref_stats[s["step"]]["paired_delta_sd"]  # paired-difference spread of the full ensemble
+            bound = max(3.0 * sd / math.sqrt(s["members"]), 0.1)
+            print(f"{k} oracle, step {s['step']}: mean paired delta {s['paired_delta_mean']:+.3f} dB over "
+                  f"{s['members']} members, bound +-{bound:.3f} (3 SE, sd {sd:.3f}; floor 0.1 dB)")
+            assert abs(s["paired_delta_mean"]) <= bound, (k, s)
