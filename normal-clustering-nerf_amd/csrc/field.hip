@@ -1019,9 +1019,13 @@ constexpr int SC_BATCH = 2;  // corners per batch of set reads in sc_add (2: 232
 // Samples per lane of a fine-level unit (unit = 1024 x C samples): 4 (4096-sample units, in grabs of
 // 64 x 2) up to level 14; level 15 takes 2 (its ~1 distinct entry per sample would overfill the
 // 4-way sets of a 4096-sample unit; units of 2048 from level 13: 198, 14: 202, 15: 190, none: 202 us).
-// (Measured round 5: 8192-sample units on levels 10-11 / 10-12: 288 / 281 us against 202.)
+// (Measured round 5: 8192-sample units on levels 10-11 / 10-12: 288 / 281 us against 202; two
+// 512-thread workgroups per CU with half the table each: slower.)
 __host__ __device__ constexpr int sc_fine_c(int l) { return l < 15 ? 4 : 2; }
-constexpr int SC_C_CELL = 4;     // samples per lane per round on the cell levels
+#ifndef NCN_SC_C_CELL
+#define NCN_SC_C_CELL 4
+#endif
+constexpr int SC_C_CELL = NCN_SC_C_CELL;     // samples per lane per round on the cell levels
 
 __device__ __forceinline__ uint32_t sc_set(uint32_t e, uint32_t sets) { return __umulhi(e * 0x9E3779B1u, sets); }
 
@@ -1416,35 +1420,35 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
     }
 }
 
-// A lane's C consecutive samples: consecutive samples in the same cell are summed in registers and
-// a finished run goes to sc_add_cell (called by the whole wave when some lane has one).
-template <int C>
-__device__ __forceinline__ void sc_cells(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
-                                         float* __restrict__ grad) {
+// A lane's run of consecutive samples in one cell of a coarse level: the 8 corners' weighted sums
+// in registers, carried over the lane's chunks of a unit; a finished run goes to sc_add_cell (called
+// by the whole wave when some lane has one).
+struct ScRun {
+    uint32_t px, py, pz;
+    bool any, init;
     float v[16];
+};
+template <int C>
+__device__ __forceinline__ void sc_cells_run(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
+                                             float* __restrict__ grad, ScRun& st, bool last) {
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = 0.f;
-    LevelPos p = level_pos(L.scale, ch.x[0], ch.y[0], ch.z[0]);
-    bool any = ch.g[0].x != 0.f || ch.g[0].y != 0.f;
-    sc_corner_sums(p, ch.g[0], v);
+    for (int i = 0; i < C; i++) {
+        const LevelPos q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
+        const bool change = st.init && (q.px != st.px || q.py != st.py || q.pz != st.pz);
+        if (__ballot(change && st.any))  // uniform
+            sc_add_cell(sh, lane, change && st.any, st.px, st.py, st.pz, st.v, L, grad);
+        if (change || !st.init) {
 #pragma unroll
-    for (int i = 1; i <= C; i++) {
-        LevelPos q = p;
-        bool emit = true;
-        if (i < C) {
-            q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
-            emit = q.px != p.px || q.py != p.py || q.pz != p.pz;
+            for (int j = 0; j < 16; j++) st.v[j] = 0.f;
+            st.any = false;
+            st.px = q.px; st.py = q.py; st.pz = q.pz;
+            st.init = true;
         }
-        if (__ballot(emit && any))  // uniform
-            sc_add_cell(sh, lane, emit && any, p.px, p.py, p.pz, v, L, grad);
-        if (i < C) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = emit ? 0.f : v[j];
-            any = (emit ? false : any) || ch.g[i].x != 0.f || ch.g[i].y != 0.f;
-            sc_corner_sums(q, ch.g[i], v);
-        }
-        p = q;
+        st.any = st.any || ch.g[i].x != 0.f || ch.g[i].y != 0.f;
+        sc_corner_sums(q, ch.g[i], st.v);
     }
+    if (last && __ballot(st.any))  // uniform: the unit's last run
+        sc_add_cell(sh, lane, st.any, st.px, st.py, st.pz, st.v, L, grad);
 }
 
 // Flush of a cell unit: 16 lanes per claimed cell (one corner component each), form the corner's
@@ -1563,10 +1567,20 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     SC_TADD(4, t3, t4);
 }
 
-// Cell units: `rounds` consecutive chunks of 1024 x C samples per unit (no barrier between them),
-// then one flush.  Rounds per level: coarse levels have few cells, so longer units mean fewer
-// flushes and barriers.
-__host__ __device__ constexpr int sc_cell_rounds(int l) { return l < 6 ? 4 : l < 10 ? 2 : 1; }
+// Cell units: 1024 x C x `rounds` consecutive samples, then one flush.  Lane t of wave w takes the
+// unit's (t * SC_WAVES + w)-th slice of C x rounds consecutive samples (neighbouring slices in
+// different waves), a chunk of C per round, and carries its current run over the rounds, so a run
+// ends only where the samples leave the cell.  Rounds per level: coarse levels have few cells, so
+// longer units mean fewer flushes and barriers.  (Round 5: carried runs with the next chunk loaded
+// at the top of the round, no prefetch: levels 0-9 95 -> 75 us, all levels 201 -> 192 us; with the
+// prefetch the carried state spilled 18 VGPRs: 199 us.)
+#ifndef NCN_SC_R_LO
+#define NCN_SC_R_LO 8
+#endif
+#ifndef NCN_SC_R_MID
+#define NCN_SC_R_MID 4
+#endif
+__host__ __device__ constexpr int sc_cell_rounds(int l) { return l < 6 ? NCN_SC_R_LO : l < 10 ? NCN_SC_R_MID : 1; }
 // samples of one unit of level l
 __host__ __device__ constexpr int64_t sc_unit_span(int l) {
     return (int64_t)SC_THREADS * (l < SC_CELL_HI ? SC_C_CELL * sc_cell_rounds(l) : sc_fine_c(l));
@@ -1579,20 +1593,17 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
                                              const int32_t* __restrict__ order) {
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
     const ScLevel L = sc_level(Lt, l, m, 61 - lg_unit);
-    // lane t of wave w takes chunk t * SC_WAVES + w of each round (neighbouring chunks in different
-    // waves); round r covers the unit's r-th slice of SC_THREADS * C samples
-    const int64_t lane_off = ((int64_t)lane * SC_WAVES + wid) * C;
-    ScChunk<C> ch;
-    sc_load_chunk<C>(ch, s0 + lane_off, s1, xyzs, dEl, de, nrm, order);
+    const int64_t lane_off = ((int64_t)lane * SC_WAVES + wid) * rounds * C;
+    ScRun st;
+    st.init = st.any = false;
+    st.px = st.py = st.pz = 0;
     for (int r = 0; r < rounds; r++) {
-        ScChunk<C> nx;
-        const bool more = r + 1 < rounds;
-        if (more) sc_load_chunk<C>(nx, s0 + (int64_t)(r + 1) * SC_THREADS * C + lane_off, s1, xyzs, dEl, de, nrm, order);
+        ScChunk<C> ch;
+        sc_load_chunk<C>(ch, s0 + lane_off + (int64_t)r * C, s1, xyzs, dEl, de, nrm, order);
         if (L.direct)
             sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
         else
-            sc_cells<C>(sh, lane, ch, L, grad);
-        if (more) ch = nx;
+            sc_cells_run<C>(sh, lane, ch, L, grad, st, r + 1 == rounds);
     }
     lds_barrier();
     sc_flush_cells(sh, L, grad);
@@ -1646,7 +1657,7 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
         sc_unit<4>(sh, wid, lane, l, s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
 }
 
-__global__ __launch_bounds__(SC_THREADS) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
+__global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
                                                                    const float* __restrict__ dE_ws,
@@ -1903,7 +1914,7 @@ int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, 
     NCN_REQUIRE(!slab || grad_w, hipErrorInvalidValue, "ncn_field_scatter_wgrad: grad_w required with a slab");
     const LevelTable Lt = make_table(levels);
     int grid = scatter_grid(n);
-    if (max_blocks > 0) grid = std::min(grid, max_blocks);
+    if (max_blocks > 0) grid = std::min(grid, max_blocks * (1024 / SC_THREADS));  // (max_blocks: CUs)
     hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
                        xyz_min, xyz_extent, dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
                        level_lo, level_hi, order, slab, n_blocks_sigma, n_blocks_rgb, grad_w);

@@ -173,6 +173,7 @@ class SplitStep:
         mlp_part(2, dsig, None)
         m._scatter(xyzs, n, n_dev, order, dE_ws, lmax, g_table, wgrad=(slab, nb[1], nb[0], g_w))
         L.last_cluster = (labels, cents, out)
+        L.last_normals = normals
         results = {"rays_a": rays_a, "deltas": deltas, "ts": ts, "rm_samples": n_dev, "vr_samples": cnt,
                    "opacity": opacity, "depth": depth, "ws": ws, "rgb": rgb, "rays_d": rays_d, "rays_o": rays_d,
                    "total_samples": total_s}

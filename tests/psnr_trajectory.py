@@ -116,7 +116,7 @@ def run_ref(steps, every, threads, log, out=None, member=None, n_rays=N_RAYS, im
             curve.append({"step": k + 1, "psnr": _psnr(se, n), "loss": loss, "samples": S,
                           "occupied_frac": float(np.unpackbits(cpu.bitfield).mean()), "t_s": round(time.time() - t0, 1)})
             log(json.dumps(curve[-1]))
-            res = {"side": "oracle CPU (fp32)", "steps": k + 1, "rays_per_step": n_rays, "gt": GT,
+            res = {"side": "oracle CPU", "steps": k + 1, "rays_per_step": n_rays, "gt": GT,
                    "member": member, "init_seed": init_seed(member), "encode_impl": impl, "emulate": emulate,
                    "emulate_bwd": emulate_bwd, "grid_sampling": sampling, "amp_scale": cpu.amp_S,
                    "amp_skips": cpu.amp_skips, "preset": preset, "eval_rays": N_RAYS * len(EVAL_SEEDS), "cpu_threads": threads,
@@ -197,6 +197,7 @@ def run_hip(steps, every, log, cross_check=False, member=None, n_rays=N_RAYS, tr
 
 
 def main():
+    global GT
     ap = argparse.ArgumentParser()
     ap.add_argument("side", choices=("ref", "hip"))
     ap.add_argument("--steps", type=int, default=3000)
@@ -217,9 +218,12 @@ def main():
                          "fp16 chain (with the GradScaler)")
     ap.add_argument("--sampling", default="device", choices=("device", "reference"),
                     help="(ref) the grid refresh's cell sampling: the device's (deviation 7) or the reference's draws")
+    ap.add_argument("--gt", default="surface_bright",
+                    help="target variant (ncnerf_amd.synthetic SyntheticScene.batch gt=...)")
     ap.add_argument("--cross-check", action="store_true",
                     help="(hip) also render the HIP parameters with the train-path renderer and the oracle's")
     a = ap.parse_args()
+    GT = a.gt
     log = lambda s: print(s, flush=True)  # noqa: E731
     if a.side == "ref":
         res = run_ref(a.steps, a.every, a.threads, log, a.out, member=a.member, n_rays=a.rays, impl=a.impl,

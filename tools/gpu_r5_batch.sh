@@ -16,6 +16,7 @@ for s in $STEPS; do
              --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu ${NEW_TESTS:-tests/test_gpu_trained_state.py} \
              > gpurun_out/new_tests_$TAG.log 2>&1; rc=$?; [ $rc -le 1 ] || exit $rc ;;  # (test failures: go on)
     plateau) timeout -k 10 600 python -u tools/plateau_probe.py > gpurun_out/plateau_$TAG.log 2>&1 || exit $? ;;
+    profile) bash tools/profile_round5.sh || exit $? ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $? ;;
   esac
 done
