@@ -1,7 +1,9 @@
 """Diagnostic (CPU): how many global flushes the table scatter's units make per distinct table entry
 under different sample processing orders, on one marched 8192-ray bench batch (oracle marcher)."""
 import sys, numpy as np, torch
-sys.path[:0]=['/root/repo','/root/repo/normal-clustering-nerf_amd']
+import os
+ROOT=os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0]=[ROOT,os.path.join(ROOT,'normal-clustering-nerf_amd')]
 from oracle import vren_ref, field_ref
 from ncnerf_amd.synthetic import SyntheticScene, morton3d_np
 scene=SyntheticScene(); b=scene.batch(8192, seed=1)

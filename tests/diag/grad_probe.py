@@ -4,7 +4,7 @@ warm-up refresh): relative L2 per block, zero patterns and sign agreement of the
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT, os.path.join(ROOT, "tests")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

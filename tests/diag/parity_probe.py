@@ -1,12 +1,12 @@
 """Diagnostic: the oracle CPU trainer and the HIP trainer side by side on identical inputs (the
 psnr_trajectory setup) for a few steps: per-step loss, marched samples, and the occupancy after
-each grid refresh.  python tools/parity_probe.py --steps 64 [--no-refresh] [--rays 8192]"""
+each grid refresh.  python tests/diag/parity_probe.py --steps 64 [--no-refresh] [--rays 8192]"""
 import argparse
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "normal-clustering-nerf_amd"), ROOT, os.path.join(ROOT, "tests")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -6,7 +6,7 @@ comparison) and plain fp32 — and prints the per-block gradient rel-L2 of the t
 field forward on the same samples (sigmas / rgbs, HIP vs the emulating oracle).  If HIP vs the
 emulating oracle is far below fp16-vs-fp32, the emulation pins the rounding; if the two are of the
 same size the state's gradient is dominated by fp16 rounding noise that two correct statements
-need not share.  Usage (GPU box): python tools/trained_state_debug.py [steps...]"""
+need not share.  Usage (GPU box): python tests/diag/trained_state_debug.py [steps...]"""
 import json
 import os
 import sys
@@ -14,7 +14,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "normal-clustering-nerf_amd"), os.path.join(ROOT, "tests")]
 
 import test_gpu_trained_state as T  # noqa: E402
