@@ -384,13 +384,15 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_windows_kernel(const float*
 
 // ---------------------------------------------------------------------------------------------
 // Forward: grid-stride over 16-sample groups, one group per wave per step.
-// (Measured: the field forward at 4 waves/SIMD (amdgpu_waves_per_eu) 101.1 us vs the compiler's
-// choice 101.5, 5 and 6 waves/SIMD spill (124.6 / 147.7 us) — it is not occupancy-bound.)
+// (Round 3 measured 4 waves/SIMD at 101 us and spills at 5-6; round 5 took the register pressure
+// out of the encoding instead — two levels' gathers in flight, below — and at 72 VGPRs the kernel
+// runs 7 waves/SIMD: 84 us.  The waves_per_eu hint keeps the allocation in that range: without it
+// the compiler's choice left 5 waves.)
 // DENSITY: the grid refresh's mode 2 (encodings from encode_xcd_kernel's scratch, sigma only) as its
 // own instantiation — the training forward's loop then carries no trace of it (with the scratch read
 // inside the shared loop the training kernel took 136 registers, 3 waves/SIMD, and ran ~10 % slower).
 template <typename T, bool DENSITY>
-__global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                         int64_t n, const int32_t* __restrict__ n_dev,
                                                         const float2* __restrict__ table, LevelTable Lt,
                                                         float xyz_min, float xyz_extent,
@@ -435,6 +437,13 @@ __global__ __launch_bounds__(256) void field_fwd_kernel(const float* __restrict_
             }
             const float2 e00 = encode_level(table, L, 2 * g, x, y, z);
             const float2 e01 = encode_level(table, L, 2 * g + 1, x, y, z);
+            // The last two levels' positions wait for the first two's results (an empty asm that
+            // reads them), so only two levels' 16 gathers are in flight per lane, not all 32: the
+            // kernel then needs 72 VGPRs instead of 120 and runs 7 waves per SIMD instead of 4 —
+            // 100 -> 84 us on the bench batch (round 5, tools/field_probe.py; one level at a time:
+            // 85; the pairs of an x-edge as one 16-B load: 90-98, the cache-line count does not
+            // bound it; buffer loads: 90).
+            asm volatile("; encode: levels 8+ after 0-7 %1 %2" : "+v"(x) : "v"(e00.x), "v"(e01.x));
             const float2 e10 = encode_level(table, L, 8 + 2 * g, x, y, z);
             const float2 e11 = encode_level(table, L, 9 + 2 * g, x, y, z);
             e = v8{(T)e00.x, (T)e00.y, (T)e01.x, (T)e01.y, (T)e10.x, (T)e10.y, (T)e11.x, (T)e11.y};

@@ -281,9 +281,12 @@ def w_sched(w, step, start=500, grow=2500):
     return max(0, min(w, (step - start) * (w / grow)))
 
 
-def cluster_losses(normals, labels):
+def cluster_losses(normals, labels, signs=None):
     """losses.py:441-478 (ort / centr_dot / centr_L1 terms), torch, differentiable w.r.t. normals.
-    `normals` are the VALID normals (after losses.py:427-430); `labels` from cluster_select."""
+    `normals` are the VALID normals (after losses.py:427-430); `labels` from cluster_select.
+    signs (optional, test infrastructure): the branches of the terms' absolute values taken from
+    another evaluation (kink_signs of it) — |v| is evaluated as s * v with s fixed, the same value
+    wherever the two agree on the sign, and the gradient of the given branch; see kink_signs."""
     labels = torch.as_tensor(labels)
     keep = labels != 0
     x = normals[keep]
@@ -293,10 +296,39 @@ def cluster_losses(normals, labels):
     lab = lab.abs()
     cl = [x[lab == k] for k in (1, 2, 3)]
     c = [F.normalize(ck.mean(dim=0, keepdim=True), p=2.0, dim=-1) for ck in cl]
-    ort = (torch.abs((c[0] * c[1]).sum()) + torch.abs((c[0] * c[2]).sum()) + torch.abs((c[1] * c[2]).sum())) / 3.0
+    dots = [(c[0] * c[1]).sum(), (c[0] * c[2]).sum(), (c[1] * c[2]).sum()]
+    if signs is None:
+        ort = (torch.abs(dots[0]) + torch.abs(dots[1]) + torch.abs(dots[2])) / 3.0
+        cl1 = sum(torch.abs(cl[k] - c[k]).sum(dim=-1).mean() for k in range(3)) / 3.0
+    else:
+        s_ort, s_l1 = signs
+        ort = sum(float(s_ort[i]) * dots[i] for i in range(3)) / 3.0
+        cl1 = sum(((cl[k] - c[k]) * torch.as_tensor(s_l1[k], dtype=x.dtype)).sum(dim=-1).mean() for k in range(3)) / 3.0
     cdot = sum(1.0 - (cl[k] * c[k]).sum(dim=-1).mean() for k in range(3)) / 3.0
-    cl1 = sum(torch.abs(cl[k] - c[k]).sum(dim=-1).mean() for k in range(3)) / 3.0
     return ort, cdot, cl1
+
+
+def kink_signs(normals, labels):
+    """The sign branches cluster_losses' absolute values take on these VALID normals and labels:
+    (signs of the three centroid dot products, per selected cluster the signs of (normal - centroid)
+    per component), float64.  The ort and L1 terms are |.| of quantities that training drives to ~0
+    (orthogonal Manhattan centroids, normals on their centroid), so at a trained state two correct
+    evaluations whose normals differ by ~5e-4 rad take opposite branches for many of them, and the
+    gradient flips there while the loss does not move: test infrastructure shares the branches as it
+    shares the labels."""
+    n = np.asarray(normals, np.float64)
+    lab = np.asarray(labels)
+    keep = lab != 0
+    x = n[keep] * np.where(lab[keep] < 0, -1.0, 1.0)[:, None]
+    la = np.abs(lab[keep])
+    cl = [x[la == k] for k in (1, 2, 3)]
+    c = []
+    for ck in cl:
+        m = ck.mean(axis=0)
+        c.append(m / max(np.linalg.norm(m), 1e-12))
+    s_ort = np.sign([c[0] @ c[1], c[0] @ c[2], c[1] @ c[2]])
+    s_l1 = [np.sign(cl[k] - c[k]) for k in range(3)]
+    return s_ort, s_l1
 
 
 def validity(loss):

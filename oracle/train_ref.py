@@ -109,7 +109,7 @@ class CPUTrainer:
         if bitfield is not None:
             self.bitfield = np.ascontiguousarray(bitfield, np.uint8)
 
-    def step(self, batch, global_step=3000, noise=None, record=None, force_labels=None):
+    def step(self, batch, global_step=3000, noise=None, record=None, force_labels=None, force_signs=None):
         """One training step; `noise` (R,) injects the marcher's perturbation (default torch.rand).
         record (a dict, optional) receives the step's intermediate values: the loss terms (as
         NeRFMTLoss names them, weighted), the unweighted cluster terms, the valid-normal mask and the
@@ -117,7 +117,10 @@ class CPUTrainer:
         unscaled gradient the optimizer receives) and whether the GradScaler skipped the step.
         force_labels (int array over the valid normals, optional): the cluster losses use these labels
         (e.g. the HIP step's) instead of this step's own k-means — whose labels are still computed and
-        recorded — so that what follows the clustering is compared on identical clusters."""
+        recorded — so that what follows the clustering is compared on identical clusters.
+        force_signs (optional, with force_labels): the branches of the cluster terms' absolute values
+        (losses_ref.kink_signs of the other side's normals); the record then counts how many of this
+        step's own branches differ from them (`sign_mismatch`)."""
         o, d = batch["rays_o"], batch["rays_d"]
         R = o.shape[0]
         _, ht, _ = vren_ref.ray_aabb_intersect(o, d, np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), 1)
@@ -158,7 +161,12 @@ class CPUTrainer:
             if force_labels is not None:
                 lab = np.asarray(force_labels).astype(np.asarray(lab).dtype)
                 assert lab.shape == rec["labels_own"].shape, (lab.shape, rec["labels_own"].shape)
-            ort, cdot, cl1 = losses_ref.cluster_losses(nv, torch.from_numpy(lab))
+            if force_signs is not None:
+                own = losses_ref.kink_signs(nv.detach().numpy(), lab)
+                rec["sign_mismatch"] = {"ort": int((own[0] != force_signs[0]).sum()),
+                                        "l1": int(sum((a != b).sum() for a, b in zip(own[1], force_signs[1]))),
+                                        "l1_total": int(sum(a.size for a in own[1]))}
+            ort, cdot, cl1 = losses_ref.cluster_losses(nv, torch.from_numpy(lab), signs=force_signs)
             w = losses_ref.w_sched(self.w_cluster, global_step)
             terms = [losses_ref.validity(t) for t in (ort, cdot, cl1)]
             rec.update(labels=np.asarray(lab).copy(), w_cluster=float(w),

@@ -1,12 +1,13 @@
 """Where does a trained-state one-step gradient difference come from?  (tests/test_gpu_trained_state.py)
 
-Trains the test's product run (hypersim, fp16) to the given steps, then from each snapshot runs the
-HIP eager step and the oracle step twice — emulating the kernel's fp16 rounding (the test's
-comparison) and plain fp32 — and prints the per-block gradient rel-L2 of the three pairs, plus the
+Trains the test's product run (PRESET, fp16) to the given steps, then from each snapshot runs the
+HIP eager step and the oracle step three times — emulating the kernel's fp16 rounding with the HIP
+step's labels and |.| branches (the test's comparison), the same in plain fp32, and emulating with
+the HIP labels but its own branches — and prints the per-block gradient rel-L2 of the pairs, plus the
 field forward on the same samples (sigmas / rgbs, HIP vs the emulating oracle).  If HIP vs the
 emulating oracle is far below fp16-vs-fp32, the emulation pins the rounding; if the two are of the
 same size the state's gradient is dominated by fp16 rounding noise that two correct statements
-need not share.  Usage (GPU box): python tests/diag/trained_state_debug.py [steps...]"""
+need not share.  Usage (GPU box): [PRESET=scannet_manhattan] python tests/diag/trained_state_debug.py [steps...]"""
 import json
 import os
 import sys
@@ -29,7 +30,7 @@ def _rel(a, b):
 def main():
     steps = tuple(int(s) for s in sys.argv[1:]) or (1000, 3000)
     dev = torch.device("cuda:0")
-    preset, precision = "hypersim", "fp16"
+    preset, precision = os.environ.get("PRESET", "hypersim"), "fp16"
     snaps = T.train_snapshots(preset, precision, dev, steps=steps)
     for step in steps:
         snap = snaps[step]
@@ -37,15 +38,19 @@ def main():
         batch = scene.batch(T.N_RAYS, seed=70_000 + step, gt="surface_bright")
         noise = torch.rand(T.N_RAYS, generator=torch.Generator().manual_seed(80_000 + step)).numpy()
         h = T._hip_step(preset, precision, snap, batch, noise, step, dev)
-        o16 = T._oracle_step(preset, precision, snap, batch, noise, step, force_labels=h["labels"])
-        o32 = T._oracle_step(preset, precision, snap, batch, noise, step, force_labels=h["labels"], emulate=False)
+        signs = T.losses_ref.kink_signs(h["normals"][h["valid"]], h["labels"])
+        kw = dict(force_labels=h["labels"], force_signs=signs)
+        o16 = T._oracle_step(preset, precision, snap, batch, noise, step, **kw)
+        o32 = T._oracle_step(preset, precision, snap, batch, noise, step, emulate=False, **kw)
+        o16n = T._oracle_step(preset, precision, snap, batch, noise, step, force_labels=h["labels"])
         n_table = h["levels"][-1][0] + h["levels"][-1][1]
         rec = {"step": step, "amp": None if snap["amp"] is None else [float(x) for x in snap["amp"]],
                "samples": [h["samples"], o16["samples"], o32["samples"]],
                "skipped": [h["skipped"], o16["skipped"], o32["skipped"]],
-               "loss_rgb": [h["rgb"], o16["rgb"], o32["rgb"]]}
+               "loss_rgb": [h["rgb"], o16["rgb"], o32["rgb"]], "preset": preset,
+               "kink_sign_mismatch": o16.get("sign_mismatch")}
         pairs = {"hip_vs_o16": (h["grad"], o16["grad"]), "hip_vs_o32": (h["grad"], o32["grad"]),
-                 "o16_vs_o32": (o16["grad"], o32["grad"])}
+                 "o16_vs_o32": (o16["grad"], o32["grad"]), "hip_vs_o16_own_branches": (h["grad"], o16n["grad"])}
         for name, (a, b) in pairs.items():
             rec[name] = {bn: round(_rel(a[sl], b[sl]), 6) for bn, sl in T._blocks(h["levels"], n_table)}
         # the field forward on the same samples (the marcher is bit-exact)
