@@ -499,7 +499,8 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
     typedef T t2 __attribute__((ext_vector_type(2)));
     // level-major scratch [16][n16] of T pairs: a workgroup's 256 points of one level are one
     // contiguous 1 KB store (a fragment-order layout scattered 4-byte pieces of 64-byte records over
-    // 16 workgroups on 8 XCDs: 179 vs 172 us for the pass)
+    // 16 workgroups on 8 XCDs: 179 vs 172 us for the pass; round 5: non-temporal point loads and
+    // scratch stores, to keep the streamed data from evicting the level's table in L2 — no change)
     ((t2*)enc)[(int64_t)l * n16 + s] = t2{(T)a.x, (T)a.y};
 }
 
