@@ -5,7 +5,7 @@ and refresh seeds).  Per checkpoint: the oracle and HIP means, the paired differ
 d_m = mean_r(HIP_m,r) - oracle_m with its standard error and 95 % interval (t, M - 1 dof), the
 member spread and the HIP run-to-run sd.
 
-Usage: python tools/plateau_compare.py HIP_LOG ORACLE_DIR [--json OUT]"""
+Usage: python tools/plateau_compare.py HIP_LOG[,HIP_LOG...] ORACLE_DIR [--json OUT]"""
 import glob
 import json
 import math
@@ -24,13 +24,14 @@ def main():
     hip_log, odir = sys.argv[1], sys.argv[2]
     out = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
     hip, gt, every = {}, None, None
-    for line in open(hip_log):
-        if not line.startswith("{"):
-            continue
-        r = json.loads(line)
-        if "member" in r and "psnr" in r:
-            hip[r["member"]] = r["psnr"]
-            gt = r["gt"]
+    for path in hip_log.split(","):  # (several logs: an ensemble extended by later runs)
+        for line in open(path):
+            if not line.startswith("{"):
+                continue
+            r = json.loads(line)
+            if "member" in r and "psnr" in r:
+                hip[r["member"]] = r["psnr"]
+                gt = r["gt"]
     orc = {}
     for f in sorted(glob.glob(os.path.join(odir, "member*.json"))):
         d = json.load(open(f))

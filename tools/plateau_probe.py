@@ -21,6 +21,7 @@ import psnr_trajectory as pt  # noqa: E402
 
 VARIANTS = os.environ.get("PLATEAU_GT", "surface_bright,surface_smooth,surface_flat").split(",")
 MEMBERS = int(os.environ.get("PLATEAU_MEMBERS", "4"))
+MEMBER0 = int(os.environ.get("PLATEAU_MEMBER0", "0"))  # first member index (extending an ensemble)
 STEPS = int(os.environ.get("PLATEAU_STEPS", "3000"))
 EVERY = int(os.environ.get("PLATEAU_EVERY", "250"))
 POOL = int(os.environ.get("PLATEAU_POOL", "0"))  # 0: fresh batches every step (drawn in parallel)
@@ -59,14 +60,14 @@ def main():
         import multiprocessing as mp
         with mp.get_context("spawn").Pool(PROCS) as pp:
             for gt in VARIANTS:
-                for m in range(MEMBERS):
+                for m in range(MEMBER0, MEMBER0 + MEMBERS):
                     seqs[gt, m] = pp.map(_draw, [(gt, k, m) for k in range(STEPS)], chunksize=32)
                     print(json.dumps({"drawn": gt, "member": m}), flush=True)
     out = {}
     for gt in VARIANTS:
         pt.GT = gt
         curves = {}
-        for m in range(MEMBERS):
+        for m in range(MEMBER0, MEMBER0 + MEMBERS):
             t0 = time.time()
             if POOL:
                 batches = Cycle([scene.batch(RAYS, seed=pt.batch_seed(k, m), gt=gt) for k in range(POOL)])
