@@ -54,7 +54,10 @@ def test_render_train_glue(name):
         np.testing.assert_allclose(np.linalg.norm(gt.astype(np.float64)), f["grad_table_norm64"], rtol=1e-4)
     else:
         np.testing.assert_allclose(np.linalg.norm(gt), f["grad_table_norm"], rtol=1e-4)
-    np.testing.assert_allclose(gt[f["grad_table_nz_idx"]], f["grad_table_nz"], rtol=1e-3, atol=1e-9)
+    # (atol: f32 summation-order noise of the table's index_add on entries whose contributions cancel —
+    # torch's CPU threads split the adds differently under load: 1.1e-9 observed once, on an entry of
+    # 2.7e-8 among gradients up to ~1e-3)
+    np.testing.assert_allclose(gt[f["grad_table_nz_idx"]], f["grad_table_nz"], rtol=1e-3, atol=5e-9)
     if "grad_table_nnz" in f:
         assert int((np.abs(gt).sum(1) > 0).sum()) == int(f["grad_table_nnz"])
 
