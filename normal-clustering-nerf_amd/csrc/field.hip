@@ -1727,6 +1727,10 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // cell -> fine: at most one layout switch.
     int layout = -1, par = 0;
     ScShared sh;
+    // (Round 5: alternating the stride's direction every round ("snake", LPT-like) 192-197 vs 188 us;
+    // rounds per coarse unit (levels 0-5 / 6-9): 8/4 188, 4/2 191, 8/8 182-187, 8/2 206, 4/4 199,
+    // 4/8 225-230, 2/8 210, 16/4 237, 8/16 317 — more than 256 coarse units, or a few very long
+    // ones, leave workgroups a second heavy unit.)
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x)
         sc_one_unit(u, n, level_lo, layout, par, sh, arena, fill, lmax_s, wid, lane, xyzs, dE, e_stride, de, nrm, Lt, grad,
                     order);
