@@ -1752,7 +1752,7 @@ static LevelTable make_table(const uint32_t* levels) {
 }
 
 
-constexpr int64_t NCN_FWD_MAX_BLOCKS = 4096;
+constexpr int64_t NCN_FWD_MAX_BLOCKS = 4096;  // (round 5: 1792 / 2048 / 8192 blocks measured the same, 84-85 us)
 static int fwd_grid(int64_t n) {
     const int64_t groups = (n + 15) / 16;
     const int64_t g = std::min<int64_t>(std::max<int64_t>((groups + 3) / 4, 1), NCN_FWD_MAX_BLOCKS);
