@@ -115,15 +115,20 @@ for name, L in libs:
     print(f"{name:16s} fwd {timeit(fwd, L):8.1f} us   bwd {timeit(bwd, L):8.1f} us   "
           f"fwd mode 1 ({pts.shape[0]} grid points) {timeit(fwd1, L):8.1f} us", flush=True)
     if hasattr(L, "ncn_diag_sc_times"):
-        buf = (ctypes.c_ulonglong * (256 * 8))()
+        # (NCN_DIAG_SC_TIMES: wave 0 of each workgroup, cycles summed over its fine-level units, in
+        # the odd slots of [256][10]: level setup, grabs (loads + set reads + claims + adds), its own
+        # LDS ops draining, the unit's closing barrier, the flush)
+        buf = (ctypes.c_ulonglong * (256 * 10))()
         L.ncn_diag_sc_times(buf, 1)
         assert bwd(L) == 0
         torch.cuda.synchronize()
         L.ncn_diag_sc_times(buf, 0)
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8).astype(np.float64)
-        names = ["load+max", "work", "barrier", "flush"]
-        print("   scatter cycles per WG (mean over WGs), run | direct:",
-              "  ".join(f"{nm} {a[:, 2 * i].mean():.0f}|{a[:, 2 * i + 1].mean():.0f}" for i, nm in enumerate(names)))
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 10).astype(np.float64)
+        names = ["setup", "grabs", "lds drain", "barrier", "flush"]
+        tot = sum(a[:, 2 * i + 1].mean() for i in range(5))
+        print("   scatter fine-level cycles per WG (wave 0, mean over WGs):",
+              "  ".join(f"{nm} {a[:, 2 * i + 1].mean():.0f} ({a[:, 2 * i + 1].mean() / tot:.0%})"
+                        for i, nm in enumerate(names)))
     if hasattr(L, "ncn_diag_read_phases"):
         buf = (ctypes.c_ulonglong * 8)()
         L.ncn_diag_read_phases(buf)
