@@ -1520,31 +1520,27 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     // (a fine unit holds at most 4096 samples: 2^46 leaves the sums four bits of headroom below 2^62)
     const ScLevel L = sc_level(Lt, l, m, 46);
     SC_TNOW(t1);
-    if constexpr (C >= 4) {
-        // The unit's 1024 x C samples in grabs of 64 lanes x 2: grab k gives lane t the samples
-        // s0 + (t * NG + k) * 2 — the 64 lanes of one wave-instruction hold samples 2 * NG = 64
-        // positions apart, so they rarely address the same LDS slot at once (same-address LDS atomics
-        // serialise).  Wave w takes grab w first, then draws grabs from the unit's LDS counter after
-        // each grab's adds, so a wave slowed by claims / set-full fallbacks takes fewer grabs and the
-        // waves reach the unit's barrier together (191 vs 195 us static; drawing one grab ahead so
-        // that its loads overlap spills 9 VGPRs: 194).
-        constexpr int NG = SC_THREADS * C / 128;
-        int k = wid;
-        ScChunk<2> cg;
-        sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, de, nrm, order);
-        while (k < NG) {  // (wave-uniform)
-            sc_direct<2>(sh, lane, cg, L, grad);
-            int kn = 0;
-            if (lane == 0) kn = atomicAdd(sh.grab, 1);
-            kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
-            if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, de, nrm, order);
-            k = kn;
-        }
-    } else {
-        // chunk of lane t of wave w: t * SC_WAVES + w (lanes SC_WAVES * C positions apart)
-        ScChunk<C> ch;
-        sc_load_chunk<C>(ch, s0 + (int64_t)(lane * SC_WAVES + wid) * C, s1, xyzs, dEl, de, nrm, order);
-        sc_direct<C>(sh, lane, ch, L, grad);
+    // The unit's 1024 x C samples in grabs of 64 lanes x 2: grab k gives lane t the samples
+    // s0 + (t * NG + k) * 2 — the 64 lanes of one wave-instruction hold samples 2 * NG positions
+    // apart, so they rarely address the same LDS slot at once (same-address LDS atomics
+    // serialise).  Wave w takes grab w first, then draws grabs from the unit's LDS counter after
+    // each grab's adds, so a wave slowed by claims / set-full fallbacks takes fewer grabs and the
+    // waves reach the unit's barrier together (191 vs 195 us static; drawing one grab ahead so
+    // that its loads overlap spills 9 VGPRs: 194).  Round 5: level 15's 2048-sample units go through
+    // the same loop (16 grabs for 16 waves: the assignment of the former static 2-sample chunks; one
+    // code path, 186-188 vs 189-190 us in the probe); 1-sample grabs (finer balance, shorter runs) on
+    // levels 13-15 were no better.
+    constexpr int NG = SC_THREADS * C / 128;
+    int k = wid;
+    ScChunk<2> cg;
+    sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, de, nrm, order);
+    while (k < NG) {  // (wave-uniform)
+        sc_direct<2>(sh, lane, cg, L, grad);
+        int kn = 0;
+        if (lane == 0) kn = atomicAdd(sh.grab, 1);
+        kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
+        if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, de, nrm, order);
+        k = kn;
     }
     SC_TNOW(t2);
 #ifdef NCN_DIAG_SC_TIMES
