@@ -1510,9 +1510,9 @@ __device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m
     return L;
 }
 
-// One fine-level unit: the samples in grabs, then the flush of the claimed slots.
-template <int C>
-__device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1,
+// One fine-level unit of 1024 x C samples: the samples in grabs, then the flush of the claimed slots.
+// (C is a run-time value: one inlined copy of the grab loop serves every fine level.)
+__device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int C, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
                                         const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
                                         const int32_t* __restrict__ order) {
@@ -1530,7 +1530,7 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     // the same loop (16 grabs for 16 waves: the assignment of the former static 2-sample chunks; one
     // code path, 186-188 vs 189-190 us in the probe); 1-sample grabs (finer balance, shorter runs) on
     // levels 13-15 were no better.
-    constexpr int NG = SC_THREADS * C / 128;
+    const int NG = SC_THREADS * C / 128;
     int k = wid;
     ScChunk<2> cg;
     sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, de, nrm, order);
@@ -1658,10 +1658,8 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
     const uint32_t* dEl = dE + (int64_t)l * e_stride;
     if (mode == SC_MODE_CELL)
         sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order);
-    else if (sc_fine_c(l) == 2)
-        sc_unit<2>(sh, wid, lane, l, s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
     else
-        sc_unit<4>(sh, wid, lane, l, s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
+        sc_unit(sh, wid, lane, l, sc_fine_c(l), s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
 }
 
 __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
