@@ -1026,7 +1026,7 @@ constexpr int sc_max(int a, int b) { return a > b ? a : b; }
 constexpr int SC_ARENA = sc_max(SC_SETS_CELL * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2), SC_SETS_DIR * SC_WAYS * SC_SLOT_BYTES);
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
 constexpr int SC_BATCH = 2;  // corners per batch of set reads in sc_add (2: 232 us, 4: 238 us (spills), 8: 298 us;
-                             // round 5, at 124 VGPRs: 2: 188-190, 4: 196 us with 4 spills)
+                             // round 5: 4 at 124 VGPRs 196 us (4 spills); at 120, no spills: 194-195 vs 190)
 // Samples per lane of a fine-level unit (unit = 1024 x C samples): 4 (4096-sample units, in grabs of
 // 64 x 2) up to level 14; level 15 takes 2 (its ~1 distinct entry per sample would overfill the
 // 4-way sets of a 4096-sample unit; units of 2048 from level 13: 198, 14: 202, 15: 190, none: 202 us).
