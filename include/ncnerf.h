@@ -86,6 +86,15 @@ int ncn_march_train_pack(const float* rays_d, const int64_t* rays_a, int64_t n_r
                          const float* slab_xyz, const float* slab_t, const float* slab_dt,
                          float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
 
+/* RayMarcher.backward (custom_functions.py:102-112): torch_scatter.segment_csr (sum) over
+ * indptr = [rays_a[:,1], rays_a[-1,1] + rays_a[-1,2]]:
+ *   dL_drays_o[r] = sum_{s in [indptr[r], indptr[r+1])} dL_dxyzs[s]              (n_rays, 3)
+ *   dL_drays_d[r] = sum_{s in [indptr[r], indptr[r+1])} dL_dxyzs[s] * ts[s] + dL_ddirs[s]
+ * One wave per row, fixed summation order (no atomics): deterministic run to run.  dL_dxyzs or
+ * dL_ddirs may be NULL (a zero gradient). */
+int ncn_segment_csr(const float* dL_dxyzs, const float* dL_ddirs, const float* ts, const int64_t* rays_a,
+                    int64_t n_rays, float* dL_drays_o, float* dL_drays_d, void* stream);
+
 /* raymarching_train for the training step in two launches (constant dt, exp_step_factor == 0):
  * render()'s single-AABB intersection + near clamp (intersection.cu:5-56, rendering.py:24-28), the
  * jitter (custom_functions.py:83; `noise` (R) or, when NULL, a counter-based uniform of (seed,

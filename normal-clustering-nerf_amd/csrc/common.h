@@ -10,6 +10,7 @@ namespace ncn {
 void set_error(const char* fmt, ...);
 
 constexpr int WAVE = 64;
+#define NCN_MAX_DEVICES 64  // per-device caches of host-side launch checks
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -7,6 +7,7 @@
 #pragma clang fp contract(off)
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <numeric>
 #include <random>
@@ -1258,11 +1259,23 @@ int ncn_cluster_loss(const float* normals, int64_t n_tri, int K, int niter, cons
     NCN_REQUIRE(n_tri >= 0 && n_tri <= CL_MAX_TRI, hipErrorInvalidValue,
                 "ncn_cluster_loss: n_tri=%lld exceeds %d", (long long)n_tri, CL_MAX_TRI);
     // refuse (rather than spin into the barrier timeout) on a device that cannot hold the workgroups
-    // at all; checked once per process (the answer depends only on the device and the kernel)
-    static int coresident = -1;
-    if (coresident < 0 && (K == 10 || K == 20)) coresident = ncn_cluster_coresidency(K, 0, nullptr) == 0 ? 1 : 0;
-    NCN_REQUIRE(coresident != 0, hipErrorCooperativeLaunchTooLarge,
-                "ncn_cluster_loss: the device cannot hold the clustering's %d co-resident workgroups", KM_BLOCKS);
+    // at all; checked once per (device, K) — the answer depends on the device and on the kernel
+    // instance (K sets its LDS) — and cached in an atomic (0 unknown, 1 resident, 2 refused; a racing
+    // first call computes the same answer twice)
+    static std::atomic<int> coresident[NCN_MAX_DEVICES][2];
+    int dev = 0;
+    NCN_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < NCN_MAX_DEVICES, hipErrorInvalidDevice,
+                "ncn_cluster_loss: current device %d out of range", dev);
+    if (K == 10 || K == 20) {
+        std::atomic<int>& c = coresident[dev][K == 20];
+        int v = c.load(std::memory_order_relaxed);
+        if (v == 0) {
+            v = ncn_cluster_coresidency(K, 0, nullptr) == 0 ? 1 : 2;
+            c.store(v, std::memory_order_relaxed);
+        }
+        NCN_REQUIRE(v == 1, hipErrorCooperativeLaunchTooLarge,
+                    "ncn_cluster_loss: the device cannot hold the clustering's %d co-resident workgroups", KM_BLOCKS);
+    }
     NCN_REQUIRE(niter >= 0 && niter <= 30, hipErrorInvalidValue, "ncn_cluster_loss: niter must be in [0, 30]");
     NCN_REQUIRE(kmeans_plan != nullptr, hipErrorInvalidValue, "ncn_cluster_loss: kmeans_plan required (ncn_kmeans_plan_fill)");
     hipStream_t s = (hipStream_t)stream;

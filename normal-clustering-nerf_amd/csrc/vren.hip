@@ -1692,6 +1692,44 @@ __global__ void packbits_kernel(const float4* __restrict__ grid, int64_t n_bytes
     bitfield[n] = (uint8_t)bits;
 }
 
+// RayMarcher.backward (custom_functions.py:102-112): torch_scatter.segment_csr over
+// indptr = [rays_a[:, 1], rays_a[-1, 1] + rays_a[-1, 2]], so row r sums samples
+// [rays_a[r, 1], rays_a[r + 1, 1]) (the last row up to its start + count; an inverted range sums to 0):
+//   dL/drays_o[r] = sum dL/dxyzs,   dL/drays_d[r] = sum (dL/dxyzs * ts + dL/ddirs).
+// One wave per row, no atomics: lane l adds samples l, l + 64, ... in order, then the fixed
+// permlane/DPP tree of wave_sum_multi — the summation order depends only on the segment, so
+// repeated launches are bit-identical.  The d-term is rounded as the reference's torch ops round it
+// (a product, then a sum: no fma contraction).  gx / gd may be NULL (that gradient is zero).
+__global__ __launch_bounds__(256) void segment_csr_kernel(const float* __restrict__ gx, const float* __restrict__ gd,
+                                                          const float* __restrict__ ts,
+                                                          const int64_t* __restrict__ rays_a, int64_t R,
+                                                          float* __restrict__ d_o, float* __restrict__ d_d) {
+#pragma clang fp contract(off)
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int64_t start = rays_a[3 * r + 1];
+    const int64_t end = (r + 1 < R) ? rays_a[3 * (r + 1) + 1] : start + rays_a[3 * r + 2];
+    float a[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int64_t s = start + lane; s < end; s += 64) {
+        const float t = ts[s];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float x = gx ? gx[3 * s + c] : 0.f;
+            const float y = gd ? gd[3 * s + c] : 0.f;
+            a[c] = a[c] + x;
+            a[3 + c] = a[3 + c] + ((x * t) + y);
+        }
+    }
+    wave_sum_multi<6>(a);
+    if (lane < 3) {
+        const float vo = lane == 0 ? a[0] : (lane == 1 ? a[1] : a[2]);
+        const float vd = lane == 0 ? a[3] : (lane == 1 ? a[4] : a[5]);
+        d_o[3 * r + lane] = vo;
+        d_d[3 * r + lane] = vd;
+    }
+}
+
 }  // namespace ncn
 
 using namespace ncn;
@@ -1720,6 +1758,15 @@ int ncn_count_samples(const int64_t* total_samples, int64_t n_rays, const int32_
     hipLaunchKernelGGL(count_samples_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, total_samples, n_rays,
                        counter, sum_out, acc);
     NCN_LAUNCH_CHECK("ncn_count_samples");
+    return 0;
+}
+
+int ncn_segment_csr(const float* dL_dxyzs, const float* dL_ddirs, const float* ts, const int64_t* rays_a,
+                    int64_t n_rays, float* dL_drays_o, float* dL_drays_d, void* stream) {
+    if (n_rays <= 0) return 0;
+    hipLaunchKernelGGL(segment_csr_kernel, dim3(cdiv(n_rays, 4)), dim3(256), 0, (hipStream_t)stream, dL_dxyzs,
+                       dL_ddirs, ts, rays_a, n_rays, dL_drays_o, dL_drays_d);
+    NCN_LAUNCH_CHECK("ncn_segment_csr");
     return 0;
 }
 

@@ -36,6 +36,7 @@ SIGNATURES = {
     "ncn_march_train_fused": [P, P, I64, F32, F32, F32, F32, F32, F32, F32, P, U64, P, P, I32, F32, I32, I32, P, P, P,
                               P, P, P, P, P, P, P, P],
     "ncn_march_train_pack": [P, P, I64, I32, P, P, P, P, P, P, P, P],
+    "ncn_segment_csr": [P, P, P, P, I64, P, P, P],
     "ncn_march_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
     "ncn_composite_train_fw": [P, P, P, P, P, I64, I64, I32, F32, P, P, P, P, P, P],
     "ncn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, I64, I32, P, P, P, F32, P, P, P],

@@ -24,7 +24,8 @@ class RayMarcher(torch.autograd.Function):
     the reference (custom_functions.py:83); tests may pass an explicit `noise` tensor (quirk q8).
     backward (:102-112): the reference's torch_scatter.segment_csr over indptr = [rays_a[:, 1],
     rays_a[-1, 1] + rays_a[-1, 2]] — row i of dL/drays_o is the sum of dL/dxyzs over samples
-    [indptr[i], indptr[i+1]), row i of dL/drays_d the same sum of dL/dxyzs * t + dL/ddirs.  Rows map
+    [indptr[i], indptr[i+1]), row i of dL/drays_d the same sum of dL/dxyzs * t + dL/ddirs — as one
+    HIP launch (ncn_segment_csr: a wave per row, fixed summation order, no atomics).  Rows map
     to ray rows by position (the reference's rows are ray-ordered, rays_a[i, 0] == i, and so are
     this marcher's, with starts in ray order, so every segment is exactly ray i's samples)."""
 
@@ -49,21 +50,8 @@ class RayMarcher(torch.autograd.Function):
         rays_a, ts = ctx.saved_tensors
         if ctx.static_capacity:
             raise NotImplementedError("ray gradients are not available on the static-capacity (graph) path")
-        dev, R = ts.device, ctx.n_rays
-        # segment_csr(src, indptr): out[i] = src[indptr[i]:indptr[i+1]].sum(0); samples outside
-        # [indptr[0], indptr[R]) belong to no segment
-        indptr = torch.cat([rays_a[:, 1], rays_a[-1:, 1] + rays_a[-1:, 2]])
-        lens = (indptr[1:] - indptr[:-1]).clamp_min(0)
-        seg = torch.repeat_interleave(torch.arange(R, device=dev), lens)
-        lo = int(indptr[0]) if R else 0
-        sl = slice(lo, lo + seg.numel())
-        dL_drays_o = torch.zeros(R, 3, device=dev)
-        dL_drays_d = torch.zeros(R, 3, device=dev)
-        if dL_dxyzs is not None:
-            dL_drays_o.index_add_(0, seg, dL_dxyzs[sl])
-            dL_drays_d.index_add_(0, seg, dL_dxyzs[sl] * ts[sl, None])
-        if dL_ddirs is not None:
-            dL_drays_d.index_add_(0, seg, dL_ddirs[sl])
+        c = lambda t: None if t is None else t.contiguous().float()  # noqa: E731
+        dL_drays_o, dL_drays_d = vren.raymarching_train_backward(c(dL_dxyzs), c(dL_ddirs), ts, rays_a)
         return dL_drays_o, dL_drays_d, None, None, None, None, None, None, None, None, None
 
 

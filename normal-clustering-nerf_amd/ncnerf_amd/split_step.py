@@ -26,8 +26,10 @@ encoding gradients.  Every per-sample value is therefore bit-identical to the au
 only the float-atomic flush order of the table gradient differs, as between any two runs.  The rgb
 pass uses at most SPLIT_BLOCKS workgroups so the clustering's 16 co-resident workgroups keep CUs
 of their own (an rgb-pass workgroup takes a whole CU's LDS); the sigma pass keeps only the
-sigma_net's fragments and exchange tiles in LDS and runs two workgroups per CU.  Only the fused-loss configuration takes this path (split_eligible); any other
-falls back to the autograd step."""
+sigma_net's fragments and exchange tiles in LDS and runs two workgroups per CU.  Only the
+fused-loss configuration takes this path (split_eligible), and only on a device that can hold the
+clustering beside the rgb pass (SplitStep refuses otherwise); anything else falls back to the
+autograd step."""
 import ctypes
 
 import torch
@@ -38,8 +40,27 @@ from .losses import N_OUT, _cluster_workspace, _standard_patch_offsets, kmeans_p
 from .ngp_mt import N_W
 from .rendering import march_train_fused
 
-SPLIT_BLOCKS = 240  # MLP-backward workgroups of each split pass: 256 CUs - the clustering's 16
+SPLIT_BLOCKS = 240  # MLP-backward workgroups of each split pass at most: 256 CUs - the clustering's 16
 K_CLUSTERS, K_ITERS = 20, 20  # NeRFMTLoss._fused (losses.py:86-89: faiss.Kmeans(3, 20, niter=20))
+KM_BLOCKS = 16  # the clustering kernel's co-resident workgroups (csrc/loss.hip KM_BLOCKS)
+
+
+def split_rgb_blocks(cus, per_cu, cap=SPLIT_BLOCKS):
+    """The rgb pass's workgroups on a device of `cus` CUs where `per_cu` clustering workgroups fit
+    per CU: every CU but the ceil(KM_BLOCKS / per_cu) the clustering needs, at most `cap` (240 on
+    MI355X's 256 CUs).  0 when the device cannot hold the clustering at all."""
+    if cus <= 0 or per_cu <= 0:
+        return 0
+    return max(0, min(cap, cus - -(-KM_BLOCKS // per_cu)))
+
+
+def device_rgb_blocks():
+    """split_rgb_blocks for the current device (ncn_cluster_coresidency with no busy CUs reports
+    cus x per_cu)."""
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    cap = ctypes.c_int(0)
+    _lib.lib().ncn_cluster_coresidency(I32(K_CLUSTERS), I32(0), ctypes.byref(cap))  # rc != 0 leaves cap < 16
+    return split_rgb_blocks(cus, cap.value // max(cus, 1))
 
 
 def split_eligible(trainer, batch):
@@ -64,17 +85,21 @@ class SplitStep:
     """One training step (forward + split backward) of `trainer`'s model; run() is graph-capturable
     (no host reads).  Buffers that depend only on the batch size are allocated once."""
 
-    def __init__(self, trainer, rgb_blocks=SPLIT_BLOCKS):
-        """rgb_blocks: the rgb pass's workgroups (one per CU), which run beside the clustering.  The
-        clustering's workgroups meet at grid barriers, so they must all stay resident on the CUs the
-        rgb pass leaves: checked here (ncn_cluster_coresidency), before the step is captured — a
-        device where they cannot is refused instead of spinning into the barrier timeout.  (At N > 1
+    def __init__(self, trainer, rgb_blocks=None):
+        """rgb_blocks: the rgb pass's workgroups (one per CU), which run beside the clustering; by
+        default sized from the device (device_rgb_blocks: 240 on MI355X, fewer on a smaller part).
+        The clustering's workgroups meet at grid barriers, so they must all stay resident on the CUs
+        the rgb pass leaves: checked here (ncn_cluster_coresidency), before the step is captured — a
+        configuration where they cannot is refused (NcnError) instead of spinning into the barrier
+        timeout, and Trainer then runs the autograd step.  (At N > 1
         nothing else shares the step: the all-reduce of step k is stream-ordered before graph k+1,
         and RCCL's channels run beside the deferred coarse-level scatter, which leaves them 32 CUs,
         distributed.DP_SCATTER_BLOCKS.)"""
         self.tr = trainer
         self._tri = None
-        self.rgb_blocks = int(rgb_blocks)
+        self.rgb_blocks = device_rgb_blocks() if rgb_blocks is None else int(rgb_blocks)
+        if self.rgb_blocks < 1:
+            raise _lib.NcnError("SplitStep: the device cannot hold the clustering's workgroups beside an rgb pass")
         cap = ctypes.c_int(0)
         call("ncn_cluster_coresidency", I32(K_CLUSTERS), I32(self.rgb_blocks), ctypes.byref(cap))
         self.cluster_capacity = cap.value

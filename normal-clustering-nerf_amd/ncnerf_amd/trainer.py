@@ -9,6 +9,7 @@ Hyper-parameters default to the Hypersim config (experiments/hypersim/hyperparam
 preset="scannet_manhattan" selects config #5's (experiments/scannet_man/hyperparameters.py)."""
 import math
 import os
+import warnings
 
 import torch
 
@@ -180,7 +181,12 @@ class Trainer:
             raise NotImplementedError("ray-range annealing is step-dependent host control flow")
         self._static = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in batch.items()}
         from .split_step import SplitStep, split_eligible
-        self._split = SplitStep(self) if self.split_backward and split_eligible(self, self._static) else None
+        self._split = None
+        if self.split_backward and split_eligible(self, self._static):
+            try:
+                self._split = SplitStep(self)
+            except _lib.NcnError as e:  # the clustering cannot stay resident beside the rgb pass
+                warnings.warn(f"split backward unavailable on this device, using the autograd step: {e}")
         self._step_dev = torch.zeros((), dtype=torch.int64, device=dev)
         # the optimizer is in the graph unless the gradient is reduced (or its scatter finished) outside
         self._with_opt = not distributed.is_distributed() and self.model.scatter_split is None

@@ -112,6 +112,35 @@ def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
     return [rays_a, xyzs, dirs, deltas, ts, counter]
 
 
+def raymarching_train_backward(dL_dxyzs, dL_ddirs, ts, rays_a):
+    """RayMarcher.backward (custom_functions.py:102-112) -> [dL_drays_o (R,3), dL_drays_d (R,3)]: the
+    reference's segment_csr over indptr = [rays_a[:,1], rays_a[-1,1] + rays_a[-1,2]] in one launch
+    (ncn_segment_csr; fixed summation order, bit-identical run to run).  dL_dxyzs / dL_ddirs may be
+    None (zero)."""
+    check_input(ts, "ts")
+    check_input(rays_a, "rays_a")
+    check_dtype(ts, torch.float32, "ts")
+    check_dtype(rays_a, torch.int64, "rays_a")
+    S = ts.shape[0]
+    for t, n in ((dL_dxyzs, "dL_dxyzs"), (dL_ddirs, "dL_ddirs")):
+        if t is not None:
+            check_input(t, n)
+            check_dtype(t, torch.float32, n)
+            if t.shape != (S, 3):
+                raise RuntimeError(f"{n} must be (S, 3) with S = ts.shape[0] = {S} (got {tuple(t.shape)})")
+    R = rays_a.shape[0]
+    d_o = torch.empty(R, 3, dtype=torch.float32, device=ts.device)
+    d_d = torch.empty(R, 3, dtype=torch.float32, device=ts.device)
+    if R:
+        # every segment end is another row's start or the last row's start + count: all must lie in [0, S]
+        st = rays_a[:, 1]
+        lo, hi = int(st.min()), max(int(st.max()), int(rays_a[-1, 1] + rays_a[-1, 2]))
+        if lo < 0 or hi > S:
+            raise RuntimeError(f"rays_a segments reach outside the {S} samples ([{lo}, {hi}))")
+    call("ncn_segment_csr", ptr(dL_dxyzs), ptr(dL_ddirs), ptr(ts), ptr(rays_a), I64(R), ptr(d_o), ptr(d_d), stream())
+    return [d_o, d_d]
+
+
 def raymarching_test(rays_o, rays_d, hits_t, alive_indices, density_bitfield, cascades, scale, exp_step_factor,
                      grid_size, max_samples, N_samples):
     """raymarching.cu:407-454 -> [xyzs (A,N,3), dirs (A,N,3), deltas (A,N), ts (A,N), N_eff i32 (A)];

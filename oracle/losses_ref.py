@@ -316,6 +316,14 @@ def kink_signs(normals, labels):
     evaluations whose normals differ by ~5e-4 rad take opposite branches for many of them, and the
     gradient flips there while the loss does not move: test infrastructure shares the branches as it
     shares the labels."""
+    v_ort, v_l1, _ = kink_values(normals, labels)
+    return np.sign(v_ort), [np.sign(v) for v in v_l1]
+
+
+def kink_values(normals, labels):
+    """The quantities whose absolute values cluster_losses takes (losses.py:461-478), float64:
+    (the three centroid dot products c_i . c_j, per selected cluster (normal - centroid) per component
+    (n_k, 3), the three unit centroids (3, 3)) — kink_signs' signs, and what a test checks them by."""
     n = np.asarray(normals, np.float64)
     lab = np.asarray(labels)
     keep = lab != 0
@@ -326,9 +334,8 @@ def kink_signs(normals, labels):
     for ck in cl:
         m = ck.mean(axis=0)
         c.append(m / max(np.linalg.norm(m), 1e-12))
-    s_ort = np.sign([c[0] @ c[1], c[0] @ c[2], c[1] @ c[2]])
-    s_l1 = [np.sign(cl[k] - c[k]) for k in range(3)]
-    return s_ort, s_l1
+    v_ort = np.array([c[0] @ c[1], c[0] @ c[2], c[1] @ c[2]])
+    return v_ort, [cl[k] - c[k] for k in range(3)], np.stack(c)
 
 
 def validity(loss):

@@ -175,3 +175,30 @@ def test_split_graph_step_matches_graph_step(dev, defer):
         assert frac < 1e-3 and big <= 5e-5 * nt and rel_w < 1e-3, (k, frac, big, rel_w)
         for a, b in zip(trs[0].opt.state_tensors(), trs[1].opt.state_tensors()):
             b.copy_(a)  # (lockstep: both continue from the autograd path's state)
+
+
+def test_split_refused_falls_back_to_autograd_step(dev, monkeypatch):
+    """A device that cannot hold the clustering beside the rgb pass (fewer CUs than
+    MI355X's 256): SplitStep refuses, and Trainer's captured step runs the autograd backward
+    instead of failing; its losses equal a trainer built without the split."""
+    from ncnerf_amd import split_step
+    scene = SyntheticScene()
+    b = _batch(scene, dev, 4096, 21)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    import ctypes
+    cap = ctypes.c_int(0)
+    assert _lib.lib().ncn_cluster_coresidency(20, 0, ctypes.byref(cap)) == 0
+    assert split_step.device_rgb_blocks() == split_step.split_rgb_blocks(cus, cap.value // cus)
+    monkeypatch.setattr(split_step, "device_rgb_blocks", lambda: cus)  # every CU busy: no room for the clustering
+    res = []
+    for split in (True, False):
+        tr = Trainer(_model(dev, scene), update_grid=False, use_graph=True, split_backward=split)
+        if split:
+            with pytest.warns(UserWarning, match="split backward unavailable"):
+                _, ld = tr.step(b, global_step=1500)
+            assert tr._split is None
+        else:
+            _, ld = tr.step(b, global_step=1500)
+        torch.cuda.synchronize()
+        res.append(float(ld["total"]))
+    assert res[0] == res[1], res

@@ -391,11 +391,36 @@ def test_composite_background_fused(dev, scene):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
 
 
+def _assert_segment_sums(rays_a, ts, gx, gd, got_o, got_d):
+    """HIP segment sums vs the oracle's sequential segment_csr, row by row within the fp32
+    summation-order bound: two orders of the same n f32 terms differ by at most
+    2 (n - 1) 2^-24 sum|terms| (each sum's error is <= (n - 1) u sum|terms|, u = 2^-24, to first order).
+    A bound relative to the result would ignore cancellation: a row that cancels to 0.08 from terms
+    of order 1 carries ~1e-5 of order noise (the round-5 driver failure)."""
+    ra = np.asarray(rays_a)
+    indptr = np.concatenate([ra[:, 1], ra[-1:, 1] + ra[-1:, 2]])
+    gx = np.zeros((ts.shape[0], 3), np.float32) if gx is None else np.asarray(gx, np.float32)
+    gd = np.zeros((ts.shape[0], 3), np.float32) if gd is None else np.asarray(gd, np.float32)
+    ref_o, ref_d = vren_ref.raymarcher_backward(ra, ts, gx, gd)
+    term_d = gx * np.asarray(ts, np.float32)[:, None] + gd
+    abs_o = vren_ref.segment_csr(np.abs(gx), indptr).astype(np.float64)
+    abs_d = vren_ref.segment_csr(np.abs(term_d), indptr).astype(np.float64)
+    n = np.maximum(indptr[1:] - indptr[:-1], 1).astype(np.float64)[:, None]
+    for got, ref, ab, what in ((got_o, ref_o, abs_o, "dL/drays_o"), (got_d, ref_d, abs_d, "dL/drays_d")):
+        bound = 2.0 * (n - 1) * 2.0 ** -24 * ab * 1.01 + 1e-30
+        err = np.abs(np.asarray(got, np.float64) - ref.astype(np.float64))
+        bad = np.argwhere(err > bound)
+        assert bad.size == 0, (f"{what}: {len(bad)} elements outside 2(n-1)u*sum|terms|; first {bad[:3].tolist()}: "
+                               f"got {np.asarray(got)[tuple(bad[0])]} ref {ref[tuple(bad[0])]} "
+                               f"bound {bound[tuple(bad[0])]}")
+
+
 @pytest.mark.parametrize("n", [512, 1])
 def test_raymarcher_backward_segment_csr(dev, scene, n):
     """RayMarcher.backward (custom_functions.py:102-112) against the reference's segment_csr
-    restated (oracle.vren_ref.raymarcher_backward), incl. rays with no samples; and against the
-    geometry it differentiates: xyzs = o + t*d, dirs = d."""
+    restated (oracle.vren_ref.raymarcher_backward), incl. rays with no samples; against the
+    geometry it differentiates (xyzs = o + t*d, dirs = d); and run to run: the HIP segment sum has a
+    fixed order, so a second backward is bit-identical."""
     from ncnerf_amd.custom_functions import RayMarcher
     o, d, ht, noise = _march_inputs(scene, n, 3 + n, dev)
     if n > 1:
@@ -407,15 +432,51 @@ def test_raymarcher_backward_segment_csr(dev, scene, n):
     g = torch.Generator(device=dev).manual_seed(n)
     wx = torch.randn(xyzs.shape, device=dev, generator=g)
     wd = torch.randn(dirs.shape, device=dev, generator=g)
-    ((xyzs * wx).sum() + (dirs * wd).sum()).backward()
-    ref_o, ref_d = vren_ref.raymarcher_backward(rays_a.cpu().numpy(), ts.detach().cpu().numpy(), wx.cpu().numpy(),
-                                                wd.cpu().numpy())
-    np.testing.assert_allclose(ro.grad.cpu().numpy(), ref_o, rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(rd.grad.cpu().numpy(), ref_d, rtol=1e-5, atol=1e-5)
+    loss = (xyzs * wx).sum() + (dirs * wd).sum()
+    loss.backward(retain_graph=True)
+    g_o, g_d = ro.grad.clone(), rd.grad.clone()
+    ro.grad = rd.grad = None
+    loss.backward()
+    assert torch.equal(ro.grad, g_o) and torch.equal(rd.grad, g_d), "RayMarcher.backward is not deterministic"
+    _assert_segment_sums(rays_a.cpu().numpy(), ts.detach().cpu().numpy(), wx.cpu().numpy(), wd.cpu().numpy(),
+                         g_o.cpu().numpy(), g_d.cpu().numpy())
     if n > 1:
         assert int(rays_a[n // 2, 2]) == 0 and float(ro.grad[n // 2].abs().sum()) == 0.0
         # rows are rays in ray order, so segment i is ray i's samples: d/do (o + t d) = I, d/dd = t I
         ra = rays_a.cpu().numpy()
         i = int(np.argmax(ra[:, 2]))
         s0, c = int(ra[i, 1]), int(ra[i, 2])
-        np.testing.assert_allclose(ro.grad[i].cpu().numpy(), wx[s0:s0 + c].sum(0).cpu().numpy(), rtol=1e-5, atol=1e-5)
+        w = wx[s0:s0 + c].cpu().numpy().astype(np.float64)
+        bound = 2.0 * c * 2.0 ** -24 * np.abs(w).sum(0) * 1.01
+        assert np.all(np.abs(ro.grad[i].cpu().numpy() - w.sum(0)) <= bound)
+
+
+def test_segment_csr_ragged(dev):
+    """ncn_segment_csr alone on hand-built segments: empty segments in the middle and at the end, a
+    one-sample segment, segments just around the 64-lane width, and segments longer than 1024 and
+    than 4096 samples; gradients of both kinds, one of them absent (None = zero), and the reference's
+    indptr rule (a segment ends where the next row starts)."""
+    from ncnerf_amd import vren
+    lens = [3, 0, 1, 63, 64, 65, 1500, 0, 4100, 2, 0]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    S = int(np.sum(lens)) + 7  # trailing samples that belong to no segment
+    ra = np.stack([np.arange(len(lens)), starts, np.asarray(lens)], 1).astype(np.int64)
+    rng = np.random.default_rng(11)
+    ts = rng.uniform(0.0, 3.0, S).astype(np.float32)
+    gx = rng.normal(size=(S, 3)).astype(np.float32)
+    gd = rng.normal(size=(S, 3)).astype(np.float32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    for x, y in ((gx, gd), (gx, None), (None, gd)):
+        d_o, d_d = vren.raymarching_train_backward(None if x is None else T(x), None if y is None else T(y), T(ts),
+                                                   T(ra))
+        d_o2, d_d2 = vren.raymarching_train_backward(None if x is None else T(x), None if y is None else T(y), T(ts),
+                                                     T(ra))
+        torch.cuda.synchronize()
+        assert torch.equal(d_o, d_o2) and torch.equal(d_d, d_d2)
+        _assert_segment_sums(ra, ts, x, y, d_o.cpu().numpy(), d_d.cpu().numpy())
+        for i in np.flatnonzero(np.asarray(lens) == 0):
+            assert float(d_o[i].abs().sum()) == 0.0 and float(d_d[i].abs().sum()) == 0.0
+    with pytest.raises(RuntimeError):
+        bad = ra.copy()
+        bad[-1, 2] = 100  # past the last sample
+        vren.raymarching_train_backward(T(gx), T(gd), T(ts), T(bad))

@@ -98,3 +98,15 @@ def test_flat_adam_set_epoch_is_cosine_annealing():
         assert abs(float(opt.lr_dev) - opt.lr) < 1e-9
         ref_opt.step()
         sch.step()
+
+
+def test_split_rgb_blocks_sized_from_the_device():
+    """the split step's rgb pass leaves the clustering's 16 workgroups the CUs
+    they need on any CU count, instead of a fixed 240."""
+    from ncnerf_amd.split_step import SPLIT_BLOCKS, split_rgb_blocks
+    assert split_rgb_blocks(256, 1) == SPLIT_BLOCKS == 240
+    assert split_rgb_blocks(256, 2) == SPLIT_BLOCKS  # capped
+    assert split_rgb_blocks(228, 1) == 212
+    assert split_rgb_blocks(104, 2) == 96
+    assert split_rgb_blocks(110, 3) == 104  # ceil(16 / 3) = 6 CUs for the clustering
+    assert split_rgb_blocks(16, 1) == 0 and split_rgb_blocks(0, 1) == 0 and split_rgb_blocks(64, 0) == 0
