@@ -250,8 +250,11 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * passes a device 1.0f: the chain then runs at the upstream scale * 128, the outputs keep the
  * upstream scale.
  * n_blocks is returned by ncn_field_bwd_blocks(n).  dE_ws is a device workspace of
- * ncn_field_bwd_dE_floats(n) floats (the level-major encoding gradient between the MLP pass and the
- * LDS-aggregating table scatter pass). */
+ * ncn_field_bwd_dE_floats(n) floats: a 4-float header, the level-major encoding gradient between the
+ * MLP pass and the LDS-aggregating table scatter pass, and the sample positions xyzs in the
+ * scatter's load order (four copies, one per unit class: a wave's round / grab reads one contiguous
+ * stretch).  The MLP pass writes those positions (its rgb part; not with `order`) and marks them in
+ * the header; the scatter uses them when marked, else reads xyzs in sample order. */
 int ncn_field_bwd_blocks(int64_t n);
 int64_t ncn_field_bwd_dE_floats(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
@@ -266,7 +269,7 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * level_max), then the table scatter of the levels [level_lo, level_hi) into grad_table (+=).
  * max_blocks > 0 caps the scatter's workgroups (one per CU otherwise), leaving CUs to a concurrent
  * collective. */
-int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+int ncn_field_bwd_mlp(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
                       const float* loss_scale, float* slab, float* dE_ws, float* level_max, void* stream);
@@ -291,13 +294,17 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
  * bit (one dsigma term). */
 int64_t ncn_field_bwd_stash_floats(int64_t n);
 int ncn_field_bwd_part_blocks(int64_t n, int part);
-int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+int ncn_field_bwd_mlp_part(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                            const uint16_t* weights_packed, int precision, const uint16_t* enc_cache,
                            const float* dL_dsigmas, const float* dL_dsigmas2, const float* dL_drgbs,
                            const float* loss_scale, int part, int n_blocks, float* slab, float* dE_ws,
                            float* level_max, float* dh_stash, void* stream);
 int ncn_field_reduce_wgrad_parts(const float* slab, int n_blocks_sigma, int n_blocks_rgb, float* grad_w,
                                  void* stream);
+/* The positions of dE_ws's permuted region written from xyzs (n capacity, n_dev the device count or
+ * NULL) and marked ready: what the MLP pass's rgb part does in the training step, for a caller that
+ * fills dE_ws itself (the scatter then loads coalesced). */
+int ncn_field_scatter_positions(const float* xyzs, int64_t n, const int32_t* n_dev, float* dE_ws, void* stream);
 int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,

@@ -516,6 +516,11 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
 // of dW, the two waves of a SIMD overlap their MFMA chains, and every tile is written once per
 // workgroup into its slab row at the end.
 constexpr int DE_HEADER_FLOATS = 4;  // the dE workspace's header (ncn_field_bwd_dE_floats)
+// (the scatter's sample layout, defined with the scatter below: the rgb / one-pass MLP pass writes
+// the positions in it, DE_POS_READY in the header)
+__host__ __device__ constexpr int64_t sc_perm_stride(int64_t n_stride);
+__device__ __forceinline__ int64_t sc_perm(int64_t s, int cls);
+constexpr int DE_POS_FLAG = 2;  // header float: 1 when the workspace holds the permuted positions
 constexpr int BWD_WAVES = 8;
 constexpr int BWD_THREADS = 64 * BWD_WAVES;
 // exchange tiles per group: dW operands, A = dY^T, B = X^T (16 features x 16 samples)
@@ -552,6 +557,7 @@ template <typename T>
 struct BwdIn {
     typename Mfma<T>::v8 e;
     float dx, dy, dz, dsig, dr0, dr1, dr2;
+    float px, py, pz;  // (rgb / one pass, with positions out) the sample's position
     typename Mfma<T>::v4 dq;  // (BWD_SIGMA) the stashed rgb part of dL/dh of this lane's tile, as operands
     float h0;                 // (BWD_SIGMA, g = 0) its row-0 element in fp32 (TruncExp's term is added to it)
 };
@@ -561,11 +567,15 @@ __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, i
                                          const float* __restrict__ dL_dsig, const float* __restrict__ dL_dsig2,
                                          const float* __restrict__ dL_drgb,
                                          const typename Mfma<T>::v4* __restrict__ stq, const float* __restrict__ sth0,
-                                         const int32_t* __restrict__ order, float S) {
+                                         const int32_t* __restrict__ order, float S, const float* __restrict__ xyzs) {
     const int64_t pos = grp * 16 + (lane & 15);  // processing position (enc_cache / dE order)
     const bool valid = pos < n;
     in.e = enc[grp * 64 + lane];
     in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
+    in.px = in.py = in.pz = 0.f;
+    if constexpr ((PART & BWD_RGB) != 0) {
+        if (xyzs && valid) { in.px = xyzs[3 * pos]; in.py = xyzs[3 * pos + 1]; in.pz = xyzs[3 * pos + 2]; }
+    }
     if constexpr (PART == BWD_SIGMA) {
         in.dq = stq[grp * 64 + lane];
         in.h0 = (lane >> 4) == 0 ? sth0[grp * 16 + (lane & 15)] : 0.f;
@@ -866,7 +876,8 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const typename Mfma<T>::v8* __restrict__ enc_cache, const float* __restrict__ dL_dsig,
     const float* __restrict__ dL_drgb, const float* __restrict__ loss_scale, float* __restrict__ dE_out,
     float* __restrict__ slab, float* __restrict__ level_max, const int32_t* __restrict__ order,
-    const float* __restrict__ dL_dsig2 = nullptr, float* __restrict__ stash = nullptr) {
+    const float* __restrict__ dL_dsig2 = nullptr, float* __restrict__ stash = nullptr,
+    const float* __restrict__ xyzs = nullptr) {
     typedef typename Mfma<T>::v4 v4;
     // AMP loss scale (GradScaler of the reference's precision=16 run) times tcnn's fp16 module loss
     // scale (128): the fp16 chain sees the upstream gradients times S (a power of two), dE and dW
@@ -880,6 +891,13 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
         dE_out[0] = inv_S;
         dE_out[1] = Mfma<T>::f16 ? 0.f : 1.f;
     }
+    // (rgb / one pass) the sample positions in the scatter's per-class load order (sc_perm), behind
+    // the encoding gradient: lane (g, r) writes sample r's position into class g's array.  In the
+    // processing order of `order` the scatter gathers them itself (no positions written).
+    const float* pos_src = ((PART & BWD_RGB) != 0 && dE_out && !order) ? xyzs : nullptr;
+    float* const pos_out = pos_src ? dE_out + DE_HEADER_FLOATS + 16 * n_stride : nullptr;
+    const int64_t pos_stride = sc_perm_stride(n_stride);
+    if ((PART & BWD_RGB) != 0 && dE_out && blockIdx.x == 0 && threadIdx.x == 0) dE_out[DE_POS_FLAG] = pos_out ? 1.f : 0.f;
     const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
     // split passes' stash (ncn_field_bwd_stash_floats): [groups][64] operand tiles, then [groups][16]
     // fp32 row-0 elements (capacity groups: the layout does not depend on the device count)
@@ -917,15 +935,21 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     int64_t base = (int64_t)blockIdx.x * BWD_WAVES;  // first group of this workgroup's step
     BwdIn<T> nxt;
     if (base + wid < n_groups)
-        bwd_load<T, PART>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order, S);
+        bwd_load<T, PART>(nxt, base + wid, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order, S,
+                          pos_src);
     for (; base < n_groups; base += stride) {
         const int64_t grp = base + wid;
         const int ng = (int)min<int64_t>(BWD_WAVES, n_groups - base);
         const BwdIn<T> cur = nxt;
         if (grp + stride < n_groups)
             bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order,
-                              S);
+                              S, pos_src);
         if (grp < n_groups) {
+            if ((PART & BWD_RGB) != 0 && pos_out && grp * 16 + (lane & 15) < n) {
+                const int cls = lane >> 4;
+                float* po = pos_out + cls * 3 * pos_stride + 3 * sc_perm(grp * 16 + (lane & 15), cls);
+                po[0] = cur.px; po[1] = cur.py; po[2] = cur.pz;
+            }
             typename std::conditional<SIGONLY, FragsSigma<T>, Frags<T>>::type F;
             const int z = opaque_zero();
             F.f32 = F32s + z;
@@ -999,15 +1023,20 @@ __global__ void reduce_wgrad_kernel(const float* __restrict__ slab, int nb_sigma
 //  * a unit of work is (span of consecutive samples, level): 1024 lanes x C samples x rounds;
 //  * a lane sums the eight corner contributions of its consecutive samples in the same cell in
 //    registers (a run) and hands a finished run to the table;
-//  * coarse levels [0, SC_CELL_HI) are CELL-keyed (sc_add_cell): a run is one lookup of its cell in
-//    a 4-way set-associative LDS table and 16 ds_add_u64 into the cell's corner-major sums; fine
+//  * the lanes' samples are read from a copy of the positions in the unit's load order (sc_perm,
+//    written by the MLP pass): a wave's round reads one contiguous stretch (round 6: 192 -> 176 us,
+//    the coarse units' strided loads had cost one cache line per lane per load);
+//  * coarse levels [0, SC_CELL_HI) are CELL-keyed: finished runs are queued per wave and added by
+//    full-wave passes (sc_drain_cells): one lookup of the run's cell in a 4-way set-associative LDS
+//    table and 16 ds_add_u64 into the cell's corner-major sums; fine
 //    levels are ENTRY-keyed (sc_add): each of the 8 corners looked up in its own 4-way set (one
 //    ds_read_b128 per set, ds_cmpst to claim a way) and its (x, y) added with two ds_add_u64;
 //  * sums are 64-bit FIXED-POINT (exact integer arithmetic: order-independent and reproducible; an
 //    LDS f32 atomic costs ~3 cycles per active lane on gfx950 against ~13 per wave-instruction for a
 //    u64 add, and f32 slot sums measured 2-3x slower under the same-slot conflicts).  The
-//    scale of a level is 2^k, k = 61 - log2(unit samples) - e, max|dE| < 2^e (the MLP pass records
-//    max|dE| per level), so an entry's unit sum stays below 2^62.  A corner whose set is full goes
+//    scale of a level is 2^k, k = 60 - log2(unit samples) - e (fine units 46 - e), max|dE| < 2^e (the
+//    MLP pass records max|dE| per level), so an entry's unit sum stays below 2^62 and every addend
+//    below 2^51 (sc_fix).  A corner whose set is full goes
 //    straight to a global f32 atomic;
 //  * at the end of the unit the claimed slots (the `used` list) are flushed with one f32 global
 //    atomic per non-zero sum and reset.  A unit whose gradient is not finite adds every run straight
@@ -1021,9 +1050,19 @@ constexpr int SC_SETS_DIR = 1536;  // entry-keyed layout: 6 144 slots (132 KB)
 // holds the 64-bit sums of its 8 corners' x and y (corner-major: vals[(2c + xy) * slots + slot]).
 constexpr int SC_CELL_HI = 10;
 constexpr int SC_CELL_VALS = 16;
-constexpr int SC_SETS_CELL = 256;  // 1 024 cell slots (137 KB)
+// Finished coarse runs are queued per wave (key + 16 f32 sums, 68 B) and added to the table by a
+// full-wave pass once the queue would overflow (sc_push_run / sc_drain_cells): a coarse sample step
+// ends a run in only ~6-30 of 64 lanes, and adding them at once cost a set read and 16 ds_add_u64
+// wave-instructions (plus 16 fixed-point conversions) per step for those few lanes.
+// (Round 6: queued 180 vs 189 us for the whole scatter, levels 0-5 alone 43 vs 62 us per unit,
+// profiles/round6/scatter_probe_queue.log; the table shrank from 1 024 cell slots for the queues.)
+constexpr int SC_SETS_CELL = 160;  // 640 cell slots (86 KB) beside the run queues (70 KB)
+constexpr int SC_QUEUE = 64;       // runs per wave queue
+constexpr int SC_CELL_TABLE_BYTES = SC_SETS_CELL * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2);
+constexpr int SC_QUEUE_BYTES = SC_WAVES * SC_QUEUE * (4 + SC_CELL_VALS * 4);
 constexpr int sc_max(int a, int b) { return a > b ? a : b; }
-constexpr int SC_ARENA = sc_max(SC_SETS_CELL * SC_WAYS * (4 + SC_CELL_VALS * 8 + 2), SC_SETS_DIR * SC_WAYS * SC_SLOT_BYTES);
+constexpr int SC_ARENA = sc_max(SC_CELL_TABLE_BYTES + SC_QUEUE_BYTES, SC_SETS_DIR * SC_WAYS * SC_SLOT_BYTES);
+static_assert(SC_CELL_TABLE_BYTES % 16 == 0, "run queues 16-B aligned");
 constexpr uint32_t SC_EMPTY = 0xFFFFFFFFu;
 constexpr int SC_BATCH = 2;  // corners per batch of set reads in sc_add (2: 232 us, 4: 238 us (spills), 8: 298 us;
                              // round 5: 4 at 124 VGPRs 196 us (4 spills); at 120, no spills: 194-195 vs 190)
@@ -1054,6 +1093,8 @@ struct ScShared {
     uint32_t* keys;
     long long *valx, *valy;  // (cell layout: valx = the 16 corner-major arrays)
     uint16_t* used;          // slots claimed since the last flush, in claim order
+    float4* qval;            // (cell layout) the waves' run queues: [wave][SC_QUEUE][4] float4 (16 sums)
+    uint32_t* qkey;          //               and their cell keys [wave][SC_QUEUE]
     uint32_t sets;
     int slots;
     int* fill;
@@ -1068,6 +1109,8 @@ __device__ __forceinline__ ScShared sc_layout(char* arena, int* fill, int mode) 
     sh.valy = mode == SC_MODE_CELL ? sh.valx + (SC_CELL_VALS - 1) * sh.slots : sh.valx + sh.slots;
     sh.keys = (uint32_t*)(sh.valy + sh.slots);
     sh.used = (uint16_t*)(sh.keys + sh.slots);
+    sh.qval = (float4*)(arena + SC_CELL_TABLE_BYTES);
+    sh.qkey = (uint32_t*)(sh.qval + SC_WAVES * SC_QUEUE * 4);
     sh.fill = fill;
     return sh;
 }
@@ -1258,10 +1301,12 @@ __device__ __forceinline__ void sc_load_de(ScChunk<C>& ch, const uint32_t* __res
         ch.g[0] = de(v.x); ch.g[1] = de(v.y);
     }
 }
+// xyzs: the unit class's permuted positions (sc_perm) with pb = the chunk's place in them, or (with
+// `order`, pb unused) the sample-ordered positions gathered through order.
 template <int C>
-__device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t s1, const float* __restrict__ xyzs,
-                                               const uint32_t* __restrict__ dEl, const ScDE& de, const ScNorm& nrm,
-                                               const int32_t* __restrict__ order) {
+__device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_t pb, int64_t s1,
+                                               const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
+                                               const ScDE& de, const ScNorm& nrm, const int32_t* __restrict__ order) {
     static_assert(C == 2 || C == 4, "chunk of 2 or 4 samples");
     float xs[3 * C];
     if (order) {  // positions sb.. in processing order: dE contiguous, positions gathered
@@ -1283,14 +1328,14 @@ __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_
         }
     } else if (sb + C <= s1) {
         if constexpr (C == 4) {
-            const float4* px = (const float4*)(xyzs + 3 * sb);
+            const float4* px = (const float4*)(xyzs + 3 * pb);
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const float4 v = px[q];
                 xs[4 * q] = v.x; xs[4 * q + 1] = v.y; xs[4 * q + 2] = v.z; xs[4 * q + 3] = v.w;
             }
         } else {
-            const float2* px = (const float2*)(xyzs + 3 * sb);
+            const float2* px = (const float2*)(xyzs + 3 * pb);
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const float2 v = px[q];
@@ -1302,11 +1347,11 @@ __device__ __forceinline__ void sc_load_chunk(ScChunk<C>& ch, int64_t sb, int64_
 #pragma unroll
         for (int i = 0; i < C; i++) {
             const bool in = sb + i < s1;
-            const int64_t sc = in ? sb + i : 0;
+            const int64_t sc = in ? sb + i : 0, pc = in ? pb + i : 0;
             ch.g[i] = in ? de(dEl[sc]) : make_float2(0.f, 0.f);
-            xs[3 * i] = in ? xyzs[3 * sc] : 0.f;
-            xs[3 * i + 1] = in ? xyzs[3 * sc + 1] : 0.f;
-            xs[3 * i + 2] = in ? xyzs[3 * sc + 2] : 0.f;
+            xs[3 * i] = in ? xyzs[3 * pc] : 0.f;
+            xs[3 * i + 1] = in ? xyzs[3 * pc + 1] : 0.f;
+            xs[3 * i + 2] = in ? xyzs[3 * pc + 2] : 0.f;
         }
     }
 #pragma unroll
@@ -1366,21 +1411,33 @@ __device__ __forceinline__ uint32_t sc_corner_entry(const ScLevel& L, uint32_t p
     return (x ^ (y * 2654435761u) ^ (z * 805459861u)) & (L.params - 1);
 }
 
-__device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, uint32_t px, uint32_t py, uint32_t pz,
-                                            const float (&v)[16], const ScLevel& L, float* __restrict__ grad) {
-    const bool inkey = px < 2048u && py < 2048u && pz < 1024u;
-    const uint32_t key = px | (py << 11) | (pz << 22);
-    const bool go = act && inkey;
+// A lane's run of consecutive samples in one cell of a coarse level: the 8 corners' weighted sums
+// in registers, carried over the lane's chunks of a unit; a finished run goes to the wave's queue
+// (sc_push_run), whose full-wave passes add the runs to the cell table (sc_drain_cells).
+struct ScRun {
+    uint32_t px, py, pz;
+    bool any, init;
+    float v[16];
+};
+
+// The wave's queued runs [0, qn) into the cell table, one run per lane: one set read and claim per
+// run, the 16 sums as fixed-point ds_add_u64 in four float4 groups; a run whose set is full goes to
+// global f32 atomics.
+__device__ __forceinline__ void sc_drain_cells(ScShared& sh, int lane, const uint32_t* qk, const float4* qv, int qn,
+                                               const ScLevel& L, float* __restrict__ grad) {
+    asm volatile("" ::: "memory");  // (the wave's queue writes come first: a wave's LDS operations execute in order)
+    const bool act = lane < qn;
+    const uint32_t key = act ? qk[lane] : 0u;
     const int p0 = SC_WAYS * (int)sc_set(key, sh.sets);
     int sl = -1;
     bool isnew = false;
     uint4 kk = make_uint4(0u, 0u, 0u, 0u);
-    if (go) {
+    if (act) {
         kk = *(const uint4*)&sh.keys[p0];
         sl = kk.x == key ? p0 : kk.y == key ? p0 + 1 : kk.z == key ? p0 + 2 : kk.w == key ? p0 + 3 : -1;
     }
-    if (__ballot(go && sl < 0)) {  // uniform: some lane claims
-        if (go && sl < 0) {
+    if (__ballot(act && sl < 0)) {  // uniform: some lane claims
+        if (act && sl < 0) {
 #pragma unroll
             for (int attempt = 0; attempt < 2 && sl < 0; attempt++) {
                 if (attempt) {  // lost a claim: look again
@@ -1398,28 +1455,28 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
             }
         }
     }
-    if (go && sl >= 0) {
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            if (v[2 * c] == 0.f && v[2 * c + 1] == 0.f) continue;
-            // x and y of corner c: arrays 2c, 2c + 1
-            atomicAdd((unsigned long long*)&sh.valx[(2 * c) * sh.slots + sl], (unsigned long long)sc_fix(v[2 * c], L.k));
-            atomicAdd((unsigned long long*)&sh.valx[(2 * c + 1) * sh.slots + sl],
-                      (unsigned long long)sc_fix(v[2 * c + 1], L.k));
-        }
-    }
     const bool fb = act && sl < 0;
-    if (__ballot(fb)) {  // uniform: set full / cell outside the key range
-        if (fb) {
+    const bool anyfb = __ballot(fb) != 0;  // uniform: a set full of other cells
 #pragma unroll
-            for (int c = 0; c < 8; c++) {
-                const uint32_t e = L.off + sc_corner_entry(L, px, py, pz, c);
-                if (v[2 * c] != 0.f) atomicAdd(grad + 2 * (size_t)e, v[2 * c]);
-                if (v[2 * c + 1] != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, v[2 * c + 1]);
+    for (int g = 0; g < 4; g++) {
+        const float4 v = act ? qv[4 * lane + g] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const int j = 4 * g + h;  // corner j / 2, component j % 2
+            if (act && sl >= 0)
+                atomicAdd((unsigned long long*)&sh.valx[j * sh.slots + sl], (unsigned long long)sc_fix(vv[h], L.k));
+        }
+        if (anyfb && fb) {
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int j = 4 * g + h;
+                const uint32_t e = L.off + sc_corner_entry(L, key & 2047u, (key >> 11) & 2047u, key >> 22, j >> 1);
+                if (vv[h] != 0.f) atomicAdd(grad + 2 * (size_t)e + (j & 1), vv[h]);
             }
         }
     }
-    // append the claimed slot to `used`: one LDS atomic per wave
+    // append the claimed slots to `used`: one LDS atomic per wave
     const uint64_t nm = __ballot(isnew);
     if (nm) {
         int base = 0;
@@ -1429,25 +1486,50 @@ __device__ __forceinline__ void sc_add_cell(ScShared& sh, int lane, bool act, ui
             sh.used[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0))] =
                 (uint16_t)sl;
     }
+    asm volatile("" ::: "memory");  // (the queue is rewritten after these reads)
 }
 
-// A lane's run of consecutive samples in one cell of a coarse level: the 8 corners' weighted sums
-// in registers, carried over the lane's chunks of a unit; a finished run goes to sc_add_cell (called
-// by the whole wave when some lane has one).
-struct ScRun {
-    uint32_t px, py, pz;
-    bool any, init;
-    float v[16];
-};
+// Queue the finished runs of the lanes with `fin` (whole wave calls; qn wave-uniform): a full queue
+// is drained first.  Cells outside the key range go straight to global memory.
+__device__ __forceinline__ void sc_push_run(ScShared& sh, int lane, bool fin, const ScRun& st, uint32_t* qk, float4* qv,
+                                            int& qn, const ScLevel& L, float* __restrict__ grad) {
+    const bool inkey = st.px < 2048u && st.py < 2048u && st.pz < 1024u;
+    const uint64_t bm = __ballot(fin && inkey);
+    if (bm) {
+        const int n = (int)__popcll(bm);
+        if (qn + n > SC_QUEUE) {
+            sc_drain_cells(sh, lane, qk, qv, qn, L, grad);
+            qn = 0;
+        }
+        if (fin && inkey) {
+            const int p = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
+            qk[p] = st.px | (st.py << 11) | (st.pz << 22);
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+                qv[4 * p + g] = make_float4(st.v[4 * g], st.v[4 * g + 1], st.v[4 * g + 2], st.v[4 * g + 3]);
+        }
+        qn += n;
+    }
+    if (__ballot(fin && !inkey)) {  // uniform: (not on the configs' levels) straight to global memory
+        if (fin && !inkey) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const uint32_t e = L.off + sc_corner_entry(L, st.px, st.py, st.pz, c);
+                if (st.v[2 * c] != 0.f) atomicAdd(grad + 2 * (size_t)e, st.v[2 * c]);
+                if (st.v[2 * c + 1] != 0.f) atomicAdd(grad + 2 * (size_t)e + 1, st.v[2 * c + 1]);
+            }
+        }
+    }
+}
 template <int C>
 __device__ __forceinline__ void sc_cells_run(ScShared& sh, int lane, const ScChunk<C>& ch, const ScLevel& L,
-                                             float* __restrict__ grad, ScRun& st, bool last) {
+                                             float* __restrict__ grad, ScRun& st, bool last, uint32_t* qk, float4* qv,
+                                             int& qn) {
 #pragma unroll
     for (int i = 0; i < C; i++) {
         const LevelPos q = level_pos(L.scale, ch.x[i], ch.y[i], ch.z[i]);
         const bool change = st.init && (q.px != st.px || q.py != st.py || q.pz != st.pz);
-        if (__ballot(change && st.any))  // uniform
-            sc_add_cell(sh, lane, change && st.any, st.px, st.py, st.pz, st.v, L, grad);
+        sc_push_run(sh, lane, change && st.any, st, qk, qv, qn, L, grad);
         if (change || !st.init) {
 #pragma unroll
             for (int j = 0; j < 16; j++) st.v[j] = 0.f;
@@ -1458,8 +1540,11 @@ __device__ __forceinline__ void sc_cells_run(ScShared& sh, int lane, const ScChu
         st.any = st.any || ch.g[i].x != 0.f || ch.g[i].y != 0.f;
         sc_corner_sums(q, ch.g[i], st.v);
     }
-    if (last && __ballot(st.any))  // uniform: the unit's last run
-        sc_add_cell(sh, lane, st.any, st.px, st.py, st.pz, st.v, L, grad);
+    if (last) {  // the unit's last runs, then the rest of the queue
+        sc_push_run(sh, lane, st.any, st, qk, qv, qn, L, grad);
+        if (qn) sc_drain_cells(sh, lane, qk, qv, qn, L, grad);
+        qn = 0;
+    }
 }
 
 // Flush of a cell unit: 16 lanes per claimed cell (one corner component each), form the corner's
@@ -1505,7 +1590,8 @@ __device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m
     L.direct = !isfinite(m);  // (uniform) non-finite gradient: every corner straight to global memory
     int e2 = 0;
     (void)frexpf(L.direct ? 1.f : m, &e2);  // m < 2^e2
-    // |sum| <= (unit samples) * m * 2^k + rounding (a sample's 8 corner weights sum to 1): < 2^62
+    // |sum| <= (unit samples) * m * 2^k + rounding (a sample's 8 corner weights sum to 1): < 2^62,
+    // and every addend (a run's corner sum) < 2^51, sc_fix's range (the callers' kbase)
     L.k = kbase - e2;
     return L;
 }
@@ -1515,7 +1601,7 @@ __device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int C, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
                                         const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
-                                        const int32_t* __restrict__ order) {
+                                        const int32_t* __restrict__ order, bool perm) {
     SC_TNOW(t0);
     // (a fine unit holds at most 4096 samples: 2^46 leaves the sums four bits of headroom below 2^62)
     const ScLevel L = sc_level(Lt, l, m, 46);
@@ -1533,13 +1619,16 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     const int NG = SC_THREADS * C / 128;
     int k = wid;
     ScChunk<2> cg;
-    sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + k) * 2, s1, xyzs, dEl, de, nrm, order);
+    // (positions: the class array holds grab k's 64 chunks of 2 side by side, sc_perm)
+#define SC_GRAB_S(k) (s0 + ((int64_t)lane * NG + (k)) * 2)
+#define SC_GRAB_P(k) (perm ? s0 + ((int64_t)(k) * 64 + lane) * 2 : SC_GRAB_S(k))
+    sc_load_chunk<2>(cg, SC_GRAB_S(k), SC_GRAB_P(k), s1, xyzs, dEl, de, nrm, order);
     while (k < NG) {  // (wave-uniform)
         sc_direct<2>(sh, lane, cg, L, grad);
         int kn = 0;
         if (lane == 0) kn = atomicAdd(sh.grab, 1);
         kn = __builtin_amdgcn_readfirstlane(kn) + SC_WAVES;
-        if (kn < NG) sc_load_chunk<2>(cg, s0 + ((int64_t)lane * NG + kn) * 2, s1, xyzs, dEl, de, nrm, order);
+        if (kn < NG) sc_load_chunk<2>(cg, SC_GRAB_S(kn), SC_GRAB_P(kn), s1, xyzs, dEl, de, nrm, order);
         k = kn;
     }
     SC_TNOW(t2);
@@ -1597,24 +1686,106 @@ template <int C>
 __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1, int rounds,
                                              const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
                                              const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
-                                             const int32_t* __restrict__ order) {
+                                             const int32_t* __restrict__ order, bool perm) {
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
-    const ScLevel L = sc_level(Lt, l, m, 61 - lg_unit);
+    // scale 2^k, k = 60 - lg_unit - e: the unit's sum of every corner stays below 2^61, and one run
+    // (at most rounds x C <= 2^(lg_unit - 10) samples) below 2^(50) — sc_fix needs |addend| < 2^51
+    const ScLevel L = sc_level(Lt, l, m, 60 - lg_unit);
     const int64_t lane_off = ((int64_t)lane * SC_WAVES + wid) * rounds * C;
     ScRun st;
     st.init = st.any = false;
     st.px = st.py = st.pz = 0;
+    uint32_t* qk = sh.qkey + wid * SC_QUEUE;  // (this wave's run queue)
+    float4* qv = sh.qval + wid * SC_QUEUE * 4;
+    int qn = 0;
     for (int r = 0; r < rounds; r++) {
         ScChunk<C> ch;
-        sc_load_chunk<C>(ch, s0 + lane_off + (int64_t)r * C, s1, xyzs, dEl, de, nrm, order);
+        // (positions: the class array holds a round's 64 chunks of a wave side by side, sc_perm)
+        const int64_t sb = s0 + lane_off + (int64_t)r * C;
+        sc_load_chunk<C>(ch, sb, perm ? s0 + (((int64_t)r * SC_WAVES + wid) * 64 + lane) * C : sb, s1, xyzs, dEl, de, nrm,
+                         order);
         if (L.direct)
             sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
         else
-            sc_cells_run<C>(sh, lane, ch, L, grad, st, r + 1 == rounds);
+            sc_cells_run<C>(sh, lane, ch, L, grad, st, r + 1 == rounds, qk, qv, qn);
     }
     lds_barrier();
     sc_flush_cells(sh, L, grad);
     lds_barrier();
+}
+
+// Unit classes by the sample layout their loads use: coarse levels 0-5 (rounds NCN_SC_R_LO) and 6-9
+// (NCN_SC_R_MID), fine levels 10-14 (C = 4) and 15 (C = 2).
+constexpr int SC_N_CLASSES = 4;
+__host__ __device__ constexpr int sc_class(int l) { return l < 6 ? 0 : l < SC_CELL_HI ? 1 : l < 15 ? 2 : 3; }
+constexpr int64_t SC_MAX_SPAN = (int64_t)SC_THREADS * SC_C_CELL * NCN_SC_R_LO;
+static_assert(sc_cell_rounds(0) == NCN_SC_R_LO && NCN_SC_R_LO >= NCN_SC_R_MID && sc_fine_c(10) <= SC_C_CELL, "spans");
+// the permuted positions' row length (every class array holds whole units)
+__host__ __device__ constexpr int64_t sc_perm_stride(int64_t n_stride) {
+    return (n_stride + SC_MAX_SPAN - 1) / SC_MAX_SPAN * SC_MAX_SPAN;
+}
+// Where sample s sits in its class's permuted position array: the samples a wave loads in one
+// instruction lie side by side, so a coarse round or a fine grab reads one contiguous stretch
+// (coalesced) while each lane keeps its own consecutive samples (the runs).  Coarse: lane t of wave
+// w owns the unit's slice t * 16 + w of 4R samples and reads chunk r in round r; fine: lane t reads
+// the pair t * NG + k in grab k.  A chunk (4 coarse / 2 fine samples) stays contiguous.
+__device__ __forceinline__ int64_t sc_perm(int64_t s, int cls) {
+    if (cls < 2) {
+        const int R = sc_cell_rounds(cls == 0 ? 0 : 6), CR = SC_C_CELL * R;
+        const int64_t U = (int64_t)SC_THREADS * CR, o = s % U;
+        const int64_t slice = o / CR, within = o % CR;
+        const int64_t t = slice / SC_WAVES, w = slice % SC_WAVES, r = within / SC_C_CELL, i = within % SC_C_CELL;
+        return (s - o) + ((r * SC_WAVES + w) * 64 + t) * SC_C_CELL + i;
+    }
+    const int C = sc_fine_c(cls == 2 ? 10 : 15), NG = SC_THREADS * C / 128;
+    const int64_t U = (int64_t)SC_THREADS * C, o = s % U;
+    const int64_t pair = o >> 1, t = pair / NG, k = pair % NG;
+    return (s - o) + (k * 64 + t) * 2 + (o & 1);
+}
+
+// The sample positions in the permuted order of each class the scatter needs (class_mask), into
+// the dE workspace behind the encoding gradient: a thread takes 4 consecutive samples (one 48-B
+// piece in, one 48-B coarse chunk / two 24-B fine pairs out per class).
+__global__ __launch_bounds__(256) void sc_perm_positions_kernel(const float* __restrict__ xyzs, int64_t n_stride,
+                                                                const int32_t* __restrict__ n_dev, int class_mask,
+                                                                float* __restrict__ xyz_perm, float* __restrict__ flag) {
+    const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 1.f;
+    const int64_t ps = sc_perm_stride(n_stride);
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; 4 * j < n; j += (int64_t)gridDim.x * 256) {
+        const int64_t sb = 4 * j;
+        float v[12];
+        if (sb + 4 <= n) {
+            const float4* px = (const float4*)(xyzs + 3 * sb);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const float4 f = px[q];
+                v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 12; i++) v[i] = sb + i / 3 < n ? xyzs[3 * sb + i] : 0.f;
+        }
+#pragma unroll
+        for (int cls = 0; cls < SC_N_CLASSES; cls++) {
+            if (!((class_mask >> cls) & 1)) continue;
+            float* out = xyz_perm + cls * 3 * ps;
+            if (cls < 2) {  // the 4 samples are one chunk
+                float4* po = (float4*)(out + 3 * sc_perm(sb, cls));
+                po[0] = make_float4(v[0], v[1], v[2], v[3]);
+                po[1] = make_float4(v[4], v[5], v[6], v[7]);
+                po[2] = make_float4(v[8], v[9], v[10], v[11]);
+            } else {  // two pairs
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    float2* po = (float2*)(out + 3 * sc_perm(sb + 2 * h, cls));
+                    po[0] = make_float2(v[6 * h], v[6 * h + 1]);
+                    po[1] = make_float2(v[6 * h + 2], v[6 * h + 3]);
+                    po[2] = make_float2(v[6 * h + 4], v[6 * h + 5]);
+                }
+            }
+        }
+    }
 }
 
 // One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
@@ -1622,7 +1793,7 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
                                             char* arena, int* fill, const float* lmax_s, int wid, int lane,
                                             const float* __restrict__ xyzs, const uint32_t* __restrict__ dE,
                                             int64_t e_stride, const ScDE& de, const ScNorm& nrm, const LevelTable& Lt,
-                                            float* __restrict__ grad, const int32_t* __restrict__ order) {
+                                            float* __restrict__ grad, const int32_t* __restrict__ order, bool perm) {
     int l = level_lo;
     int64_t v = u, span = sc_unit_span(l);
     for (;; l++) {  // (uniform, at most 16 steps) level-major unit order
@@ -1656,10 +1827,12 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
     if (threadIdx.x == 0) { fill[par ^ 1] = 0; fill[2 + (par ^ 1)] = 0; }
     par ^= 1;
     const uint32_t* dEl = dE + (int64_t)l * e_stride;
+    // (positions: the level's class array, or the sample-ordered ones)
+    if (perm) xyzs = xyzs + sc_class(l) * 3 * sc_perm_stride(e_stride);
     if (mode == SC_MODE_CELL)
-        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order);
+        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order, perm);
     else
-        sc_unit(sh, wid, lane, l, sc_fine_c(l), s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order);
+        sc_unit(sh, wid, lane, l, sc_fine_c(l), s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order, perm);
 }
 
 __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
@@ -1711,6 +1884,10 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     de.inv = dE_ws[0];
     de.bf16 = dE_ws[1] != 0.f;
     const uint32_t* dE = (const uint32_t*)(dE_ws + DE_HEADER_FLOATS);
+    // positions: permuted per class behind dE when the MLP pass (or ncn_field_scatter_positions)
+    // wrote them there (header flag), else the sample-ordered xyzs (strided loads)
+    const bool perm = !order && dE_ws[DE_POS_FLAG] == 1.f;
+    if (perm) xyzs = dE_ws + DE_HEADER_FLOATS + 16 * e_stride;
     // units, level-major over the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell
     // levels [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
     int64_t n_units = 0;
@@ -1727,7 +1904,7 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // ones, leave workgroups a second heavy unit.)
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x)
         sc_one_unit(u, n, level_lo, layout, par, sh, arena, fill, lmax_s, wid, lane, xyzs, dE, e_stride, de, nrm, Lt, grad,
-                    order);
+                    order, perm);
 }
 
 static int scatter_grid(int64_t n_cap) {
@@ -1758,18 +1935,18 @@ static int fwd_grid(int64_t n) {
 using namespace ncn;
 
 template <int PART>
-static void launch_bwd_part(int precision, int nb, hipStream_t st, const float* dirs, int64_t n, const int32_t* n_dev,
-                            const uint16_t* wp, const uint16_t* enc, const float* dsig, const float* drgb,
-                            const float* loss_scale, float* dE_ws, float* slab, float* level_max,
+static void launch_bwd_part(int precision, int nb, hipStream_t st, const float* xyzs, const float* dirs, int64_t n,
+                            const int32_t* n_dev, const uint16_t* wp, const uint16_t* enc, const float* dsig,
+                            const float* drgb, const float* loss_scale, float* dE_ws, float* slab, float* level_max,
                             const int32_t* order, const float* dsig2, float* stash) {
     if (precision == NCN_PREC_F16)
         hipLaunchKernelGGL((field_bwd_kernel<_Float16, PART>), dim3(nb), dim3(BWD_THREADS), 0, st, dirs, n, n_dev, wp,
                            (const Mfma<_Float16>::v8*)enc, dsig, drgb, loss_scale, dE_ws, slab, level_max, order, dsig2,
-                           stash);
+                           stash, xyzs);
     else
         hipLaunchKernelGGL((field_bwd_kernel<__bf16, PART>), dim3(nb), dim3(BWD_THREADS), 0, st, dirs, n, n_dev, wp,
                            (const Mfma<__bf16>::v8*)enc, dsig, drgb, loss_scale, dE_ws, slab, level_max, order, dsig2,
-                           stash);
+                           stash, xyzs);
 }
 
 extern "C" {
@@ -1847,9 +2024,14 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
 
 int ncn_field_bwd_blocks(int64_t n) { return bwd_blocks_of(n); }
 
-int64_t ncn_field_bwd_dE_floats(int64_t n) { return n > 0 ? DE_HEADER_FLOATS + 16 * ((n + 3) & ~(int64_t)3) : 0; }
+int64_t ncn_field_bwd_dE_floats(int64_t n) {
+    if (n <= 0) return 0;
+    const int64_t e_stride = (n + 3) & ~(int64_t)3;
+    // header, the level-major encoding gradient, then the scatter's permuted positions per class
+    return DE_HEADER_FLOATS + 16 * e_stride + SC_N_CLASSES * 3 * sc_perm_stride(e_stride);
+}
 
-int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+int ncn_field_bwd_mlp(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint16_t* weights_packed,
                       int precision, const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs,
                       const float* loss_scale, float* slab, float* dE_ws, float* level_max, void* stream) {
@@ -1859,14 +2041,10 @@ int ncn_field_bwd_mlp(const float* dirs, int64_t n, const int32_t* n_dev, const 
     NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)enc_cache & 15) == 0 && ((uintptr_t)weights_packed & 15) == 0,
                 hipErrorInvalidValue, "ncn_field_bwd_mlp: dE_ws / enc_cache / weights_packed must be 16-byte aligned");
     NCN_REQUIRE(level_max != nullptr, hipErrorInvalidValue, "ncn_field_bwd_mlp: level_max workspace required");
-    if (precision == NCN_PREC_F16)
-        hipLaunchKernelGGL(field_bwd_kernel<_Float16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
-                           (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<_Float16>::v8*)enc_cache,
-                           dL_dsigmas, dL_drgbs, loss_scale, dE_ws, slab, level_max, order);
-    else
-        hipLaunchKernelGGL(field_bwd_kernel<__bf16>, dim3(ncn_field_bwd_blocks(n)), dim3(BWD_THREADS), 0,
-                           (hipStream_t)stream, dirs, n, n_dev, weights_packed, (const Mfma<__bf16>::v8*)enc_cache,
-                           dL_dsigmas, dL_drgbs, loss_scale, dE_ws, slab, level_max, order);
+    NCN_REQUIRE(((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue, "ncn_field_bwd_mlp: xyzs must be 16-byte aligned");
+    launch_bwd_part<BWD_ALL>(precision, ncn_field_bwd_blocks(n), (hipStream_t)stream, xyzs, dirs, n, n_dev,
+                             weights_packed, enc_cache, dL_dsigmas, dL_drgbs, loss_scale, dE_ws, slab, level_max, order,
+                             nullptr, nullptr);
     NCN_LAUNCH_CHECK("ncn_field_bwd_mlp");
     return 0;
 }
@@ -1880,7 +2058,7 @@ int ncn_field_bwd_part_blocks(int64_t n, int part) {
     return part == 2 ? std::min(512, 2 * nb) : nb;
 }
 
-int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
+int ncn_field_bwd_mlp_part(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
                            const uint16_t* weights_packed, int precision, const uint16_t* enc_cache,
                            const float* dL_dsigmas, const float* dL_dsigmas2, const float* dL_drgbs,
                            const float* loss_scale, int part, int n_blocks, float* slab, float* dE_ws,
@@ -1899,13 +2077,13 @@ int ncn_field_bwd_mlp_part(const float* dirs, int64_t n, const int32_t* n_dev, c
                                 : ncn_field_bwd_part_blocks(n, part);
     const hipStream_t st = (hipStream_t)stream;
     if (part == 1)
-        launch_bwd_part<1>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
+        launch_bwd_part<1>(precision, nb, st, xyzs, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
                            loss_scale, dE_ws, slab, level_max, order, dL_dsigmas2, dh_stash);
     else if (part == 2)
-        launch_bwd_part<2>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
+        launch_bwd_part<2>(precision, nb, st, xyzs, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
                            loss_scale, dE_ws, slab, level_max, order, dL_dsigmas2, dh_stash);
     else
-        launch_bwd_part<3>(precision, nb, st, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
+        launch_bwd_part<3>(precision, nb, st, xyzs, dirs, n, n_dev, weights_packed, enc_cache, dL_dsigmas, dL_drgbs,
                            loss_scale, dE_ws, slab, level_max, order, dL_dsigmas2, dh_stash);
     NCN_LAUNCH_CHECK("ncn_field_bwd_mlp_part");
     return 0;
@@ -1931,6 +2109,18 @@ int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, 
     return 0;
 }
 
+int ncn_field_scatter_positions(const float* xyzs, int64_t n, const int32_t* n_dev, float* dE_ws, void* stream) {
+    if (n <= 0) return 0;
+    NCN_REQUIRE(((uintptr_t)dE_ws & 15) == 0 && ((uintptr_t)xyzs & 15) == 0, hipErrorInvalidValue,
+                "ncn_field_scatter_positions: dE_ws and xyzs must be 16-byte aligned");
+    const int64_t e_stride = (n + 3) & ~(int64_t)3;
+    const int pgrid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, cdiv(cdiv(n, 4), 256)));
+    hipLaunchKernelGGL(sc_perm_positions_kernel, dim3(pgrid), dim3(256), 0, (hipStream_t)stream, xyzs, n, n_dev,
+                       (1 << SC_N_CLASSES) - 1, dE_ws + DE_HEADER_FLOATS + 16 * e_stride, dE_ws + DE_POS_FLAG);
+    NCN_LAUNCH_CHECK("ncn_field_scatter_positions");
+    return 0;
+}
+
 int ncn_field_scatter(const float* xyzs, int64_t n, const int32_t* n_dev, const int32_t* order,
                       const uint32_t* levels, float xyz_min,
                       float xyz_extent, const float* dE_ws, const float* level_max, int level_lo, int level_hi,
@@ -1945,7 +2135,7 @@ int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
                   const uint16_t* enc_cache, const float* dL_dsigmas, const float* dL_drgbs, const float* loss_scale,
                   float* grad_table, float* slab, float* dE_ws, float* level_max, void* stream) {
     if (n <= 0) return 0;
-    const int e = ncn_field_bwd_mlp(dirs, n, n_dev, order, weights_packed, precision, enc_cache, dL_dsigmas, dL_drgbs,
+    const int e = ncn_field_bwd_mlp(xyzs, dirs, n, n_dev, order, weights_packed, precision, enc_cache, dL_dsigmas, dL_drgbs,
                                     loss_scale, slab, dE_ws, level_max, stream);
     if (e) return e;
     return ncn_field_scatter(xyzs, n, n_dev, order, levels, xyz_min, xyz_extent, dE_ws, level_max, 0, 16, 0,

@@ -58,11 +58,12 @@ SIGNATURES = {
     "ncn_field_bwd_blocks": [I64],
     "ncn_field_bwd_dE_floats": [I64],
     "ncn_field_bwd": [P, P, I64, P, P, P, F32, F32, P, I32, P, P, P, P, P, P, P, P, P],
-    "ncn_field_bwd_mlp": [P, I64, P, P, P, I32, P, P, P, P, P, P, P, P],
+    "ncn_field_bwd_mlp": [P, P, I64, P, P, P, I32, P, P, P, P, P, P, P, P],
     "ncn_field_bwd_stash_floats": [I64],
     "ncn_field_bwd_part_blocks": [I64, I32],
     "ncn_field_reduce_wgrad_parts": [P, I32, I32, P, P],
-    "ncn_field_bwd_mlp_part": [P, I64, P, P, P, I32, P, P, P, P, P, I32, I32, P, P, P, P, P],
+    "ncn_field_bwd_mlp_part": [P, P, I64, P, P, P, I32, P, P, P, P, P, I32, I32, P, P, P, P, P],
+    "ncn_field_scatter_positions": [P, I64, P, P, P],
     "ncn_field_scatter": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P],
     "ncn_field_scatter_wgrad": [P, I64, P, P, P, F32, F32, P, P, I32, I32, I32, P, P, I32, I32, P, P],
     "ncn_field_reduce_wgrad": [P, I32, P, P],

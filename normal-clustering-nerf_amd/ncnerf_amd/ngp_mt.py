@@ -107,7 +107,7 @@ class _FieldFunction(torch.autograd.Function):
                  ptr(model._bwd_loss_scale()), ptr(g_table), ptr(slab), ptr(dE_ws), ptr(model._level_max()), stream())
         else:
             lmax = model._level_max()
-            call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(model._prec), ptr(enc),
+            call("ncn_field_bwd_mlp", ptr(x), ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(model._prec), ptr(enc),
                  ptr(dsig), ptr(drgb), ptr(model._bwd_loss_scale()),
                  ptr(slab), ptr(dE_ws), ptr(lmax), stream())
             model._scatter(x, n, n_dev, order, dE_ws, lmax, g_table)

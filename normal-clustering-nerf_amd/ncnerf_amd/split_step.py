@@ -164,7 +164,7 @@ class SplitStep:
         g_table, g_w = m._grad_views()
 
         def mlp_part(part, dsig, drw):
-            call("ncn_field_bwd_mlp_part", ptr(dirs), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec),
+            call("ncn_field_bwd_mlp_part", ptr(xyzs), ptr(dirs), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec),
                  ptr(enc), ptr(dsig), ptr(None), ptr(drw), ptr(scale), I32(part), I32(nb[part - 1]), ptr(slab),
                  ptr(dE_ws),
                  ptr(lmax), ptr(stash), stream())

@@ -63,7 +63,7 @@ def test_mlp_parts_equal_one_pass(dev, precision, n, sort):
         slab = torch.full((nb_full * N_W,), float("nan"), device=dev)
         dE = torch.zeros(dE_n, device=dev)
         lmax = torch.full((16 * 256,), -1.0, device=dev)
-        _lib.call("ncn_field_bwd_mlp", ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec), ptr(enc),
+        _lib.call("ncn_field_bwd_mlp", ptr(x), ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec), ptr(enc),
                   ptr(dsig), ptr(drgb), ptr(scale), ptr(slab), ptr(dE), ptr(lmax), stream())
         return slab, dE, lmax
 
@@ -75,7 +75,7 @@ def test_mlp_parts_equal_one_pass(dev, precision, n, sort):
         lmax = torch.full((16 * 256,), -1.0, device=dev)
         stash = torch.empty(int(L.ncn_field_bwd_stash_floats(I64(n))), device=dev)
         for part, ds, nb in ((1, None, nb1), (2, dsig, nb2)):
-            _lib.call("ncn_field_bwd_mlp_part", ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec),
+            _lib.call("ncn_field_bwd_mlp_part", ptr(x), ptr(d), I64(n), ptr(n_dev), ptr(order), ptr(packed), I32(m._prec),
                       ptr(enc), ptr(ds), ptr(None), ptr(drgb), ptr(scale), I32(part), I32(nb), ptr(slab), ptr(dE),
                       ptr(lmax), ptr(stash), stream())
         w = torch.zeros(N_W, device=dev)

@@ -68,7 +68,7 @@ def prepare(sorted_):
     fwd = lambda: main.ncn_field_fwd(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(o), ptr(table),  # noqa: E731
                                      model._levels_ptr, F32(model._xyz_min), F32(model._xyz_extent), ptr(packed),
                                      I32(0), I32(0), ptr(sig), ptr(rgb), ptr(enc), stream())
-    mlp = lambda: main.ncn_field_bwd_mlp(ptr(dirs), I64(n), ptr(None), ptr(o), ptr(packed), I32(0), ptr(enc),  # noqa: E731
+    mlp = lambda: main.ncn_field_bwd_mlp(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(o), ptr(packed), I32(0), ptr(enc),  # noqa: E731
                                          ptr(dsig), ptr(drgb), ptr(None), ptr(slab), ptr(dE), ptr(lmax), stream())
     print(f"  field_fwd {ev_time(fwd):7.1f} us   bwd_mlp {ev_time(mlp):7.1f} us", flush=True)
     return sig.clone(), rgb.clone()
