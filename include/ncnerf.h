@@ -253,8 +253,9 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * ncn_field_bwd_dE_floats(n) floats: a 4-float header, the level-major encoding gradient between the
  * MLP pass and the LDS-aggregating table scatter pass, and the sample positions xyzs in the
  * scatter's load order (four copies, one per unit class: a wave's round / grab reads one contiguous
- * stretch).  The MLP pass writes those positions (its rgb part; not with `order`) and marks them in
- * the header; the scatter uses them when marked, else reads xyzs in sample order. */
+ * stretch).  The MLP pass (its rgb part; not with `order`) writes the two coarse classes' positions
+ * and marks them in the header (a class mask); the scatter reads a marked class's copy, and xyzs in
+ * sample order for the others. */
 int ncn_field_bwd_blocks(int64_t n);
 int64_t ncn_field_bwd_dE_floats(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,

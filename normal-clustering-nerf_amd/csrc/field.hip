@@ -520,7 +520,14 @@ constexpr int DE_HEADER_FLOATS = 4;  // the dE workspace's header (ncn_field_bwd
 // the positions in it, DE_POS_READY in the header)
 __host__ __device__ constexpr int64_t sc_perm_stride(int64_t n_stride);
 __device__ __forceinline__ int64_t sc_perm(int64_t s, int cls);
-constexpr int DE_POS_FLAG = 2;  // header float: 1 when the workspace holds the permuted positions
+constexpr int DE_POS_FLAG = 2;  // header float: the mask of unit classes whose permuted positions the workspace holds
+// The MLP pass writes the coarse classes' positions only: the coarse units' strided loads cost
+// 16-20 us per unit, the fine units' grabs measured no faster from permuted positions (round 6,
+// profiles/round6/scatter_probe_perm.log), and the writes run beside the clustering.
+#ifndef NCN_POS_MLP_CLASSES
+#define NCN_POS_MLP_CLASSES 2
+#endif
+constexpr int DE_POS_MLP_CLASSES = NCN_POS_MLP_CLASSES;
 constexpr int BWD_WAVES = 8;
 constexpr int BWD_THREADS = 64 * BWD_WAVES;
 // exchange tiles per group: dW operands, A = dY^T, B = X^T (16 features x 16 samples)
@@ -897,7 +904,8 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const float* pos_src = ((PART & BWD_RGB) != 0 && dE_out && !order) ? xyzs : nullptr;
     float* const pos_out = pos_src ? dE_out + DE_HEADER_FLOATS + 16 * n_stride : nullptr;
     const int64_t pos_stride = sc_perm_stride(n_stride);
-    if ((PART & BWD_RGB) != 0 && dE_out && blockIdx.x == 0 && threadIdx.x == 0) dE_out[DE_POS_FLAG] = pos_out ? 1.f : 0.f;
+    if ((PART & BWD_RGB) != 0 && dE_out && blockIdx.x == 0 && threadIdx.x == 0)
+        dE_out[DE_POS_FLAG] = pos_out ? (float)((1 << DE_POS_MLP_CLASSES) - 1) : 0.f;
     const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
     // split passes' stash (ncn_field_bwd_stash_floats): [groups][64] operand tiles, then [groups][16]
     // fp32 row-0 elements (capacity groups: the layout does not depend on the device count)
@@ -945,7 +953,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order,
                               S, pos_src);
         if (grp < n_groups) {
-            if ((PART & BWD_RGB) != 0 && pos_out && grp * 16 + (lane & 15) < n) {
+            if ((PART & BWD_RGB) != 0 && pos_out && (lane >> 4) < DE_POS_MLP_CLASSES && grp * 16 + (lane & 15) < n) {
                 const int cls = lane >> 4;
                 float* po = pos_out + cls * 3 * pos_stride + 3 * sc_perm(grp * 16 + (lane & 15), cls);
                 po[0] = cur.px; po[1] = cur.py; po[2] = cur.pz;
@@ -1420,12 +1428,28 @@ struct ScRun {
     float v[16];
 };
 
+// Diagnostic builds (tools/scatter_probe.py): NCN_DIAG_SC_TIMES records wave 0's cycles per phase of
+// the fine-level units; NCN_DIAG_SC_LEVELS_MASK skips the levels whose bit is clear.
+#ifdef NCN_DIAG_SC_TIMES
+__device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: cycles per phase
+#define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
+#define SC_TADD(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2 + 1] += (b) - (a)
+#define SC_TADDC(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2] += (b) - (a)
+#define SC_TWAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#else
+#define SC_TNOW(v)
+#define SC_TADD(i, a, b)
+#define SC_TADDC(i, a, b)
+#define SC_TWAIT()
+#endif
+
 // The wave's queued runs [0, qn) into the cell table, one run per lane: one set read and claim per
 // run, the 16 sums as fixed-point ds_add_u64 in four float4 groups; a run whose set is full goes to
 // global f32 atomics.
 __device__ __forceinline__ void sc_drain_cells(ScShared& sh, int lane, const uint32_t* qk, const float4* qv, int qn,
                                                const ScLevel& L, float* __restrict__ grad) {
     asm volatile("" ::: "memory");  // (the wave's queue writes come first: a wave's LDS operations execute in order)
+    SC_TNOW(td0);
     const bool act = lane < qn;
     const uint32_t key = act ? qk[lane] : 0u;
     const int p0 = SC_WAYS * (int)sc_set(key, sh.sets);
@@ -1487,6 +1511,9 @@ __device__ __forceinline__ void sc_drain_cells(ScShared& sh, int lane, const uin
                 (uint16_t)sl;
     }
     asm volatile("" ::: "memory");  // (the queue is rewritten after these reads)
+    SC_TWAIT();
+    SC_TNOW(td1);
+    SC_TADDC(2, td0, td1);
 }
 
 // Queue the finished runs of the lanes with `fin` (whole wave calls; qn wave-uniform): a full queue
@@ -1569,16 +1596,6 @@ __device__ __forceinline__ void sc_flush_cells(ScShared& sh, const ScLevel& L, f
     }
 }
 
-// Diagnostic builds (tools/scatter_probe.py): NCN_DIAG_SC_TIMES records wave 0's cycles per phase of
-// the fine-level units; NCN_DIAG_SC_LEVELS_MASK skips the levels whose bit is clear.
-#ifdef NCN_DIAG_SC_TIMES
-__device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: cycles per phase
-#define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
-#define SC_TADD(i, a, b) if (threadIdx.x == 0 && blockIdx.x < 256) ncn_sc_times[blockIdx.x][(i) * 2 + 1] += (b) - (a)
-#else
-#define SC_TNOW(v)
-#define SC_TADD(i, a, b)
-#endif
 
 __device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m, int kbase) {
     ScLevel L;
@@ -1702,16 +1719,28 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
         ScChunk<C> ch;
         // (positions: the class array holds a round's 64 chunks of a wave side by side, sc_perm)
         const int64_t sb = s0 + lane_off + (int64_t)r * C;
+        SC_TNOW(tc0);
         sc_load_chunk<C>(ch, sb, perm ? s0 + (((int64_t)r * SC_WAVES + wid) * 64 + lane) * C : sb, s1, xyzs, dEl, de, nrm,
                          order);
+        SC_TWAIT();
+        SC_TNOW(tc1);
+        SC_TADDC(0, tc0, tc1);
         if (L.direct)
             sc_direct<C>(sh, lane, ch, L, grad);  // (sc_add's direct form: f32 global adds, NaN/Inf propagate)
         else
             sc_cells_run<C>(sh, lane, ch, L, grad, st, r + 1 == rounds, qk, qv, qn);
+        SC_TWAIT();
+        SC_TNOW(tc2);
+        SC_TADDC(1, tc1, tc2);  // (run work including the drains, which add to slot 2 as well)
     }
+    SC_TNOW(tc3);
     lds_barrier();
+    SC_TNOW(tc4);
     sc_flush_cells(sh, L, grad);
     lds_barrier();
+    SC_TNOW(tc5);
+    SC_TADDC(3, tc3, tc4);
+    SC_TADDC(4, tc4, tc5);
 }
 
 // Unit classes by the sample layout their loads use: coarse levels 0-5 (rounds NCN_SC_R_LO) and 6-9
@@ -1748,9 +1777,10 @@ __device__ __forceinline__ int64_t sc_perm(int64_t s, int cls) {
 // piece in, one 48-B coarse chunk / two 24-B fine pairs out per class).
 __global__ __launch_bounds__(256) void sc_perm_positions_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                 const int32_t* __restrict__ n_dev, int class_mask,
-                                                                float* __restrict__ xyz_perm, float* __restrict__ flag) {
+                                                                float* __restrict__ xyz_perm, float* __restrict__ flag,
+                                                                float flag_value) {
     const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 1.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = flag_value;
     const int64_t ps = sc_perm_stride(n_stride);
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; 4 * j < n; j += (int64_t)gridDim.x * 256) {
         const int64_t sb = 4 * j;
@@ -1791,9 +1821,10 @@ __global__ __launch_bounds__(256) void sc_perm_positions_kernel(const float* __r
 // One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
 __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, int& layout, int& par, ScShared& sh,
                                             char* arena, int* fill, const float* lmax_s, int wid, int lane,
-                                            const float* __restrict__ xyzs, const uint32_t* __restrict__ dE,
+                                            const float* __restrict__ xyzs, const float* __restrict__ pos, int perm_mask,
+                                            const uint32_t* __restrict__ dE,
                                             int64_t e_stride, const ScDE& de, const ScNorm& nrm, const LevelTable& Lt,
-                                            float* __restrict__ grad, const int32_t* __restrict__ order, bool perm) {
+                                            float* __restrict__ grad, const int32_t* __restrict__ order) {
     int l = level_lo;
     int64_t v = u, span = sc_unit_span(l);
     for (;; l++) {  // (uniform, at most 16 steps) level-major unit order
@@ -1828,7 +1859,8 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
     par ^= 1;
     const uint32_t* dEl = dE + (int64_t)l * e_stride;
     // (positions: the level's class array, or the sample-ordered ones)
-    if (perm) xyzs = xyzs + sc_class(l) * 3 * sc_perm_stride(e_stride);
+    const bool perm = (perm_mask >> sc_class(l)) & 1;
+    if (perm) xyzs = pos + sc_class(l) * 3 * sc_perm_stride(e_stride);
     if (mode == SC_MODE_CELL)
         sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order, perm);
     else
@@ -1884,10 +1916,10 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     de.inv = dE_ws[0];
     de.bf16 = dE_ws[1] != 0.f;
     const uint32_t* dE = (const uint32_t*)(dE_ws + DE_HEADER_FLOATS);
-    // positions: permuted per class behind dE when the MLP pass (or ncn_field_scatter_positions)
-    // wrote them there (header flag), else the sample-ordered xyzs (strided loads)
-    const bool perm = !order && dE_ws[DE_POS_FLAG] == 1.f;
-    if (perm) xyzs = dE_ws + DE_HEADER_FLOATS + 16 * e_stride;
+    // positions: a unit class's permuted copy behind dE when the MLP pass (or
+    // ncn_field_scatter_positions) wrote it (header mask), else the sample-ordered xyzs (strided loads)
+    const int perm_mask = order ? 0 : (int)dE_ws[DE_POS_FLAG];
+    const float* pos = dE_ws + DE_HEADER_FLOATS + 16 * e_stride;
     // units, level-major over the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell
     // levels [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
     int64_t n_units = 0;
@@ -1903,8 +1935,8 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // 4/8 225-230, 2/8 210, 16/4 237, 8/16 317 — more than 256 coarse units, or a few very long
     // ones, leave workgroups a second heavy unit.)
     for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x)
-        sc_one_unit(u, n, level_lo, layout, par, sh, arena, fill, lmax_s, wid, lane, xyzs, dE, e_stride, de, nrm, Lt, grad,
-                    order, perm);
+        sc_one_unit(u, n, level_lo, layout, par, sh, arena, fill, lmax_s, wid, lane, xyzs, pos, perm_mask, dE, e_stride, de,
+                    nrm, Lt, grad, order);
 }
 
 static int scatter_grid(int64_t n_cap) {
@@ -2116,7 +2148,8 @@ int ncn_field_scatter_positions(const float* xyzs, int64_t n, const int32_t* n_d
     const int64_t e_stride = (n + 3) & ~(int64_t)3;
     const int pgrid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, cdiv(cdiv(n, 4), 256)));
     hipLaunchKernelGGL(sc_perm_positions_kernel, dim3(pgrid), dim3(256), 0, (hipStream_t)stream, xyzs, n, n_dev,
-                       (1 << SC_N_CLASSES) - 1, dE_ws + DE_HEADER_FLOATS + 16 * e_stride, dE_ws + DE_POS_FLAG);
+                       (1 << SC_N_CLASSES) - 1, dE_ws + DE_HEADER_FLOATS + 16 * e_stride, dE_ws + DE_POS_FLAG,
+                       (float)((1 << SC_N_CLASSES) - 1));
     NCN_LAUNCH_CHECK("ncn_field_scatter_positions");
     return 0;
 }

@@ -50,6 +50,13 @@ def test_two_backwards_both_deferred_scatters_run(dev, later):
     assert rel < 1e-6, rel
     # the same non-zero set, up to exact cancellations whose outcome depends on the float order of the
     # flushes (the encoding gradient is stored in fp16, so equal and opposite contributions of two
-    # backwards are common: an entry's +q - q + r and +r + q - q can round differently); a dropped
-    # scatter would zero thousands of entries
-    assert int(((got == 0) != (ref == 0)).sum()) <= 4
+    # backwards are common: an entry's (q - q) + r and (r + q) - q can round differently).  Such an
+    # entry is zero on one side and, on the other, the rounding residual of partials no larger than
+    # the table's largest entries: a few ulps of them.  So every entry zero on one side only must lie
+    # below ORDER_FLOOR = 2^-20 (16 ulps) of the largest entry, on either side; a dropped scatter zeroes
+    # thousands of entries of ordinary size.
+    ORDER_FLOOR = 2.0 ** -20 * float(ref.abs().max())
+    one_side = (got == 0) != (ref == 0)
+    resid = torch.maximum(got[one_side].abs(), ref[one_side].abs())
+    assert resid.numel() == 0 or float(resid.max()) <= ORDER_FLOOR, (int(one_side.sum()), float(resid.max()),
+                                                                     ORDER_FLOOR)

@@ -44,17 +44,19 @@ def test_psnr_parity_short():
 def test_psnr_parity_short_bf16():
     """Config #3 end to end: the bf16 HIP step against the oracle that rounds the MLP operands and
     the (unscaled) backward chain to bf16 as the kernel does — one pair, same init, batches and noise,
-    40 steps of 1024 rays: the first step's loss within 1e-3, the first 5 steps' within 1 % (later
-    the pair decorrelates: bf16's coarse rounding turns summation-order differences into 1-ulp flips
-    of 0.4 %, and one measured pair was 1.8 % apart at step 15), PSNR within 0.1 dB on the same
-    renderer after the 40 steps."""
+    40 steps of 1024 rays: the first step's loss within 1e-3 (the same parameters: the two sides differ
+    only by summation order); step k's loss (k = 0, 1, ...) within (k + 1) bf16 unit roundoffs
+    (2^-8) of the reference's — the pair drifts apart because bf16's coarse rounding turns
+    summation-order differences into 1-ulp flips of the operands, each step adding at most about one
+    such rounding of relative size 2^-8 to the loss (measured: 1.8 % at step 15, inside 16 x 2^-8 =
+    6.3 %); PSNR within 0.1 dB on the same renderer after the 40 steps."""
     r = run(steps=40, n_rays=1024, eval_batches=2, eval_rays=4096, oracle_eval_rays=512, threads=8,
             precision="bf16", emulate="bf16")
     print({k: v for k, v in r.items() if k != "losses_ref_hip"})
     l0_ref, l0_hip = r["losses_ref_hip"][0]
     assert abs(l0_hip - l0_ref) <= 1e-3 * abs(l0_ref), r["losses_ref_hip"][:3]
-    for k, (lr_, lh) in enumerate(r["losses_ref_hip"][:5]):
-        assert abs(lh - lr_) <= 1e-2 * abs(lr_), (k, lr_, lh)
+    for k, (lr_, lh) in enumerate(r["losses_ref_hip"]):
+        assert abs(lh - lr_) <= (k + 1) * 2.0 ** -8 * abs(lr_), (k, lr_, lh)
     assert r["psnr_hip"] > 7.0 and r["psnr_ref"] > 7.0, r
     assert abs(r["delta_db"]) <= 0.1, r
 

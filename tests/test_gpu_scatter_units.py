@@ -88,7 +88,7 @@ def test_scatter_matches_serial_oracle(dev, n, op, mode):
                                           stream())
         assert rc == 0, _lib.lib().ncn_last_error()
         torch.cuda.synchronize()
-        assert float(ws[2]) == (1.0 if permuted else 0.0)
+        assert float(ws[2]) == (15.0 if permuted else 0.0)  # (the mask of the four unit classes)
         _check(grad.cpu().numpy().astype(np.float64), ref.copy(), n, op, mode, permuted)
 
 

@@ -102,6 +102,11 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
     else:
         s0 = so
     for name, L in libs:
+        # each library's own MLP pass first: it writes the positions in that library's unit layout
+        L.ncn_field_bwd_mlp.argtypes = _lib.SIGNATURES["ncn_field_bwd_mlp"]
+        L.ncn_field_bwd_mlp.restype = ctypes.c_int
+        assert L.ncn_field_bwd_mlp(ptr(xyzs), ptr(dirs), I64(n), ptr(None), ptr(ORDER[0]), ptr(packed), I32(0), ptr(enc),
+                                   ptr(dsig), ptr(drgb), ptr(None), ptr(slab), ptr(dE), ptr(lmax), stream()) == 0
         gtab.zero_()
         assert scat(L) == 0
         torch.cuda.synchronize()
