@@ -142,5 +142,8 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
             L.ncn_diag_sc_times(buf, 0)
             a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 10).astype(np.float64)
             names = ["load", "work", "drain", "barrier", "flush"]
-            print("     cycles per WG (wave 0, mean), run | direct:",
+            print("     cycles per WG (wave 0, mean), coarse | fine:",
                   "  ".join(f"{nm} {a[:, 2 * i].mean():.0f}|{a[:, 2 * i + 1].mean():.0f}" for i, nm in enumerate(names)))
+            tot = a.sum(1) - a[:, 4]  # (the coarse drains are inside the coarse work)
+            q = np.percentile(tot, [0, 10, 50, 90, 100])
+            print("     total cycles per WG: min %.0f p10 %.0f median %.0f p90 %.0f max %.0f" % tuple(q))
