@@ -442,6 +442,11 @@ class NGPMT(nn.Module):
                 valid_mask = (count > 0) & (~too_near_to_cam.any(0))
                 self.density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
 
+    def _grid_side_stream(self):
+        if getattr(self, "_grid_side", None) is None:
+            self._grid_side = torch.cuda.Stream(device=self.density_grid.device)
+        return self._grid_side
+
     def _grid_ws(self):
         """Device workspace of the grid refresh: hit list (positions, cell indices, densities) of one
         cascade's capacity, the list count, the effective threshold and the reduction scratch."""
@@ -458,7 +463,7 @@ class NGPMT(nn.Module):
         return ws
 
     @torch.no_grad()
-    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False, seed=None):
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False, seed=None, beside=None):
         """ngp_mt.py:340-368 on the device (csrc/grid.hip): per cascade ncn_grid_sample -> density
         pass (ncn_field_fwd mode 2 over the hit list, device count) -> ncn_grid_apply, then
         ncn_grid_packbits.  Cells hit: all of them in warmup (get_all_cells), else each cell with the
@@ -466,7 +471,10 @@ class NGPMT(nn.Module):
         (sample_uniform_and_occupied_cells, M = G^3/4) — the documented sampling deviation of
         grid.hip.  The density grid is updated in place (the reference rebinds it to the same values).
         Quirk q12: with no cell > 0 the mean is NaN and the bitfield is cleared — reproduced.
-        No host synchronisation; `seed` (default: drawn from torch's CPU generator) fixes the draw."""
+        No host synchronisation; `seed` (default: drawn from torch's CPU generator) fixes the draw.
+        beside (optional callable): work issued on the current stream while the first cascade's cell
+        sampling — which reads the density grid only, not the parameters — runs on a side stream
+        (Trainer: the optimizer step the refresh waits for); joined before the density pass."""
         G, C = self.grid_size, self.cascades
         N = G ** 3
         dg = self.density_grid
@@ -479,17 +487,32 @@ class NGPMT(nn.Module):
         n_list = ws["scal"][0:1]
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        packed = self._take_packed()
         table = self.xyz_encoder.params
+        packed = None
         for c in range(C):
             s = min(2 ** (c - 1), self.scale)
             half_grid_size = s / G
             dgc = dg[c]
             cc = cnt[c] if cnt is not None else None
-            call("ncn_grid_sample", ptr(dgc), I64(N), I32(G), F32(s - half_grid_size), F32(half_grid_size),
-                 F32(density_threshold), I64(N // 4), I32(1 if warmup else 0),
-                 _lib.U64((seed + 0x9E3779B97F4A7C15 * c) % 2 ** 64), F32(decay), ptr(cc), ptr(ws["xyzs"]),
-                 ptr(ws["idx"]), ptr(n_list), ptr(ws["work"]), stream())
+
+            def sample():
+                call("ncn_grid_sample", ptr(dgc), I64(N), I32(G), F32(s - half_grid_size), F32(half_grid_size),
+                     F32(density_threshold), I64(N // 4), I32(1 if warmup else 0),
+                     _lib.U64((seed + 0x9E3779B97F4A7C15 * c) % 2 ** 64), F32(decay), ptr(cc), ptr(ws["xyzs"]),
+                     ptr(ws["idx"]), ptr(n_list), ptr(ws["work"]), stream())
+
+            if c == 0 and beside is not None:
+                cur = torch.cuda.current_stream(dg.device)
+                side = self._grid_side_stream()
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    sample()
+                beside()
+                cur.wait_stream(side)
+            else:
+                sample()
+            if packed is None:
+                packed = self._take_packed()  # (after `beside`: the optimizer may have refreshed the fragments)
             # density pass, mode 2: the hash-grid encoding split by level over the XCDs into the
             # scratch ws["enc"] (each L2 serves two levels' tables), then sigma_net from it
             call("ncn_field_fwd", ptr(ws["xyzs"]), ptr(None), I64(N), ptr(n_list), ptr(None), ptr(table), self._levels_ptr,

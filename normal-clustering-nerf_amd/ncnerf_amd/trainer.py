@@ -101,10 +101,11 @@ class Trainer:
     def _maybe_update_grid(self, global_step):
         m = self.model
         if self.update_grid and global_step % self.update_interval == 0:
-            self.flush_optimizer()  # (the refresh reads the parameters)
             thr = 0.01 * self.h["rend_max_samples"] / 3 ** 0.5 * self.h["density_tresh_decay"]
             seed = self.grid_seed(global_step) if self.grid_seed is not None else None
-            m.update_density_grid(thr, warmup=global_step < self.warmup_steps, seed=seed)
+            # the pending optimizer step first (the density pass reads the parameters), issued beside
+            # the refresh's cell sampling, which reads only the density grid
+            m.update_density_grid(thr, warmup=global_step < self.warmup_steps, seed=seed, beside=self.flush_optimizer)
             distributed.broadcast_occupancy(m)
 
     # -- graph-captured step ---------------------------------------------------------------------
