@@ -524,10 +524,10 @@ constexpr int DE_POS_FLAG = 2;  // header float: the mask of unit classes whose 
 // The MLP pass writes the coarse classes' positions only: the coarse units' strided loads cost
 // 16-20 us per unit, the fine units' grabs measured no faster from permuted positions (round 6,
 // profiles/round6/scatter_probe_perm.log), and the writes run beside the clustering.
-#ifndef NCN_POS_MLP_CLASSES
-#define NCN_POS_MLP_CLASSES 2
-#endif
-constexpr int DE_POS_MLP_CLASSES = NCN_POS_MLP_CLASSES;
+constexpr int DE_POS_MLP_CLASSES = 2;
+// The pass that writes them: the rgb pass, beside the clustering (round 6 A/B against the sigma pass
+// after the join: 14.28 / 14.29 M rays/s alike).
+constexpr int DE_POS_PART = 1;  // BWD_RGB
 constexpr int BWD_WAVES = 8;
 constexpr int BWD_THREADS = 64 * BWD_WAVES;
 // exchange tiles per group: dW operands, A = dY^T, B = X^T (16 features x 16 samples)
@@ -580,7 +580,7 @@ __device__ __forceinline__ void bwd_load(BwdIn<T>& in, int64_t grp, int64_t n, i
     in.e = enc[grp * 64 + lane];
     in.dx = in.dy = in.dz = in.dsig = in.dr0 = in.dr1 = in.dr2 = 0.f;
     in.px = in.py = in.pz = 0.f;
-    if constexpr ((PART & BWD_RGB) != 0) {
+    if constexpr ((PART & DE_POS_PART) != 0) {
         if (xyzs && valid) { in.px = xyzs[3 * pos]; in.py = xyzs[3 * pos + 1]; in.pz = xyzs[3 * pos + 2]; }
     }
     if constexpr (PART == BWD_SIGMA) {
@@ -901,10 +901,10 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     // (rgb / one pass) the sample positions in the scatter's per-class load order (sc_perm), behind
     // the encoding gradient: lane (g, r) writes sample r's position into class g's array.  In the
     // processing order of `order` the scatter gathers them itself (no positions written).
-    const float* pos_src = ((PART & BWD_RGB) != 0 && dE_out && !order) ? xyzs : nullptr;
+    const float* pos_src = ((PART & DE_POS_PART) != 0 && dE_out && !order) ? xyzs : nullptr;
     float* const pos_out = pos_src ? dE_out + DE_HEADER_FLOATS + 16 * n_stride : nullptr;
     const int64_t pos_stride = sc_perm_stride(n_stride);
-    if ((PART & BWD_RGB) != 0 && dE_out && blockIdx.x == 0 && threadIdx.x == 0)
+    if ((PART & DE_POS_PART) != 0 && dE_out && blockIdx.x == 0 && threadIdx.x == 0)
         dE_out[DE_POS_FLAG] = pos_out ? (float)((1 << DE_POS_MLP_CLASSES) - 1) : 0.f;
     const int lm_rows = bwd_blocks_of(n);            // level_max rows the scatter reads
     // split passes' stash (ncn_field_bwd_stash_floats): [groups][64] operand tiles, then [groups][16]
@@ -953,7 +953,7 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
             bwd_load<T, PART>(nxt, grp + stride, n, lane, enc_cache, dirs, dL_dsig, dL_dsig2, dL_drgb, stq, sth0, order,
                               S, pos_src);
         if (grp < n_groups) {
-            if ((PART & BWD_RGB) != 0 && pos_out && (lane >> 4) < DE_POS_MLP_CLASSES && grp * 16 + (lane & 15) < n) {
+            if ((PART & DE_POS_PART) != 0 && pos_out && (lane >> 4) < DE_POS_MLP_CLASSES && grp * 16 + (lane & 15) < n) {
                 const int cls = lane >> 4;
                 float* po = pos_out + cls * 3 * pos_stride + 3 * sc_perm(grp * 16 + (lane & 15), cls);
                 po[0] = cur.px; po[1] = cur.py; po[2] = cur.pz;
