@@ -521,6 +521,11 @@ constexpr int DE_HEADER_FLOATS = 4;  // the dE workspace's header (ncn_field_bwd
 __host__ __device__ constexpr int64_t sc_perm_stride(int64_t n_stride);
 __device__ __forceinline__ int64_t sc_perm(int64_t s, int cls);
 constexpr int DE_POS_FLAG = 2;  // header float: the mask of unit classes whose permuted positions the workspace holds
+// The table scatter's unit queue at the end of the workspace: per level_lo of a launch, a grab counter
+// and a departure counter (field_scatter_kernel); zeroed by the MLP pass that writes the header, and
+// left zero by every scatter launch (its last workgroup out resets them).
+constexpr int SC_QUEUE_WORDS = 32;
+__host__ __device__ int64_t de_queue_offset(int64_t e_stride);
 // The MLP pass writes the coarse classes' positions only: the coarse units' strided loads cost
 // 16-20 us per unit, the fine units' grabs measured no faster from permuted positions (round 6,
 // profiles/round6/scatter_probe_perm.log), and the writes run beside the clustering.
@@ -894,9 +899,12 @@ __global__ __launch_bounds__(BWD_THREADS) void field_bwd_kernel(
     const int64_t n_stride = (n + 3) & ~(int64_t)3;  // dE layout [16][n_stride] (16-B aligned rows)
     // dE workspace: a 16-B header {1 / S, operand type (0 fp16, 1 bf16)} then the pairs
     float* const dE_pairs = dE_out ? dE_out + DE_HEADER_FLOATS : nullptr;
-    if (PART != BWD_RGB && dE_out && blockIdx.x == 0 && threadIdx.x == 0) {
-        dE_out[0] = inv_S;
-        dE_out[1] = Mfma<T>::f16 ? 0.f : 1.f;
+    if (PART != BWD_RGB && dE_out && blockIdx.x == 0 && threadIdx.x < SC_QUEUE_WORDS) {
+        if (threadIdx.x == 0) {
+            dE_out[0] = inv_S;
+            dE_out[1] = Mfma<T>::f16 ? 0.f : 1.f;
+        }
+        ((unsigned*)(dE_out + de_queue_offset(n_stride)))[threadIdx.x] = 0u;  // the scatter's unit queue
     }
     // (rgb / one pass) the sample positions in the scatter's per-class load order (sc_perm), behind
     // the encoding gradient: lane (g, r) writes sample r's position into class g's array.  In the
@@ -1430,6 +1438,10 @@ struct ScRun {
 
 // Diagnostic builds (tools/scatter_probe.py): NCN_DIAG_SC_TIMES records wave 0's cycles per phase of
 // the fine-level units; NCN_DIAG_SC_LEVELS_MASK skips the levels whose bit is clear.
+#ifdef NCN_DIAG_SC_SPAN
+__device__ unsigned long long ncn_sc_span[256][20];  // per workgroup: realtime (100 MHz) start/end, cycles start/end,
+                                                     // then (unit, realtime at its end) for the first 8 units
+#endif
 #ifdef NCN_DIAG_SC_TIMES
 __device__ unsigned long long ncn_sc_times[256][10];  // per workgroup, wave 0: cycles per phase
 #define SC_TNOW(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -1613,12 +1625,20 @@ __device__ __forceinline__ ScLevel sc_level(const LevelTable& Lt, int l, float m
     return L;
 }
 
+// The next unit of the workgroup (field_scatter_kernel's queue): thread 0 draws it when its samples
+// are done (few live registers there; the atomic's return is hidden behind the unit's barrier wait
+// and flush) and publishes it in LDS before the unit's closing barrier.
+struct ScDraw {
+    unsigned* queue;
+    int* slot;
+};
+
 // One fine-level unit of 1024 x C samples: the samples in grabs, then the flush of the claimed slots.
 // (C is a run-time value: one inlined copy of the grab loop serves every fine level.)
 __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, int C, int64_t s0, int64_t s1,
                                         const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
                                         const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
-                                        const int32_t* __restrict__ order, bool perm) {
+                                        const int32_t* __restrict__ order, bool perm, const ScDraw& draw) {
     SC_TNOW(t0);
     // (a fine unit holds at most 4096 samples: 2^46 leaves the sums four bits of headroom below 2^62)
     const ScLevel L = sc_level(Lt, l, m, 46);
@@ -1653,6 +1673,8 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (diagnostic: the wave's own LDS ops drain)
 #endif
     SC_TNOW(t2b);
+    unsigned next = 0;
+    if (threadIdx.x == 0) next = atomicAdd(draw.queue, 1u);  // (its return waits behind the barrier and the flush)
     lds_barrier();
     SC_TNOW(t3);
     // flush: the claimed slots, two lanes per slot (x and y of one entry are adjacent floats, one
@@ -1671,6 +1693,7 @@ __device__ __forceinline__ void sc_unit(ScShared& sh, int wid, int lane, int l, 
             sh.keys[slot] = SC_EMPTY;
         }
     }
+    if (threadIdx.x == 0) *draw.slot = (int)next;
     lds_barrier();
     SC_TNOW(t4);
     SC_TADD(0, t0, t1);
@@ -1703,7 +1726,7 @@ template <int C>
 __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, int l, int64_t s0, int64_t s1, int rounds,
                                              const float* __restrict__ xyzs, const uint32_t* __restrict__ dEl,
                                              const ScDE& de, const ScNorm& nrm, const LevelTable& Lt, float m, float* __restrict__ grad,
-                                             const int32_t* __restrict__ order, bool perm) {
+                                             const int32_t* __restrict__ order, bool perm, const ScDraw& draw) {
     const int lg_unit = (31 - __builtin_clz(SC_THREADS * C)) + (31 - __builtin_clz((unsigned)rounds));
     // scale 2^k, k = 60 - lg_unit - e: the unit's sum of every corner stays below 2^61, and one run
     // (at most rounds x C <= 2^(lg_unit - 10) samples) below 2^(50) — sc_fix needs |addend| < 2^51
@@ -1734,9 +1757,12 @@ __device__ __forceinline__ void sc_cell_unit(ScShared& sh, int wid, int lane, in
         SC_TADDC(1, tc1, tc2);  // (run work including the drains, which add to slot 2 as well)
     }
     SC_TNOW(tc3);
+    unsigned next = 0;
+    if (threadIdx.x == 0) next = atomicAdd(draw.queue, 1u);  // (its return waits behind the barrier and the flush)
     lds_barrier();
     SC_TNOW(tc4);
     sc_flush_cells(sh, L, grad);
+    if (threadIdx.x == 0) *draw.slot = (int)next;
     lds_barrier();
     SC_TNOW(tc5);
     SC_TADDC(3, tc3, tc4);
@@ -1752,6 +1778,9 @@ static_assert(sc_cell_rounds(0) == NCN_SC_R_LO && NCN_SC_R_LO >= NCN_SC_R_MID &&
 // the permuted positions' row length (every class array holds whole units)
 __host__ __device__ constexpr int64_t sc_perm_stride(int64_t n_stride) {
     return (n_stride + SC_MAX_SPAN - 1) / SC_MAX_SPAN * SC_MAX_SPAN;
+}
+__host__ __device__ int64_t de_queue_offset(int64_t e_stride) {
+    return DE_HEADER_FLOATS + 16 * e_stride + SC_N_CLASSES * 3 * sc_perm_stride(e_stride);
 }
 // Where sample s sits in its class's permuted position array: the samples a wave loads in one
 // instruction lie side by side, so a coarse round or a fine grab reads one contiguous stretch
@@ -1818,21 +1847,33 @@ __global__ __launch_bounds__(256) void sc_perm_positions_kernel(const float* __r
     }
 }
 
+// The scatter's processing order of the levels: the cell levels' long units first, then the fine
+// levels by their measured unit cost (round 6, per-unit durations in the step's scatter,
+// profiles/round6/scatter_probe_span.log: medians 36.5 / 26.1 / 23.6 / 22.9 / 23.1 / 22.4 us for
+// levels 14 / 13 / 15 / 12 / 11 / 10; levels 0-9 37-52 us), one nibble per position.
+constexpr uint64_t sc_order_nibbles() {
+#ifdef NCN_SC_ORDER
+    return NCN_SC_ORDER;
+#endif
+    constexpr int o[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 14, 13, 15, 12, 11, 10};
+    uint64_t v = 0;
+    for (int i = 0; i < 16; i++) v |= (uint64_t)o[i] << (4 * i);
+    return v;
+}
+__device__ __forceinline__ int sc_level_at(int i) { return (int)((sc_order_nibbles() >> (4 * i)) & 15u); }
+
 // One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
-__device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, int& layout, int& par, ScShared& sh,
+__device__ __forceinline__ bool sc_one_unit(int64_t u, int64_t n, const int* unit_start, const int* unit_level, int& layout,
+                                            int& par, const ScDraw& draw, ScShared& sh,
                                             char* arena, int* fill, const float* lmax_s, int wid, int lane,
                                             const float* __restrict__ xyzs, const float* __restrict__ pos, int perm_mask,
                                             const uint32_t* __restrict__ dE,
                                             int64_t e_stride, const ScDE& de, const ScNorm& nrm, const LevelTable& Lt,
                                             float* __restrict__ grad, const int32_t* __restrict__ order) {
-    int l = level_lo;
-    int64_t v = u, span = sc_unit_span(l);
-    for (;; l++) {  // (uniform, at most 16 steps) level-major unit order
-        span = sc_unit_span(l);
-        const int64_t nu = (n + span - 1) / span;
-        if (v < nu) break;
-        v -= nu;
-    }
+    int i = 0;  // (uniform) the launch's levels in processing order: unit u is unit v of level l
+    while (i < 15 && u >= unit_start[i + 1]) i++;
+    const int l = unit_level[i];
+    const int64_t v = u - unit_start[i], span = sc_unit_span(l);
     const int64_t s0 = v * span, s1 = min(n, s0 + span);
     const int mode = l < SC_CELL_HI ? SC_MODE_CELL : SC_MODE_DIR;
     if (mode != layout) {  // (re)initialise the table of the new layout
@@ -1850,7 +1891,7 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
 #ifdef NCN_DIAG_SC_LEVELS_MASK
     if (!((NCN_DIAG_SC_LEVELS_MASK >> l) & 1)) m = 0.f;  // diagnostic: skip this level
 #endif
-    if (m == 0.f) return;  // uniform: nothing to add on this level (no barrier, parity kept)
+    if (m == 0.f) return false;  // uniform: nothing to add on this level (no barrier, parity kept; no draw)
     // the unit claims into fill[par]; fill[par ^ 1] (read by every lane before the previous
     // unit's closing barrier) is reset here for the next unit
     sh.fill = fill + par;
@@ -1862,9 +1903,11 @@ __device__ __forceinline__ void sc_one_unit(int64_t u, int64_t n, int level_lo, 
     const bool perm = (perm_mask >> sc_class(l)) & 1;
     if (perm) xyzs = pos + sc_class(l) * 3 * sc_perm_stride(e_stride);
     if (mode == SC_MODE_CELL)
-        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order, perm);
+        sc_cell_unit<SC_C_CELL>(sh, wid, lane, l, s0, s1, sc_cell_rounds(l), xyzs, dEl, de, nrm, Lt, m, grad, order, perm,
+                                draw);
     else
-        sc_unit(sh, wid, lane, l, sc_fine_c(l), s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order, perm);
+        sc_unit(sh, wid, lane, l, sc_fine_c(l), s0, s1, xyzs, dEl, de, nrm, Lt, m, grad, order, perm, draw);
+    return true;
 }
 
 __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
@@ -1877,13 +1920,29 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                                                                    const int32_t* __restrict__ order,
                                                                    const float* __restrict__ wslab = nullptr,
                                                                    int nb_sigma = 0, int nb_rgb = 0,
-                                                                   float* __restrict__ gw = nullptr) {
+                                                                   float* __restrict__ gw = nullptr,
+                                                                   unsigned* __restrict__ queue = nullptr) {
     __shared__ __attribute__((aligned(16))) char arena[SC_ARENA];
     __shared__ int fill[4];  // claimed-slot counts [0, 2) and grab counters [2, 4), alternating per unit (reset one unit ahead)
     // per-level max |dE| over the MLP pass's workgroup rows (the fixed-point scale of each level);
     // visible to every thread at the first layout barrier
     __shared__ float lmax_s[16];
+    // the launch's levels in sc_level_at order: unit_start[i] = the first unit of the i-th of them
+    // (padded with the unit count to 16), unit_level[i] its level
+    __shared__ int unit_start[17], unit_level[16];
+    const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
     if (threadIdx.x < 16) lmax_s[threadIdx.x] = 0.f;
+    if (threadIdx.x == 0) {
+        int acc = 0, k = 0;
+        for (int i = 0; i < 16; i++) {
+            const int l = sc_level_at(i);
+            if (l < level_lo || l >= level_hi) continue;
+            unit_start[k] = acc;
+            unit_level[k++] = l;
+            acc += (int)((n + sc_unit_span(l) - 1) / sc_unit_span(l));
+        }
+        for (; k < 17; k++) unit_start[k] = acc;
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < lm_rows * 16; i += SC_THREADS)  // one load per thread, LDS max
         atomicMax((unsigned*)&lmax_s[i & 15], __float_as_uint(level_max[i]));  // (non-negative floats)
@@ -1904,7 +1963,12 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
+#ifdef NCN_DIAG_SC_SPAN
+    if (threadIdx.x == 0 && blockIdx.x < 256) {
+        ncn_sc_span[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+        ncn_sc_span[blockIdx.x][2] = __builtin_readcyclecounter();
+    }
+#endif
     const int64_t e_stride = (n_stride + 3) & ~(int64_t)3;  // dE row stride (as written by field_bwd)
     ScNorm nrm;
     nrm.mn = xyz_min;
@@ -1920,23 +1984,55 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // ncn_field_scatter_positions) wrote it (header mask), else the sample-ordered xyzs (strided loads)
     const int perm_mask = order ? 0 : (int)dE_ws[DE_POS_FLAG];
     const float* pos = dE_ws + DE_HEADER_FLOATS + 16 * e_stride;
-    // units, level-major over the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell
-    // levels [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
-    int64_t n_units = 0;
-    for (int l = level_lo; l < level_hi; l++) n_units += (n + sc_unit_span(l) - 1) / sc_unit_span(l);
-    // Units are ordered heaviest first (the coarse cell levels' long units, then the finer levels);
-    // workgroup b takes units b, b + gridDim.x, ...  (a dynamic unit queue measured no better: 191 vs
-    // 196 us, then 194 vs 190 — the static stride is not load-imbalanced).  A workgroup's units go
-    // cell -> fine: at most one layout switch.
+    // units of the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell levels
+    // [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
+    const int64_t n_units = unit_start[16];
+    // Units in sc_level_at order (the cell levels' long units, then the fine levels by cost): workgroup b
+    // takes unit b first, then draws the next from the launch's queue — during each unit's flush
+    // (ScDraw), so the draw's return is hidden.  A workgroup's units go cell -> fine: at most one
+    // layout switch.  (Round 6: a static stride b, b + gridDim.x, ... left the workgroups' ends spread
+    // over 94-169 us for a mean of 142 us of work — about five units of 20-55 us each —
+    // profiles/round6/scatter_probe_span.log; the queue in level-major order gave nothing (round 3):
+    // the cost order is what lets it balance.)
     int layout = -1, par = 0;
     ScShared sh;
-    // (Round 5: alternating the stride's direction every round ("snake", LPT-like) 192-197 vs 188 us;
-    // rounds per coarse unit (levels 0-5 / 6-9): 8/4 188, 4/2 191, 8/8 182-187, 8/2 206, 4/4 199,
-    // 4/8 225-230, 2/8 210, 16/4 237, 8/16 317 — more than 256 coarse units, or a few very long
-    // ones, leave workgroups a second heavy unit.)
-    for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x)
-        sc_one_unit(u, n, level_lo, layout, par, sh, arena, fill, lmax_s, wid, lane, xyzs, pos, perm_mask, dE, e_stride, de,
-                    nrm, Lt, grad, order);
+    __shared__ int next_unit[2];  // (alternating: a slot is rewritten only after a barrier every reader passed)
+#ifdef NCN_DIAG_SC_SPAN
+    int diag_k = 0;
+#endif
+    int64_t u = blockIdx.x;
+    for (int qpar = 0; u < n_units; qpar ^= 1) {  // (uniform)
+        ScDraw draw;
+        draw.queue = queue;
+        draw.slot = next_unit + qpar;
+        const bool drew = sc_one_unit(u, n, unit_start, unit_level, layout, par, draw, sh, arena, fill, lmax_s, wid, lane,
+                                      xyzs, pos, perm_mask, dE, e_stride, de, nrm, Lt, grad, order);
+#ifdef NCN_DIAG_SC_SPAN
+        if (threadIdx.x == 0 && blockIdx.x < 256 && diag_k < 8) {
+            ncn_sc_span[blockIdx.x][4 + 2 * diag_k] = (unsigned long long)u;
+            ncn_sc_span[blockIdx.x][5 + 2 * diag_k] = __builtin_amdgcn_s_memrealtime();
+        }
+        diag_k++;
+#endif
+        if (!drew) {  // (uniform) a skipped unit: draw here
+            if (threadIdx.x == 0) next_unit[qpar] = (int)atomicAdd(queue, 1u);
+            __syncthreads();
+        }
+        u = (int64_t)next_unit[qpar] + gridDim.x;
+    }
+    // the last workgroup out leaves the queue zero for the next launch on this workspace (every
+    // workgroup has made its last draw before it departs)
+    if (threadIdx.x == 0 && atomicAdd(queue + 1, 1u) == gridDim.x - 1) {
+        __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#ifdef NCN_DIAG_SC_SPAN
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 256) {
+        ncn_sc_span[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+        ncn_sc_span[blockIdx.x][3] = __builtin_readcyclecounter();
+    }
+#endif
 }
 
 static int scatter_grid(int64_t n_cap) {
@@ -2059,8 +2155,9 @@ int ncn_field_bwd_blocks(int64_t n) { return bwd_blocks_of(n); }
 int64_t ncn_field_bwd_dE_floats(int64_t n) {
     if (n <= 0) return 0;
     const int64_t e_stride = (n + 3) & ~(int64_t)3;
-    // header, the level-major encoding gradient, then the scatter's permuted positions per class
-    return DE_HEADER_FLOATS + 16 * e_stride + SC_N_CLASSES * 3 * sc_perm_stride(e_stride);
+    // header, the level-major encoding gradient, the scatter's permuted positions per class, then
+    // the scatter's unit-queue words
+    return de_queue_offset(e_stride) + SC_QUEUE_WORDS;
 }
 
 int ncn_field_bwd_mlp(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
@@ -2136,7 +2233,8 @@ int ncn_field_scatter_wgrad(const float* xyzs, int64_t n, const int32_t* n_dev, 
     if (max_blocks > 0) grid = std::min(grid, max_blocks * (1024 / SC_THREADS));  // (max_blocks: CUs)
     hipLaunchKernelGGL(field_scatter_kernel, dim3(grid), dim3(SC_THREADS), 0, (hipStream_t)stream, xyzs, n, n_dev, Lt,
                        xyz_min, xyz_extent, dE_ws, grad_table, level_max, ncn_field_bwd_blocks(n),
-                       level_lo, level_hi, order, slab, n_blocks_sigma, n_blocks_rgb, grad_w);
+                       level_lo, level_hi, order, slab, n_blocks_sigma, n_blocks_rgb, grad_w,
+                       (unsigned*)const_cast<float*>(dE_ws + de_queue_offset((n + 3) & ~(int64_t)3)) + 2 * level_lo);
     NCN_LAUNCH_CHECK("ncn_field_scatter");
     return 0;
 }
@@ -2183,6 +2281,12 @@ int ncn_diag_sc_times(unsigned long long* host, int reset) {
         return (int)hipMemcpyToSymbol(HIP_SYMBOL(ncn_sc_times), zero, sizeof(zero));
     }
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_times), 256 * 10 * sizeof(unsigned long long));
+}
+#endif
+
+#ifdef NCN_DIAG_SC_SPAN
+int ncn_diag_sc_span(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ncn_sc_span), 256 * 20 * sizeof(unsigned long long));
 }
 #endif
 

@@ -134,6 +134,42 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
         print(f"  {name:24s} all {t:7.1f} us  levels0-9 {coarse:7.1f}  levels10-15 {fine:7.1f}  {msg}", flush=True)
         if os.environ.get("SCATTER_PROBE_PER_LEVEL"):
             print("   per level:", " ".join(f"{l}:{timeit(L, lo=l, hi=l + 1):.1f}" for l in range(16)), flush=True)
+        if hasattr(L, "ncn_diag_sc_span"):  # per-workgroup start/end (100 MHz realtime) and shader cycles
+            assert scat(L) == 0
+            torch.cuda.synchronize()
+            buf = (ctypes.c_ulonglong * (256 * 20))()
+            L.ncn_diag_sc_span(buf)
+            a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 20).astype(np.float64)
+            os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+            np.save(os.path.join(ROOT, "gpurun_out", f"sc_span_{name}.npy"), a)
+            # per-unit durations (us) by level, and a greedy dynamic assignment of the same units in
+            # the same order (each to the earliest-free workgroup) with those durations
+            spans = [32768 if l < 6 else 16384 if l < 10 else 4096 if l < 15 else 2048 for l in range(16)]
+            lev = np.concatenate([np.full(-(-n // sp), l) for l, sp in enumerate(spans)])
+            dur = {}
+            for b in range(256):
+                prev = a[b, 0]
+                for k in range(8):
+                    if a[b, 5 + 2 * k] == 0:
+                        break
+                    u = int(a[b, 4 + 2 * k])
+                    dur[u] = (a[b, 5 + 2 * k] - prev) / 100.0
+                    prev = a[b, 5 + 2 * k]
+            byl = {}
+            for u, d in dur.items():
+                byl.setdefault(int(lev[u]), []).append(d)
+            print("     unit us by level (median):", " ".join(f"{l}:{np.median(v):.1f}" for l, v in sorted(byl.items())))
+            free = np.zeros(256)
+            for u in sorted(dur):
+                i = int(np.argmin(free))
+                free[i] += dur[u]
+            print(f"     greedy dynamic makespan with these durations: {free.max():.1f} us (static: {(a[:, 1] - a[:, 0]).max() / 100:.1f})")
+            t0 = a[:, 0].min()
+            st, en = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0  # us
+            ghz = np.median((a[:, 3] - a[:, 2]) / ((a[:, 1] - a[:, 0]) * 10.0))
+            pq = lambda v: " ".join(f"{x:.1f}" for x in np.percentile(v, [0, 10, 50, 90, 100]))  # noqa: E731
+            print(f"     WG span (us; min p10 p50 p90 max): start {pq(st)}  end {pq(en)}  busy {pq(en - st)}  "
+                  f"shader clock {ghz:.2f} GHz", flush=True)
         if hasattr(L, "ncn_diag_sc_times"):
             buf = (ctypes.c_ulonglong * (256 * 10))()
             L.ncn_diag_sc_times(buf, 1)
