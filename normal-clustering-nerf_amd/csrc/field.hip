@@ -1847,21 +1847,6 @@ __global__ __launch_bounds__(256) void sc_perm_positions_kernel(const float* __r
     }
 }
 
-// The scatter's processing order of the levels: the cell levels' long units first, then the fine
-// levels by their measured unit cost (round 6, per-unit durations in the step's scatter,
-// profiles/round6/scatter_probe_span.log: medians 36.5 / 26.1 / 23.6 / 22.9 / 23.1 / 22.4 us for
-// levels 14 / 13 / 15 / 12 / 11 / 10; levels 0-9 37-52 us), one nibble per position.
-constexpr uint64_t sc_order_nibbles() {
-#ifdef NCN_SC_ORDER
-    return NCN_SC_ORDER;
-#endif
-    constexpr int o[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 14, 13, 15, 12, 11, 10};
-    uint64_t v = 0;
-    for (int i = 0; i < 16; i++) v |= (uint64_t)o[i] << (4 * i);
-    return v;
-}
-__device__ __forceinline__ int sc_level_at(int i) { return (int)((sc_order_nibbles() >> (4 * i)) & 15u); }
-
 // One unit u of the scatter (see field_scatter_kernel): its level, span and layout.
 __device__ __forceinline__ bool sc_one_unit(int64_t u, int64_t n, const int* unit_start, const int* unit_level, int& layout,
                                             int& par, const ScDraw& draw, ScShared& sh,
@@ -1870,7 +1855,7 @@ __device__ __forceinline__ bool sc_one_unit(int64_t u, int64_t n, const int* uni
                                             const uint32_t* __restrict__ dE,
                                             int64_t e_stride, const ScDE& de, const ScNorm& nrm, const LevelTable& Lt,
                                             float* __restrict__ grad, const int32_t* __restrict__ order) {
-    int i = 0;  // (uniform) the launch's levels in processing order: unit u is unit v of level l
+    int i = 0;  // (uniform) unit u is unit v of level l
     while (i < 15 && u >= unit_start[i + 1]) i++;
     const int l = unit_level[i];
     const int64_t v = u - unit_start[i], span = sc_unit_span(l);
@@ -1927,16 +1912,14 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // per-level max |dE| over the MLP pass's workgroup rows (the fixed-point scale of each level);
     // visible to every thread at the first layout barrier
     __shared__ float lmax_s[16];
-    // the launch's levels in sc_level_at order: unit_start[i] = the first unit of the i-th of them
-    // (padded with the unit count to 16), unit_level[i] its level
+    // the launch's levels in order: unit_start[i] = the first unit of the i-th of them (padded with
+    // the unit count to 16), unit_level[i] its level
     __shared__ int unit_start[17], unit_level[16];
     const int64_t n = n_dev ? min<int64_t>(n_stride, *n_dev) : n_stride;
     if (threadIdx.x < 16) lmax_s[threadIdx.x] = 0.f;
     if (threadIdx.x == 0) {
         int acc = 0, k = 0;
-        for (int i = 0; i < 16; i++) {
-            const int l = sc_level_at(i);
-            if (l < level_lo || l >= level_hi) continue;
+        for (int l = level_lo; l < level_hi; l++) {
             unit_start[k] = acc;
             unit_level[k++] = l;
             acc += (int)((n + sc_unit_span(l) - 1) / sc_unit_span(l));
@@ -1987,13 +1970,14 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // units of the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell levels
     // [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
     const int64_t n_units = unit_start[16];
-    // Units in sc_level_at order (the cell levels' long units, then the fine levels by cost): workgroup b
-    // takes unit b first, then draws the next from the launch's queue — during each unit's flush
-    // (ScDraw), so the draw's return is hidden.  A workgroup's units go cell -> fine: at most one
-    // layout switch.  (Round 6: a static stride b, b + gridDim.x, ... left the workgroups' ends spread
-    // over 94-169 us for a mean of 142 us of work — about five units of 20-55 us each —
-    // profiles/round6/scatter_probe_span.log; the queue in level-major order gave nothing (round 3):
-    // the cost order is what lets it balance.)
+    // Units level-major (the cell levels' long units first): workgroup b takes unit b first, then draws
+    // the next from the launch's queue — at the end of each unit's samples (ScDraw), so the draw's
+    // return is hidden behind the unit's barrier wait and flush.  A workgroup's units go cell -> fine:
+    // at most one layout switch.  (Round 6: the static stride b, b + gridDim.x, ... left the
+    // workgroups' ends spread over 94-169 us for a mean of 142 us of work — about five units of 20-55
+    // us each, profiles/round6/scatter_probe_span.log; with the queue 130-159 us and the scatter 175.8
+    // -> 164-165 us, scatter_probe_queue_dynamic.log.  Fine levels drawn in cost order instead of
+    // level-major, or coarse units of half the samples, measured no better: scatter_probe_order.log.)
     int layout = -1, par = 0;
     ScShared sh;
     __shared__ int next_unit[2];  // (alternating: a slot is rewritten only after a barrier every reader passed)
