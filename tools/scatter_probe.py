@@ -156,8 +156,8 @@ for sorted_ in (False,) if os.environ.get("SCATTER_PROBE_MAIN_ONLY") or os.envir
                     dur[u] = (a[b, 5 + 2 * k] - prev) / 100.0
                     prev = a[b, 5 + 2 * k]
             byl = {}
-            for u, d in dur.items():
-                byl.setdefault(int(lev[u]), []).append(d)
+            for u, d in dur.items():  # (a variant with other unit spans: levels past the default table as -1)
+                byl.setdefault(int(lev[u]) if u < len(lev) else -1, []).append(d)
             print("     unit us by level (median):", " ".join(f"{l}:{np.median(v):.1f}" for l, v in sorted(byl.items())))
             free = np.zeros(256)
             for u in sorted(dur):
