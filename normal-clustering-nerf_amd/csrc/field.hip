@@ -1895,6 +1895,27 @@ __device__ __forceinline__ bool sc_one_unit(int64_t u, int64_t n, const int* uni
     return true;
 }
 
+// (ncn_field_scatter_wgrad) the MLP weight-gradient slab rows summed into gw, in SC_WGRAD_SLICES
+// contiguous slices of the weights, one per queue entry behind the table units (so the workgroups that
+// finish their table units first take them; round 6: the reduction at the start of every workgroup
+// delayed all units by its duration): the threads of a slice take (weight, 16-row chunk) pairs with
+// the weight varying fastest (coalesced rows); one f32 atomic per pair, as reduce_wgrad_kernel.
+constexpr int SC_WGRAD_SLICES = 256;
+__device__ __forceinline__ void sc_wgrad_slice(int slice, const float* __restrict__ wslab, int nb_sigma, int nb_rgb,
+                                               float* __restrict__ gw) {
+    const int per = (NCN_FIELD_NW + SC_WGRAD_SLICES - 1) / SC_WGRAD_SLICES;
+    const int w0 = slice * per, nw = min(NCN_FIELD_NW, w0 + per) - w0;
+    const int chunks = (max(nb_sigma, nb_rgb) + WRED_CHUNK - 1) / WRED_CHUNK;
+    for (int idx = threadIdx.x; idx < nw * chunks; idx += SC_THREADS) {
+        const int w = w0 + idx % nw, c = idx / nw;
+        const int nb = w < W3_OFF ? nb_sigma : nb_rgb;
+        const int b1 = min(nb, (c + 1) * WRED_CHUNK);
+        float acc = 0.f;
+        for (int b = c * WRED_CHUNK; b < b1; b++) acc += wslab[(int64_t)b * NCN_FIELD_NW + w];
+        if (c * WRED_CHUNK < nb) atomicAdd(gw + w, acc);
+    }
+}
+
 __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void field_scatter_kernel(const float* __restrict__ xyzs, int64_t n_stride,
                                                                    const int32_t* __restrict__ n_dev, LevelTable Lt,
                                                                    float xyz_min, float xyz_extent,
@@ -1929,22 +1950,6 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     __syncthreads();
     for (int i = threadIdx.x; i < lm_rows * 16; i += SC_THREADS)  // one load per thread, LDS max
         atomicMax((unsigned*)&lmax_s[i & 15], __float_as_uint(level_max[i]));  // (non-negative floats)
-    if (wslab) {
-        // (ncn_field_scatter_wgrad) the MLP weight-gradient slab rows summed into gw first: each
-        // workgroup a contiguous slice of the weights, its threads (weight, 16-row chunk) pairs with
-        // the weight varying fastest (coalesced rows); one f32 atomic per pair, as reduce_wgrad_kernel
-        const int per = (NCN_FIELD_NW + (int)gridDim.x - 1) / (int)gridDim.x;
-        const int w0 = (int)blockIdx.x * per, nw = min(NCN_FIELD_NW, w0 + per) - w0;
-        const int chunks = (max(nb_sigma, nb_rgb) + WRED_CHUNK - 1) / WRED_CHUNK;
-        for (int idx = threadIdx.x; idx < nw * chunks; idx += SC_THREADS) {
-            const int w = w0 + idx % nw, c = idx / nw;
-            const int nb = w < W3_OFF ? nb_sigma : nb_rgb;
-            const int b1 = min(nb, (c + 1) * WRED_CHUNK);
-            float acc = 0.f;
-            for (int b = c * WRED_CHUNK; b < b1; b++) acc += wslab[(int64_t)b * NCN_FIELD_NW + w];
-            if (c * WRED_CHUNK < nb) atomicAdd(gw + w, acc);
-        }
-    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #ifdef NCN_DIAG_SC_SPAN
     if (threadIdx.x == 0 && blockIdx.x < 256) {
@@ -1969,7 +1974,7 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     const float* pos = dE_ws + DE_HEADER_FLOATS + 16 * e_stride;
     // units of the levels [level_lo, level_hi), sc_unit_span(l) samples each: cell levels
     // [0, SC_CELL_HI) in spans of 1024 * C_CELL * rounds(l), fine levels 1024 * sc_fine_c(l)
-    const int64_t n_units = unit_start[16];
+    const int64_t n_units = unit_start[16], n_all = n_units + (wslab ? SC_WGRAD_SLICES : 0);
     // Units level-major (the cell levels' long units first): workgroup b takes unit b first, then draws
     // the next from the launch's queue — at the end of each unit's samples (ScDraw), so the draw's
     // return is hidden behind the unit's barrier wait and flush.  A workgroup's units go cell -> fine:
@@ -1985,12 +1990,16 @@ __global__ __launch_bounds__(SC_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     int diag_k = 0;
 #endif
     int64_t u = blockIdx.x;
-    for (int qpar = 0; u < n_units; qpar ^= 1) {  // (uniform)
+    for (int qpar = 0; u < n_all; qpar ^= 1) {  // (uniform)
         ScDraw draw;
         draw.queue = queue;
         draw.slot = next_unit + qpar;
-        const bool drew = sc_one_unit(u, n, unit_start, unit_level, layout, par, draw, sh, arena, fill, lmax_s, wid, lane,
-                                      xyzs, pos, perm_mask, dE, e_stride, de, nrm, Lt, grad, order);
+        bool drew = false;
+        if (u < n_units)
+            drew = sc_one_unit(u, n, unit_start, unit_level, layout, par, draw, sh, arena, fill, lmax_s, wid, lane, xyzs, pos,
+                               perm_mask, dE, e_stride, de, nrm, Lt, grad, order);
+        else
+            sc_wgrad_slice((int)(u - n_units), wslab, nb_sigma, nb_rgb, gw);
 #ifdef NCN_DIAG_SC_SPAN
         if (threadIdx.x == 0 && blockIdx.x < 256 && diag_k < 8) {
             ncn_sc_span[blockIdx.x][4 + 2 * diag_k] = (unsigned long long)u;
