@@ -255,7 +255,11 @@ int ncn_field_fwd(const float* xyzs, const float* dirs, int64_t n, const int32_t
  * scatter's load order (four copies, one per unit class: a wave's round / grab reads one contiguous
  * stretch).  The MLP pass (its rgb part; not with `order`) writes the two coarse classes' positions
  * and marks them in the header (a class mask); the scatter reads a marked class's copy, and xyzs in
- * sample order for the others. */
+ * sample order for the others.  The last 32 words are the scatter's unit queue (a draw and a
+ * departure counter per launch's first level): the MLP pass that writes the header (its sigma part,
+ * or the one-pass MLP) zeroes them, and every scatter launch leaves them zero, so a workspace the
+ * caller fills itself starts from zeroed memory.  Two scatter launches with the same level_lo must
+ * not run concurrently on one workspace. */
 int ncn_field_bwd_blocks(int64_t n);
 int64_t ncn_field_bwd_dE_floats(int64_t n);
 int ncn_field_bwd(const float* xyzs, const float* dirs, int64_t n, const int32_t* n_dev, const int32_t* order,
