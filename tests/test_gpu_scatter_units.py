@@ -89,6 +89,8 @@ def test_scatter_matches_serial_oracle(dev, n, op, mode):
         assert rc == 0, _lib.lib().ncn_last_error()
         torch.cuda.synchronize()
         assert float(ws[2]) == (15.0 if permuted else 0.0)  # (the mask of the four unit classes)
+        # the unit queue (the workspace's last 32 words) is left zero: the second pass draws from it again
+        assert int(ws[-32:].view(torch.int32).abs().sum()) == 0
         _check(grad.cpu().numpy().astype(np.float64), ref.copy(), n, op, mode, permuted)
 
 
