@@ -462,6 +462,19 @@ def main():
 
     GT = "surface_bright"  # synthetic target colours (ncnerf_amd.synthetic)
 
+    def window_start(base, warmup, steps, every=16):
+        """The first global step (>= base) of the warm-up + timed steps whose timed window holds the
+        long-run share of grid refreshes, round(steps / every) of the global steps that are multiples
+        of `every` (Trainer.update_interval: train_nerf.py:318 refreshes every 16 steps).  Without it a
+        window's count depends on where it falls: 20 steps from 3005 held two refreshes (one per 10
+        steps instead of one per 16).  Returns (step0, refreshes in the timed window)."""
+        want = int(steps / every + 0.5)
+        count = lambda a: (a + steps - 1) // every - (a - 1) // every  # noqa: E731
+        for s0 in range(base, base + every):
+            if count(s0 + warmup) == want:
+                return s0, want
+        return base, count(base + warmup)
+
     def measure(precision, steps, kernel_table, pretrain, state="procedural", preset="hypersim"):
         """Build the model in `precision`, pretrain it `pretrain` untimed steps, warm up, time `steps`
         graph-replayed training steps (barrier + synchronize on both sides), max over ranks.
@@ -499,7 +512,10 @@ def main():
             del pool
         n_batches = 8
         batches = [scene.torch_batch(args.rays, seed=rank * 10007 + i, device=dev, gt=GT) for i in range(n_batches)]
-        step0 = max(3000, pretrain)  # past the clustering ramp (losses.py:217): full 2e-3 weights
+        # past the clustering ramp (losses.py:217): full 2e-3 weights; refresh phase as window_start
+        step0, n_refresh = window_start(max(3000, pretrain), args.warmup, steps)
+        if args.no_grid_update:
+            n_refresh = 0
         if trainer.update_grid and state != "refreshed":  # first-call costs of the refresh path stay out of the timed region
             model.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
         for k in range(args.warmup):
@@ -543,11 +559,12 @@ def main():
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         return dict(el=float(elapsed.item()), tot=tot, rank_ms=rank_ms, timing=timing, model=model, batches=batches,
-                    distill=distill)
+                    distill=distill, n_refresh=n_refresh)
 
     main_run = measure(args.precision, args.steps, True, args.pretrain)
     el, tot, rank_ms, timing = main_run["el"], main_run["tot"], main_run["rank_ms"], main_run["timing"]
     model, batches = main_run["model"], main_run["batches"]
+    n_refresh = main_run["n_refresh"]
     kern = {}
     for name, evs in timing.items():
         if evs:
@@ -644,6 +661,7 @@ def main():
         "config": {"workload": "configs[1]+[2]: full training step, 8192 rays/GPU, normal clustering on",
                    "rays_per_gpu": args.rays, "global_batch": args.rays * world, "grid": 128, "max_samples": 1024,
                    "parallelism": f"dp{world}", "grid_update_every_16": not args.no_grid_update,
+                   "grid_refreshes_timed": n_refresh,
                    "grad_wire": ("fp16(fp16(S*g)/world): the reference's DDP wire, divided by the world before "
                                  "the SUM as DDP's default hook; optimizer grad_scale 1" if args.precision == "fp16" and
                                  distributed.DP_WIRE != "fp32" else "fp32 (SUM, 1/world in the optimizer)")
