@@ -22,7 +22,10 @@ model = register_grid_buffers(NGPMT(scale=0.5, grid_size=128).to(dev))
 model.density_bitfield.copy_(torch.from_numpy(scene.bitfield).to(dev))
 with torch.no_grad():
     model.flat_params()[: model._n_table].uniform_(-1e-2, 1e-2)
-    model.density_grid.copy_((torch.rand_like(model.density_grid) < 0.05).float())
+    if os.environ.get("DENSITY_PROBE_BENCH_GRID"):  # the bench's grid (the room's density x 10)
+        model.density_grid.copy_(torch.from_numpy(scene.density_grid).to(dev) * 10.0)
+    else:
+        model.density_grid.copy_((torch.rand_like(model.density_grid) < 0.05).float())
 thr = 0.01 * 1024 / 3 ** 0.5
 model.update_density_grid(thr, warmup=False, seed=7)  # fills the hit list of the (single) cascade
 torch.cuda.synchronize()
@@ -34,9 +37,9 @@ packed = model._take_packed()
 table = model.xyz_encoder.params
 
 
-def run(lib):
+def run(lib, mode=2):
     return lib.ncn_field_fwd(ptr(ws["xyzs"]), ptr(None), I64(N), ptr(n_list), ptr(None), ptr(table), model._levels_ptr,
-                             F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(model._prec), I32(2),
+                             F32(model._xyz_min), F32(model._xyz_extent), ptr(packed), I32(model._prec), I32(mode),
                              ptr(ws["sigmas"]), ptr(None), ptr(ws["enc"]), stream())
 
 
@@ -67,3 +70,7 @@ for name, L in libs:
     if ref is None:
         ref = sig
     print(f"  {name:24s} density pass {t:7.1f} us  bit-identical to main: {torch.equal(sig, ref)}", flush=True)
+    if name == "main":  # the sample-major density pass (mode 1: encoding + sigma_net in one launch)
+        t1 = ev_time(lambda: run(L, 1))
+        print(f"  {'main, mode 1':24s} density pass {t1:7.1f} us  bit-identical to mode 2: "
+              f"{torch.equal(ws['sigmas'][:n], ref)}", flush=True)
