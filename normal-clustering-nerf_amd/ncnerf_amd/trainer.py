@@ -8,7 +8,6 @@ training set's 1000 items, base.py:78-81, split over the ranks by DDP's Distribu
 Hyper-parameters default to the Hypersim config (experiments/hypersim/hyperparameters.py);
 preset="scannet_manhattan" selects config #5's (experiments/scannet_man/hyperparameters.py)."""
 import math
-import os
 import warnings
 
 import torch
@@ -16,10 +15,7 @@ import torch
 from . import _lib, distributed
 from .losses import NeRFMTLoss, check_cluster_status
 from .optim import FlatAdam
-from .rendering import march_buffers, march_train_fused, render
-
-# (variant) deferred optimizer on the graph's main stream and the marcher on the side stream
-DEFER_ADAM_MAIN = os.environ.get("NCN_DEFER_ADAM_MAIN", "0") == "1"
+from .rendering import march_train_fused, render
 
 HYPERSIM_HPARAMS = dict(
     scale=0.5, grid_size=128, rend_max_samples=1024, rend_near_dist=0.01, density_tresh_decay=1.0,
@@ -140,18 +136,11 @@ class Trainer:
                 return march_train_fused(m, batch["rays_o"], batch["rays_d"], kw["near_distance"], kw["max_samples"],
                                          kw.get("march_noise"), kw.get("march_rng"), out=out)
 
-            if DEFER_ADAM_MAIN:
-                # (variant) the optimizer on this stream, the marcher on the side one: the field
-                # forward then follows the optimizer (the longer branch) on its own queue, and the
-                # cross-queue dependency is on the marcher's earlier end
+            # (the optimizer on the main stream and the marcher on the side one measured the same:
+            # DESIGN.md §7, rounds 4 and 6)
+            with torch.cuda.stream(side):
                 optimizer()
-                bufs = march_buffers(batch["rays_o"].shape[0], kw["max_samples"], batch["rays_o"].device)
-                with torch.cuda.stream(side):
-                    kw["premarched"] = marcher(bufs)
-            else:
-                with torch.cuda.stream(side):
-                    optimizer()
-                kw["premarched"] = marcher()
+            kw["premarched"] = marcher()
             cur.wait_stream(side)
         if self._split is not None:
             results, loss_d = self._split.run(batch, step_dev, premarched=kw.get("premarched"))
