@@ -94,6 +94,20 @@ TIMED = ("ncn_composite_train_fw_bg", "ncn_composite_train_bw_bg", "ncn_march_tr
          "ncn_field_bwd", "ncn_field_bwd_mlp_part", "ncn_field_scatter", "ncn_field_scatter_wgrad", "ncn_cluster_loss")
 
 
+def window_start(base, warmup, steps, every=16):
+    """The first global step (>= base) of the warm-up + timed steps whose timed window holds the
+    long-run share of grid refreshes, round(steps / every) of the global steps that are multiples
+    of `every` (Trainer.update_interval: train_nerf.py:318 refreshes every 16 steps).  Without it a
+    window's count depends on where it falls: 20 steps from 3005 held two refreshes (one per 10
+    steps instead of one per 16).  Returns (step0, refreshes in the timed window)."""
+    want = int(steps / every + 0.5)
+    count = lambda a: (a + steps - 1) // every - (a - 1) // every  # noqa: E731
+    for s0 in range(base, base + every):
+        if count(s0 + warmup) == want:
+            return s0, want
+    return base, count(base + warmup)
+
+
 def pmc_traffic():
     """HBM bytes per composite_fw launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2 +
     WRITE_SIZE, separate passes; profiles/<round>/composite_fw_traffic.json), or None."""
@@ -461,19 +475,6 @@ def main():
     torch.manual_seed(1234 + rank)
 
     GT = "surface_bright"  # synthetic target colours (ncnerf_amd.synthetic)
-
-    def window_start(base, warmup, steps, every=16):
-        """The first global step (>= base) of the warm-up + timed steps whose timed window holds the
-        long-run share of grid refreshes, round(steps / every) of the global steps that are multiples
-        of `every` (Trainer.update_interval: train_nerf.py:318 refreshes every 16 steps).  Without it a
-        window's count depends on where it falls: 20 steps from 3005 held two refreshes (one per 10
-        steps instead of one per 16).  Returns (step0, refreshes in the timed window)."""
-        want = int(steps / every + 0.5)
-        count = lambda a: (a + steps - 1) // every - (a - 1) // every  # noqa: E731
-        for s0 in range(base, base + every):
-            if count(s0 + warmup) == want:
-                return s0, want
-        return base, count(base + warmup)
 
     def measure(precision, steps, kernel_table, pretrain, state="procedural", preset="hypersim"):
         """Build the model in `precision`, pretrain it `pretrain` untimed steps, warm up, time `steps`
