@@ -470,9 +470,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void f
 
 // The hash-grid encoding of the density pass (grid refresh: ~1 M points, one per hit cell, with no
 // ray coherence) split by level over the XCDs: block b runs on XCD b % 8 (dispatch round-robin — a
-// placement hint, nothing depends on it) and XCD x encodes levels x and x + 8 of every point, so each
+// placement hint, nothing depends on it) and XCD x encodes levels x and 15 - x of every point, so each
 // 4 MB L2 holds at most two levels' tables instead of serving all 16 (45.8 MB) from the Infinity
-// Cache (the sample-major forward on Morton-ordered grid points: 436 us; with every hashed level
+// Cache, and every XCD pairs a cheap coarse level with a costly fine one (round 6: x and x + 8 left
+// XCDs 5-7 with levels 13-15 and the rest waiting: 225.6 -> 214.5 us for the pass on the bench grid's
+// 706 K cells, profiles/round6/density_probe_pairing.log) (the sample-major forward on Morton-ordered grid points: 436 us; with every hashed level
 // reading one table: 206 us — tools/field_probe.py).  Output: a level-major scratch [16][n16] of T
 // pairs (172 vs 179 us for the pass with the forward's fragment-order layout, tools/density_probe.py), each level's pairs written by its own block; field_fwd_kernel mode 2
 // gathers lane (g, r)'s levels {2g, 2g+1 | 8+2g, 9+2g} from it and runs sigma_net.  Same
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(256) void encode_xcd_kernel(const float* __restrict
     const int64_t n16 = (n + 15) & ~(int64_t)15;  // per-level stride of the level-major scratch
     if (n_dev) n = min<int64_t>(n, *n_dev);
     const int x8 = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int l = j < nb ? x8 : x8 + 8, blk = j < nb ? j : j - nb;
+    const int l = j < nb ? x8 : 15 - x8, blk = j < nb ? j : j - nb;
     const int64_t s = (int64_t)blk * 256 + threadIdx.x;
     if (s >= n) return;
     const float x = (xyzs[3 * s] - xyz_min) / xyz_extent;
