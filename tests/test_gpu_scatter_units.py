@@ -36,7 +36,9 @@ def _ray_samples(n, seed):
 
 
 @pytest.mark.parametrize("n,op,mode", [(70001, "fp16", "unit"), (40960, "fp16", "unit"), (70001, "bf16", "unit"),
-                                       (70001, "fp16", "scaled"), (40960, "bf16", "scaled"), (40960, "fp16", "inf")])
+                                       (70001, "fp16", "scaled"), (40960, "bf16", "scaled"), (40960, "fp16", "inf"),
+                                       # fewer units than workgroups: most draw nothing from the unit queue
+                                       (5, "fp16", "unit"), (301, "bf16", "scaled")])
 def test_scatter_matches_serial_oracle(dev, n, op, mode):
     """mode "unit": the stored pairs are the gradient (header 1/S = 1); "scaled": the pairs carry the
     loss scale S = 2^23 (values ~2^-12 stored as ~2^11) and the scatter multiplies by the header's
